@@ -1,0 +1,188 @@
+// capi.hip -- the extern "C" boundary of libccphylo_amd.so (include/ccphylo_amd.h).
+#include <stdio.h>
+#include <string.h>
+#include <stdlib.h>
+#include "ccg_internal.h"
+
+int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out);
+int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
+                  double *final_d, int64_t *stats);
+
+static char g_last_error[512];
+
+void ccg_set_last_error(hipError_t e, const char *what, const char *file, int line) {
+	snprintf(g_last_error, sizeof(g_last_error), "%s (%d) in %s at %s:%d", hipGetErrorString(e), (int) e, what, file,
+	         line);
+	fprintf(stderr, "ccphylo_amd: HIP error: %s\n", g_last_error);
+}
+
+extern "C" {
+
+const char *ccg_strerror(int code) {
+	switch(code) {
+		case CCG_OK: return "success";
+		case CCG_EINVAL: return "invalid argument";
+		case CCG_ENODEV: return "no gfx950 (MI355X) HIP device available";
+		case CCG_ENOMEM: return "device out of memory";
+		case CCG_EHIP: return g_last_error[0] ? g_last_error : "HIP runtime error";
+		case CCG_EUNSUP: return "not supported by the GPU engine";
+		default: return "unknown error";
+	}
+}
+
+int ccg_init(int device, ccg_ctx **out) {
+	if(!out) return CCG_EINVAL;
+	*out = NULL;
+	int count = 0;
+	if(hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count) {
+		return CCG_ENODEV;
+	}
+	hipDeviceProp_t prop;
+	if(hipGetDeviceProperties(&prop, device) != hipSuccess) return CCG_ENODEV;
+	if(strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+		snprintf(g_last_error, sizeof(g_last_error), "device %d is %s, this build targets gfx950", device,
+		         prop.gcnArchName);
+		return CCG_ENODEV;
+	}
+	CCG_CHECK(hipSetDevice(device));
+	ccg_ctx *c = (ccg_ctx *) calloc(1, sizeof(ccg_ctx));
+	if(!c) return CCG_ENOMEM;
+	c->device = device;
+	snprintf(c->name, sizeof(c->name), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+	if(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+	   hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+		free(c);
+		return CCG_EHIP;
+	}
+	*out = c;
+	return CCG_OK;
+}
+
+void ccg_destroy(ccg_ctx *c) {
+	if(!c) return;
+	hipSetDevice(c->device);
+	hipStreamSynchronize(c->stream);
+	hipEventDestroy(c->ev0);
+	hipEventDestroy(c->ev1);
+	hipStreamDestroy(c->stream);
+	free(c);
+}
+
+int ccg_device_info(ccg_ctx *c, char *buf, size_t len) {
+	if(!c || !buf || !len) return CCG_EINVAL;
+	snprintf(buf, len, "%s", c->name);
+	return CCG_OK;
+}
+
+int ccg_snp_ltd_dev(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
+	if(!c || !a || !D) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	return ccg_snp_dev_impl(c, a, D, N, inc_out);
+}
+
+int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
+	if(!c || !a || !D || !a->seqs || !a->incs) return CCG_EINVAL;
+	if(a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	size_t n = (size_t) a->n;
+	size_t seq_bytes = n * (size_t) a->stride * 8;
+	size_t inc_bytes = (a->pair ? n : 1) * (size_t) a->stride * 4;
+	size_t lt = n > 1 ? n * (n - 1) / 2 * (size_t) a->etype : 0;
+	void *d_seq = NULL, *d_inc = NULL, *d_D = NULL, *d_N = NULL;
+	int rc = CCG_OK;
+	ccg_snp_args da = *a;
+	if(hipMalloc(&d_seq, seq_bytes ? seq_bytes : 8) != hipSuccess || hipMalloc(&d_inc, inc_bytes ? inc_bytes : 4) != hipSuccess ||
+	   hipMalloc(&d_D, lt ? lt : 8) != hipSuccess || (N && a->pair && hipMalloc(&d_N, lt ? lt : 8) != hipSuccess)) {
+		rc = CCG_ENOMEM;
+		goto done;
+	}
+	if(hipMemcpy(d_seq, a->seqs, seq_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+	   hipMemcpy(d_inc, a->incs, inc_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+		rc = CCG_EHIP;
+		goto done;
+	}
+	// untouched cells (outside a row range) keep the caller's contents
+	if(lt && (a->row_begin || a->row_end)) {
+		if(hipMemcpy(d_D, D, lt, hipMemcpyHostToDevice) != hipSuccess ||
+		   (d_N && hipMemcpy(d_N, N, lt, hipMemcpyHostToDevice) != hipSuccess)) {
+			rc = CCG_EHIP;
+			goto done;
+		}
+	}
+	da.seqs = (const uint64_t *) d_seq;
+	da.incs = (const uint32_t *) d_inc;
+	rc = ccg_snp_dev_impl(c, &da, d_D, d_N, inc_out);
+	if(rc == CCG_OK && lt) {
+		if(hipMemcpy(D, d_D, lt, hipMemcpyDeviceToHost) != hipSuccess ||
+		   (d_N && hipMemcpy(N, d_N, lt, hipMemcpyDeviceToHost) != hipSuccess)) {
+			rc = CCG_EHIP;
+		}
+	}
+done:
+	if(d_seq) hipFree(d_seq);
+	if(d_inc) hipFree(d_inc);
+	if(d_D) hipFree(d_D);
+	if(d_N) hipFree(d_N);
+	return rc;
+}
+
+int ccg_tree_dev(ccg_ctx *c, const ccg_tree_args *a, void *D, ccg_join *joins, int *njoins, int *final_n,
+                 double *final_d, int64_t *stats) {
+	if(!c || !a || !D || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
+	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ)) return CCG_EINVAL;
+	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
+	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats);
+}
+
+int ccg_tree(ccg_ctx *c, const ccg_tree_args *a, const void *D, ccg_join *joins, int *njoins, int *final_n,
+             double *final_d, int64_t *stats) {
+	if(!c || !a || !D) return CCG_EINVAL;
+	if(a->n < 3) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	size_t bytes = (size_t) a->n * (size_t) (a->n - 1) / 2 * (size_t) a->etype;
+	void *d = NULL;
+	if(hipMalloc(&d, bytes) != hipSuccess) return CCG_ENOMEM;
+	int rc = CCG_OK;
+	if(hipMemcpy(d, D, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+		rc = CCG_EHIP;
+	} else {
+		rc = ccg_tree_dev(c, a, d, joins, njoins, final_n, final_d, stats);
+	}
+	hipFree(d);
+	return rc;
+}
+
+int ccg_malloc(ccg_ctx *c, void **p, size_t bytes) {
+	if(!c || !p) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipMalloc(p, bytes ? bytes : 1));
+	return CCG_OK;
+}
+
+int ccg_free(ccg_ctx *c, void *p) {
+	if(!c) return CCG_EINVAL;
+	CCG_CHECK(hipFree(p));
+	return CCG_OK;
+}
+
+int ccg_memcpy_h2d(ccg_ctx *c, void *dst, const void *src, size_t bytes) {
+	if(!c) return CCG_EINVAL;
+	CCG_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+	return CCG_OK;
+}
+
+int ccg_memcpy_d2h(ccg_ctx *c, void *dst, const void *src, size_t bytes) {
+	if(!c) return CCG_EINVAL;
+	CCG_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+	return CCG_OK;
+}
+
+int ccg_synchronize(ccg_ctx *c) {
+	if(!c) return CCG_EINVAL;
+	CCG_CHECK(hipStreamSynchronize(c->stream));
+	return CCG_OK;
+}
+
+}   // extern "C"

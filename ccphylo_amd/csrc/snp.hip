@@ -1,0 +1,339 @@
+// snp.hip -- all-pairs SNP distances on gfx950 (the `ccphylo dist` hot loop).
+//
+// Reference: fsacmp.c:552 fsacmp (count of included positions where the
+// 2-bit codes differ), fsacmp.c:587 fsacmpair (same over inc_i & inc_j, plus
+// the number of compared positions), driven by fsacmpthrd.c:108 cmpFsaThrd /
+// :261 cmpairFsaThrd which store nFactor*dist (resp. the A7 epilogue) into
+// LT cell (i, j).
+//
+// Data layout in HBM ("bit planes"): for taxon t and 32-position word w,
+//   hi[t][w] = high code bits, lo[t][w] = low code bits, MSB = first position
+// (the include-mask bit order of fsacmp.c:200).  Non-pair mode pre-applies
+// the global include mask to both planes, so a pair's count is
+//   sum_w popc((hi_a ^ hi_b) | (lo_a ^ lo_b))        -- 4 VALU ops / 32 nt.
+// Pair mode keeps each taxon's mask m beside its planes:
+//   d += popc(((hi_a ^ hi_b) | (lo_a ^ lo_b)) & m_a & m_b), n += popc(m_a & m_b).
+// This is VALU-integer-bound (no dense contraction, MFMA not used): 128x128
+// pair tiles, 8x8 pairs per thread in registers, KC-word chunks of both row
+// panels staged through LDS.
+#include "ccg_internal.h"
+
+#define TILE 128
+#define KC 16          // words per LDS chunk (non-pair)
+#define KCP 8          // words per LDS chunk (pair)
+#define RS 130         // LDS row stride in 8-byte units: 16-byte aligned, 2-way write conflicts at most
+#define RSP 130        // pair: stride in 16-byte units
+
+__device__ __forceinline__ uint32_t compress_even(uint64_t x) {
+	x &= 0x5555555555555555ull;
+	x = (x | (x >> 1)) & 0x3333333333333333ull;
+	x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+	x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+	x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+	x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+	return (uint32_t) x;
+}
+
+// qseq2nibble word (position p at bits 63-2p..62-2p) -> (hi, lo) planes
+__global__ void k_planes(const uint64_t *__restrict__ seqs, const uint32_t *__restrict__ incs, int n, int stride,
+                         int W32, int Wp, int pair, uint2 *__restrict__ out2, uint4 *__restrict__ out4) {
+	long long e = (long long) blockIdx.x * blockDim.x + threadIdx.x;
+	long long total = (long long) n * Wp;
+	if(e >= total) return;
+	int t = (int) (e / Wp), w = (int) (e % Wp);
+	uint32_t hi = 0, lo = 0, m = 0;
+	if(w < W32) {
+		uint64_t x = seqs[(size_t) t * stride + w];
+		hi = compress_even(x >> 1);
+		lo = compress_even(x);
+		m = pair ? incs[(size_t) t * stride + w] : incs[w];
+	}
+	if(pair) {
+		out4[e] = make_uint4(hi, lo, m, 0);
+	} else {
+		out2[e] = make_uint2(hi & m, lo & m);
+	}
+}
+
+__global__ void k_popsum(const uint32_t *__restrict__ inc, int W32, int *out) {
+	int s = 0;
+	for(int w = threadIdx.x; w < W32; w += blockDim.x) s += __popc(inc[w]);
+	for(int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+	__shared__ int ws[16];
+	if((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		int t = 0;
+		for(int k = 0; k < (int) (blockDim.x >> 6); ++k) t += ws[k];
+		*out = t;
+	}
+}
+
+// linear tile index -> (I, J), I >= J, row-major over the lower triangle
+__device__ __forceinline__ void tile_ij(long long t, int &I, int &J) {
+	long long r = (long long) ((sqrt(8.0 * (double) t + 1.0) - 1.0) * 0.5);
+	while(r * (r + 1) / 2 > t) --r;
+	while((r + 1) * (r + 2) / 2 <= t) ++r;
+	I = (int) r;
+	J = (int) (t - r * (r + 1) / 2);
+}
+
+template <int ET>
+__global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P, int Wp, int n, long long t0,
+                                                     double nFactor, double bs, typename Elem<ET>::T *__restrict__ D,
+                                                     long long rowBegin, long long rowEnd) {
+	__shared__ __attribute__((aligned(16))) uint2 As[KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[KC * RS];
+	int I, J;
+	tile_ij(t0 + blockIdx.x, I, J);
+	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+	const uint2 *Ap = P + (size_t) I * TILE * Wp;
+	const uint2 *Bp = P + (size_t) J * TILE * Wp;
+	uint32_t acc[8][8];
+#pragma unroll
+	for(int a = 0; a < 8; ++a)
+#pragma unroll
+		for(int c = 0; c < 8; ++c) acc[a][c] = 0;
+
+	for(int w0 = 0; w0 < Wp; w0 += KC) {
+#pragma unroll
+		for(int q = 0; q < 4; ++q) {
+			int e = q * 256 + threadIdx.x;
+			int row = e >> 3, wp = e & 7;
+			uint4 va = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + 2 * wp);
+			uint4 vb = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + 2 * wp);
+			As[(2 * wp) * RS + row] = make_uint2(va.x, va.y);
+			As[(2 * wp + 1) * RS + row] = make_uint2(va.z, va.w);
+			Bs[(2 * wp) * RS + row] = make_uint2(vb.x, vb.y);
+			Bs[(2 * wp + 1) * RS + row] = make_uint2(vb.z, vb.w);
+		}
+		__syncthreads();
+#pragma unroll 2
+		for(int w = 0; w < KC; ++w) {
+			uint4 a[4], b[4];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				a[q] = *(const uint4 *) &As[w * RS + 2 * ty + 32 * q];
+				b[q] = *(const uint4 *) &Bs[w * RS + 2 * tx + 32 * q];
+			}
+#pragma unroll
+			for(int qa = 0; qa < 4; ++qa) {
+#pragma unroll
+				for(int qb = 0; qb < 4; ++qb) {
+					acc[2 * qa][2 * qb] += __popc((a[qa].x ^ b[qb].x) | (a[qa].y ^ b[qb].y));
+					acc[2 * qa][2 * qb + 1] += __popc((a[qa].x ^ b[qb].z) | (a[qa].y ^ b[qb].w));
+					acc[2 * qa + 1][2 * qb] += __popc((a[qa].z ^ b[qb].x) | (a[qa].w ^ b[qb].y));
+					acc[2 * qa + 1][2 * qb + 1] += __popc((a[qa].z ^ b[qb].z) | (a[qa].w ^ b[qb].w));
+				}
+			}
+		}
+		__syncthreads();
+	}
+	// epilogue: D[i][j] = nFactor * dist (fsacmpthrd.c:247-255), j < i only
+#pragma unroll
+	for(int a = 0; a < 8; ++a) {
+		long long i = (long long) I * TILE + 2 * ty + 32 * (a >> 1) + (a & 1);
+		if(i >= n || i < rowBegin || i >= rowEnd) continue;
+		long long base = tri(i);
+#pragma unroll
+		for(int c = 0; c < 8; ++c) {
+			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
+			if(j < i) {
+				double v = nFactor * (double) acc[a][c];
+				D[base + j] = Elem<ET>::put(v, 0.5, bs);
+			}
+		}
+	}
+}
+
+// A7 epilogue (fsacmpthrd.c:420-475) for one pair
+template <int ET>
+__device__ __forceinline__ void pair_store(typename Elem<ET>::T *D, typename Elem<ET>::T *N, long long f, uint32_t dist,
+                                           uint32_t inc, unsigned norm, unsigned minLength, double bs) {
+	typedef typename Elem<ET>::T T;
+	if(ET == 8) {
+		double v;
+		if(minLength <= inc) {
+			v = norm ? (double) ((unsigned long long) dist * norm) / inc : (double) dist;
+		} else {
+			v = -1.0;
+		}
+		D[f] = (T) v;
+		if(N) N[f] = (T) (double) inc;
+	} else if(ET == 4) {
+		float v;
+		if(minLength <= inc) {
+			if(norm) {
+				v = (float) ((unsigned long long) dist * norm);
+				v = v / (float) inc;
+			} else {
+				v = (float) dist;
+			}
+		} else {
+			v = -1.0f;
+		}
+		D[f] = (T) v;
+		if(N) N[f] = (T) (float) inc;
+	} else {
+		double v;
+		if(minLength <= inc) {
+			v = norm ? ((double) ((unsigned long long) dist * norm) * bs + 0.5) / inc : (double) dist * bs + 0.5;
+		} else {
+			v = -1.0 * bs + 0;
+		}
+		D[f] = (T) cvt_i32_x86(v);
+		if(N) N[f] = (T) cvt_i32_x86(inc * bs + 0.5);
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
+                                                          unsigned norm, unsigned minLength, double bs,
+                                                          typename Elem<ET>::T *__restrict__ D,
+                                                          typename Elem<ET>::T *__restrict__ Nm,
+                                                          long long rowBegin, long long rowEnd) {
+	__shared__ __attribute__((aligned(16))) uint4 As[KCP * RSP];
+	__shared__ __attribute__((aligned(16))) uint4 Bs[KCP * RSP];
+	int I, J;
+	tile_ij(t0 + blockIdx.x, I, J);
+	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+	const uint4 *Ap = P + (size_t) I * TILE * Wp;
+	const uint4 *Bp = P + (size_t) J * TILE * Wp;
+	uint32_t ad[8][8], an[8][8];
+#pragma unroll
+	for(int a = 0; a < 8; ++a)
+#pragma unroll
+		for(int c = 0; c < 8; ++c) {
+			ad[a][c] = 0;
+			an[a][c] = 0;
+		}
+	for(int w0 = 0; w0 < Wp; w0 += KCP) {
+#pragma unroll
+		for(int q = 0; q < 4; ++q) {
+			int e = q * 256 + threadIdx.x;
+			int row = e >> 3, wp = e & 7;
+			As[wp * RSP + row] = Ap[(size_t) row * Wp + w0 + wp];
+			Bs[wp * RSP + row] = Bp[(size_t) row * Wp + w0 + wp];
+		}
+		__syncthreads();
+		for(int w = 0; w < KCP; ++w) {
+			uint4 a[8], b[8];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				a[2 * q] = As[w * RSP + 2 * ty + 32 * q];
+				a[2 * q + 1] = As[w * RSP + 2 * ty + 32 * q + 1];
+				b[2 * q] = Bs[w * RSP + 2 * tx + 32 * q];
+				b[2 * q + 1] = Bs[w * RSP + 2 * tx + 32 * q + 1];
+			}
+#pragma unroll
+			for(int x = 0; x < 8; ++x) {
+#pragma unroll
+				for(int y = 0; y < 8; ++y) {
+					uint32_t m = a[x].z & b[y].z;
+					ad[x][y] += __popc(((a[x].x ^ b[y].x) | (a[x].y ^ b[y].y)) & m);
+					an[x][y] += __popc(m);
+				}
+			}
+		}
+		__syncthreads();
+	}
+#pragma unroll
+	for(int a = 0; a < 8; ++a) {
+		long long i = (long long) I * TILE + 2 * ty + 32 * (a >> 1) + (a & 1);
+		if(i >= n || i < rowBegin || i >= rowEnd) continue;
+		long long base = tri(i);
+#pragma unroll
+		for(int c = 0; c < 8; ++c) {
+			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
+			if(j < i) pair_store<ET>(D, Nm, base + j, ad[a][c], an[a][c], norm, minLength, bs);
+		}
+	}
+}
+
+// ------------------------------------------------------------------ host
+static inline long long cdivll(long long a, long long b) { return (a + b - 1) / b; }
+
+template <int ET>
+static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D, void *N,
+                      long long rb, long long re) {
+	typedef typename Elem<ET>::T T;
+	int nb = (int) cdivll(a->n, TILE);
+	long long Ilo = rb / TILE, Ihi = (re - 1) / TILE;   // tile rows touching [rb, re)
+	long long t_begin = Ilo * (Ilo + 1) / 2, t_end = (Ihi + 1) * (Ihi + 2) / 2;
+	(void) nb;
+	const long long batch = 1 << 14;
+	for(long long t = t_begin; t < t_end; t += batch) {
+		long long cnt = t_end - t < batch ? t_end - t : batch;
+		if(a->pair) {
+			k_snp_tile_pair<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>(
+			    (const uint4 *) planes, Wp, a->n, t, a->norm, a->minLength, a->byteScale, (T *) D, (T *) N, rb, re);
+		} else {
+			k_snp_tile<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, nFactor,
+			                                                       a->byteScale, (T *) D, rb, re);
+		}
+		CCG_CHECK(hipGetLastError());
+	}
+	return CCG_OK;
+}
+
+int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
+	if(!a || a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
+	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
+	if(a->proxi && a->pair) return CCG_EUNSUP;
+	if(a->n < 2) {
+		if(inc_out && !a->pair) {
+			int *d_inc;
+			CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
+			k_popsum<<<1, 256, 0, ctx->stream>>>(a->incs, (a->len + 31) / 32, d_inc);
+			CCG_CHECK(hipMemcpy(inc_out, d_inc, sizeof(int), hipMemcpyDeviceToHost));
+			CCG_CHECK(hipFree(d_inc));
+		}
+		return CCG_OK;
+	}
+	const int W32 = (a->len + 31) / 32;
+	const int kc = a->pair ? KCP : KC;
+	const int Wp = (int) (cdivll(W32, kc) * kc);
+	const long long npad = cdivll(a->n, TILE) * TILE;
+	const size_t esz = a->pair ? sizeof(uint4) : sizeof(uint2);
+	void *planes = NULL;
+	int *d_inc = NULL;
+	CCG_CHECK(hipMalloc(&planes, (size_t) npad * Wp * esz));
+	CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
+	CCG_CHECK(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream));
+	long long total = (long long) a->n * Wp;
+	k_planes<<<(unsigned) cdivll(total, 256), 256, 0, ctx->stream>>>(a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair,
+	                                                                (uint2 *) planes, (uint4 *) planes);
+	CCG_CHECK(hipGetLastError());
+	int inc = 0;
+	if(!a->pair) {
+		k_popsum<<<1, 1024, 0, ctx->stream>>>(a->incs, W32, d_inc);
+		CCG_CHECK(hipMemcpyAsync(&inc, d_inc, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+		CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	}
+	double nFactor = 1.0;
+	if(!a->pair && a->norm) {
+		nFactor = a->norm;
+		nFactor /= inc;   // fsacmpthrd.c:171-176
+	}
+	long long rb = a->row_begin, re = a->row_end;
+	if(rb == 0 && re == 0) re = a->n;
+	if(rb < 0 || re > a->n || rb > re) {
+		hipFree(planes);
+		hipFree(d_inc);
+		return CCG_EINVAL;
+	}
+	int rc = CCG_OK;
+	if(re > rb) {
+		switch(a->etype) {
+			case 8: rc = snp_launch<8>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
+			case 4: rc = snp_launch<4>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
+			case 2: rc = snp_launch<2>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
+			default: rc = snp_launch<1>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
+		}
+	}
+	CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	CCG_CHECK(hipFree(planes));
+	CCG_CHECK(hipFree(d_inc));
+	if(inc_out) *inc_out = inc;
+	return rc;
+}

@@ -1,0 +1,522 @@
+/*
+ * main.c -- `ccphylo dist` and `ccphylo tree`, the stable CLI surface, with
+ * the hot path on the GPU engine (include/ccphylo_amd.h).
+ *
+ * Mirrors ref main.c:99 (dispatch), dist.c:473 main_dist / :42 makeMatrix /
+ * cdist.c:196 ltdMsaMatrix_get, and tree.c:146 main_tree / :37 formTree:
+ * same options, same stdout bytes, same stderr progress lines.  Option forms
+ * the GPU engine does not implement (-V, -y, -a, -P with pairwise masks,
+ * count-matrix / multi-file / union inputs, non-NJ tree methods) are refused
+ * with an error instead of being silently approximated.
+ *
+ * Extra (not in the reference): `tree --fast_sums` uses a fixed-order
+ * parallel row sum instead of the reference's serial one;
+ * `--device N` selects the GPU.
+ */
+#include <ctype.h>
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "ccphylo_amd.h"
+#include "ccphylo_host.h"
+
+static void die_opt(const char *kind, const char *opt) {
+	fprintf(stderr, "%s argument:\t\"%s\"\n", kind, opt);
+	exit(1);
+}
+
+static int is_num(const char *s) {
+	char *e;
+	if(!s || !*s) return 0;
+	strtod(s, &e);
+	return *e == 0;
+}
+
+typedef struct {
+	int argc, k;
+	char **argv;
+} Args;
+
+/* value of an option: attached ("-x5", "--opt=5") or the next argv word */
+static char *opt_value(Args *A, const char *attached, const char *opt) {
+	if(attached && *attached) return (char *) attached;
+	if(A->k + 1 < A->argc) return A->argv[++A->k];
+	die_opt("Missing", opt);
+	return NULL;
+}
+
+/* optional numeric value (cmdline.c getdDefArg): only if it does not start with '-' */
+static double opt_dvalue_def(Args *A, const char *attached, double def, const char *opt) {
+	const char *v = NULL;
+	if(attached && *attached) {
+		v = attached;
+	} else if(A->k + 1 < A->argc && A->argv[A->k + 1][0] != '-') {
+		v = A->argv[++A->k];
+	}
+	if(!v) return def;
+	if(!is_num(v)) die_opt("Invalid", opt);
+	return strtod(v, NULL);
+}
+
+static long opt_num(Args *A, const char *attached, const char *opt) {
+	char *v = opt_value(A, attached, opt), *e;
+	long x = strtol(v, &e, 10);
+	if(*e) die_opt("Invalid", opt);
+	return x;
+}
+
+static ccg_ctx *open_gpu(int device) {
+	ccg_ctx *ctx = NULL;
+	int rc = ccg_init(device, &ctx);
+	if(rc) {
+		fprintf(stderr, "ccphylo_amd: cannot open GPU %d: %s\n", device, ccg_strerror(rc));
+		exit(1);
+	}
+	return ctx;
+}
+
+/* ================================================================ tree */
+static int tree_help(FILE *out) {
+	fprintf(out, "#CCPhylo forms tree(s) in newick format given a set of phylip distance matrices.\n");
+	fprintf(out, "#   %-24s\t%-32s\t%s\n", "Options are:", "Desc:", "Default:");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'i', "input", "Input file", "stdin");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'o', "output", "Output file", "stdout");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'S', "separator", "Separator", "\\t");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'q', "quotes", "Quote taxa", "\\0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'x', "print_precision", "Floating point print precision", "9");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'm', "method", "Tree construction method.", "dnj");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'M', "method_help", "Help on option \"-m\"", "");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'f', "flag", "Output flags", "0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'F', "flag_help", "Help on option \"-f\"", "");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'p', "float_precision", "Float precision on distance matrix", "False / double");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 's', "short_precision", "Short precision on distance matrix", "False / double / 1e0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'b', "byte_precision", "Byte precision on distance matrix", "False / double / 1e0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'g', "free", "Gradually free up D", "False");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'H', "mmap", "Allocate matrix on the disk", "False");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'T', "tmp", "Set directory for temporary files", "");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
+	return out == stderr;
+}
+
+static int main_tree(int argc, char **argv) {
+	const char *in = "-", *outname = "-", *method = "dnj";
+	int flag = 0, precision = 9, et = 8, fast = 0, device = 0, stats = 0;
+	char sep = '\t', quotes = 0;
+	double bs = 1.0;
+	Args A = {argc, 0, argv};
+	for(A.k = 1; A.k < argc; ++A.k) {
+		char *a = argv[A.k];
+		if(a[0] != '-' || a[1] == 0) {
+			in = a;
+			if(A.k + 1 < argc) {
+				fprintf(stderr, "Unexpected non-option argument(s).\n");
+				return 1;
+			}
+			break;
+		}
+		if(a[1] == '-') {
+			char *name = a + 2, *eq = strchr(name, '=');
+			char *att = NULL;
+			if(eq) {
+				*eq = 0;
+				att = eq + 1;
+			}
+			if(*name == 0) { continue; }
+			else if(!strcmp(name, "input")) in = opt_value(&A, att, "input");
+			else if(!strcmp(name, "output")) outname = opt_value(&A, att, "output");
+			else if(!strcmp(name, "separator")) sep = opt_value(&A, att, "separator")[0];
+			else if(!strcmp(name, "quotes")) quotes = opt_value(&A, att, "quotes")[0];
+			else if(!strcmp(name, "print_precision")) precision = (int) opt_num(&A, att, "print_precision");
+			else if(!strcmp(name, "method")) method = opt_value(&A, att, "method");
+			else if(!strcmp(name, "method_help")) method = "mh";
+			else if(!strcmp(name, "flag")) flag = (int) opt_num(&A, att, "flag");
+			else if(!strcmp(name, "flag_help")) flag = -1;
+			else if(!strcmp(name, "threads")) (void) opt_num(&A, att, "threads");
+			else if(!strcmp(name, "float_precision")) et = 4;
+			else if(!strcmp(name, "short_precision")) { et = 2; bs = opt_dvalue_def(&A, att, bs, "short_precision"); }
+			else if(!strcmp(name, "byte_precision")) { et = 1; bs = opt_dvalue_def(&A, att, bs, "byte_precision"); }
+			else if(!strcmp(name, "free") || !strcmp(name, "mmap")) { /* host memory knobs: no effect on HBM */ }
+			else if(!strcmp(name, "tmp")) (void) opt_value(&A, att, "tmp");
+			else if(!strcmp(name, "fast_sums")) fast = 1;
+			else if(!strcmp(name, "device")) device = (int) opt_num(&A, att, "device");
+			else if(!strcmp(name, "stats")) stats = 1;
+			else if(!strcmp(name, "help")) return tree_help(stdout);
+			else die_opt("Unknown", a);
+			continue;
+		}
+		for(char *p = a + 1; *p; ++p) {
+			char o = *p, *att = p + 1;
+			int took = 1;
+			switch(o) {
+				case 'i': in = opt_value(&A, att, "i"); break;
+				case 'o': outname = opt_value(&A, att, "o"); break;
+				case 'S': sep = opt_value(&A, att, "S")[0]; break;
+				case 'q': quotes = opt_value(&A, att, "q")[0]; break;
+				case 'x': precision = (int) opt_num(&A, att, "x"); break;
+				case 'm': method = opt_value(&A, att, "m"); break;
+				case 'f': flag = (int) opt_num(&A, att, "f"); break;
+				case 't': (void) opt_num(&A, att, "t"); break;
+				case 'T': (void) opt_value(&A, att, "T"); break;
+				case 's': et = 2; bs = opt_dvalue_def(&A, att, bs, "s"); break;
+				case 'b': et = 1; bs = opt_dvalue_def(&A, att, bs, "b"); break;
+				case 'M': method = "mh"; took = 0; break;
+				case 'F': flag = -1; took = 0; break;
+				case 'p': et = 4; took = 0; break;
+				case 'g': case 'H': took = 0; break;
+				case 'h': return tree_help(stdout);
+				default: {
+					char bad[3] = {'-', o, 0};
+					die_opt("Unknown", bad);
+				}
+			}
+			if(took) break;
+		}
+	}
+	if(flag == -1) {
+		fprintf(stdout, "# Format flags output, add them to combine them.\n");
+		fprintf(stdout, "#\n");
+		fprintf(stdout, "#   1:\tStrictly bifurcate the root\n");
+		fprintf(stdout, "#   2:\tAllow negative branchlengths\n");
+		fprintf(stdout, "#\n");
+		return 0;
+	}
+	int m;
+	if(!strcmp(method, "dnj")) {
+		m = CCG_TREE_DNJ;
+	} else if(!strcmp(method, "nj")) {
+		m = CCG_TREE_NJ;
+	} else if(!strcmp(method, "mh")) {
+		fprintf(stdout, "# Tree construction methods:\n#\n");
+		fprintf(stdout, "# %-8s\t%s\n", "nj", "Neighbor-Joining");
+		fprintf(stdout, "# %-8s\t%s\n", "dnj", "Dynamic Neighbor-Joining");
+		fprintf(stdout, "#\n");
+		return 0;
+	} else if(!strcmp(method, "upgma") || !strcmp(method, "cf") || !strcmp(method, "ff") || !strcmp(method, "mn") ||
+	          !strcmp(method, "hnj") || !strcmp(method, "frank")) {
+		fprintf(stderr, "ccphylo_amd: tree method \"%s\" is not implemented by the GPU engine (nj, dnj are).\n", method);
+		return 1;
+	} else {
+		die_opt("Invalid", "\"-m\"");
+		return 1;
+	}
+	if((et == 2 || et == 1) && bs == 0) die_opt("Invalid", et == 2 ? "\"--short_precision\"" : "\"--byte_precision\"");
+
+	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
+	if(!out) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return errno ? errno : 1;
+	}
+	ccq_reader *r = ccq_open(in);
+	if(!r) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return errno ? errno : 1;
+	}
+	ccg_ctx *ctx = NULL;
+	ccq_ltd *D = ccq_ltd_new(32, et, bs);        /* tree.c:52 */
+	ccq_names *T = ccq_names_new(32, 4);         /* tree.c:61-66 */
+	int err = 0, n;
+	ccg_join *joins = NULL;
+	size_t jcap = 0;
+	clock_t t0 = clock(), t1;
+	while((n = ccq_load_phy(r, D, T, sep, quotes, &err)) > 0) {
+		t1 = clock();
+		fprintf(stderr, "# Total time used loading matrix: %.2f s.\n", (double) (t1 - t0) / 1000000);
+		t0 = t1;
+		if(n > 2) {
+			if(!ctx) ctx = open_gpu(device);
+			if(jcap < (size_t) n) {
+				jcap = n;
+				joins = realloc(joins, jcap * sizeof(ccg_join));
+			}
+			ccg_tree_args ta = {n, et, bs, m, flag, !fast};
+			int nj = 0, fn = 0;
+			double fd = 0;
+			int64_t st[4];
+			int rc = ccg_tree(ctx, &ta, D->mat, joins, &nj, &fn, &fd, st);
+			if(rc) {
+				fprintf(stderr, "ccphylo_amd: tree construction failed: %s\n", ccg_strerror(rc));
+				return 1;
+			}
+			if(stats) {
+				fprintf(stderr, "# gpu: %d joins, %lld rows / %lld cells rescanned, %lld launches, %.3f ms\n", nj,
+				        (long long) st[0], (long long) st[1], (long long) st[2], st[3] / 1000.0);
+			}
+			ccq_replay_newick(T, n, (const ccq_join *) joins, nj, fn, fd, flag, precision);
+		} else if(n == 2) {
+			ccq_newick_pair(T, ccq_ltd_get(D, 0), precision);
+		}
+		if(T->header->len) {
+			fprintf(out, ">%s%s;\n", (char *) T->header->seq, (char *) T->names[0]->seq);
+		} else {
+			fprintf(out, "%s;\n", (char *) T->names[0]->seq);
+		}
+		t1 = clock();
+		fprintf(stderr, "# Total time used Constructing tree: %.2f s.\n", (double) (t1 - t0) / 1000000);
+		t0 = t1;
+	}
+	if(out != stdout) fclose(out);
+	else fflush(stdout);
+	ccq_close(r);
+	ccq_ltd_free(D);
+	ccq_names_free(T);
+	free(joins);
+	if(ctx) ccg_destroy(ctx);
+	return err ? 1 : 0;
+}
+
+/* ================================================================ dist */
+static int dist_help(FILE *out) {
+	fprintf(out, "#CCPhylo dist calculates distances between samples based on overlaps between nucleotide count matrices created by e.g. KMA.\n");
+	fprintf(out, "#   %-24s\t%-32s\t%s\n", "Options are:", "Desc:", "Default:");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'i', "input", "Input file(s)", "stdin");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'o', "output", "Output file", "stdout");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'n', "nucleotide_numbers", "Output number of nucleotides included", "False/None");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'x', "print_precision", "Floating point print precision", "9");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'L', "min_len", "Minimum overlapping length", "1");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'C', "min_cov", "Minimum coverage", "50.0%");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'W', "normalization_weight", "Normalization weight", "0 / None");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'P', "proximity", "Minimum proximity between SNPs", "0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'f', "flag", "Output flags", "1");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'F', "flag_help", "Help on option \"-f\"", "");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'p', "float_precision", "Float precision on distance matrix", "double");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 's', "short_precision", "Short precision on distance matrix", "double / 1e0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'b', "byte_precision", "Byte precision on distance matrix", "double / 1e0");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
+	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
+	return out == stderr;
+}
+
+static int main_dist(int argc, char **argv) {
+	const char *outname = "-", *noutname = NULL;
+	char **files = NULL;
+	int nfiles = 0, precision = 9, et = 8, device = 0;
+	unsigned flag = 1, norm = 0, minLength = 1, proxi = 0;
+	double minCov = 0.5, bs = 1.0;
+	const char *unsup = NULL;
+	Args A = {argc, 0, argv};
+	for(A.k = 1; A.k < argc; ++A.k) {
+		char *a = argv[A.k];
+		if(a[0] != '-' || a[1] == 0) {
+			files = argv + A.k;
+			nfiles = argc - A.k;
+			break;
+		}
+		if(a[1] == '-') {
+			char *name = a + 2, *eq = strchr(name, '=');
+			char *att = NULL;
+			if(eq) {
+				*eq = 0;
+				att = eq + 1;
+			}
+			if(!strcmp(name, "input")) {
+				if(att) {
+					files = &argv[A.k];
+					argv[A.k] = att;
+					nfiles = 1;
+				} else {
+					files = argv + A.k + 1;
+					nfiles = 0;
+				}
+				while(A.k + 1 < argc && (argv[A.k + 1][0] != '-' || argv[A.k + 1][1] == 0)) {
+					++A.k;
+					++nfiles;
+				}
+			}
+			else if(!strcmp(name, "output")) outname = opt_value(&A, att, "output");
+			else if(!strcmp(name, "nucleotide_numbers")) noutname = opt_value(&A, att, "nucleotide_numbers");
+			else if(!strcmp(name, "separator")) (void) opt_value(&A, att, "separator");
+			else if(!strcmp(name, "print_precision")) precision = (int) opt_num(&A, att, "print_precision");
+			else if(!strcmp(name, "min_len")) minLength = (unsigned) opt_num(&A, att, "min_len");
+			else if(!strcmp(name, "min_cov")) minCov = strtod(opt_value(&A, att, "min_cov"), NULL) / 100;
+			else if(!strcmp(name, "normalization_weight")) norm = (unsigned) opt_num(&A, att, "normalization_weight");
+			else if(!strcmp(name, "proximity")) proxi = (unsigned) opt_num(&A, att, "proximity");
+			else if(!strcmp(name, "flag")) flag = (unsigned) opt_num(&A, att, "flag");
+			else if(!strcmp(name, "flag_help")) flag = (unsigned) -1;
+			else if(!strcmp(name, "threads")) (void) opt_num(&A, att, "threads");
+			else if(!strcmp(name, "float_precision")) et = 4;
+			else if(!strcmp(name, "short_precision")) { et = 2; bs = opt_dvalue_def(&A, att, bs, "short_precision"); }
+			else if(!strcmp(name, "byte_precision")) { et = 1; bs = opt_dvalue_def(&A, att, bs, "byte_precision"); }
+			else if(!strcmp(name, "mmap")) { }
+			else if(!strcmp(name, "tmp")) (void) opt_value(&A, att, "tmp");
+			else if(!strcmp(name, "device")) device = (int) opt_num(&A, att, "device");
+			else if(!strcmp(name, "distance") || !strcmp(name, "min_depth") || !strcmp(name, "significance_lvl")) (void) opt_value(&A, att, name);
+			else if(!strcmp(name, "reference") || !strcmp(name, "add") || !strcmp(name, "methylation_motifs") ||
+			        !strcmp(name, "nucleotide_variations")) { (void) opt_value(&A, att, name); unsup = name; }
+			else if(!strcmp(name, "help")) return dist_help(stdout);
+			else die_opt("Unknown", a);
+			continue;
+		}
+		for(char *p = a + 1; *p; ++p) {
+			char o = *p, *att = p + 1;
+			int took = 1;
+			switch(o) {
+				case 'i':
+					if(*att) {
+						argv[A.k] = att;
+						files = argv + A.k;
+						nfiles = 1;
+					} else {
+						files = argv + A.k + 1;
+						nfiles = 0;
+					}
+					while(A.k + 1 < argc && (argv[A.k + 1][0] != '-' || argv[A.k + 1][1] == 0)) {
+						++A.k;
+						++nfiles;
+					}
+					break;
+				case 'o': outname = opt_value(&A, att, "o"); break;
+				case 'n': noutname = opt_value(&A, att, "n"); break;
+				case 'S': (void) opt_value(&A, att, "S"); break;
+				case 'x': precision = (int) opt_num(&A, att, "x"); break;
+				case 'L': minLength = (unsigned) opt_num(&A, att, "L"); break;
+				case 'C': minCov = strtod(opt_value(&A, att, "C"), NULL) / 100; break;
+				case 'W': norm = (unsigned) opt_num(&A, att, "W"); break;
+				case 'P': proxi = (unsigned) opt_num(&A, att, "P"); break;
+				case 'f': flag = (unsigned) opt_num(&A, att, "f"); break;
+				case 't': (void) opt_num(&A, att, "t"); break;
+				case 'T': (void) opt_value(&A, att, "T"); break;
+				case 'd': case 'E': case 'l': (void) opt_value(&A, att, "d"); break;
+				case 'r': case 'a': case 'y': case 'V': {
+					static char nm[2];
+					nm[0] = o;
+					(void) opt_value(&A, att, nm);
+					unsup = nm;
+					break;
+				}
+				case 's': et = 2; bs = opt_dvalue_def(&A, att, bs, "s"); break;
+				case 'b': et = 1; bs = opt_dvalue_def(&A, att, bs, "b"); break;
+				case 'p': et = 4; took = 0; break;
+				case 'F': flag = (unsigned) -1; took = 0; break;
+				case 'D': case 'H': took = 0; break;
+				case 'h': return dist_help(stdout);
+				default: {
+					char bad[3] = {'-', o, 0};
+					die_opt("Unknown", bad);
+				}
+			}
+			if(took) break;
+		}
+	}
+	if(minCov < 0 || 1 < minCov) die_opt("Invalid", "\"--min_cov\"");
+	if(bs == 0) die_opt("Invalid", et == 2 ? "\"--short_precision\"" : "\"--byte_precision\"");
+	if(flag == (unsigned) -1) {
+		fprintf(stdout, "# Format flags output, add them to combine them.\n");
+		fprintf(stdout, "#\n");
+		fprintf(stdout, "#   1:\tRelaxed Phylip\n");
+		fprintf(stdout, "#   2:\tDistances are pairwise, always true on *.mat files\n");
+		fprintf(stdout, "#   4:\tInclude template name in phylip file\n");
+		fprintf(stdout, "#   8:\tInclude insignificant bases in distance calculation, only affects fasta input\n");
+		fprintf(stdout, "#  16:\tDistances based on fasta input\n");
+		fprintf(stdout, "#  32:\tDo not include insignificant bases in pruning\n");
+		fprintf(stdout, "#\n");
+		return 0;
+	}
+	if(unsup) {
+		fprintf(stderr, "ccphylo_amd: dist option \"%s\" is not implemented by the GPU engine.\n", unsup);
+		return 1;
+	}
+	if(nfiles > 1) {
+		fprintf(stderr, "ccphylo_amd: multi-file dist input is not implemented by the GPU engine (use one MSA).\n");
+		return 1;
+	}
+	if((flag & 2) && proxi) {
+		fprintf(stderr, "ccphylo_amd: pairwise proximity masking (-f 2 with -P) is not implemented by the GPU engine.\n");
+		return 1;
+	}
+	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
+	if(!out) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	FILE *nout = NULL;
+	if(noutname) {
+		/* dist.c:74-84 opens (truncates) it; cdist.c:367 then prints N to outfile */
+		if(!strcmp(noutname, outname)) nout = out;
+		else if(noutname[0] == '-' && noutname[1] == 0) nout = stdout;
+		else nout = fopen(noutname, "wb");
+	}
+	const char *in = nfiles ? files[0] : "-";
+	ccq_reader *r = ccq_open(in);
+	if(!r) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	if(!(flag & 16) && ccq_peek(r) != '>') {
+		fprintf(stderr, "ccphylo_amd: count-matrix (.mat) / union input is not implemented by the GPU engine.\n");
+		return 1;
+	}
+	ccq_msa *M = ccq_load_msa(r, flag, minLength, minCov, proxi, stderr);
+	ccq_close(r);
+	int n = M->n;
+	if(n * (n - 1) / 2 < 1) {
+		fprintf(stderr, "Adjustning number of nodes to %d, to conform with the matrix size.\n", n * (n - 1) / 2);
+	}
+	ccq_ltd *D = ccq_ltd_new(n > 1 ? n : 2, et, bs), *N = NULL;
+	if(!n) {
+		fprintf(stderr, "All sequences were trimmed away.\n");
+		D->n = 0;
+	} else {
+		if(noutname) N = ccq_ltd_new(n > 1 ? n : 2, et, bs);
+		ccg_ctx *ctx = open_gpu(device);
+		ccg_snp_args sa;
+		memset(&sa, 0, sizeof(sa));
+		sa.n = n;
+		sa.len = M->len;
+		sa.stride = M->W;
+		sa.seqs = M->seqs;
+		sa.incs = M->incs;
+		sa.pair = M->pair;
+		sa.norm = norm;
+		sa.minLength = M->minLength;
+		sa.proxi = M->pair ? proxi : 0;
+		sa.etype = et;
+		sa.byteScale = bs;
+		int inc = 0;
+		if(!M->pair) {
+			inc = ccq_npos(M->incs, M->len);
+			fprintf(stderr, "# %d / %d bases included in distance matrix.\n", inc, M->len);
+		}
+		int rc = ccg_snp_ltd(ctx, &sa, D->mat, N ? N->mat : NULL, NULL);
+		if(rc) {
+			fprintf(stderr, "ccphylo_amd: distance computation failed: %s\n", ccg_strerror(rc));
+			return 1;
+		}
+		ccg_destroy(ctx);
+		D->n = n;
+		if(N) N->n = M->pair ? n : 0;
+	}
+	if(1 < D->n) {
+		ccq_print_phy(out, D, M->headers, NULL, NULL, flag, precision);
+		if(N && 1 < N->n) ccq_print_phy(out, N, M->headers, NULL, NULL, flag, precision);
+	}
+	if(out != stdout) fclose(out);
+	else fflush(stdout);
+	if(nout && nout != out && nout != stdout) fclose(nout);
+	ccq_ltd_free(D);
+	ccq_ltd_free(N);
+	ccq_msa_free(M);
+	return 0;
+}
+
+static int main_help(FILE *out) {
+	fprintf(out, "# CCPhylo (ccphylo_amd: MI355X engine for dist and tree)\n");
+	fprintf(out, "# Usage: ccphylo <command> [options]\n");
+	fprintf(out, "#    %-16s\t%s\n", "dist", "all-pairs SNP distances of an MSA (GPU)");
+	fprintf(out, "#    %-16s\t%s\n", "tree", "NJ / DNJ trees from Phylip matrices (GPU)");
+	return out == stderr;
+}
+
+int main(int argc, char **argv) {
+	if(argc < 2) {
+		fprintf(stderr, "Too few arguments handed.\n");
+		return main_help(stderr);
+	}
+	if(!strcmp(argv[1], "dist")) return main_dist(argc - 1, argv + 1);
+	if(!strcmp(argv[1], "tree")) return main_tree(argc - 1, argv + 1);
+	if(!strcmp(argv[1], "-h") || !strcmp(argv[1], "--help")) return main_help(stdout);
+	fprintf(stderr, "ccphylo_amd: command \"%s\" is outside the GPU engine's scope (dist, tree).\n", argv[1]);
+	return 1;
+}

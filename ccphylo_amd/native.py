@@ -1,0 +1,326 @@
+"""ctypes bindings of the two in-tree shared libraries.
+
+- ``lib/libccphylo_amd.so``  -- the gfx950 engine, C-ABI ``include/ccphylo_amd.h``
+  (replaces ``fsaCmpThreadOut`` fsacmpthrd.h:49 and ``dnj_thread``/``nj_thread``
+  dnj.c:1054 / nj.c:1612 of the reference).
+- ``lib/libccphylo_host.so`` -- Phylip / Newick / FASTA host layer,
+  ``include/ccphylo_host.h`` (ref phy.c, nwck.c, seqparse.c, fsacmp.c masks).
+
+There is deliberately no CPU fallback: every GPU entry point raises
+``CcgError`` when the engine library is missing or no gfx950 device exists.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+ENGINE_PATH = os.path.join(LIBDIR, "libccphylo_amd.so")
+HOST_PATH = os.path.join(LIBDIR, "libccphylo_host.so")
+CLI_PATH = os.path.join(HERE, "bin", "ccphylo")
+
+ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
+
+CCG_TREE_NJ = 0
+CCG_TREE_DNJ = 1
+
+
+class CcgError(RuntimeError):
+    pass
+
+
+class SnpArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int), ("len", C.c_int), ("stride", C.c_int),
+        ("seqs", C.c_void_p), ("incs", C.c_void_p),
+        ("pair", C.c_int), ("norm", C.c_uint), ("minLength", C.c_uint), ("proxi", C.c_uint),
+        ("etype", C.c_int), ("byteScale", C.c_double),
+        ("row_begin", C.c_int64), ("row_end", C.c_int64),
+    ]
+
+
+class TreeArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int), ("etype", C.c_int), ("byteScale", C.c_double),
+        ("method", C.c_int), ("flags", C.c_int), ("exact", C.c_int),
+    ]
+
+
+class Join(C.Structure):
+    _fields_ = [("i", C.c_int32), ("j", C.c_int32), ("Li", C.c_double), ("Lj", C.c_double)]
+
+
+JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("Lj", np.float64)])
+
+# every symbol of include/ccphylo_amd.h
+ENGINE_SYMBOLS = [
+    "ccg_init", "ccg_destroy", "ccg_strerror", "ccg_device_info",
+    "ccg_snp_ltd", "ccg_snp_ltd_dev", "ccg_tree", "ccg_tree_dev",
+    "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
+]
+# every symbol of include/ccphylo_host.h
+HOST_SYMBOLS = [
+    "ccq_new", "ccq_free", "ccq_open", "ccq_close", "ccq_peek",
+    "ccq_ltd_new", "ccq_ltd_free", "ccq_ltd_reserve", "ccq_ltd_get", "ccq_ltd_set",
+    "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
+    "ccq_replay_newick", "ccq_newick_pair",
+    "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
+    "ccq_load_msa", "ccq_msa_free",
+]
+
+_engine = None
+_host = None
+
+
+def engine_lib():
+    """Loads libccphylo_amd.so (raises if it was not built)."""
+    global _engine
+    if _engine is None:
+        if not os.path.exists(ENGINE_PATH):
+            raise CcgError(f"{ENGINE_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+        lib = C.CDLL(ENGINE_PATH)
+        lib.ccg_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        lib.ccg_destroy.argtypes = [C.c_void_p]
+        lib.ccg_destroy.restype = None
+        lib.ccg_strerror.argtypes = [C.c_int]
+        lib.ccg_strerror.restype = C.c_char_p
+        lib.ccg_device_info.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        lib.ccg_snp_ltd.argtypes = [C.c_void_p, C.POINTER(SnpArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        lib.ccg_snp_ltd_dev.argtypes = lib.ccg_snp_ltd.argtypes
+        lib.ccg_tree.argtypes = [C.c_void_p, C.POINTER(TreeArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int),
+                                 C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+        lib.ccg_tree_dev.argtypes = lib.ccg_tree.argtypes
+        lib.ccg_malloc.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_size_t]
+        lib.ccg_free.argtypes = [C.c_void_p, C.c_void_p]
+        lib.ccg_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.ccg_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.ccg_synchronize.argtypes = [C.c_void_p]
+        _engine = lib
+    return _engine
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_PATH):
+            raise CcgError(f"{HOST_PATH} missing: run __graft_entry__.build()")
+        lib = C.CDLL(HOST_PATH)
+        lib.ccq_new.restype = C.c_void_p
+        lib.ccq_new.argtypes = [C.c_uint32]
+        lib.ccq_open.restype = C.c_void_p
+        lib.ccq_open.argtypes = [C.c_char_p]
+        lib.ccq_close.argtypes = [C.c_void_p]
+        lib.ccq_ltd_new.restype = C.c_void_p
+        lib.ccq_ltd_new.argtypes = [C.c_int, C.c_int, C.c_double]
+        lib.ccq_ltd_free.argtypes = [C.c_void_p]
+        lib.ccq_names_new.restype = C.c_void_p
+        lib.ccq_names_new.argtypes = [C.c_int, C.c_uint32]
+        lib.ccq_names_free.argtypes = [C.c_void_p]
+        lib.ccq_load_phy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_char, C.c_char, C.POINTER(C.c_int)]
+        lib.ccq_replay_newick.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int]
+        lib.ccq_newick_pair.argtypes = [C.c_void_p, C.c_double, C.c_int]
+        lib.ccq_code_table.argtypes = [C.c_uint, C.c_void_p]
+        lib.ccq_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        lib.ccq_init_inc.argtypes = [C.c_void_p, C.c_int]
+        lib.ccq_inc_update.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_int]
+        lib.ccq_npos.argtypes = [C.c_void_p, C.c_int]
+        lib.ccq_load_msa.restype = C.c_void_p
+        lib.ccq_load_msa.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_double, C.c_uint, C.c_void_p]
+        lib.ccq_msa_free.argtypes = [C.c_void_p]
+        _host = lib
+    return _host
+
+
+# ---------------------------------------------------------------- host structs
+class _Str(C.Structure):
+    _fields_ = [("size", C.c_uint32), ("len", C.c_uint32), ("seq", C.c_char_p)]
+
+
+class _Ltd(C.Structure):
+    _fields_ = [("n", C.c_int), ("size", C.c_int), ("et", C.c_int), ("bs", C.c_double), ("mat", C.c_void_p)]
+
+
+class _Names(C.Structure):
+    _fields_ = [("cap", C.c_int), ("names", C.POINTER(C.POINTER(_Str))), ("header", C.POINTER(_Str))]
+
+
+class _Msa(C.Structure):
+    _fields_ = [("n", C.c_int), ("len", C.c_int), ("W", C.c_int), ("pair", C.c_int),
+                ("headers", C.POINTER(C.c_char_p)), ("seqs", C.POINTER(C.c_uint64)),
+                ("incs", C.POINTER(C.c_uint32)), ("minLength", C.c_uint)]
+
+
+# ---------------------------------------------------------------- engine API
+class Device:
+    """An open gfx950 device + engine stream (ccg_init)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = engine_lib()
+        h = C.c_void_p()
+        rc = self.lib.ccg_init(int(device), C.byref(h))
+        if rc != 0:
+            raise CcgError(f"ccg_init({device}) failed: {self.lib.ccg_strerror(rc).decode()}")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.ccg_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> str:
+        buf = C.create_string_buffer(256)
+        self.lib.ccg_device_info(self.h, buf, 256)
+        return buf.value.decode()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise CcgError(f"{what}: {self.lib.ccg_strerror(rc).decode()}")
+
+    def snp_ltd(self, seqs, incs, n, length, pair=False, norm=0, min_length=1, etype=8, byte_scale=1.0,
+                proxi=0, want_n=False, row_range=(0, 0)):
+        """All-pairs SNP distances (ccg_snp_ltd).  seqs: uint64[n, stride]
+        (qseq2nibble layout); incs: uint32[stride] or uint32[n, stride].
+        Returns (D, N, inc) with D/N packed LT arrays of the element type."""
+        seqs = np.ascontiguousarray(seqs, dtype=np.uint64)
+        incs = np.ascontiguousarray(incs, dtype=np.uint32)
+        stride = seqs.shape[1]
+        m = n * (n - 1) // 2
+        D = np.zeros(max(m, 1), dtype=ETYPES[etype])
+        N = np.zeros(max(m, 1), dtype=ETYPES[etype]) if (want_n and pair) else None
+        a = SnpArgs(n, length, stride, seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length, proxi,
+                    etype, byte_scale, row_range[0], row_range[1])
+        inc = C.c_int(0)
+        rc = self.lib.ccg_snp_ltd(self.h, C.byref(a), D.ctypes.data, N.ctypes.data if N is not None else None,
+                                  C.byref(inc))
+        self._check(rc, "ccg_snp_ltd")
+        return D[:m], (N[:m] if N is not None else None), inc.value
+
+    def tree(self, D, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True):
+        """NJ/DNJ on a packed LT (ccg_tree).  Returns (joins, final_n, final_d, stats)."""
+        D = np.ascontiguousarray(D, dtype=ETYPES[etype])
+        assert D.size == n * (n - 1) // 2
+        joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
+        nj = C.c_int(0)
+        fn = C.c_int(0)
+        fd = C.c_double(0)
+        st = (C.c_int64 * 4)()
+        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact))
+        rc = self.lib.ccg_tree(self.h, C.byref(a), D.ctypes.data, joins.ctypes.data, C.byref(nj), C.byref(fn),
+                               C.byref(fd), st)
+        self._check(rc, "ccg_tree")
+        return joins[:nj.value], fn.value, fd.value, list(st)
+
+
+# ---------------------------------------------------------------- host API
+def load_phylip(path, etype=8, byte_scale=1.0, sep="\t", quotes=""):
+    """All matrices of a Phylip file (ccq_load_phy).  Returns a list of
+    (names, D) with D the packed LT array."""
+    lib = host_lib()
+    r = lib.ccq_open(path.encode())
+    if not r:
+        raise FileNotFoundError(path)
+    D = lib.ccq_ltd_new(32, etype, byte_scale)
+    T = lib.ccq_names_new(32, 4)
+    out = []
+    err = C.c_int(0)
+    try:
+        while True:
+            n = lib.ccq_load_phy(r, D, T, sep.encode()[:1] or b"\t", quotes.encode()[:1] or b"\0", C.byref(err))
+            if n <= 0:
+                break
+            ltd = _Ltd.from_address(D)
+            names = _Names.from_address(T)
+            nm = [names.names[k].contents.seq[:names.names[k].contents.len].decode() for k in range(n)]
+            m = n * (n - 1) // 2
+            buf = (C.c_char * (m * etype)).from_address(ltd.mat) if m else b""
+            arr = np.frombuffer(bytes(buf), dtype=ETYPES[etype]).copy() if m else np.zeros(0, ETYPES[etype])
+            out.append((nm, arr))
+    finally:
+        lib.ccq_close(r)
+        lib.ccq_ltd_free(D)
+        lib.ccq_names_free(T)
+    return out
+
+
+def newick_from_phylip(path, joins_fn, etype=8, byte_scale=1.0, flags=0, precision=9):
+    """Runs `joins_fn(D, n) -> (joins, final_n, final_d)` on every matrix of a
+    Phylip file and rebuilds the Newick strings exactly as `ccphylo tree`
+    prints them (one per matrix, with the trailing ';').  The name table is
+    shared across matrices like the reference's (tree.c:61-66)."""
+    lib = host_lib()
+    r = lib.ccq_open(path.encode())
+    if not r:
+        raise FileNotFoundError(path)
+    D = lib.ccq_ltd_new(32, etype, byte_scale)
+    T = lib.ccq_names_new(32, 4)
+    err = C.c_int(0)
+    trees = []
+    try:
+        while True:
+            n = lib.ccq_load_phy(r, D, T, b"\t", b"\0", C.byref(err))
+            if n <= 0:
+                break
+            ltd = _Ltd.from_address(D)
+            m = n * (n - 1) // 2
+            if n > 2:
+                arr = np.frombuffer((C.c_char * (m * etype)).from_address(ltd.mat), dtype=ETYPES[etype]).copy()
+                joins, fn, fd = joins_fn(arr, n)
+                joins = np.ascontiguousarray(joins, dtype=JOIN_DTYPE)
+                lib.ccq_replay_newick(T, n, joins.ctypes.data, len(joins), fn, fd, flags, precision)
+            elif n == 2:
+                lib.ccq_newick_pair(T, float(np.frombuffer((C.c_char * etype).from_address(ltd.mat),
+                                                           dtype=ETYPES[etype])[0]) / (byte_scale if etype <= 2 else 1.0),
+                                    precision)
+            names = _Names.from_address(T)
+            s = names.names[0].contents.seq.decode()
+            hdr = names.header.contents
+            trees.append((">" + hdr.seq.decode() if hdr.len else "") + s + ";")
+    finally:
+        lib.ccq_close(r)
+        lib.ccq_ltd_free(D)
+        lib.ccq_names_free(T)
+    return trees
+
+
+def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0):
+    """FASTA MSA -> (headers, seqs uint64[n, W], incs, minLength) per ltdMsaMatrix_get."""
+    lib = host_lib()
+    r = lib.ccq_open(path.encode())
+    if not r:
+        raise FileNotFoundError(path)
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    log = libc.fopen(b"/dev/null", b"w")
+    try:
+        Mp = lib.ccq_load_msa(r, flag, min_length, min_cov, proxi, log)
+    finally:
+        lib.ccq_close(r)
+        libc.fclose(log)
+    M = _Msa.from_address(Mp)
+    n, W = M.n, M.W
+    heads = [M.headers[k].decode() for k in range(n)]
+    seqs = np.ctypeslib.as_array(M.seqs, shape=(max(n, 1) * W,))[: n * W].reshape(n, W).copy() if n else np.zeros((0, W), np.uint64)
+    ninc = n if M.pair else 1
+    incs = np.ctypeslib.as_array(M.incs, shape=(max(ninc, 1) * W,))[: ninc * W].copy() if (n and W) else np.zeros(W, np.uint32)
+    if M.pair:
+        incs = incs.reshape(n, W)
+    res = (heads, seqs, incs, M.len, M.minLength)
+    lib.ccq_msa_free(Mp)
+    return res

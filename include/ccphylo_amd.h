@@ -1,0 +1,122 @@
+/*
+ * ccphylo_amd.h -- C-ABI of the MI355X (gfx950) hot-path engine.
+ *
+ * Plain pointers and sizes only.  Every entry point is synchronous to the
+ * caller and returns 0 or a negative CCG_E* code (never exit()s, unlike the
+ * reference's ERROR(), pherror.h:28).  There is no CPU fallback: if the HIP
+ * runtime or a gfx950 device is missing, ccg_init fails with CCG_ENODEV.
+ *
+ * Drop-in mapping (reference ccphylo 0.8.5):
+ *   ccg_snp_ltd   replaces fsaCmpThreadOut(tnum, &cmpFsaThrd | &cmpairFsaThrd, D, N, ...)
+ *                 declared fsacmpthrd.h:49, impl fsacmpthrd.c:76-106,
+ *                 called from cdist.c:351/:354 (MSA) and cdist.c:181/:184.
+ *   ccg_tree      replaces dnj_thread(D, sD, Q, N, names, t) (dnj.c:1054,
+ *                 called tree.c:89) and nj_thread(D, sD, N, names, t)
+ *                 (nj.c:1612, called tree.c:91).  It returns the join list;
+ *                 the Newick string is rebuilt on the host by replaying
+ *                 formNode (nwck.c:35) over it -- see include/ccphylo_host.h.
+ */
+#ifndef CCPHYLO_AMD_H
+#define CCPHYLO_AMD_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCG_OK        0
+#define CCG_EINVAL   -1   /* bad argument */
+#define CCG_ENODEV   -2   /* no HIP device / not gfx950 */
+#define CCG_ENOMEM   -3   /* device allocation failed */
+#define CCG_EHIP     -4   /* other HIP runtime error */
+#define CCG_EUNSUP   -5   /* valid request the GPU engine does not implement */
+
+typedef struct ccg_ctx ccg_ctx;
+
+/* Opens `device` (ordinal in HIP_VISIBLE_DEVICES numbering) and creates the
+ * engine stream.  Fails with CCG_ENODEV when no gfx950 device is present. */
+int ccg_init(int device, ccg_ctx **ctx);
+void ccg_destroy(ccg_ctx *ctx);
+const char *ccg_strerror(int code);
+/* device name + arch, for logs */
+int ccg_device_info(ccg_ctx *ctx, char *buf, size_t len);
+
+/* ------------------------------------------------------------------ */
+/* dist: all-pairs SNP distances (fsacmp.c:552 / :587 per pair)        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+	int n;                 /* taxa, all included (cdist.c:331 include[] == 1) */
+	int len;               /* alignment length */
+	int stride;            /* u64 words per taxon in seqs/incs rows (>= ceil(len/32)) */
+	const uint64_t *seqs;  /* n*stride words, qseq2nibble layout (qseqs.c:60) */
+	const uint32_t *incs;  /* stride words (pair = 0) or n*stride (pair = 1), fsacmp.c:164 layout */
+	int pair;              /* 0: cmpFsaThrd semantics, 1: cmpairFsaThrd semantics */
+	unsigned norm;         /* -W */
+	unsigned minLength;    /* already max(minLength, minCov*len) (cdist.c:289) */
+	unsigned proxi;        /* -P; the GPU engine supports 0 only (CCG_EUNSUP otherwise) */
+	int etype;             /* 8 double, 4 float, 2 u16, 1 u8 (matrix.c:59-71) */
+	double byteScale;      /* ByteScale for etype 2/1 (bytescale.c:45) */
+	int64_t row_begin;     /* LT rows [row_begin, row_end) to compute; 0,0 = all */
+	int64_t row_end;
+} ccg_snp_args;
+
+/* Host buffers: D (and N when pair && N != NULL) receive the packed LT of
+ * n(n-1)/2 elements of `etype` bytes in reference cell order (pi, pj).  With
+ * a row range, only cells of those rows are written (offsets still global).
+ * *inc_out (may be NULL) receives getNpos(mask) for pair == 0. */
+int ccg_snp_ltd(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out);
+
+/* Same, with a->seqs / a->incs and D / N all DEVICE pointers (HBM-resident
+ * pipeline: dist writes the LT that ccg_tree_dev consumes in place). */
+int ccg_snp_ltd_dev(ccg_ctx *ctx, const ccg_snp_args *a, void *D_dev, void *N_dev, int *inc_out);
+
+/* ------------------------------------------------------------------ */
+/* tree: NJ / DNJ on an HBM-resident packed LT matrix                  */
+/* ------------------------------------------------------------------ */
+typedef struct {
+	int32_t i, j;          /* rows joined (j < i) at the time of the join */
+	double Li, Lj;         /* limb lengths (nj.c:42 / :81) */
+} ccg_join;
+
+#define CCG_TREE_NJ   0    /* -m nj  (nj.c:1560, the -t 1 semantics) */
+#define CCG_TREE_DNJ  1    /* -m dnj (dnj.c:985, default) */
+
+typedef struct {
+	int n;                 /* taxa (> 2) */
+	int etype;             /* 8, 4, 2, 1 */
+	double byteScale;
+	int method;            /* CCG_TREE_NJ / CCG_TREE_DNJ */
+	int flags;             /* tree -f: bit 2 = limbLengthNeg (nj.c:81) */
+	int exact;             /* 1: row sums of a join accumulated serially in the
+	                          reference order (bit-identical to the reference);
+	                          0: fixed-order parallel tree sum (deterministic,
+	                          may differ from the reference in the last ulp) */
+} ccg_tree_args;
+
+/* D: host LT (n(n-1)/2 elements), left unmodified.  joins: room for n-2.
+ * On return *njoins joins were made; *final_n is the matrix size at exit
+ * (2 normally; > 2 when the reference loop would stop early with pos == 0)
+ * and *final_d the remaining pair's distance (D(1,0)) when *final_n == 2.
+ * stats (may be NULL, 4 entries): [0] rows rescanned, [1] cells rescanned,
+ * [2] kernel launches, [3] device time in microseconds. */
+int ccg_tree(ccg_ctx *ctx, const ccg_tree_args *a, const void *D,
+             ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
+
+/* Same on a DEVICE LT buffer, which is consumed (overwritten). */
+int ccg_tree_dev(ccg_ctx *ctx, const ccg_tree_args *a, void *D_dev,
+                 ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
+
+/* ------------------------------------------------------------------ */
+/* device memory helpers (for callers that keep the pipeline in HBM)   */
+/* ------------------------------------------------------------------ */
+int ccg_malloc(ccg_ctx *ctx, void **ptr, size_t bytes);
+int ccg_free(ccg_ctx *ctx, void *ptr);
+int ccg_memcpy_h2d(ccg_ctx *ctx, void *dst, const void *src, size_t bytes);
+int ccg_memcpy_d2h(ccg_ctx *ctx, void *dst, const void *src, size_t bytes);
+int ccg_synchronize(ccg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,76 @@
+"""ctypes view of oracle/_build/liboracle.so (the CPU restatement, ccoracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker -- never by ccphylo_amd/.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "ccphylo")
+ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
+JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("Lj", np.float64)])
+
+_lib = None
+
+
+def build():
+    """Builds liboracle.so (and, where /root/reference exists, the reference binary)."""
+    targets = ["oracle"] + (["all"] if os.path.isdir("/root/reference") else [])
+    subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.orc_tree.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                               C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_void_p]
+        L.orc_snp_ltd.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_uint, C.c_double,
+                                  C.c_uint, C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+        L.orc_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.orc_init_inc.argtypes = [C.c_void_p, C.c_int]
+        L.orc_inc_update.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_int]
+        L.orc_npos.argtypes = [C.c_void_p, C.c_int]
+        L.orc_fsacmp.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_fsacmp.restype = C.c_uint32
+        L.orc_fsacmpair.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_fsacmpair.restype = C.c_uint64
+        L.orc_code_table.argtypes = [C.c_uint, C.c_void_p]
+        L.orc_init_sums.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False):
+    """Serial NJ (method 0) / DNJ (method 1) exactly as the reference.
+    Returns (joins, final_n, final_d[, stats])."""
+    D = np.array(D, dtype=ETYPES[etype], copy=True)
+    joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
+    fn = C.c_int(0)
+    fd = C.c_double(0)
+    st = np.zeros(2, dtype=np.int64)
+    nj = lib().orc_tree(n, etype, byte_scale, D.ctypes.data, method, flags, joins.ctypes.data, C.byref(fn),
+                        C.byref(fd), st.ctypes.data)
+    res = (joins[:nj], fn.value, fd.value)
+    return res + (st,) if stats else res
+
+
+def snp_ltd(seqs, incs, n, length, pair=False, norm=0, min_length=1, min_cov=0.0, proxi=0, etype=8,
+            byte_scale=1.0, want_n=False):
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint64)
+    incs = np.ascontiguousarray(incs, dtype=np.uint32)
+    W = length // 32 + 1
+    assert seqs.shape[1] == W
+    m = n * (n - 1) // 2
+    D = np.zeros(max(m, 1), dtype=ETYPES[etype])
+    N = np.zeros(max(m, 1), dtype=ETYPES[etype]) if want_n else None
+    inc = lib().orc_snp_ltd(n, length, seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length, min_cov,
+                            proxi, etype, byte_scale, D.ctypes.data, N.ctypes.data if N is not None else None)
+    return D[:m], (N[:m] if N is not None else None), inc

@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Generates the golden vectors of tests/golden/ by running the REFERENCE
+ccphylo 0.8.5 binary built by oracle/Makefile (oracle/_ref/ccphylo) on
+synthetic inputs made here with fixed seeds, plus the reference's own bundled
+fixture test.phy.gz.  Run in the build container (needs /root/reference):
+
+    make -C oracle && python tests/golden/gen_golden.py
+
+Outputs (all data, committed): inputs *.fsa / *.phy(.gz) and expected outputs
+*.out, listed with their command lines in golden.json.
+"""
+import gzip
+import hashlib
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
+
+
+def msa(path, n, L, seed, mut=0.03, nrate=0.002, gaps=True, lower=True, iupac=True, crlf=False, wrap=60,
+        exclude=1, tree_like=True):
+    """Writes a FASTA MSA.  Taxa descend from random ancestors (tree_like) so
+    the distance matrix has real structure and many ties."""
+    rng = random.Random(seed)
+    base = [rng.choice("ACGT") for _ in range(L)]
+    pool = [base]
+    seqs = []
+    for t in range(n):
+        parent = rng.choice(pool) if tree_like else base
+        s = list(parent)
+        for p in range(L):
+            if rng.random() < mut:
+                s[p] = rng.choice("ACGT")
+        if tree_like and rng.random() < 0.3:
+            pool.append(s[:])
+        for p in range(L):
+            r = rng.random()
+            if r < nrate:
+                s[p] = "N"
+            elif gaps and r < 2 * nrate:
+                s[p] = "-"
+            elif iupac and r < 2.5 * nrate:
+                s[p] = rng.choice("RYSWKMBDHVX")
+            elif lower and r < 3.5 * nrate:
+                s[p] = s[p].lower()
+        seqs.append(s)
+    for t in range(exclude):   # mostly-N taxa: excluded by minCov (cdist.c:270)
+        k = rng.randrange(n)
+        for p in range(L):
+            if rng.random() < 0.7:
+                seqs[k][p] = "N"
+    nl = "\r\n" if crlf else "\n"
+    with open(path, "w", newline="") as f:
+        for t, s in enumerate(seqs):
+            f.write(f">taxon_{t:03d} sample/{t}{nl}")
+            txt = "".join(s)
+            for k in range(0, L, wrap):
+                f.write(txt[k:k + wrap] + nl)
+
+
+def euclid_phy(path, n, seed, dim=8, fmt="%.9f", gz=False):
+    rng = random.Random(seed)
+    pts = [[rng.random() for _ in range(dim)] for _ in range(n)]
+    op = gzip.open if gz else open
+    with op(path, "wt") as f:
+        f.write("%10d\n" % n)
+        for i in range(n):
+            row = [f"e{i}"]
+            for j in range(i):
+                d = sum((a - b) ** 2 for a, b in zip(pts[i], pts[j])) ** 0.5
+                row.append(fmt % d)
+            f.write("\t".join(row) + "\n")
+
+
+def run(args, out):
+    p = subprocess.run([REF] + args, capture_output=True, check=True)
+    with open(out, "wb") as f:
+        f.write(p.stdout)
+    return hashlib.md5(p.stdout).hexdigest()
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("build the reference first: make -C oracle")
+    os.chdir(HERE)
+    cases = []
+
+    def case(name, args, out, kind):
+        md5 = run(args, out)
+        cases.append({"name": name, "kind": kind, "args": args, "out": out, "md5": md5})
+
+    # (i) the reference's bundled fixture
+    shutil.copyfile("/root/reference/test.phy.gz", "test.phy.gz")
+    for m in ("dnj", "nj"):
+        case(f"test_{m}", ["tree", "-i", "test.phy.gz", "-m", m], f"test_{m}.out", "tree")
+    case("test_dnj_p", ["tree", "-i", "test.phy.gz", "-p"], "test_dnj_p.out", "tree")
+    case("test_dnj_f1", ["tree", "-i", "test.phy.gz", "-f", "1"], "test_dnj_f1.out", "tree")
+    case("test_dnj_f2", ["tree", "-i", "test.phy.gz", "-f", "2"], "test_dnj_f2.out", "tree")
+    case("test_dnj_x4", ["tree", "-i", "test.phy.gz", "-x", "4"], "test_dnj_x4.out", "tree")
+    case("test_dnj_s", ["tree", "-i", "test.phy.gz", "-s", "1000"], "test_dnj_s.out", "tree")
+    case("test_nj_b", ["tree", "-i", "test.phy.gz", "-m", "nj", "-b", "100"], "test_nj_b.out", "tree")
+
+    # (ii) MSAs -> dist
+    msa("msa64.fsa", 64, 3000, seed=1)
+    msa("msa_crlf.fsa", 40, 2500, seed=2, crlf=True, wrap=70)
+    msa("msa_odd.fsa", 33, 1027, seed=3, exclude=2)      # len % 32 != 0, two excluded taxa
+    msa("msa_word.fsa", 48, 2048, seed=4, exclude=0)     # len % 32 == 0
+    for f in ("msa64.fsa", "msa_crlf.fsa", "msa_odd.fsa", "msa_word.fsa"):
+        b = f[:-4]
+        case(f"{b}_f1", ["dist", "-i", f], f"{b}_f1.out", "dist")
+        case(f"{b}_f3", ["dist", "-i", f, "-f", "3"], f"{b}_f3.out", "dist")
+    b = "msa64"
+    case(f"{b}_f0", ["dist", "-i", "msa64.fsa", "-f", "0"], f"{b}_f0.out", "dist")
+    case(f"{b}_f9", ["dist", "-i", "msa64.fsa", "-f", "9"], f"{b}_f9.out", "dist")
+    case(f"{b}_f33", ["dist", "-i", "msa64.fsa", "-f", "33"], f"{b}_f33.out", "dist")
+    case(f"{b}_f11", ["dist", "-i", "msa64.fsa", "-f", "11"], f"{b}_f11.out", "dist")
+    case(f"{b}_W", ["dist", "-i", "msa64.fsa", "-W", "1000"], f"{b}_W.out", "dist")
+    case(f"{b}_f3W", ["dist", "-i", "msa64.fsa", "-f", "3", "-W", "1000"], f"{b}_f3W.out", "dist")
+    case(f"{b}_p", ["dist", "-i", "msa64.fsa", "-p"], f"{b}_p.out", "dist")
+    case(f"{b}_f3pW", ["dist", "-i", "msa64.fsa", "-f", "3", "-p", "-W", "999"], f"{b}_f3pW.out", "dist")
+    case(f"{b}_s", ["dist", "-i", "msa64.fsa", "-s", "10"], f"{b}_s.out", "dist")
+    case(f"{b}_f3sW", ["dist", "-i", "msa64.fsa", "-f", "3", "-s", "2", "-W", "100"], f"{b}_f3sW.out", "dist")
+    case(f"{b}_b", ["dist", "-i", "msa64.fsa", "-b"], f"{b}_b.out", "dist")
+    case(f"{b}_P", ["dist", "-i", "msa64.fsa", "-P", "10"], f"{b}_P.out", "dist")
+    case(f"{b}_P2", ["dist", "-i", "msa_odd.fsa", "-P", "2"], f"msa_odd_P2.out", "dist")
+    case(f"{b}_L", ["dist", "-i", "msa64.fsa", "-f", "3", "-L", "2978", "-C", "0"], f"{b}_L.out", "dist")
+    case(f"{b}_n", ["dist", "-i", "msa64.fsa", "-f", "3", "-n", "/dev/null"], f"{b}_n.out", "dist")
+    case(f"{b}_x3", ["dist", "-i", "msa64.fsa", "-W", "7", "-x", "3"], f"{b}_x3.out", "dist")
+
+    # (iii) trees on an integer SNP matrix (tie-heavy) and a Euclidean one
+    msa("msa300.fsa", 300, 2000, seed=5, exclude=0, mut=0.01)
+    run(["dist", "-i", "msa300.fsa"], "snp300.phy")
+    for m in ("dnj", "nj"):
+        case(f"snp300_{m}", ["tree", "-i", "snp300.phy", "-m", m], f"snp300_{m}.out", "tree")
+    case("snp300_s", ["tree", "-i", "snp300.phy", "-s"], "snp300_s.out", "tree")
+    case("snp300_b", ["tree", "-i", "snp300.phy", "-b"], "snp300_b.out", "tree")
+    euclid_phy("euc400.phy.gz", 400, seed=6, gz=True)
+    for m in ("dnj", "nj"):
+        case(f"euc400_{m}", ["tree", "-i", "euc400.phy.gz", "-m", m], f"euc400_{m}.out", "tree")
+    case("euc400_p", ["tree", "-i", "euc400.phy.gz", "-p"], "euc400_p.out", "tree")
+
+    # (iv) missing data: pairwise distances with -1 where the overlap is short
+    msa("msa_miss.fsa", 80, 1500, seed=7, nrate=0.12, exclude=0, gaps=False, iupac=False, lower=False)
+    run(["dist", "-i", "msa_miss.fsa", "-f", "3", "-L", "1150", "-C", "0"], "miss80.phy")
+    for m in ("dnj", "nj"):
+        case(f"miss80_{m}", ["tree", "-i", "miss80.phy", "-m", m], f"miss80_{m}.out", "tree")
+    case("miss80_p", ["tree", "-i", "miss80.phy", "-p"], "miss80_p.out", "tree")
+
+    # multi-matrix Phylip with a comment header (tree.c:101-104, phy.c:275)
+    with open("multi.phy", "w") as f:
+        for k, fn in enumerate(("snp300.phy", "miss80.phy")):
+            f.write(f"#matrix{k}\n")
+            f.write(open(fn).read())
+    case("multi_dnj", ["tree", "-i", "multi.phy"], "multi_dnj.out", "tree")
+
+    with open("golden.json", "w") as f:
+        json.dump({"reference": "ccphylo 0.8.5 (oracle/_ref/ccphylo, built by oracle/Makefile)",
+                   "cases": cases}, f, indent=1)
+    print(f"{len(cases)} golden cases")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+"""GPU parity: the gfx950 engine through the C-ABI (ctypes) and through the
+`ccphylo` CLI, against the golden vectors and the oracle.  Bit-exact for the
+integer SNP counts / LT matrices and for exact-mode trees; fast-mode trees
+must have the same topology with branch lengths within 1e-9 relative."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_bytes, golden_cases, parse_dist_args, parse_tree_args, print_phylip
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import ccphylo_amd as cg
+    d = cg.Device(0)
+    yield d
+    d.close()
+
+
+def test_device_is_gfx950(dev):
+    assert "gfx950" in dev.info()
+
+
+@pytest.mark.parametrize("case", golden_cases("tree"), ids=lambda c: c["name"])
+def test_tree_golden_engine(dev, case):
+    import ccphylo_amd as cg
+    path, method, et, bs, flags, prec = parse_tree_args(case["args"])
+
+    def run(D, n):
+        joins, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=method, flags=flags, exact=True)
+        return joins, fn, fd
+    trees = cg.newick_from_phylip(path, run, etype=et, byte_scale=bs, flags=flags, precision=prec)
+    assert ("\n".join(trees) + "\n").encode() == golden_bytes(case)
+
+
+@pytest.mark.parametrize("case", golden_cases(), ids=lambda c: c["name"])
+def test_cli_golden(case):
+    import ccphylo_amd as cg
+    args = list(case["args"])
+    if case["kind"] == "dist" and any(a == "-P" for a in args) and "3" in args:
+        pytest.skip("pairwise proximity masking is not on the GPU engine")
+    p = subprocess.run([cg.CLI_PATH] + args, cwd=GOLDEN, capture_output=True, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    assert p.stdout == golden_bytes(case)
+
+
+@pytest.mark.parametrize("case", [c for c in golden_cases("dist")], ids=lambda c: c["name"])
+def test_dist_golden_engine(dev, case):
+    import ccphylo_amd as cg
+    o = parse_dist_args(case["args"])
+    heads, seqs, incs, L, minLength = cg.load_msa(o["inp"], o["flag"], o["minLength"], o["minCov"], o["proxi"])
+    n = len(heads)
+    pair = bool(o["flag"] & 2)
+    out = b""
+    if n > 1:
+        D, N, inc = dev.snp_ltd(seqs, incs, n, L, pair=pair, norm=o["norm"], min_length=minLength, etype=o["et"],
+                                byte_scale=o["bs"], want_n=o["nout"])
+        out = print_phylip(D, n, heads, o["flag"], o["prec"], o["et"], o["bs"])
+        if N is not None:
+            out += print_phylip(N, n, heads, o["flag"], o["prec"], o["et"], o["bs"])
+    assert out == golden_bytes(case)
+
+
+def _euclid(n, seed, dim=8):
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n, dim))
+    i, j = np.tril_indices(n, -1)
+    return np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
+
+
+def _snp(n, seed, L=4000):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 4, L)
+    anc = [base]
+    rows = []
+    for t in range(n):
+        p = anc[rng.integers(len(anc))].copy()
+        m = rng.random(L) < 0.01
+        p[m] = rng.integers(0, 4, m.sum())
+        if rng.random() < 0.3:
+            anc.append(p)
+        rows.append(p)
+    X = np.array(rows)
+    i, j = np.tril_indices(n, -1)
+    return (X[i] != X[j]).sum(1).astype(np.float64)
+
+
+@pytest.mark.parametrize("n,kind,method", [(600, "euc", 1), (600, "euc", 0), (1500, "snp", 1), (1500, "snp", 0),
+                                          (2500, "euc", 1)])
+def test_tree_exact_vs_oracle(dev, n, kind, method):
+    from oracle import pyoracle
+    D = _euclid(n, n) if kind == "euc" else _snp(n, n)
+    joins, fn, fd, st = dev.tree(D, n, method=method, exact=True)
+    rj, rfn, rfd = pyoracle.tree(D, n, method=method)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(joins) == len(rj)
+    assert (joins["i"] == rj["i"]).all() and (joins["j"] == rj["j"]).all()
+    assert (joins["Li"] == rj["Li"]).all() and (joins["Lj"] == rj["Lj"]).all()
+
+
+@pytest.mark.parametrize("et", [4, 2, 1])
+def test_tree_types_vs_oracle(dev, et):
+    from oracle import pyoracle
+    n = 700
+    D = _snp(n, 11)
+    bs = {4: 1.0, 2: 4.0, 1: 1.0}[et]
+    if et == 4:
+        Dt = D.astype(np.float32)
+    else:
+        Dt = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
+    for method in (0, 1):
+        joins, fn, fd, _ = dev.tree(Dt, n, etype=et, byte_scale=bs, method=method, exact=True)
+        rj, rfn, rfd = pyoracle.tree(Dt, n, etype=et, byte_scale=bs, method=method)
+        assert (fn, fd) == (rfn, rfd)
+        assert (joins == rj).all()
+
+
+def test_tree_fast_sums_topology(dev):
+    """--fast_sums: same join sequence, limb lengths within 1e-9 relative (stated tolerance)."""
+    from oracle import pyoracle
+    n = 2000
+    D = _euclid(n, 3)
+    joins, fn, fd, _ = dev.tree(D, n, method=1, exact=False)
+    rj, rfn, rfd = pyoracle.tree(D, n, method=1)
+    assert fn == rfn and (joins["i"] == rj["i"]).all() and (joins["j"] == rj["j"]).all()
+    for f in ("Li", "Lj"):
+        np.testing.assert_allclose(joins[f], rj[f], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,L,pair,et,norm", [(257, 5000, False, 8, 0), (300, 4097, True, 8, 0),
+                                              (130, 70000, False, 4, 1000), (129, 3000, True, 2, 100),
+                                              (200, 1024, False, 1, 0)])
+def test_dist_random_vs_oracle(dev, n, L, pair, et, norm):
+    from oracle import pyoracle
+    rng = np.random.default_rng(n + L)
+    W = L // 32 + 1
+    seqs = rng.integers(0, 2 ** 63, size=(n, W), dtype=np.uint64) | (rng.integers(0, 2, size=(n, W), dtype=np.uint64) << np.uint64(63))
+    nw = (L + 31) // 32
+    def mask():
+        m = rng.integers(0, 2 ** 32, size=W, dtype=np.uint64).astype(np.uint32) | np.uint32(0xF7FFFFFF)
+        m[nw:] = 0
+        if L % 32:
+            m[nw - 1] &= np.uint32((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF)
+        return m
+    incs = np.stack([mask() for _ in range(n)]) if pair else mask()
+    ml = int(0.9 * L) if pair else 1
+    Dg, Ng, _ = dev.snp_ltd(seqs, incs, n, L, pair=pair, norm=norm, min_length=ml, etype=et, byte_scale=2.0,
+                            want_n=pair)
+    Do, No, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=pair, norm=norm, min_length=ml, etype=et, byte_scale=2.0,
+                                 want_n=pair)
+    assert (Dg == Do).all()
+    if pair:
+        assert (Ng == No).all()
+
+
+def test_dist_row_range(dev):
+    from oracle import pyoracle
+    rng = np.random.default_rng(5)
+    n, L = 300, 3000
+    W = L // 32 + 1
+    seqs = rng.integers(0, 2 ** 63, size=(n, W), dtype=np.uint64)
+    incs = np.zeros(W, np.uint32)
+    incs[: (L + 31) // 32] = 0xFFFFFFFF
+    incs[(L + 31) // 32 - 1] = (0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF
+    Do, _, _ = pyoracle.snp_ltd(seqs, incs, n, L)
+    parts = [(0, 77), (77, 200), (200, 300)]
+    acc = np.zeros_like(Do)
+    for rb, re_ in parts:
+        Dg, _, _ = dev.snp_ltd(seqs, incs, n, L, row_range=(rb, re_))
+        lo, hi = rb * (rb - 1) // 2, re_ * (re_ - 1) // 2
+        assert (Dg[lo:hi] == Do[lo:hi]).all()
+        acc[lo:hi] = Dg[lo:hi]
+    assert (acc == Do).all()
