@@ -9,60 +9,193 @@
 //
 // Layout in HBM: D is the reference's contiguous LT buffer (row r starts at
 // r(r-1)/2, element type ET), plus n-vectors sD (f64), N (i32), Q (f64),
-// P (i32).  All control state lives in a device TreeCtl; the host only
-// enqueues kernels (n shrinks by exactly one per join, so every grid is known
-// in advance) and reads the join list at the end.
+// P (i32).  All loop state (n, the current join, the DNJ selection) lives in
+// a device TreeCtl, so every per-iteration kernel takes the same arguments;
+// each one finishes with a "last block" (agent-scope ticket) that folds the
+// per-block partials in a fixed order and prepares the next kernel's input.
 //
-// DNJ selection (minQpair) is a strict serial scan in the reference: row i is
-// rescanned iff its stale bound Q[i] is below the running minimum m(i) of the
-// rows above it.  Here:
-//   k_dnj_top    rescans the top-B candidate rows (Q[i] < m0) in parallel;
-//   k_dnj_rest   computes U = min(m0, min_{k in S} max(fresh_k, Q_k)), an upper
-//                bound of m(i) for every row below S (a row k above i that the
-//                serial scan rescans gives m(i) <= fresh_k, one it skips gives
-//                m(i) <= m(k) <= Q_k), and rescans every row with Q[i] < U;
-//   k_dnj_replay replays the reference's decisions serially over that set,
-//                so Q/P and the chosen pair are identical to minQpair's.
+// DNJ selection (minQpair) is a serial scan in the reference: row i is
+// rescanned iff its stale bound Q[i] is below the running minimum m(i) of
+// the rows above it.  Here, per join:
+//   k_dnj_top   rescans the top-B candidate rows S (Q[r] < m0) in 2048-cell
+//               units spread over the whole GPU; its last block derives
+//               U = min(m0, min_{k in S} max(fresh_k, Q_k)), an upper bound of
+//               m(i) for every row below S (a row k above i that the serial
+//               scan rescans gives m(i) <= fresh_k, one it skips gives
+//               m(i) <= m(k) <= Q_k);
+//   k_dnj_rest  rescans every row below S with Q[r] < U (any other row is
+//               provably skipped by the reference); its last block replays
+//               the reference's accept/reject decisions over S then C1 in
+//               descending row order.  When every fresh min is >= its stale
+//               bound the running minimum is exactly the prefix minimum of the
+//               fresh values, so the replay is a parallel scan; otherwise it
+//               runs serially.  Either way Q/P and the pair are minQpair's.
 #include <string.h>
 #include "ccg_internal.h"
 
-#define TB 256           // threads per block for the vector kernels
-#define DNJ_B 64         // top candidates rescanned speculatively
-#define REST_BLOCKS 128  // blocks of k_dnj_rest
+#define TB 256           // threads per block of the vector kernels
+#define DNJ_B 128        // |S|: top candidate rows rescanned speculatively
+#define SEG 2048         // cells per rescan unit (8 per thread)
+#define RPB 16           // rows per block slice in k_dnj_rest
+#define TOP_BLOCKS 1024  // grid of k_dnj_top
+#define REPLAY_CAP 2048  // entries replayed from LDS at once
 
 struct TreeCtl {
+	int n;               // current matrix size
 	int done;            // the reference loop stopped (pos == 0)
-	int final_n;         // n when done was set
+	int final_n;
 	int njoins;
-	int first;           // cand comes from minQ (first DNJ iteration)
-	int cand;
-	int mi, mj;
 	int i, j;            // current join
 	double Li, Lj, Dij;
-	double m0;           // minQpair's initial min
+	int cand;            // minQpair's candidate row
 	int pos_i, pos_j;    // minQpair's initial pos
-	int nS;              // |S|
-	int has_missing;     // D holds entries < 0 (or NaN): general updateD path
-	unsigned counter;    // last-block ticket, reset by the last block
-	int neg;             // limbLengthNeg
-	int exact;
-	int exact_fast;      // stats: exact sums resolved without the serial chain
+	double m0;           // minQpair's initial min
+	double U;            // bound for rows below S
+	int nS, nunits, smin;
+	int mi, mj;
+	int neg, exact, method;
+	int serial_sums, serial_replays;
+	unsigned tick[4];    // last-block tickets (reset by their last block)
 	long long rows, cells;
+	int has_missing;
 };
 
 struct TreeBufs {
 	double *sD, *Q, *fq, *contrib;
-	int *N, *P, *fj, *S, *seg, *segcnt;
-	double *wsum;        // per-block partial sums
-	int *wcnt;
-	double *qpart;       // per-block QArg partials (4 per block)
+	int *N, *P, *fj;
+	int *S, *uoff;       // DNJ_B rows, DNJ_B+1 unit offsets
+	double *uq;          // per-unit partial (q, j)
+	int *uj;
+	int *blk_rows, *blk_cnt;
+	double *wsum, *wabs; // per-block partial sums / sum |c|
+	int *wcnt, *wexp;    // per-block count / min exponent of the contributions
+	double *qpart;       // 4 (q, idx) partials per block
 	int *ipart;
-	double *absb;        // per-block sum |c|, for the exactness test
-	int *qmin;           // per-block minimum quantum exponent
 	long long *fpart;
 	ccg_join *joins;
 	TreeCtl *ctl;
 };
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ double lds_min_reduce(double v, double *s) {
+	for(int off = 32; off > 0; off >>= 1) {
+		double o = __shfl_xor(v, off, 64);
+		v = o < v ? o : v;
+	}
+	__syncthreads();
+	if((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+	__syncthreads();
+	v = s[0];
+	for(int w = 1; w < (int) (blockDim.x >> 6); ++w) v = s[w] < v ? s[w] : v;
+	__syncthreads();
+	return v;
+}
+
+// block-wide exclusive prefix sum of a per-thread int; *total receives the sum
+__device__ __forceinline__ int block_excl_scan(int v, int *s, int *total) {
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	int x = v;
+	for(int off = 1; off < 64; off <<= 1) {
+		int y = __shfl_up(x, off, 64);
+		if(lane >= off) x += y;
+	}
+	__syncthreads();
+	if(lane == 63) s[wid] = x;
+	__syncthreads();
+	int pre = 0, tot = 0;
+	for(int w = 0; w < nw; ++w) {
+		if(w < wid) pre += s[w];
+		tot += s[w];
+	}
+	__syncthreads();
+	*total = tot;
+	return pre + x - v;
+}
+
+// nj.c:42 limbLength / nj.c:81 limbLengthNeg
+__device__ void limb_length(double *Li, double *Lj, int i, int j, const double *sD, const int *N, double Dij,
+                            int neg) {
+	int Ni = N[i] - 2, Nj = N[j] - 2;
+	if(0 < Ni && 0 < Nj) {
+		double delta = ((sD[i] - Dij) / Ni) - ((sD[j] - Dij) / Nj);
+		*Li = (Dij + delta) / 2;
+		*Lj = (Dij - delta) / 2;
+		if(!neg) {
+			if(*Li < 0) {
+				*Lj = Dij;
+				*Li = 0;
+			} else if(*Lj < 0) {
+				*Li = Dij;
+				*Lj = 0;
+			}
+		}
+	} else if(0 < Ni) {
+		*Li = 0;
+		*Lj = Dij;
+	} else if(0 < Nj) {
+		*Li = Dij;
+		*Lj = 0;
+	} else {
+		*Li = *Lj = Dij / 2;
+	}
+}
+
+template <int ET>
+__device__ void record_join(const typename Elem<ET>::T *D, double bs, const TreeBufs &b, int i, int j) {
+	TreeCtl *ctl = b.ctl;
+	double Dij = Elem<ET>::get(D[tri(i) + j], bs), Li, Lj;
+	limb_length(&Li, &Lj, i, j, b.sD, b.N, Dij, ctl->neg);
+	ctl->i = i;
+	ctl->j = j;
+	ctl->Li = Li;
+	ctl->Lj = Lj;
+	ctl->Dij = Dij;
+	ccg_join J;
+	J.i = i;
+	J.j = j;
+	J.Li = Li;
+	J.Lj = Lj;
+	b.joins[ctl->njoins++] = J;
+}
+
+// (q, j) min of LT row r over columns [c0, c1), whole block, 8 loads in flight
+// per thread (dnj.c:99-112 with the `<=` last-wins rule)
+template <int ET>
+__device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__restrict__ D, double bs,
+                                                const double *__restrict__ sD, const int *__restrict__ N, int r,
+                                                int c0, int c1, double &q, int &idx) {
+	const typename Elem<ET>::T *row = D + tri(r);
+	const int Nr = N[r];
+	const double sDr = sD[r];
+	for(int base = c0; base < c1; base += 8 * TB) {
+		typename Elem<ET>::T v[8];
+		int nk[8];
+		double sk[8];
+#pragma unroll
+		for(int m = 0; m < 8; ++m) {
+			int c = base + m * TB + (int) threadIdx.x;
+			if(c < c1) {
+				v[m] = row[c];
+				nk[m] = N[c];
+				sk[m] = sD[c];
+			}
+		}
+#pragma unroll
+		for(int m = 0; m < 8; ++m) {
+			int c = base + m * TB + (int) threadIdx.x;
+			if(c < c1) {
+				double d = Elem<ET>::get(v[m], bs);
+				if(0 <= d) {
+					double x = qcrit(Nr, nk[m], d, sDr, sk[m]);
+					if(qarg_better(x, c, q, idx)) {
+						q = x;
+						idx = c;
+					}
+				}
+			}
+		}
+	}
+}
 
 // ------------------------------------------------------------------ init
 template <int ET>
@@ -136,316 +269,352 @@ __global__ void k_init_hnj(const typename Elem<ET>::T *__restrict__ D, int n, do
 	}
 }
 
-// hclust.c:353 minQ -> the first candidate row of dnj.c:997-998
-__global__ void k_min_q_row(const double *__restrict__ Q, int n, TreeCtl *ctl) {
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	double q = DBL_MAX;
-	int idx = 0;
-	for(int i = 1 + threadIdx.x; i < n; i += blockDim.x) {
-		if(qarg_better(Q[i], i, q, idx)) {
-			q = Q[i];
-			idx = i;
-		}
-	}
-	qarg_block_reduce(q, idx, sq, si);
-	if(threadIdx.x == 0) {
-		ctl->cand = idx;
-		ctl->first = 1;
-	}
-}
-
-// nj.c:42 limbLength / nj.c:81 limbLengthNeg
-__device__ void limb_length(double *Li, double *Lj, int i, int j, const double *sD, const int *N,
-                            double Dij, int neg) {
-	int Ni = N[i] - 2, Nj = N[j] - 2;
-	if(0 < Ni && 0 < Nj) {
-		double delta = ((sD[i] - Dij) / Ni) - ((sD[j] - Dij) / Nj);
-		*Li = (Dij + delta) / 2;
-		*Lj = (Dij - delta) / 2;
-		if(!neg) {
-			if(*Li < 0) {
-				*Lj = Dij;
-				*Li = 0;
-			} else if(*Lj < 0) {
-				*Li = Dij;
-				*Lj = 0;
-			}
-		}
-	} else if(0 < Ni) {
-		*Li = 0;
-		*Lj = Dij;
-	} else if(0 < Nj) {
-		*Li = Dij;
-		*Lj = 0;
-	} else {
-		*Li = *Lj = Dij / 2;
-	}
-}
-
-template <int ET>
-__device__ void record_join(const typename Elem<ET>::T *D, double bs, const TreeBufs &b, int i, int j) {
+// ------------------------------------------------------------------ DNJ selection setup
+// Computes minQpair's starting point and the top-B candidate set S for the
+// current n; run by ONE block (the last block of k_dnj_requeue, or k_dnj_prep).
+__device__ void prepare_selection(const TreeBufs &b, int n, int cand) {
+	__shared__ int s_scan[TB / 64];
+	__shared__ int s_cnt;
 	TreeCtl *ctl = b.ctl;
-	double Dij = Elem<ET>::get(D[tri(i) + j], bs), Li, Lj;
-	limb_length(&Li, &Lj, i, j, b.sD, b.N, Dij, ctl->neg);
-	ctl->i = i;
-	ctl->j = j;
-	ctl->Li = Li;
-	ctl->Lj = Lj;
-	ctl->Dij = Dij;
-	ccg_join J;
-	J.i = i;
-	J.j = j;
-	J.Li = Li;
-	J.Lj = Lj;
-	b.joins[ctl->njoins++] = J;
-}
-
-// fresh (q, j) min of LT row r over j < r, whole block (dnj.c:99-112)
-template <int ET>
-__device__ __forceinline__ void rescan_row(const typename Elem<ET>::T *__restrict__ D, double bs,
-                                           const double *__restrict__ sD, const int *__restrict__ N,
-                                           int r, double *sq, int *si, double &oq, int &oj) {
-	const typename Elem<ET>::T *row = D + tri(r);
-	int Nr = N[r];
-	double sDr = sD[r];
-	double q = DBL_MAX;
-	int idx = 0;
-	for(int j = threadIdx.x; j < r; j += blockDim.x) {
-		double d = Elem<ET>::get(row[j], bs);
-		if(0 <= d) {
-			double v = qcrit(Nr, N[j], d, sDr, sD[j]);
-			if(qarg_better(v, j, q, idx)) {
-				q = v;
-				idx = j;
-			}
-		}
-	}
-	qarg_block_reduce(q, idx, sq, si);
-	oq = q;
-	oj = idx;
-}
-
-// ------------------------------------------------------------------ DNJ
-__device__ __forceinline__ int dnj_candidate(const TreeCtl *ctl, const double *Q, int n) {
-	if(ctl->first) return ctl->cand;
-	int mi = ctl->mi, mj = ctl->mj;
-	if(mj == n) return mi;
-	if(mi == n) return mj;
-	// dnj.c:977 minPos
-	return (Q[mj] < Q[mi] || (mi < mj && Q[mj] == Q[mi])) ? mj : mi;
-}
-
-// ordered block compaction of flags (descending row order = thread order)
-__device__ __forceinline__ int block_compact(bool flag, int value, int *out, int base, int cap, int *wcount) {
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	unsigned long long m = __ballot(flag);
-	if(lane == 0) wcount[wid] = __popcll(m);
-	__syncthreads();
-	int off = 0, tot = 0;
-	for(int w = 0; w < nw; ++w) {
-		if(w < wid) off += wcount[w];
-		tot += wcount[w];
-	}
-	if(flag) {
-		int pos = base + off + __popcll(m & ((1ull << lane) - 1));
-		if(pos < cap) out[pos] = value;
-	}
-	__syncthreads();
-	return tot;
-}
-
-template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                TreeBufs b) {
-	__shared__ int list[DNJ_B + TB];
-	__shared__ int wcount[TB / 64];
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	int cand = dnj_candidate(ctl, b.Q, n);
 	double m0 = DBL_MAX;
 	if(cand && m0 != b.Q[cand]) m0 = b.Q[cand];
-	// the first DNJ_B rows (descending) with Q[r] < m0
-	int cnt = 0;
-	for(int base = n - 1; base >= 1 && cnt < DNJ_B; base -= blockDim.x) {
-		int r = base - (int) threadIdx.x;
-		bool f = r >= 1 && b.Q[r] < m0;
-		cnt += block_compact(f, r, list, cnt, DNJ_B, wcount);
-	}
-	int nS = cnt < DNJ_B ? cnt : DNJ_B;
-	if(blockIdx.x == 0 && threadIdx.x == 0) {
+	if(threadIdx.x == 0) {
 		ctl->cand = cand;
 		ctl->m0 = m0;
 		ctl->pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
 		ctl->pos_j = (cand && m0 != DBL_MAX) ? b.P[cand] : 0;
-		ctl->nS = nS;
+		s_cnt = 0;
 	}
-	if(blockIdx.x == 0) {
-		for(int t = threadIdx.x; t < nS; t += blockDim.x) b.S[t] = list[t];
-	}
-	for(int t = blockIdx.x; t < nS; t += gridDim.x) {
-		int r = list[t];
-		double q;
-		int j;
-		rescan_row<ET>(D, bs, b.sD, b.N, r, sq, si, q, j);
-		if(threadIdx.x == 0) {
-			b.fq[r] = q;
-			b.fj[r] = j;
+	__syncthreads();
+	// rows n-1, n-2, ... with Q[r] < m0, 4 rows per thread per step
+	for(int base = n - 1; base >= 1; base -= 4 * (int) blockDim.x) {
+		int cnt = s_cnt;
+		if(cnt >= DNJ_B) break;
+		int rows[4], k = 0;
+#pragma unroll
+		for(int m = 0; m < 4; ++m) {
+			int r = base - 4 * (int) threadIdx.x - m;
+			if(r >= 1 && b.Q[r] < m0) rows[k++] = r;
 		}
+		int tot;
+		int off = block_excl_scan(k, s_scan, &tot);
+		for(int m = 0; m < k; ++m) {
+			if(cnt + off + m < DNJ_B) b.S[cnt + off + m] = rows[m];
+		}
+		__syncthreads();
+		if(threadIdx.x == 0) s_cnt = cnt + tot;
+		__syncthreads();
+	}
+	__threadfence_block();
+	__syncthreads();
+	int nS = s_cnt < DNJ_B ? s_cnt : DNJ_B;
+	// rescan units per row of S
+	int t = threadIdx.x;
+	int u = 0;
+	if(t < nS) u = (b.S[t] + SEG - 1) / SEG;
+	int tot;
+	int off = block_excl_scan(u, s_scan, &tot);
+	if(t < nS) b.uoff[t] = off;
+	if(t == 0) {
+		b.uoff[nS] = tot;
+		ctl->nS = nS;
+		ctl->nunits = tot;
 	}
 }
 
-template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                 TreeBufs b) {
-	__shared__ int list[TB];
-	__shared__ int wcount[TB / 64];
+// hclust.c:353 minQ -> the first candidate (dnj.c:997-998), then selection setup
+__global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b) {
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
-	__shared__ double sU;
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	int nS = ctl->nS;
-	int w = blockIdx.x;
-	if(nS < DNJ_B) {
-		if(threadIdx.x == 0) b.segcnt[w] = 0;
-		return;
-	}
-	int smin = b.S[DNJ_B - 1];
-	if(threadIdx.x < 64) {
-		double U = ctl->m0;
-		for(int t = threadIdx.x; t < DNJ_B; t += 64) {
-			int k = b.S[t];
-			double u = b.fq[k] > b.Q[k] ? b.fq[k] : b.Q[k];
-			if(u < U) U = u;
-		}
-#pragma unroll
-		for(int off = 32; off > 0; off >>= 1) {
-			double o = __shfl_xor(U, off, 64);
-			if(o < U) U = o;
-		}
-		if(threadIdx.x == 0) sU = U;
-	}
-	__syncthreads();
-	double U = sU;
-	// rows [1, smin) in gridDim.x slices; slice w covers [lo, hi)
-	int rows = smin - 1;
-	int lo = 1 + (int) ((long long) rows * w / gridDim.x);
-	int hi = 1 + (int) ((long long) rows * (w + 1) / gridDim.x);
-	int cnt = 0;
-	for(int base = hi - 1; base >= lo; base -= blockDim.x) {
-		int r = base - (int) threadIdx.x;
-		bool f = r >= lo && b.Q[r] < U;
-		int got = block_compact(f, r, list, 0, TB, wcount);
-		for(int t = 0; t < got; ++t) {
-			int rr = list[t];
-			double q;
-			int j;
-			rescan_row<ET>(D, bs, b.sD, b.N, rr, sq, si, q, j);
-			if(threadIdx.x == 0) {
-				b.fq[rr] = q;
-				b.fj[rr] = j;
-				b.seg[lo + cnt] = rr;
-			}
-			++cnt;
+	const int n = b.ctl->n;
+	double q = DBL_MAX;
+	int idx = 0;
+	for(int i = 1 + threadIdx.x; i < n; i += blockDim.x) {
+		if(qarg_better(b.Q[i], i, q, idx)) {
+			q = b.Q[i];
+			idx = i;
 		}
 	}
-	if(threadIdx.x == 0) b.segcnt[w] = cnt;
+	qarg_block_reduce(q, idx, sq, si);
+	prepare_selection(b, n, idx);
 }
 
-// serial replay of minQpair's decisions over S then the slices, descending
+// ------------------------------------------------------------------ DNJ rescans
 template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_replay(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                   TreeBufs b, int nrest) {
-	__shared__ int rr[TB], rj[TB];
-	__shared__ double rq[TB], rf[TB];
-	__shared__ double s_m;
-	__shared__ int s_pi, s_pj, s_total;
-	__shared__ int sl_base[REST_BLOCKS + 1];
+__global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
+	__shared__ double sq[TB / 64];
+	__shared__ int si[TB / 64];
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	const int nS = ctl->nS;
-	const bool more = nS == DNJ_B;
-	const int rows = (more ? b.S[DNJ_B - 1] : 1) - 1;   // rows [1, smin) went to k_dnj_rest
-	if(threadIdx.x == 0) {
-		s_m = ctl->m0;
-		s_pi = ctl->pos_i;
-		s_pj = ctl->pos_j;
-		// slice t of the replay order is rest block w = nrest-1-t (higher rows first)
-		int acc = nS;
-		for(int t = 0; t < nrest; ++t) {
-			sl_base[t] = acc;
-			acc += more ? b.segcnt[nrest - 1 - t] : 0;
-		}
-		sl_base[nrest] = acc;
-		s_total = acc;
+	const int nS = ctl->nS, nunits = ctl->nunits;
+	for(int t = threadIdx.x; t <= nS; t += blockDim.x) {
+		if(t < nS) sS[t] = b.S[t];
+		so[t] = b.uoff[t];
 	}
 	__syncthreads();
-	const int total = s_total;
-	int nrows = 0;
+	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
+		int lo = 0, hi = nS - 1;   // last t with so[t] <= u
+		while(lo < hi) {
+			int mid = (lo + hi + 1) >> 1;
+			if(so[mid] <= u) lo = mid; else hi = mid - 1;
+		}
+		int r = sS[lo];
+		int c0 = (u - so[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		double q = DBL_MAX;
+		int idx = 0;
+		row_segment_min<ET>(D, bs, b.sD, b.N, r, c0, c1, q, idx);
+		qarg_block_reduce(q, idx, sq, si);
+		if(threadIdx.x == 0) {
+			b.uq[u] = q;
+			b.uj[u] = idx;
+		}
+	}
+	if(!last_block_arrive(&ctl->tick[0])) return;
+	// fold the units of every row of S; derive U
+	double U = ctl->m0;
 	long long cells = 0;
-	for(int c0 = 0; c0 < total; c0 += blockDim.x) {
-		int e = c0 + threadIdx.x;
-		if(e < total) {
+	for(int t = threadIdx.x; t < nS; t += blockDim.x) {
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int u = so[t]; u < so[t + 1]; ++u) {
+			double uq = b.uq[u];
+			int uj = b.uj[u];
+			if(qarg_better(uq, uj, q, idx)) {
+				q = uq;
+				idx = uj;
+			}
+		}
+		int r = sS[t];
+		b.fq[r] = q;
+		b.fj[r] = idx;
+		double Qr = b.Q[r];
+		double v = q > Qr ? q : Qr;
+		U = v < U ? v : U;
+		cells += r;
+	}
+	U = lds_min_reduce(U, sq);
+	for(int off = 32; off > 0; off >>= 1) cells += __shfl_xor(cells, off, 64);
+	if((threadIdx.x & 63) == 0 && cells) atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+	if(threadIdx.x == 0) {
+		ctl->U = U;
+		ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
+		ctl->rows += nS;
+		ctl->tick[0] = 0;
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+	__shared__ double sq[TB / 64];
+	__shared__ int si[TB / 64];
+	__shared__ int scan[TB / 64];
+	__shared__ double wmin[TB / 64];
+	__shared__ int list[RPB];
+	__shared__ int s_cnt;
+	__shared__ int e_row[REPLAY_CAP], e_j[REPLAY_CAP];
+	__shared__ double e_b[REPLAY_CAP], e_f[REPLAY_CAP];
+	__shared__ int s_pi, s_pj;
+	TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const int smin = ctl->smin;
+	const double U = ctl->U;
+	const int nblk = (smin - 1 + RPB - 1) / RPB;   // slices of rows [1, smin)
+	const int w = blockIdx.x;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	for(int sl = w; sl < nblk; sl += gridDim.x) {
+		int lo = 1 + sl * RPB, hi = lo + RPB < smin ? lo + RPB : smin;
+		if(threadIdx.x < 64) {
+			int r = hi - 1 - (int) threadIdx.x;
+			bool f = r >= lo && b.Q[r] < U;
+			unsigned long long m = __ballot(f);
+			if(f) list[__popcll(m & ((1ull << threadIdx.x) - 1))] = r;
+			if(threadIdx.x == 0) s_cnt = __popcll(m);
+		}
+		__syncthreads();
+		const int cnt = s_cnt;
+		long long cells = 0;
+		for(int t = 0; t < cnt; ++t) {
+			int r = list[t];
+			double q = DBL_MAX;
+			int idx = 0;
+			row_segment_min<ET>(D, bs, b.sD, b.N, r, 0, r, q, idx);
+			qarg_block_reduce(q, idx, sq, si);
+			if(threadIdx.x == 0) {
+				b.fq[r] = q;
+				b.fj[r] = idx;
+				b.blk_rows[sl * RPB + t] = r;
+			}
+			cells += r;
+		}
+		if(threadIdx.x == 0) {
+			b.blk_cnt[sl] = cnt;
+			if(cnt) {
+				atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+				atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) cnt);
+			}
+		}
+		__syncthreads();
+	}
+	if(!last_block_arrive(&ctl->tick[1])) return;
+
+	// ---- replay of minQpair's decisions: S (descending) then slices nblk-1 .. 0
+	const int nS = ctl->nS;
+	const double m0 = ctl->m0;
+	if(threadIdx.x == 0) {
+		s_pi = ctl->pos_i;
+		s_pj = ctl->pos_j;
+	}
+	int carry = nS;
+	for(int c0 = 0; c0 < nblk; c0 += blockDim.x) {
+		int t = c0 + threadIdx.x;
+		int c = t < nblk ? b.blk_cnt[nblk - 1 - t] : 0;
+		int tot;
+		int off = block_excl_scan(c, scan, &tot);
+		for(int k = 0; k < c; ++k) {
+			int e = carry + off + k;
+			if(e < REPLAY_CAP) e_row[e] = b.blk_rows[(nblk - 1 - t) * RPB + k];
+		}
+		carry += tot;
+	}
+	for(int t = threadIdx.x; t < nS; t += blockDim.x) e_row[t] = b.S[t];
+	const int total = carry;
+	__syncthreads();
+	if(total <= REPLAY_CAP) {
+		// gather (bound, fresh, j) and test the prefix-min condition fresh >= bound
+		int bad = 0;
+		for(int e = threadIdx.x; e < total; e += blockDim.x) {
+			int r = e_row[e];
+			double bq = b.Q[r], fq = b.fq[r];
+			e_b[e] = bq;
+			e_f[e] = fq;
+			e_j[e] = b.fj[r];
+			bad |= !(fq >= bq);
+		}
+		bad = __syncthreads_or(bad);
+		if(!bad) {
+			// running min before entry e = min(m0, f[0..e-1]); accepted iff bound < it
+			double carry_m = m0;
+			for(int c0 = 0; c0 < total; c0 += blockDim.x) {
+				int e = c0 + threadIdx.x;
+				double f = e < total ? e_f[e] : DBL_MAX;
+				double x = f;   // inclusive wave min-scan
+				for(int off = 1; off < 64; off <<= 1) {
+					double y = __shfl_up(x, off, 64);
+					if(lane >= off) x = y < x ? y : x;
+				}
+				if(lane == 63) wmin[wid] = x;
+				__syncthreads();
+				double pre = carry_m;
+				for(int k = 0; k < wid; ++k) pre = wmin[k] < pre ? wmin[k] : pre;
+				double excl = __shfl_up(x, 1, 64);
+				if(lane > 0) pre = excl < pre ? excl : pre;
+				double chunk_min = carry_m;
+				for(int k = 0; k < (int) (blockDim.x >> 6); ++k) chunk_min = wmin[k] < chunk_min ? wmin[k] : chunk_min;
+				if(e < total && e_b[e] < pre) {
+					int r = e_row[e];
+					b.Q[r] = f;
+					b.P[r] = e_j[e];
+				}
+				__syncthreads();
+				carry_m = chunk_min;
+			}
+			// the pair: first entry reaching the final minimum, if below m0
+			double q = DBL_MAX;
+			int idx = 0x7fffffff;
+			for(int e = threadIdx.x; e < total; e += blockDim.x) {
+				double f = e_f[e];
+				if(f < q || (f == q && e < idx)) {
+					q = f;
+					idx = e;
+				}
+			}
+			for(int off = 32; off > 0; off >>= 1) {
+				double oq = __shfl_xor(q, off, 64);
+				int oi = __shfl_xor(idx, off, 64);
+				if(oq < q || (oq == q && oi < idx)) {
+					q = oq;
+					idx = oi;
+				}
+			}
+			if(lane == 0) {
+				sq[wid] = q;
+				si[wid] = idx;
+			}
+			__syncthreads();
+			if(threadIdx.x == 0) {
+				for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
+					if(sq[k] < q || (sq[k] == q && si[k] < idx)) {
+						q = sq[k];
+						idx = si[k];
+					}
+				}
+				if(total && q < m0) {
+					s_pi = e_row[idx];
+					s_pj = e_j[idx];
+				}
+			}
+			__syncthreads();
+		} else {
+			if(threadIdx.x == 0) {
+				double m = m0;
+				int pi = s_pi, pj = s_pj;
+				for(int e = 0; e < total; ++e) {
+					if(e_b[e] < m) {
+						int r = e_row[e];
+						b.Q[r] = e_f[e];
+						b.P[r] = e_j[e];
+						if(e_f[e] < m) {
+							m = e_f[e];
+							pi = r;
+							pj = e_j[e];
+						}
+					}
+				}
+				s_pi = pi;
+				s_pj = pj;
+				ctl->serial_replays++;
+			}
+			__syncthreads();
+		}
+	} else if(threadIdx.x == 0) {
+		// very large candidate sets: serial replay straight from global memory
+		double m = m0;
+		int pi = s_pi, pj = s_pj;
+		int t = 0, k = 0;
+		for(int e = 0; e < total; ++e) {
 			int r;
 			if(e < nS) {
 				r = b.S[e];
 			} else {
-				int lo_t = 0, hi_t = nrest - 1;   // last t with sl_base[t] <= e
-				while(lo_t < hi_t) {
-					int mid = (lo_t + hi_t + 1) >> 1;
-					if(sl_base[mid] <= e) lo_t = mid; else hi_t = mid - 1;
+				while(k >= b.blk_cnt[nblk - 1 - t]) {
+					++t;
+					k = 0;
 				}
-				int w = nrest - 1 - lo_t;
-				int lo = 1 + (int) ((long long) rows * w / nrest);
-				r = b.seg[lo + (e - sl_base[lo_t])];
+				r = b.blk_rows[(nblk - 1 - t) * RPB + k];
+				++k;
 			}
-			rr[threadIdx.x] = r;
-			rq[threadIdx.x] = b.Q[r];
-			rf[threadIdx.x] = b.fq[r];
-			rj[threadIdx.x] = b.fj[r];
-			++nrows;
-			cells += r;
-		}
-		__syncthreads();
-		if(threadIdx.x == 0) {
-			double m = s_m;
-			int pi = s_pi, pj = s_pj;
-			int lim = total - c0 < (int) blockDim.x ? total - c0 : (int) blockDim.x;
-			for(int u = 0; u < lim; ++u) {
-				if(rq[u] < m) {
-					// the reference rescans this row (dnj.c:78-123)
-					int r = rr[u];
-					b.Q[r] = rf[u];
-					b.P[r] = rj[u];
-					if(rf[u] < m) {
-						m = rf[u];
-						pi = r;
-						pj = rj[u];
-					}
+			if(b.Q[r] < m) {
+				double f = b.fq[r];
+				b.Q[r] = f;
+				b.P[r] = b.fj[r];
+				if(f < m) {
+					m = f;
+					pi = r;
+					pj = b.fj[r];
 				}
 			}
-			s_m = m;
-			s_pi = pi;
-			s_pj = pj;
 		}
-		__syncthreads();
+		s_pi = pi;
+		s_pj = pj;
+		ctl->serial_replays++;
 	}
-	for(int off = 32; off > 0; off >>= 1) {
-		nrows += __shfl_xor(nrows, off, 64);
-		cells += __shfl_xor(cells, off, 64);
-	}
-	if((threadIdx.x & 63) == 0 && nrows) {
-		atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) nrows);
-		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
-	}
+	__syncthreads();
 	if(threadIdx.x == 0) {
-		ctl->first = 0;
+		ctl->tick[1] = 0;
 		if(s_pi == 0 && s_pj == 0) {
 			ctl->done = 1;
-			ctl->final_n = n;
+			ctl->final_n = ctl->n;
 		} else {
 			record_join<ET>(D, bs, b, s_pi, s_pj);
 		}
@@ -455,50 +624,61 @@ __global__ __launch_bounds__(TB) void k_dnj_replay(const typename Elem<ET>::T *_
 // ------------------------------------------------------------------ NJ argmin
 // nj.c:182 initQ: min starts at 1, the last minimal cell in row-major order
 template <int ET>
-__global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                  TreeBufs b, long long chunk) {
+__global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
 	__shared__ double sq[TB / 64];
 	__shared__ long long sf[TB / 64];
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	long long cells = tri(n);
-	long long f0 = (long long) blockIdx.x * chunk;
-	long long f1 = f0 + chunk < cells ? f0 + chunk : cells;
+	const int n = ctl->n;
+	const long long cells = tri(n);
+	const long long chunk = (cells + gridDim.x - 1) / gridDim.x;
+	const long long f0 = (long long) blockIdx.x * chunk;
+	const long long f1 = f0 + chunk < cells ? f0 + chunk : cells;
 	double bq = 1.0;
 	long long bf = -1;
 	if(f0 < f1) {
 		long long f = f0 + threadIdx.x;
-		// row of f: largest r with r(r-1)/2 <= f
 		long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
-		while(tri(r) > f) --r;
+		while(r > 1 && tri(r) > f) --r;
 		while(tri(r + 1) <= f) ++r;
 		long long c = f - tri(r);
-		int Nr = b.N[r];
-		double sDr = b.sD[r];
-		for(; f < f1; f += blockDim.x) {
-			double d = Elem<ET>::get(D[f], bs);
-			if(0 <= d) {
-				double q = qcrit(Nr, b.N[c], d, sDr, b.sD[c]);
-				if(q < bq || (q == bq && f > bf)) {
-					bq = q;
-					bf = f;
+		for(; f < f1; f += 4 * TB) {
+			// four cells of this thread: f, f+TB, f+2TB, f+3TB
+			typename Elem<ET>::T v[4];
+			int nr[4], nc[4];
+			double sr[4], sc[4];
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				if(f + m * TB < f1) {
+					v[m] = D[f + m * TB];
+					nr[m] = b.N[r];
+					sr[m] = b.sD[r];
+					nc[m] = b.N[c];
+					sc[m] = b.sD[c];
 				}
-			}
-			c += blockDim.x;
-			if(c >= r) {
-				do {
+				c += TB;
+				while(c >= r && r < n) {
 					c -= r;
 					++r;
-				} while(c >= r);
-				if(r < n) {
-					Nr = b.N[r];
-					sDr = b.sD[r];
+				}
+			}
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				long long fm = f + m * TB;
+				if(fm < f1) {
+					double d = Elem<ET>::get(v[m], bs);
+					if(0 <= d) {
+						double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
+						if(q < bq || (q == bq && fm > bf)) {
+							bq = q;
+							bf = fm;
+						}
+					}
 				}
 			}
 		}
 	}
 	// block reduce (min q, max f)
-#pragma unroll
 	for(int off = 32; off > 0; off >>= 1) {
 		double oq = __shfl_xor(bq, off, 64);
 		long long of = __shfl_xor(bf, off, 64);
@@ -507,60 +687,99 @@ __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__
 			bf = of;
 		}
 	}
-	int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	if(lane == 0) {
 		sq[wid] = bq;
 		sf[wid] = bf;
 	}
 	__syncthreads();
 	if(threadIdx.x == 0) {
-		for(int w = 1; w < (int) (blockDim.x >> 6); ++w) {
-			if(sq[w] < bq || (sq[w] == bq && sf[w] > bf)) {
-				bq = sq[w];
-				bf = sf[w];
+		for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
+			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
+				bq = sq[k];
+				bf = sf[k];
 			}
 		}
 		b.qpart[blockIdx.x] = bq;
 		b.fpart[blockIdx.x] = bf;
 	}
-	if(last_block_arrive(&ctl->counter)) {
-		if(threadIdx.x == 0) {
-			ctl->counter = 0;
-			double q = 1.0;
-			long long f = -1;
-			for(unsigned w = 0; w < gridDim.x; ++w) {
-				double oq = __hip_atomic_load(&b.qpart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-				long long of = __hip_atomic_load(&b.fpart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-				if(oq < q || (oq == q && of > f)) {
-					q = oq;
-					f = of;
-				}
+	if(!last_block_arrive(&ctl->tick[1])) return;
+	bq = 1.0;
+	bf = -1;
+	for(unsigned k = threadIdx.x; k < gridDim.x; k += blockDim.x) {
+		double oq = b.qpart[k];
+		long long of = b.fpart[k];
+		if(oq < bq || (oq == bq && of > bf)) {
+			bq = oq;
+			bf = of;
+		}
+	}
+	for(int off = 32; off > 0; off >>= 1) {
+		double oq = __shfl_xor(bq, off, 64);
+		long long of = __shfl_xor(bf, off, 64);
+		if(oq < bq || (oq == bq && of > bf)) {
+			bq = oq;
+			bf = of;
+		}
+	}
+	__syncthreads();
+	if(lane == 0) {
+		sq[wid] = bq;
+		sf[wid] = bf;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
+			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
+				bq = sq[k];
+				bf = sf[k];
 			}
-			if(f < 0) {
-				ctl->done = 1;
-				ctl->final_n = n;
-			} else {
-				long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
-				while(tri(r) > f) --r;
-				while(tri(r + 1) <= f) ++r;
-				record_join<ET>(D, bs, b, (int) r, (int) (f - tri(r)));
-			}
+		}
+		ctl->tick[1] = 0;
+		if(bf < 0) {
+			ctl->done = 1;
+			ctl->final_n = n;
+		} else {
+			long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) bf)) * 0.5);
+			while(r > 1 && tri(r) > bf) --r;
+			while(tri(r + 1) <= bf) ++r;
+			record_join<ET>(D, bs, b, (int) r, (int) (bf - tri(r)));
 		}
 	}
 }
 
 // ------------------------------------------------------------------ updateD
+// exponent e of the lowest set bit of x (x = odd * 2^e); INT32_MAX for 0,
+// INT32_MIN for inf / NaN
+__device__ __forceinline__ int low_exp(double x) {
+	unsigned long long u = (unsigned long long) __double_as_longlong(x);
+	int ex = (int) ((u >> 52) & 0x7FF);
+	unsigned long long m = u & ((1ull << 52) - 1);
+	if(ex == 0x7FF) return INT32_MIN;
+	if(ex == 0) {
+		if(m == 0) return INT32_MAX;
+		return -1074 + __ffsll((long long) m) - 1;
+	}
+	m |= 1ull << 52;
+	return ex - 1075 + __ffsll((long long) m) - 1;
+}
+
 // nj.c:836-1044 without missing entries: every k takes the (D_ik, D_kj >= 0)
-// branch, so the sD/N cursor never lags.
+// branch, so the sD/N cursor never lags.  The new row sum sD[j] is the
+// reference's serial sum over k (exact mode) or a fixed-order tree sum; both
+// are the same number whenever every partial sum is exactly representable
+// (all terms multiples of 2^e and sum |c| < 2^53 * 2^e), e.g. integer SNP data.
 template <int ET>
-__global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict__ D, int n, double bs, TreeBufs b) {
-	__shared__ double ssum[TB / 64];
-	__shared__ int scnt[TB / 64];
+__global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+	__shared__ double ssum[TB / 64], sabs[TB / 64];
+	__shared__ int scnt[TB / 64], sexp[TB / 64];
+	__shared__ double buf[TB];
+	__shared__ double red[1024];
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	int i = ctl->i, j = ctl->j;
-	double Dij = ctl->Dij;
-	int k = blockIdx.x * blockDim.x + threadIdx.x;
+	const int n = ctl->n, i = ctl->i, j = ctl->j;
+	const double Dij = ctl->Dij;
+	const int k = blockIdx.x * blockDim.x + threadIdx.x;
 	double d = 0;
 	int cnt = 0;
 	if(k < n && k != i && k != j) {
@@ -574,45 +793,93 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 		b.N[k] -= 1;
 		cnt = 1;
 	}
-	if(ctl->exact && k < n) b.contrib[k] = d;
-	// fixed-order block partials
-	double s = d;
-#pragma unroll
+	const bool exact = ctl->exact;
+	if(exact && k < n) b.contrib[k] = d;
+	double s = d, a = fabs(d);
+	int e = low_exp(d);
 	for(int off = 32; off > 0; off >>= 1) {
 		s += __shfl_down(s, off, 64);
+		a += __shfl_down(a, off, 64);
 		cnt += __shfl_down(cnt, off, 64);
+		int oe = __shfl_down(e, off, 64);
+		e = oe < e ? oe : e;
 	}
-	int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	if(lane == 0) {
 		ssum[wid] = s;
+		sabs[wid] = a;
 		scnt[wid] = cnt;
+		sexp[wid] = e;
 	}
 	__syncthreads();
 	if(threadIdx.x == 0) {
-		double t = 0;
-		int c = 0;
+		double t = 0, ta = 0;
+		int c = 0, te = INT32_MAX;
 		for(int w = 0; w < (int) (blockDim.x >> 6); ++w) {
 			t += ssum[w];
+			ta += sabs[w];
 			c += scnt[w];
+			te = sexp[w] < te ? sexp[w] : te;
 		}
 		b.wsum[blockIdx.x] = t;
+		b.wabs[blockIdx.x] = ta;
 		b.wcnt[blockIdx.x] = c;
+		b.wexp[blockIdx.x] = te;
 	}
-	if(last_block_arrive(&ctl->counter)) {
-		__shared__ double buf[TB];
-		int c = 0;
-		for(unsigned w = threadIdx.x; w < gridDim.x; w += blockDim.x) {
-			c += __hip_atomic_load(&b.wcnt[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		}
-		for(int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-		__shared__ int sc[TB / 64];
-		if(lane == 0) sc[wid] = c;
-		double sd = 0;
-		if(ctl->exact) {
-			// serial sum in increasing k (nj.c:911/:1002), staged through LDS
+	if(!last_block_arrive(&ctl->tick[2])) return;
+	// fixed-order fold of the block partials: 1024 leaves (block g -> leaf
+	// g mod 1024, folded in order), then a pairwise tree
+	const int G = gridDim.x;
+	for(int leaf = threadIdx.x; leaf < 1024; leaf += blockDim.x) {
+		double v = 0;
+		for(int g = leaf; g < G; g += 1024) v += b.wsum[g];
+		red[leaf] = v;
+	}
+	double tabs = 0;
+	int tcnt = 0, texp = INT32_MAX;
+	for(int g = threadIdx.x; g < G; g += blockDim.x) {
+		tabs += b.wabs[g];
+		tcnt += b.wcnt[g];
+		int oe = b.wexp[g];
+		texp = oe < texp ? oe : texp;
+	}
+	__syncthreads();
+	for(int stride = 512; stride > 0; stride >>= 1) {
+		for(int leaf = threadIdx.x; leaf < stride; leaf += blockDim.x) red[leaf] += red[leaf + stride];
+		__syncthreads();
+	}
+	const double total = red[0];
+	for(int off = 32; off > 0; off >>= 1) {
+		tabs += __shfl_xor(tabs, off, 64);
+		tcnt += __shfl_xor(tcnt, off, 64);
+		int oe = __shfl_xor(texp, off, 64);
+		texp = oe < texp ? oe : texp;
+	}
+	__syncthreads();
+	if(lane == 0) {
+		sabs[wid] = tabs;
+		scnt[wid] = tcnt;
+		sexp[wid] = texp;
+	}
+	__syncthreads();
+	tabs = 0;
+	tcnt = 0;
+	texp = INT32_MAX;
+	for(int w = 0; w < (int) (blockDim.x >> 6); ++w) {
+		tabs += sabs[w];
+		tcnt += scnt[w];
+		texp = sexp[w] < texp ? sexp[w] : texp;
+	}
+	double sd = total;
+	if(exact) {
+		bool provable = texp != INT32_MIN &&
+		                (texp == INT32_MAX || (texp > -1000 && tabs * (1.0 + 1e-9) < ldexp(1.0, 53 + texp)));
+		if(!provable) {
+			// the reference's serial sum in increasing k (nj.c:911 / :1002)
+			sd = 0;
 			for(int c0 = 0; c0 < n; c0 += blockDim.x) {
 				int kk = c0 + threadIdx.x;
-				buf[threadIdx.x] = kk < n ? __hip_atomic_load(&b.contrib[kk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+				buf[threadIdx.x] = kk < n ? b.contrib[kk] : 0.0;
 				__syncthreads();
 				if(threadIdx.x == 0) {
 					int lim = n - c0 < (int) blockDim.x ? n - c0 : (int) blockDim.x;
@@ -620,19 +887,13 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 				}
 				__syncthreads();
 			}
-		} else if(threadIdx.x == 0) {
-			for(unsigned w = 0; w < gridDim.x; ++w) {
-				sd += __hip_atomic_load(&b.wsum[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			}
+			if(threadIdx.x == 0) ctl->serial_sums++;
 		}
-		__syncthreads();
-		if(threadIdx.x == 0) {
-			int tot = 0;
-			for(int w = 0; w < (int) (blockDim.x >> 6); ++w) tot += sc[w];
-			b.N[j] = 1 + tot;
-			b.sD[j] = sd;
-			ctl->counter = 0;
-		}
+	}
+	if(threadIdx.x == 0) {
+		b.N[j] = 1 + tcnt;
+		b.sD[j] = sd;
+		ctl->tick[2] = 0;
 	}
 }
 
@@ -640,14 +901,14 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 // in chunks, reproducing the lagging sD/N cursor and the out-of-row read
 // D_j[k] of the D_kj-only column branch (nj.c:1022).
 template <int ET>
-__global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                         TreeBufs b) {
+__global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
 	typedef typename Elem<ET>::T T;
 	__shared__ int wsc[16];
 	__shared__ double sbuf[1024];
 	__shared__ int s_carry, s_cnt;
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
+	const int n = ctl->n;
 	const int i = ctl->i, j = ctl->j;
 	const double Dij = ctl->Dij, Li = ctl->Li, Lj = ctl->Lj;
 	const long long rj = tri(j), ri = tri(i);
@@ -767,25 +1028,28 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 }
 
 // ------------------------------------------------------------------ DNJ requeue
-// updateDNJ's Q/P part (dnj.c:618-709) followed by DNJ_popArrange (dnj.c:817-975)
+// updateDNJ's Q/P part (dnj.c:618-709) followed by DNJ_popArrange
+// (dnj.c:817-975) and minPos (dnj.c:1026-1032); the last block folds the four
+// (q, idx) reductions, shrinks n and prepares the next minQpair.
 template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, int n, double bs, TreeBufs b) {
+__global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
+	__shared__ int s_cand;
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	const int i = ctl->i, j = ctl->j, nn = n - 1;
+	const int n = ctl->n, i = ctl->i, j = ctl->j, nn = n - 1;
 	const int Nj = b.N[j];
 	const double sDj = b.sD[j];
 	const bool move = i != nn;
 	const int Nm = move ? b.N[nn] : 0;
 	const double sDm = move ? b.sD[nn] : 0;
-	int k = blockIdx.x * blockDim.x + threadIdx.x;
+	const int k = blockIdx.x * blockDim.x + threadIdx.x;
 	double rq = DBL_MAX, pq = DBL_MAX, r2q = DBL_MAX, p2q = DBL_MAX;
 	int rj = 0, pk = -1, r2j = 0, p2k = -1;
 	if(k < n) {
-		int Nk = b.N[k];
-		double sDk = b.sD[k];
+		const int Nk = b.N[k];
+		const double sDk = b.sD[k];
 		if(k < j) {
 			double d = Elem<ET>::get(D[tri(j) + k], bs);
 			if(0 <= d) {
@@ -838,7 +1102,6 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			}
 		}
 	}
-	// four (q, idx) block reductions -> per-block partials
 	qarg_block_reduce(rq, rj, sq, si);
 	qarg_block_reduce(pq, pk, sq, si);
 	qarg_block_reduce(r2q, r2j, sq, si);
@@ -851,58 +1114,76 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		qp[2] = r2q; ip[2] = r2j;
 		qp[3] = p2q; ip[3] = p2k;
 	}
-	if(last_block_arrive(&ctl->counter)) {
-		if(threadIdx.x == 0) {
-			double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
-			int ix[4] = {0, -1, 0, -1};
-			for(unsigned w = 0; w < gridDim.x; ++w) {
-				for(int t = 0; t < 4; ++t) {
-					double oq = __hip_atomic_load(&b.qpart[4 * w + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					int oi = __hip_atomic_load(&b.ipart[4 * w + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					if(qarg_better(oq, oi, q[t], ix[t])) {
-						q[t] = oq;
-						ix[t] = oi;
-					}
-				}
+	if(!last_block_arrive(&ctl->tick[3])) return;
+	double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
+	int ix[4] = {0, -1, 0, -1};
+	for(unsigned w = threadIdx.x; w < gridDim.x; w += blockDim.x) {
+#pragma unroll
+		for(int t = 0; t < 4; ++t) {
+			double oq = b.qpart[4 * w + t];
+			int oi = b.ipart[4 * w + t];
+			if(qarg_better(oq, oi, q[t], ix[t])) {
+				q[t] = oq;
+				ix[t] = oi;
 			}
-			// row j (dnj.c:619-663) and p over the lowered column entries
-			b.Q[j] = q[0];
-			b.P[j] = ix[0];
-			int p = j;
-			if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
-			int p2 = 0;
-			if(move) {
-				b.sD[i] = sDm;
-				b.N[i] = Nm;
-				b.Q[i] = q[2];
-				b.P[i] = ix[2];
-				p2 = i;
-				if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
-			}
-			ctl->mi = p;
-			ctl->mj = p2;
-			ctl->counter = 0;
 		}
 	}
+#pragma unroll
+	for(int t = 0; t < 4; ++t) qarg_block_reduce(q[t], ix[t], sq, si);
+	if(threadIdx.x == 0) {
+		// row j (dnj.c:619-663) and p over the lowered column entries
+		b.Q[j] = q[0];
+		b.P[j] = ix[0];
+		int p = j;
+		if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
+		int p2 = 0;
+		if(move) {
+			b.sD[i] = sDm;
+			b.N[i] = Nm;
+			b.Q[i] = q[2];
+			b.P[i] = ix[2];
+			p2 = i;
+			if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
+		}
+		ctl->mi = p;
+		ctl->mj = p2;
+		ctl->n = nn;
+		ctl->tick[3] = 0;
+		// dnj.c:1026-1032: next candidate row
+		int cand;
+		if(p2 == nn) cand = p;
+		else if(p == nn) cand = p2;
+		else cand = (b.Q[p2] < b.Q[p] || (p < p2 && b.Q[p2] == b.Q[p])) ? p2 : p;
+		s_cand = cand;
+	}
+	__threadfence_block();
+	__syncthreads();
+	if(nn > 2) prepare_selection(b, nn, s_cand);
 }
 
 // ------------------------------------------------------------------ NJ pop
 // matrix.c:518 ltdMatrix_popArrange + nj.c:1588-1589
 template <int ET>
-__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, int n, TreeBufs b) {
+__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b) {
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	const int i = ctl->i, nn = n - 1;
-	if(i == nn) return;
-	int k = blockIdx.x * blockDim.x + threadIdx.x;
-	if(k < i) {
-		D[tri(i) + k] = D[tri(nn) + k];
-	} else if(k > i && k < nn) {
-		D[tri(k) + i] = D[tri(nn) + k];
+	const int n = ctl->n, i = ctl->i, nn = n - 1;
+	const int k = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i != nn) {
+		if(k < i) {
+			D[tri(i) + k] = D[tri(nn) + k];
+		} else if(k > i && k < nn) {
+			D[tri(k) + i] = D[tri(nn) + k];
+		}
 	}
-	if(k == 0) {
-		b.sD[i] = b.sD[nn];
-		b.N[i] = b.N[nn];
+	if(!last_block_arrive(&ctl->tick[3])) return;
+	if(threadIdx.x == 0) {
+		if(i != nn) {
+			b.sD[i] = b.sD[nn];
+			b.N[i] = b.N[nn];
+		}
+		ctl->n = nn;
+		ctl->tick[3] = 0;
 	}
 }
 
@@ -915,16 +1196,24 @@ struct TreeWork {
 };
 
 static int tree_alloc(TreeWork *w, int n) {
-	size_t nb = (size_t) cdiv(n, TB) + 1;
-	size_t nq = 4096;   // NJ argmin partials
+	const size_t nb = (size_t) cdiv(n, TB) + 1;
+	const size_t maxunits = (size_t) DNJ_B * (cdiv(n, SEG) + 1);
+	const size_t nslices = (size_t) cdiv(n, RPB) + 1;
+	const size_t nq = 4096;
 	size_t sz = 0;
-	auto take = [&](size_t bytes) { size_t off = sz; sz += (bytes + 255) & ~(size_t) 255; return off; };
+	auto take = [&](size_t bytes) {
+		size_t off = sz;
+		sz += (bytes + 255) & ~(size_t) 255;
+		return off;
+	};
 	size_t o_sD = take(n * 8), o_Q = take(n * 8), o_fq = take(n * 8), o_c = take(n * 8);
-	size_t o_N = take(n * 4), o_P = take(n * 4), o_fj = take(n * 4), o_S = take(DNJ_B * 4);
-	size_t o_seg = take((size_t) n * 4 + 64), o_segc = take(REST_BLOCKS * 4);
-	size_t o_ws = take(nb * 8), o_wc = take(nb * 4);
+	size_t o_N = take(n * 4), o_P = take(n * 4), o_fj = take(n * 4);
+	size_t o_S = take(DNJ_B * 4), o_uo = take((DNJ_B + 1) * 4);
+	size_t o_uq = take(maxunits * 8), o_uj = take(maxunits * 4);
+	size_t o_br = take(nslices * RPB * 4), o_bc = take(nslices * 4);
+	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
 	size_t o_qp = take((nb > nq ? nb : nq) * 4 * 8), o_ip = take((nb > nq ? nb : nq) * 4 * 4);
-	size_t o_ab = take(nb * 8), o_qm = take(nb * 4), o_fp = take(nq * 8);
+	size_t o_fp = take(nq * 8);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
@@ -939,18 +1228,49 @@ static int tree_alloc(TreeWork *w, int n) {
 	b.P = (int *) (m + o_P);
 	b.fj = (int *) (m + o_fj);
 	b.S = (int *) (m + o_S);
-	b.seg = (int *) (m + o_seg);
-	b.segcnt = (int *) (m + o_segc);
+	b.uoff = (int *) (m + o_uo);
+	b.uq = (double *) (m + o_uq);
+	b.uj = (int *) (m + o_uj);
+	b.blk_rows = (int *) (m + o_br);
+	b.blk_cnt = (int *) (m + o_bc);
 	b.wsum = (double *) (m + o_ws);
+	b.wabs = (double *) (m + o_wa);
 	b.wcnt = (int *) (m + o_wc);
+	b.wexp = (int *) (m + o_we);
 	b.qpart = (double *) (m + o_qp);
 	b.ipart = (int *) (m + o_ip);
-	b.absb = (double *) (m + o_ab);
-	b.qmin = (int *) (m + o_qm);
 	b.fpart = (long long *) (m + o_fp);
 	b.joins = (ccg_join *) (m + o_j);
 	b.ctl = (TreeCtl *) (m + o_ctl);
 	return CCG_OK;
+}
+
+// One join's kernels, for a matrix of (at most) n taxa.
+template <int ET>
+static void enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n,
+                              int method, bool general) {
+	if(method == CCG_TREE_DNJ) {
+		k_dnj_top<ET><<<TOP_BLOCKS, TB, 0, st>>>(D, bs, b);
+		unsigned g2 = cdiv(n, RPB);
+		if(g2 > 2048) g2 = 2048;
+		k_dnj_rest<ET><<<g2, TB, 0, st>>>(D, bs, b);
+	} else {
+		long long cells = tri(n);
+		unsigned g = cdiv(cells, 8 * TB);
+		if(g > 2048) g = 2048;
+		if(g < 1) g = 1;
+		k_nj_argmin<ET><<<g, TB, 0, st>>>(D, bs, b);
+	}
+	if(general) {
+		k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b);
+	} else {
+		k_update<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
+	}
+	if(method == CCG_TREE_DNJ) {
+		k_dnj_requeue<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
+	} else {
+		k_nj_pop<ET><<<cdiv(n, TB), TB, 0, st>>>(D, b);
+	}
 }
 
 template <int ET>
@@ -967,8 +1287,10 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	TreeBufs b = w.b;
 	TreeCtl init;
 	memset(&init, 0, sizeof(init));
+	init.n = n0;
 	init.neg = (a->flags & 2) != 0;
 	init.exact = a->exact != 0;
+	init.method = a->method;
 	CCG_CHECK(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	long long launches = 0;
 	CCG_CHECK(hipEventRecord(ctx->ev0, st));
@@ -976,7 +1298,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	++launches;
 	if(a->method == CCG_TREE_DNJ) {
 		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.Q, b.P);
-		k_min_q_row<<<1, TB, 0, st>>>(b.Q, n0, b.ctl);
+		k_dnj_prep<<<1, TB, 0, st>>>(b);
 		launches += 2;
 	}
 	CCG_CHECK(hipGetLastError());
@@ -987,35 +1309,11 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	int n = n0;
 	int since_check = 0;
 	while(n != 2) {
-		if(a->method == CCG_TREE_DNJ) {
-			k_dnj_top<ET><<<DNJ_B, TB, 0, st>>>(D, n, bs, b);
-			k_dnj_rest<ET><<<REST_BLOCKS, TB, 0, st>>>(D, n, bs, b);
-			k_dnj_replay<ET><<<1, TB, 0, st>>>(D, n, bs, b, REST_BLOCKS);
-			launches += 3;
-		} else {
-			long long cells = tri(n);
-			unsigned g = cdiv(cells, 4096);
-			if(g > 2048) g = 2048;
-			if(g < 1) g = 1;
-			long long chunk = (cells + g - 1) / g;
-			k_nj_argmin<ET><<<g, TB, 0, st>>>(D, n, bs, b, chunk);
-			launches += 1;
-		}
-		if(general) {
-			k_update_general<ET><<<1, 1024, 0, st>>>(D, n, bs, b);
-		} else {
-			k_update<ET><<<cdiv(n, TB), TB, 0, st>>>(D, n, bs, b);
-		}
-		++launches;
-		if(a->method == CCG_TREE_DNJ) {
-			k_dnj_requeue<ET><<<cdiv(n, TB), TB, 0, st>>>(D, n, bs, b);
-		} else {
-			k_nj_pop<ET><<<cdiv(n, TB), TB, 0, st>>>(D, n, b);
-		}
-		++launches;
+		enqueue_iteration<ET>(st, D, bs, b, n, a->method, general);
+		launches += a->method == CCG_TREE_DNJ ? 4 : 3;
 		CCG_CHECK(hipGetLastError());
 		--n;
-		if(++since_check == 512) {
+		if(++since_check == 1024) {
 			since_check = 0;
 			CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 			CCG_CHECK(hipStreamSynchronize(st));
@@ -1028,7 +1326,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	float ms = 0;
 	CCG_CHECK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
 	*njoins = h.njoins;
-	*final_n = h.done ? h.final_n : n;
+	*final_n = h.done ? h.final_n : h.n;
 	if(h.njoins) {
 		CCG_CHECK(hipMemcpy(joins, b.joins, (size_t) h.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost));
 	}
