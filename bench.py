@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of ccphylo_amd (driver contract).
+
+Metric (BASELINE.json): "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa".
+`value` is NJ iterations (joins) per second of `ccphylo tree -m dnj` (the
+reference's default method, which yields the exact NJ join sequence) on
+configs[1]: an N=10,000-taxon distance matrix, one full tree per step, the
+packed LT already resident in HBM when the timed region starts (one fresh
+device copy per step; the engine consumes its input).
+
+Multi-GPU (torchrun, one process per GPU): every rank builds its own tree on
+its own GPU ("replicas": the NJ loop is a strict dependency chain; the sharded
+DNJ of SURVEY 8(e) is later work) -> scaling "weak", value = all ranks' joins
+divided by the max over ranks of the timed span.
+
+Also reported: the dominant kernel's roofline (HIP-event timing of every
+kernel in one profiled extra step on the engine stream; algorithmic bytes as
+defined in DESIGN.md), the reference CPU path on the same matrix (rank 0,
+N=1), and extras (exact-row-sum mode, -m nj, and SNP `dist` throughput).
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+KNAMES = ["init", "dnj_top", "dnj_rest", "nj_argmin", "update", "dnj_requeue", "nj_pop"]
+
+
+def euclid_ltd(n, seed=1, dim=8):
+    """Distances of n points U[0,1)^dim, quantized like a %.9f Phylip."""
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n, dim))
+    D = np.empty(n * (n - 1) // 2)
+    for i in range(1, n):
+        o = i * (i - 1) // 2
+        D[o:o + i] = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
+    return np.round(D * 1e9) / 1e9
+
+
+def algorithmic_bytes(kernel, n_join, s, cells):
+    """Compulsory HBM bytes of one launch ('Roofline accounting')."""
+    if kernel in ("dnj_top", "dnj_rest"):
+        return s * cells + 12.0 * n_join          # rescanned D cells + N/sD once
+    if kernel == "nj_argmin":
+        return s * n_join * (n_join - 1) / 2 + 12.0 * n_join
+    if kernel in ("update", "dnj_requeue"):
+        return 3.0 * s * n_join + 24.0 * n_join   # rows/cols i, j (+ moved row) and the n-vectors
+    if kernel == "nj_pop":
+        return 2.0 * s * n_join
+    return 0.0
+
+
+def roofline(stats, n, s):
+    """Dominant kernel (largest total device time) of a profiled run."""
+    per = {}
+    for c, name in enumerate(KNAMES):
+        cnt, ns = stats[4 + 2 * c], stats[5 + 2 * c]
+        if cnt:
+            per[name] = (cnt, ns)
+    name = max(per, key=lambda k: per[k][1])
+    cnt, ns = per[name]
+    cells = stats[4 + 2 * len(KNAMES)] if name == "dnj_top" else stats[5 + 2 * len(KNAMES)]
+    # mean n over the joins (n runs from N down to 3)
+    if name == "nj_argmin":
+        tot = sum(algorithmic_bytes(name, k, s, 0) for k in range(3, n + 1))
+    elif name in ("dnj_top", "dnj_rest"):
+        tot = s * cells + 12.0 * sum(range(3, n + 1))
+    elif name == "init":
+        tot = 2 * s * n * (n - 1) / 2
+    else:
+        tot = sum(algorithmic_bytes(name, k, s, 0) for k in range(3, n + 1))
+    avg_s = ns / cnt / 1e9
+    achieved = tot / cnt / avg_s / 1e9
+    shares = {k: round(v[1] / sum(x[1] for x in per.values()), 4) for k, v in per.items()}
+    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
+            "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares}
+
+
+def cpu_baseline(D, n, tmpdir):
+    """The reference binary (oracle/_ref, built from /root/reference by
+    oracle/Makefile) on the same matrix written as Phylip, 1 thread; falls back
+    to the oracle's C restatement in-process."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
+    if os.path.exists(ref):
+        from ccphylo_amd import native
+        path = os.path.join(tmpdir, "bench_ref.phy")
+        native.write_phylip(path, D, n, [f"t{k}" for k in range(n)])
+        t0 = time.perf_counter()
+        p = subprocess.run([ref, "tree", "-i", path, "-m", "dnj", "-t", "1", "-o", os.path.join(tmpdir, "ref.nwk")],
+                           capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t0
+        m = re.search(r"Constructing tree: ([0-9.]+) s", p.stderr)
+        ld = re.search(r"loading matrix: ([0-9.]+) s", p.stderr)
+        cons = float(m.group(1)) if m else wall
+        os.unlink(path)
+        return {"value": round((n - 2) / cons, 2), "unit": "NJ joins/s", "cores": 1, "kind": "reference",
+                "sample": f"full N={n} DNJ tree, reference ccphylo 0.8.5 `tree -m dnj -t 1` on the same matrix "
+                          f"(Phylip %.9f); construction {cons:.2f} s (its own clock() report), "
+                          f"Phylip load {float(ld.group(1)) if ld else -1:.2f} s, process wall {wall:.2f} s"}
+    from oracle import pyoracle
+    t0 = time.perf_counter()
+    j, _, _ = pyoracle.tree(D, n, method=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(j) / dt, 2), "unit": "NJ joins/s", "cores": 1, "kind": "port",
+            "sample": f"full N={n} DNJ tree with the oracle's serial C restatement (reference binary absent)"}
+
+
+def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3):
+    """SNP distances (non-pair, double) with device-resident packed input."""
+    W = L // 32 + 1
+    g = torch.Generator(device="cuda").manual_seed(3)
+    seqs = torch.randint(-2**62, 2**62, (n, W), dtype=torch.int64, device="cuda", generator=g)
+    incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
+    incs[(L + 31) // 32:] = 0
+    if L % 32:
+        incs[(L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    m = n * (n - 1) // 2
+    Dd = torch.empty(m, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    dt = min(times)
+    words = (L + 31) // 32
+    ops = m * words * 4.0
+    del seqs, incs, Dd
+    return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
+            "config": f"N={n} x L={L} random MSA (non-pair, double), input in HBM",
+            "valu_frac": round(ops / dt / VALU_LANE_OPS, 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=10000)
+    ap.add_argument("--sums", choices=["fast", "exact"], default="fast")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    import ccphylo_amd as cg
+
+    n = args.n
+    s = 8
+    D = euclid_ltd(n, seed=1)
+    dev = cg.Device(local)
+    exact = args.sums == "exact"
+    nbytes = D.nbytes
+    bufs = [dev.malloc(nbytes) for _ in range(args.steps + args.warmup)]
+    for b in bufs:
+        dev.h2d(b, D)
+    for w in range(args.warmup):
+        dev.tree_dev(bufs[w], n, method=cg.CCG_TREE_DNJ, exact=exact)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    joins = 0
+    for k in range(args.steps):
+        j, fn, fd, st = dev.tree_dev(bufs[args.warmup + k], n, method=cg.CCG_TREE_DNJ, exact=exact)
+        joins += len(j)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+        jt = torch.tensor([joins], dtype=torch.float64)
+        dist.all_reduce(jt, op=dist.ReduceOp.SUM)
+        joins_all = float(jt[0])
+    else:
+        joins_all = float(joins)
+    for b in bufs:
+        dev.free(b)
+
+    # one profiled extra step (HIP events around every kernel, engine stream)
+    pb = dev.malloc(nbytes)
+    dev.h2d(pb, D)
+    _, _, _, pst = dev.tree_dev(pb, n, method=cg.CCG_TREE_DNJ, exact=exact, profile=True)
+    dev.free(pb)
+    roof = roofline(pst, n, s)
+
+    result = {
+        "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
+        "value": round(joins_all / dt, 2),
+        "unit": "NJ iterations (joins)/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic: N={n} Euclidean distances of U[0,1)^8 points (seed 1), quantized to 9 decimals "
+                f"as a %.9f Phylip would be; one full tree per step per GPU",
+        "config": {"workload": f"ccphylo tree -m dnj (configs[1]: N={n} synthetic Phylip matrix, NJ/DNJ on 1 "
+                               f"MI355X per rank)", "n_taxa": n, "method": "dnj", "elem": "double",
+                   "row_sums": args.sums, "parallelism": f"replicas x{world}"},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = {}
+        pb = dev.malloc(nbytes)
+        for label, method, ex in (("dnj_exact_sums" if not exact else "dnj_fast_sums", cg.CCG_TREE_DNJ, not exact),
+                                  ("nj", cg.CCG_TREE_NJ, exact)):
+            dev.h2d(pb, D)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            j, _, _, st = dev.tree_dev(pb, n, method=method, exact=ex)
+            t2 = time.perf_counter() - t1
+            extras[label] = {"joins_per_s": round(len(j) / t2, 2), "seconds": round(t2, 4)}
+        dev.h2d(pb, D)
+        _, _, _, nst = dev.tree_dev(pb, n, method=cg.CCG_TREE_NJ, exact=exact, profile=True)
+        extras["nj"]["roofline"] = roofline(nst, n, s)
+        dev.free(pb)
+        try:
+            extras["dist"] = dist_extra(dev, torch)
+        except Exception as e:  # noqa: BLE001
+            extras["dist"] = {"error": str(e)}
+        result["extras"] = extras
+    if rank == 0 and world == 1 and not args.no_cpu:
+        with tempfile.TemporaryDirectory(dir="/tmp") as td:
+            result["cpu_baseline"] = cpu_baseline(D, n, td)
+    dev.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,15 +96,15 @@ int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_ou
 		rc = CCG_ENOMEM;
 		goto done;
 	}
-	if(hipMemcpy(d_seq, a->seqs, seq_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-	   hipMemcpy(d_inc, a->incs, inc_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+	if(hipMemcpyAsync(d_seq, a->seqs, seq_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+	   hipMemcpyAsync(d_inc, a->incs, inc_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
 		rc = CCG_EHIP;
 		goto done;
 	}
 	// untouched cells (outside a row range) keep the caller's contents
 	if(lt && (a->row_begin || a->row_end)) {
-		if(hipMemcpy(d_D, D, lt, hipMemcpyHostToDevice) != hipSuccess ||
-		   (d_N && hipMemcpy(d_N, N, lt, hipMemcpyHostToDevice) != hipSuccess)) {
+		if(hipMemcpyAsync(d_D, D, lt, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+		   (d_N && hipMemcpyAsync(d_N, N, lt, hipMemcpyHostToDevice, c->stream) != hipSuccess)) {
 			rc = CCG_EHIP;
 			goto done;
 		}
@@ -113,12 +113,14 @@ int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_ou
 	da.incs = (const uint32_t *) d_inc;
 	rc = ccg_snp_dev_impl(c, &da, d_D, d_N, inc_out);
 	if(rc == CCG_OK && lt) {
-		if(hipMemcpy(D, d_D, lt, hipMemcpyDeviceToHost) != hipSuccess ||
-		   (d_N && hipMemcpy(N, d_N, lt, hipMemcpyDeviceToHost) != hipSuccess)) {
+		if(hipMemcpyAsync(D, d_D, lt, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+		   (d_N && hipMemcpyAsync(N, d_N, lt, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
+		   hipStreamSynchronize(c->stream) != hipSuccess) {
 			rc = CCG_EHIP;
 		}
 	}
 done:
+	hipStreamSynchronize(c->stream);
 	if(d_seq) hipFree(d_seq);
 	if(d_inc) hipFree(d_inc);
 	if(d_D) hipFree(d_D);
@@ -145,11 +147,12 @@ int ccg_tree(ccg_ctx *c, const ccg_tree_args *a, const void *D, ccg_join *joins,
 	void *d = NULL;
 	if(hipMalloc(&d, bytes) != hipSuccess) return CCG_ENOMEM;
 	int rc = CCG_OK;
-	if(hipMemcpy(d, D, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+	if(hipMemcpyAsync(d, D, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
 		rc = CCG_EHIP;
 	} else {
 		rc = ccg_tree_dev(c, a, d, joins, njoins, final_n, final_d, stats);
 	}
+	hipStreamSynchronize(c->stream);
 	hipFree(d);
 	return rc;
 }
@@ -169,13 +172,15 @@ int ccg_free(ccg_ctx *c, void *p) {
 
 int ccg_memcpy_h2d(ccg_ctx *c, void *dst, const void *src, size_t bytes) {
 	if(!c) return CCG_EINVAL;
-	CCG_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+	CCG_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+	CCG_CHECK(hipStreamSynchronize(c->stream));
 	return CCG_OK;
 }
 
 int ccg_memcpy_d2h(ccg_ctx *c, void *dst, const void *src, size_t bytes) {
 	if(!c) return CCG_EINVAL;
-	CCG_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+	CCG_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+	CCG_CHECK(hipStreamSynchronize(c->stream));
 	return CCG_OK;
 }
 

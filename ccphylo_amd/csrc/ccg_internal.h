@@ -121,21 +121,29 @@ __device__ __forceinline__ void qarg_block_reduce(double &q, int &idx, double *s
 	__syncthreads();
 }
 
-// last-block-done ticket (Guideline 16: agent-scope release before the
-// arrival, acquire in the last block)
+// ---------------------------------------------------- in-kernel hand-offs
+// Guideline 16 form R1: every handed-off byte is stored write-through (sc1)
+// and loaded with sc1 loads by the consumer; each storing wave drains its
+// stores (vmcnt(0)) before the workgroup barrier, then ONE lane takes an
+// agent-scope ticket.  No release/acquire fences (an L2 write-back per block).
+template <typename T>
+__device__ __forceinline__ void st_wt(T *p, T v) {
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_wt(const T *p) {
+	return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true in every thread of the last block to arrive
 __device__ __forceinline__ bool last_block_arrive(unsigned *counter) {
 	__shared__ int s_last;
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	__syncthreads();
 	if(threadIdx.x == 0) {
-		__threadfence();
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		unsigned t = atomicAdd(counter, 1u);
+		unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		s_last = (t == gridDim.x * gridDim.y - 1);
 	}
 	__syncthreads();
-	if(s_last) {
-		__threadfence();
-		return true;
-	}
-	return false;
+	return s_last;
 }

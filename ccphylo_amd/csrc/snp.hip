@@ -285,7 +285,8 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 			int *d_inc;
 			CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
 			k_popsum<<<1, 256, 0, ctx->stream>>>(a->incs, (a->len + 31) / 32, d_inc);
-			CCG_CHECK(hipMemcpy(inc_out, d_inc, sizeof(int), hipMemcpyDeviceToHost));
+			CCG_CHECK(hipMemcpyAsync(inc_out, d_inc, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+			CCG_CHECK(hipStreamSynchronize(ctx->stream));
 			CCG_CHECK(hipFree(d_inc));
 		}
 		return CCG_OK;

@@ -57,6 +57,7 @@ struct TreeCtl {
 	int serial_sums, serial_replays;
 	unsigned tick[4];    // last-block tickets (reset by their last block)
 	long long rows, cells;
+	long long cells_top, cells_rest;
 	int has_missing;
 };
 
@@ -160,19 +161,19 @@ __device__ void record_join(const typename Elem<ET>::T *D, double bs, const Tree
 
 // (q, j) min of LT row r over columns [c0, c1), whole block, 8 loads in flight
 // per thread (dnj.c:99-112 with the `<=` last-wins rule)
-template <int ET>
+template <int ET, int UNR = 8>
 __device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__restrict__ D, double bs,
                                                 const double *__restrict__ sD, const int *__restrict__ N, int r,
                                                 int c0, int c1, double &q, int &idx) {
 	const typename Elem<ET>::T *row = D + tri(r);
 	const int Nr = N[r];
 	const double sDr = sD[r];
-	for(int base = c0; base < c1; base += 8 * TB) {
-		typename Elem<ET>::T v[8];
-		int nk[8];
-		double sk[8];
+	for(int base = c0; base < c1; base += UNR * TB) {
+		typename Elem<ET>::T v[UNR];
+		int nk[UNR];
+		double sk[UNR];
 #pragma unroll
-		for(int m = 0; m < 8; ++m) {
+		for(int m = 0; m < UNR; ++m) {
 			int c = base + m * TB + (int) threadIdx.x;
 			if(c < c1) {
 				v[m] = row[c];
@@ -181,7 +182,7 @@ __device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__re
 			}
 		}
 #pragma unroll
-		for(int m = 0; m < 8; ++m) {
+		for(int m = 0; m < UNR; ++m) {
 			int c = base + m * TB + (int) threadIdx.x;
 			if(c < c1) {
 				double d = Elem<ET>::get(v[m], bs);
@@ -277,12 +278,12 @@ __device__ void prepare_selection(const TreeBufs &b, int n, int cand) {
 	__shared__ int s_cnt;
 	TreeCtl *ctl = b.ctl;
 	double m0 = DBL_MAX;
-	if(cand && m0 != b.Q[cand]) m0 = b.Q[cand];
+	if(cand && m0 != ld_wt(&b.Q[cand])) m0 = ld_wt(&b.Q[cand]);
 	if(threadIdx.x == 0) {
 		ctl->cand = cand;
 		ctl->m0 = m0;
 		ctl->pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
-		ctl->pos_j = (cand && m0 != DBL_MAX) ? b.P[cand] : 0;
+		ctl->pos_j = (cand && m0 != DBL_MAX) ? ld_wt(&b.P[cand]) : 0;
 		s_cnt = 0;
 	}
 	__syncthreads();
@@ -294,7 +295,7 @@ __device__ void prepare_selection(const TreeBufs &b, int n, int cand) {
 #pragma unroll
 		for(int m = 0; m < 4; ++m) {
 			int r = base - 4 * (int) threadIdx.x - m;
-			if(r >= 1 && b.Q[r] < m0) rows[k++] = r;
+			if(r >= 1 && ld_wt(&b.Q[r]) < m0) rows[k++] = r;
 		}
 		int tot;
 		int off = block_excl_scan(k, s_scan, &tot);
@@ -366,8 +367,8 @@ __global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__re
 		row_segment_min<ET>(D, bs, b.sD, b.N, r, c0, c1, q, idx);
 		qarg_block_reduce(q, idx, sq, si);
 		if(threadIdx.x == 0) {
-			b.uq[u] = q;
-			b.uj[u] = idx;
+			st_wt(&b.uq[u], q);
+			st_wt(&b.uj[u], idx);
 		}
 	}
 	if(!last_block_arrive(&ctl->tick[0])) return;
@@ -378,8 +379,8 @@ __global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__re
 		double q = DBL_MAX;
 		int idx = 0;
 		for(int u = so[t]; u < so[t + 1]; ++u) {
-			double uq = b.uq[u];
-			int uj = b.uj[u];
+			double uq = ld_wt(&b.uq[u]);
+			int uj = ld_wt(&b.uj[u]);
 			if(qarg_better(uq, uj, q, idx)) {
 				q = uq;
 				idx = uj;
@@ -395,7 +396,10 @@ __global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__re
 	}
 	U = lds_min_reduce(U, sq);
 	for(int off = 32; off > 0; off >>= 1) cells += __shfl_xor(cells, off, 64);
-	if((threadIdx.x & 63) == 0 && cells) atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+	if((threadIdx.x & 63) == 0 && cells) {
+		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+		atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) cells);
+	}
 	if(threadIdx.x == 0) {
 		ctl->U = U;
 		ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
@@ -438,19 +442,20 @@ __global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__r
 			int r = list[t];
 			double q = DBL_MAX;
 			int idx = 0;
-			row_segment_min<ET>(D, bs, b.sD, b.N, r, 0, r, q, idx);
+			row_segment_min<ET, 16>(D, bs, b.sD, b.N, r, 0, r, q, idx);
 			qarg_block_reduce(q, idx, sq, si);
 			if(threadIdx.x == 0) {
-				b.fq[r] = q;
-				b.fj[r] = idx;
-				b.blk_rows[sl * RPB + t] = r;
+				st_wt(&b.fq[r], q);
+				st_wt(&b.fj[r], idx);
+				st_wt(&b.blk_rows[sl * RPB + t], r);
 			}
 			cells += r;
 		}
 		if(threadIdx.x == 0) {
-			b.blk_cnt[sl] = cnt;
+			st_wt(&b.blk_cnt[sl], cnt);
 			if(cnt) {
 				atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+				atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) cells);
 				atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) cnt);
 			}
 		}
@@ -468,12 +473,12 @@ __global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__r
 	int carry = nS;
 	for(int c0 = 0; c0 < nblk; c0 += blockDim.x) {
 		int t = c0 + threadIdx.x;
-		int c = t < nblk ? b.blk_cnt[nblk - 1 - t] : 0;
+		int c = t < nblk ? ld_wt(&b.blk_cnt[nblk - 1 - t]) : 0;
 		int tot;
 		int off = block_excl_scan(c, scan, &tot);
 		for(int k = 0; k < c; ++k) {
 			int e = carry + off + k;
-			if(e < REPLAY_CAP) e_row[e] = b.blk_rows[(nblk - 1 - t) * RPB + k];
+			if(e < REPLAY_CAP) e_row[e] = ld_wt(&b.blk_rows[(nblk - 1 - t) * RPB + k]);
 		}
 		carry += tot;
 	}
@@ -485,10 +490,10 @@ __global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__r
 		int bad = 0;
 		for(int e = threadIdx.x; e < total; e += blockDim.x) {
 			int r = e_row[e];
-			double bq = b.Q[r], fq = b.fq[r];
+			double bq = b.Q[r], fq = ld_wt(&b.fq[r]);
 			e_b[e] = bq;
 			e_f[e] = fq;
-			e_j[e] = b.fj[r];
+			e_j[e] = ld_wt(&b.fj[r]);
 			bad |= !(fq >= bq);
 		}
 		bad = __syncthreads_or(bad);
@@ -587,21 +592,22 @@ __global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__r
 			if(e < nS) {
 				r = b.S[e];
 			} else {
-				while(k >= b.blk_cnt[nblk - 1 - t]) {
+				while(k >= ld_wt(&b.blk_cnt[nblk - 1 - t])) {
 					++t;
 					k = 0;
 				}
-				r = b.blk_rows[(nblk - 1 - t) * RPB + k];
+				r = ld_wt(&b.blk_rows[(nblk - 1 - t) * RPB + k]);
 				++k;
 			}
 			if(b.Q[r] < m) {
-				double f = b.fq[r];
+				double f = ld_wt(&b.fq[r]);
+				int fj = ld_wt(&b.fj[r]);
 				b.Q[r] = f;
-				b.P[r] = b.fj[r];
+				b.P[r] = fj;
 				if(f < m) {
 					m = f;
 					pi = r;
-					pj = b.fj[r];
+					pj = fj;
 				}
 			}
 		}
@@ -700,15 +706,15 @@ __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__
 				bf = sf[k];
 			}
 		}
-		b.qpart[blockIdx.x] = bq;
-		b.fpart[blockIdx.x] = bf;
+		st_wt(&b.qpart[blockIdx.x], bq);
+		st_wt(&b.fpart[blockIdx.x], bf);
 	}
 	if(!last_block_arrive(&ctl->tick[1])) return;
 	bq = 1.0;
 	bf = -1;
 	for(unsigned k = threadIdx.x; k < gridDim.x; k += blockDim.x) {
-		double oq = b.qpart[k];
-		long long of = b.fpart[k];
+		double oq = ld_wt(&b.qpart[k]);
+		long long of = ld_wt(&b.fpart[k]);
 		if(oq < bq || (oq == bq && of > bf)) {
 			bq = oq;
 			bf = of;
@@ -773,7 +779,7 @@ template <int ET>
 __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
 	__shared__ double ssum[TB / 64], sabs[TB / 64];
 	__shared__ int scnt[TB / 64], sexp[TB / 64];
-	__shared__ double buf[TB];
+	__shared__ double buf[8 * TB];
 	__shared__ double red[1024];
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
@@ -794,7 +800,7 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 		cnt = 1;
 	}
 	const bool exact = ctl->exact;
-	if(exact && k < n) b.contrib[k] = d;
+	if(exact && k < n) st_wt(&b.contrib[k], d);
 	double s = d, a = fabs(d);
 	int e = low_exp(d);
 	for(int off = 32; off > 0; off >>= 1) {
@@ -821,10 +827,10 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 			c += scnt[w];
 			te = sexp[w] < te ? sexp[w] : te;
 		}
-		b.wsum[blockIdx.x] = t;
-		b.wabs[blockIdx.x] = ta;
-		b.wcnt[blockIdx.x] = c;
-		b.wexp[blockIdx.x] = te;
+		st_wt(&b.wsum[blockIdx.x], t);
+		st_wt(&b.wabs[blockIdx.x], ta);
+		st_wt(&b.wcnt[blockIdx.x], c);
+		st_wt(&b.wexp[blockIdx.x], te);
 	}
 	if(!last_block_arrive(&ctl->tick[2])) return;
 	// fixed-order fold of the block partials: 1024 leaves (block g -> leaf
@@ -832,15 +838,15 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 	const int G = gridDim.x;
 	for(int leaf = threadIdx.x; leaf < 1024; leaf += blockDim.x) {
 		double v = 0;
-		for(int g = leaf; g < G; g += 1024) v += b.wsum[g];
+		for(int g = leaf; g < G; g += 1024) v += ld_wt(&b.wsum[g]);
 		red[leaf] = v;
 	}
 	double tabs = 0;
 	int tcnt = 0, texp = INT32_MAX;
 	for(int g = threadIdx.x; g < G; g += blockDim.x) {
-		tabs += b.wabs[g];
-		tcnt += b.wcnt[g];
-		int oe = b.wexp[g];
+		tabs += ld_wt(&b.wabs[g]);
+		tcnt += ld_wt(&b.wcnt[g]);
+		int oe = ld_wt(&b.wexp[g]);
 		texp = oe < texp ? oe : texp;
 	}
 	__syncthreads();
@@ -877,14 +883,27 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 		if(!provable) {
 			// the reference's serial sum in increasing k (nj.c:911 / :1002)
 			sd = 0;
-			for(int c0 = 0; c0 < n; c0 += blockDim.x) {
-				int kk = c0 + threadIdx.x;
-				buf[threadIdx.x] = kk < n ? b.contrib[kk] : 0.0;
-				__syncthreads();
-				if(threadIdx.x == 0) {
-					int lim = n - c0 < (int) blockDim.x ? n - c0 : (int) blockDim.x;
-					for(int u = 0; u < lim; ++u) sd += buf[u];
+			double nxt[4];
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				int kk = m * TB + threadIdx.x;
+				buf[m * TB + threadIdx.x] = kk < n ? ld_wt(&b.contrib[kk]) : 0.0;
+			}
+			__syncthreads();
+			for(int c0 = 0, p = 0; c0 < n; c0 += 4 * TB, p ^= 1) {
+				// fetch the next chunk while thread 0 runs the serial chain
+#pragma unroll
+				for(int m = 0; m < 4; ++m) {
+					int kk = c0 + 4 * TB + m * TB + threadIdx.x;
+					nxt[m] = kk < n ? ld_wt(&b.contrib[kk]) : 0.0;
 				}
+				if(threadIdx.x == 0) {
+					const double *cur = buf + p * 4 * TB;
+					int lim = n - c0 < 4 * TB ? n - c0 : 4 * TB;
+					for(int u = 0; u < lim; ++u) sd += cur[u];
+				}
+#pragma unroll
+				for(int m = 0; m < 4; ++m) buf[(p ^ 1) * 4 * TB + m * TB + threadIdx.x] = nxt[m];
 				__syncthreads();
 			}
 			if(threadIdx.x == 0) ctl->serial_sums++;
@@ -1088,8 +1107,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				}
 			}
 			if(upd) {
-				b.Q[k] = qk;
-				b.P[k] = pkk;
+				st_wt(&b.Q[k], qk);
+				st_wt(&b.P[k], pkk);
 			}
 		}
 		if(move && k < i) {
@@ -1109,10 +1128,10 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	if(threadIdx.x == 0) {
 		double *qp = b.qpart + 4 * blockIdx.x;
 		int *ip = b.ipart + 4 * blockIdx.x;
-		qp[0] = rq; ip[0] = rj;
-		qp[1] = pq; ip[1] = pk;
-		qp[2] = r2q; ip[2] = r2j;
-		qp[3] = p2q; ip[3] = p2k;
+		st_wt(&qp[0], rq); st_wt(&ip[0], rj);
+		st_wt(&qp[1], pq); st_wt(&ip[1], pk);
+		st_wt(&qp[2], r2q); st_wt(&ip[2], r2j);
+		st_wt(&qp[3], p2q); st_wt(&ip[3], p2k);
 	}
 	if(!last_block_arrive(&ctl->tick[3])) return;
 	double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
@@ -1120,8 +1139,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	for(unsigned w = threadIdx.x; w < gridDim.x; w += blockDim.x) {
 #pragma unroll
 		for(int t = 0; t < 4; ++t) {
-			double oq = b.qpart[4 * w + t];
-			int oi = b.ipart[4 * w + t];
+			double oq = ld_wt(&b.qpart[4 * w + t]);
+			int oi = ld_wt(&b.ipart[4 * w + t]);
 			if(qarg_better(oq, oi, q[t], ix[t])) {
 				q[t] = oq;
 				ix[t] = oi;
@@ -1132,16 +1151,16 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	for(int t = 0; t < 4; ++t) qarg_block_reduce(q[t], ix[t], sq, si);
 	if(threadIdx.x == 0) {
 		// row j (dnj.c:619-663) and p over the lowered column entries
-		b.Q[j] = q[0];
-		b.P[j] = ix[0];
+		st_wt(&b.Q[j], q[0]);
+		st_wt(&b.P[j], ix[0]);
 		int p = j;
 		if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
 		int p2 = 0;
 		if(move) {
 			b.sD[i] = sDm;
 			b.N[i] = Nm;
-			b.Q[i] = q[2];
-			b.P[i] = ix[2];
+			st_wt(&b.Q[i], q[2]);
+			st_wt(&b.P[i], ix[2]);
 			p2 = i;
 			if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
 		}
@@ -1153,10 +1172,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		int cand;
 		if(p2 == nn) cand = p;
 		else if(p == nn) cand = p2;
-		else cand = (b.Q[p2] < b.Q[p] || (p < p2 && b.Q[p2] == b.Q[p])) ? p2 : p;
+		else {
+			double Qp = ld_wt(&b.Q[p]), Qp2 = ld_wt(&b.Q[p2]);
+			cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
+		}
 		s_cand = cand;
 	}
-	__threadfence_block();
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	__syncthreads();
 	if(nn > 2) prepare_selection(b, nn, s_cand);
 }
@@ -1195,7 +1217,7 @@ struct TreeWork {
 	void *mem;
 };
 
-static int tree_alloc(TreeWork *w, int n) {
+static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
 	const size_t maxunits = (size_t) DNJ_B * (cdiv(n, SEG) + 1);
 	const size_t nslices = (size_t) cdiv(n, RPB) + 1;
@@ -1217,7 +1239,7 @@ static int tree_alloc(TreeWork *w, int n) {
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
-	CCG_CHECK(hipMemset(m, 0, sz));
+	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
 	w->mem = m;
 	TreeBufs &b = w->b;
 	b.sD = (double *) (m + o_sD);
@@ -1245,31 +1267,84 @@ static int tree_alloc(TreeWork *w, int n) {
 	return CCG_OK;
 }
 
+// Per-kernel HIP-event timing (profile mode): one event after every launch,
+// harvested in batches.
+struct KTimer {
+	bool on;
+	hipStream_t st;
+	hipEvent_t ev[1025];
+	int cls[1025];
+	int used;
+	long long cnt[CCG_NKSTAT], ns[CCG_NKSTAT];
+	void init(hipStream_t s, bool enable) {
+		on = enable;
+		st = s;
+		used = 0;
+		memset(cnt, 0, sizeof(cnt));
+		memset(ns, 0, sizeof(ns));
+		if(on) {
+			for(int k = 0; k < 1025; ++k) hipEventCreate(&ev[k]);
+			hipEventRecord(ev[0], st);
+			used = 1;
+		}
+	}
+	void harvest() {
+		hipEventSynchronize(ev[used - 1]);
+		for(int k = 1; k < used; ++k) {
+			float ms = 0;
+			hipEventElapsedTime(&ms, ev[k - 1], ev[k]);
+			cnt[cls[k]] += 1;
+			ns[cls[k]] += (long long) (ms * 1.0e6);
+		}
+		hipEvent_t t = ev[0];
+		ev[0] = ev[used - 1];
+		ev[used - 1] = t;
+		used = 1;
+	}
+	void mark(int c) {
+		if(!on) return;
+		cls[used] = c;
+		hipEventRecord(ev[used++], st);
+		if(used == 1025) harvest();
+	}
+	void finish() {
+		if(!on) return;
+		harvest();
+		for(int k = 0; k < 1025; ++k) hipEventDestroy(ev[k]);
+	}
+};
+
 // One join's kernels, for a matrix of (at most) n taxa.
 template <int ET>
 static void enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n,
-                              int method, bool general) {
+                              int method, bool general, KTimer &kt) {
 	if(method == CCG_TREE_DNJ) {
 		k_dnj_top<ET><<<TOP_BLOCKS, TB, 0, st>>>(D, bs, b);
+		kt.mark(CCG_K_TOP);
 		unsigned g2 = cdiv(n, RPB);
 		if(g2 > 2048) g2 = 2048;
 		k_dnj_rest<ET><<<g2, TB, 0, st>>>(D, bs, b);
+		kt.mark(CCG_K_REST);
 	} else {
 		long long cells = tri(n);
 		unsigned g = cdiv(cells, 8 * TB);
 		if(g > 2048) g = 2048;
 		if(g < 1) g = 1;
 		k_nj_argmin<ET><<<g, TB, 0, st>>>(D, bs, b);
+		kt.mark(CCG_K_ARGMIN);
 	}
 	if(general) {
 		k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b);
 	} else {
 		k_update<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
 	}
+	kt.mark(CCG_K_UPDATE);
 	if(method == CCG_TREE_DNJ) {
 		k_dnj_requeue<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
+		kt.mark(CCG_K_REQUEUE);
 	} else {
 		k_nj_pop<ET><<<cdiv(n, TB), TB, 0, st>>>(D, b);
+		kt.mark(CCG_K_POP);
 	}
 }
 
@@ -1282,7 +1357,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	const double bs = a->byteScale;
 	hipStream_t st = ctx->stream;
 	TreeWork w;
-	int rc = tree_alloc(&w, n0);
+	int rc = tree_alloc(&w, n0, st);
 	if(rc) return rc;
 	TreeBufs b = w.b;
 	TreeCtl init;
@@ -1293,7 +1368,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	init.method = a->method;
 	CCG_CHECK(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	long long launches = 0;
+	static KTimer kt;
 	CCG_CHECK(hipEventRecord(ctx->ev0, st));
+	kt.init(st, a->profile != 0);
 	k_init_sums<ET><<<cdiv(n0, TB), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
 	++launches;
 	if(a->method == CCG_TREE_DNJ) {
@@ -1301,6 +1378,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		k_dnj_prep<<<1, TB, 0, st>>>(b);
 		launches += 2;
 	}
+	kt.mark(CCG_K_INIT);
 	CCG_CHECK(hipGetLastError());
 	TreeCtl h;
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -1309,7 +1387,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	int n = n0;
 	int since_check = 0;
 	while(n != 2) {
-		enqueue_iteration<ET>(st, D, bs, b, n, a->method, general);
+		enqueue_iteration<ET>(st, D, bs, b, n, a->method, general, kt);
 		launches += a->method == CCG_TREE_DNJ ? 4 : 3;
 		CCG_CHECK(hipGetLastError());
 		--n;
@@ -1321,6 +1399,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		}
 	}
 	CCG_CHECK(hipEventRecord(ctx->ev1, st));
+	kt.finish();
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 	CCG_CHECK(hipStreamSynchronize(st));
 	float ms = 0;
@@ -1328,12 +1407,13 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	*njoins = h.njoins;
 	*final_n = h.done ? h.final_n : h.n;
 	if(h.njoins) {
-		CCG_CHECK(hipMemcpy(joins, b.joins, (size_t) h.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost));
+		CCG_CHECK(hipMemcpyAsync(joins, b.joins, (size_t) h.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
 	}
 	*final_d = -1.0;
 	if(*final_n == 2) {
 		T v;
-		CCG_CHECK(hipMemcpy(&v, D, sizeof(T), hipMemcpyDeviceToHost));
+		CCG_CHECK(hipMemcpyAsync(&v, D, sizeof(T), hipMemcpyDeviceToHost, st));
+		CCG_CHECK(hipStreamSynchronize(st));
 		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
 	}
 	if(stats) {
@@ -1341,7 +1421,16 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		stats[1] = h.cells;
 		stats[2] = launches;
 		stats[3] = (int64_t) (ms * 1000.0);
+		if(a->profile) {
+			for(int c = 0; c < CCG_NKSTAT; ++c) {
+				stats[4 + 2 * c] = kt.cnt[c];
+				stats[5 + 2 * c] = kt.ns[c];
+			}
+			stats[4 + 2 * CCG_NKSTAT] = h.cells_top;
+			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest;
+		}
 	}
+	CCG_CHECK(hipStreamSynchronize(st));
 	CCG_CHECK(hipFree(w.mem));
 	return CCG_OK;
 }

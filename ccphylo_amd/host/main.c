@@ -231,10 +231,10 @@ static int main_tree(int argc, char **argv) {
 				jcap = n;
 				joins = realloc(joins, jcap * sizeof(ccg_join));
 			}
-			ccg_tree_args ta = {n, et, bs, m, flag, !fast};
+			ccg_tree_args ta = {n, et, bs, m, flag, !fast, 0};
 			int nj = 0, fn = 0;
 			double fd = 0;
-			int64_t st[4];
+			int64_t st[6 + 2 * CCG_NKSTAT];
 			int rc = ccg_tree(ctx, &ta, D->mat, joins, &nj, &fn, &fd, st);
 			if(rc) {
 				fprintf(stderr, "ccphylo_amd: tree construction failed: %s\n", ccg_strerror(rc));

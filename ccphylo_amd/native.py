@@ -26,6 +26,8 @@ ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
 
 CCG_TREE_NJ = 0
 CCG_TREE_DNJ = 1
+NKSTAT = 7
+KSTAT_NAMES = ["init", "dnj_top", "dnj_rest", "nj_argmin", "update", "dnj_requeue", "nj_pop"]
 
 
 class CcgError(RuntimeError):
@@ -45,7 +47,7 @@ class SnpArgs(C.Structure):
 class TreeArgs(C.Structure):
     _fields_ = [
         ("n", C.c_int), ("etype", C.c_int), ("byteScale", C.c_double),
-        ("method", C.c_int), ("flags", C.c_int), ("exact", C.c_int),
+        ("method", C.c_int), ("flags", C.c_int), ("exact", C.c_int), ("profile", C.c_int),
     ]
 
 
@@ -210,20 +212,55 @@ class Device:
         self._check(rc, "ccg_snp_ltd")
         return D[:m], (N[:m] if N is not None else None), inc.value
 
-    def tree(self, D, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True):
-        """NJ/DNJ on a packed LT (ccg_tree).  Returns (joins, final_n, final_d, stats)."""
+    def tree(self, D, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False):
+        """NJ/DNJ on a packed host LT (ccg_tree).  Returns (joins, final_n, final_d, stats)."""
         D = np.ascontiguousarray(D, dtype=ETYPES[etype])
         assert D.size == n * (n - 1) // 2
+        return self._tree(self.lib.ccg_tree, D.ctypes.data, n, etype, byte_scale, method, flags, exact, profile)
+
+    def tree_dev(self, dptr, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False):
+        """Same on a device LT (ccg_tree_dev); the buffer is consumed."""
+        return self._tree(self.lib.ccg_tree_dev, dptr, n, etype, byte_scale, method, flags, exact, profile)
+
+    def _tree(self, fn_, dptr, n, etype, byte_scale, method, flags, exact, profile):
         joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * 4)()
-        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact))
-        rc = self.lib.ccg_tree(self.h, C.byref(a), D.ctypes.data, joins.ctypes.data, C.byref(nj), C.byref(fn),
-                               C.byref(fd), st)
+        st = (C.c_int64 * (6 + 2 * NKSTAT))()
+        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile))
+        rc = fn_(self.h, C.byref(a), C.c_void_p(dptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd), st)
         self._check(rc, "ccg_tree")
         return joins[:nj.value], fn.value, fd.value, list(st)
+
+    # ---- device memory (ccg_malloc & co.) for HBM-resident inputs
+    def malloc(self, nbytes):
+        p = C.c_void_p()
+        self._check(self.lib.ccg_malloc(self.h, C.byref(p), nbytes), "ccg_malloc")
+        return p.value
+
+    def free(self, p):
+        self._check(self.lib.ccg_free(self.h, C.c_void_p(p)), "ccg_free")
+
+    def h2d(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        self._check(self.lib.ccg_memcpy_h2d(self.h, C.c_void_p(dst), arr.ctypes.data, arr.nbytes), "h2d")
+
+    def d2h(self, arr, src):
+        self._check(self.lib.ccg_memcpy_d2h(self.h, arr.ctypes.data, C.c_void_p(src), arr.nbytes), "d2h")
+
+    def sync(self):
+        self._check(self.lib.ccg_synchronize(self.h), "ccg_synchronize")
+
+    def snp_ltd_dev(self, seqs_ptr, incs_ptr, n, length, stride, D_ptr, N_ptr=None, pair=False, norm=0,
+                    min_length=1, etype=8, byte_scale=1.0, row_range=(0, 0)):
+        """ccg_snp_ltd_dev on device pointers.  Returns getNpos(mask) (non-pair)."""
+        a = SnpArgs(n, length, stride, seqs_ptr, incs_ptr, int(pair), norm, min_length, 0, etype, byte_scale,
+                    row_range[0], row_range[1])
+        inc = C.c_int(0)
+        self._check(self.lib.ccg_snp_ltd_dev(self.h, C.byref(a), C.c_void_p(D_ptr),
+                                             C.c_void_p(N_ptr) if N_ptr else None, C.byref(inc)), "ccg_snp_ltd_dev")
+        return inc.value
 
 
 # ---------------------------------------------------------------- host API
@@ -324,3 +361,22 @@ def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0):
     res = (heads, seqs, incs, M.len, M.minLength)
     lib.ccq_msa_free(Mp)
     return res
+
+
+def write_phylip(path, D, n, names, flag=1, precision=9, etype=8, byte_scale=1.0):
+    """Writes a packed LT with the host writer (ccq_print_phy, ref phy.c:59)."""
+    lib = host_lib()
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    lib.ccq_print_phy.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_char_p), C.c_void_p, C.c_char_p,
+                                  C.c_uint, C.c_int]
+    D = np.ascontiguousarray(D, dtype=ETYPES[etype])
+    ltd = _Ltd(n, n, etype, byte_scale, D.ctypes.data if D.size else None)
+    arr = (C.c_char_p * max(n, 1))(*[s.encode() for s in names])
+    fp = libc.fopen(path.encode(), b"wb")
+    if not fp:
+        raise OSError(path)
+    lib.ccq_print_phy(fp, C.byref(ltd), arr, None, None, flag, precision)
+    libc.fclose(fp)

@@ -92,7 +92,23 @@ typedef struct {
 	                          reference order (bit-identical to the reference);
 	                          0: fixed-order parallel tree sum (deterministic,
 	                          may differ from the reference in the last ulp) */
+	int profile;           /* 1: time every kernel with HIP events on the engine
+	                          stream; per-kernel totals go to stats[4..] */
 } ccg_tree_args;
+
+/* stats layout (ccg_tree / ccg_tree_dev, 6 + 2*CCG_NKSTAT entries when
+ * profile = 1, else 4): [0] rows rescanned, [1] cells rescanned, [2] kernel
+ * launches, [3] device time (us); then for kernel class c: [4+2c] launches,
+ * [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT] cells rescanned by
+ * CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST.  Classes: */
+#define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
+#define CCG_K_TOP      1   /* DNJ: rescans of the top candidate rows */
+#define CCG_K_REST     2   /* DNJ: bounded rescans + replay of minQpair */
+#define CCG_K_ARGMIN   3   /* NJ: full Q argmin (initQ) */
+#define CCG_K_UPDATE   4   /* updateD */
+#define CCG_K_REQUEUE  5   /* DNJ: updateDNJ Q/P + DNJ_popArrange */
+#define CCG_K_POP      6   /* NJ: ltdMatrix_popArrange */
+#define CCG_NKSTAT     7
 
 /* D: host LT (n(n-1)/2 elements), left unmodified.  joins: room for n-2.
  * On return *njoins joins were made; *final_n is the matrix size at exit
