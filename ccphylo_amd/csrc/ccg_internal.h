@@ -76,8 +76,99 @@ __device__ __forceinline__ double qcrit(int Ni, int Nj, double d, double sDi, do
 }
 
 // ------------------------------------------------------------ reductions
+// ------------------------------------------------------------ DPP wave ops
+// Wave64 scans/reductions with DPP row shifts and row broadcasts (GFX9
+// family): a few cycles per step instead of an LDS-crossbar ds_bpermute per
+// __shfl.  Steps: row_shr 1,2,4,8 (inclusive within each 16-lane row), then
+// row_bcast:15 into rows 1,3 and row_bcast:31 into rows 2,3; lanes without a
+// source keep `old` (the identity).  Lane 63 ends with the whole wave.
+#define DPP_ROW_SHR1 0x111
+#define DPP_ROW_SHR2 0x112
+#define DPP_ROW_SHR4 0x114
+#define DPP_ROW_SHR8 0x118
+#define DPP_WAVE_SHR1 0x138
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int old, int src) {
+	return __builtin_amdgcn_update_dpp(old, src, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_d(double old, double src) {
+	const long long o = __double_as_longlong(old), v = __double_as_longlong(src);
+	const int lo = __builtin_amdgcn_update_dpp((int) o, (int) v, CTRL, RM, 0xF, false);
+	const int hi = __builtin_amdgcn_update_dpp((int) (o >> 32), (int) (v >> 32), CTRL, RM, 0xF, false);
+	return __longlong_as_double(((long long) hi << 32) | (unsigned) lo);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp_l(long long old, long long src) {
+	const int lo = __builtin_amdgcn_update_dpp((int) old, (int) src, CTRL, RM, 0xF, false);
+	const int hi = __builtin_amdgcn_update_dpp((int) (old >> 32), (int) (src >> 32), CTRL, RM, 0xF, false);
+	return ((long long) hi << 32) | (unsigned) lo;
+}
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+	const long long x = __double_as_longlong(v);
+	const int lo = __builtin_amdgcn_readlane((int) x, lane), hi = __builtin_amdgcn_readlane((int) (x >> 32), lane);
+	return __longlong_as_double(((long long) hi << 32) | (unsigned) lo);
+}
+__device__ __forceinline__ long long readlane_l(long long x, int lane) {
+	const int lo = __builtin_amdgcn_readlane((int) x, lane), hi = __builtin_amdgcn_readlane((int) (x >> 32), lane);
+	return ((long long) hi << 32) | (unsigned) lo;
+}
+
+#define CCG_DPP_STEPS(STEP)         \
+	STEP(DPP_ROW_SHR1, 0xF)         \
+	STEP(DPP_ROW_SHR2, 0xF)         \
+	STEP(DPP_ROW_SHR4, 0xF)         \
+	STEP(DPP_ROW_SHR8, 0xF)         \
+	STEP(DPP_ROW_BCAST15, 0xA)      \
+	STEP(DPP_ROW_BCAST31, 0xC)
+
+// inclusive prefix sum over the wave
+__device__ __forceinline__ int wave_incl_sum(int x) {
+#define S_(C, R) x += dpp_i<C, R>(0, x);
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return x;
+}
+__device__ __forceinline__ long long wave_incl_sum_l(long long x) {
+#define S_(C, R) x += dpp_l<C, R>(0, x);
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return x;
+}
+// inclusive prefix min over the wave
+__device__ __forceinline__ double wave_incl_min(double x) {
+#define S_(C, R)                               \
+	{                                          \
+		const double t_ = dpp_d<C, R>(DBL_MAX, x); \
+		x = t_ < x ? t_ : x;                   \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return x;
+}
+__device__ __forceinline__ int wave_incl_min_i(int x) {
+#define S_(C, R)                                 \
+	{                                            \
+		const int t_ = dpp_i<C, R>(INT32_MAX, x);  \
+		x = t_ < x ? t_ : x;                     \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return x;
+}
+// exclusive prefix min: lane l gets min(carry, x[0..l-1])
+__device__ __forceinline__ double wave_excl_min(double x, double carry) {
+	const double inc = wave_incl_min(x);
+	const double ex = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);
+	return ex < carry ? ex : carry;
+}
+
 // (q, idx) candidates: smaller q wins, equal q -> larger idx wins.  This is
-// the closed form of the reference's sequential `q <= min` last-wins scans.
+// the closed form of the reference's sequential `q <= min` last-wins scans;
+// being a total order, any association of the fold gives the same winner.
 struct QArg {
 	double q;
 	int idx;
@@ -87,16 +178,21 @@ __device__ __forceinline__ bool qarg_better(double q, int idx, double bq, int bi
 	return q < bq || (q == bq && idx > bidx);
 }
 
+// wave-wide (q, idx) reduce; the result in every lane
 __device__ __forceinline__ void qarg_wave_reduce(double &q, int &idx) {
-#pragma unroll
-	for(int off = 32; off > 0; off >>= 1) {
-		double oq = __shfl_xor(q, off, 64);
-		int oi = __shfl_xor(idx, off, 64);
-		if(qarg_better(oq, oi, q, idx)) {
-			q = oq;
-			idx = oi;
-		}
+#define S_(C, R)                                          \
+	{                                                     \
+		const double oq_ = dpp_d<C, R>(DBL_MAX, q);       \
+		const int oi_ = dpp_i<C, R>(INT32_MIN, idx);      \
+		if(qarg_better(oq_, oi_, q, idx)) {               \
+			q = oq_;                                      \
+			idx = oi_;                                    \
+		}                                                 \
 	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	q = readlane_d(q, 63);
+	idx = __builtin_amdgcn_readlane(idx, 63);
 }
 
 // block-wide (q, idx) reduce; result valid in every thread.  `sq`/`si` are

@@ -9,39 +9,59 @@
 //
 // Layout in HBM: D is the reference's contiguous LT buffer (row r starts at
 // r(r-1)/2, element type ET), plus n-vectors sD (f64), N (i32), Q (f64),
-// P (i32).  All loop state (n, the current join, the DNJ selection) lives in
-// a device TreeCtl, so every per-iteration kernel takes the same arguments;
-// each one finishes with a "last block" (agent-scope ticket) that folds the
-// per-block partials in a fixed order and prepares the next kernel's input.
+// P (i32).  The matrix size n of a join is a launch argument; the join and
+// the DNJ selection live in a device TreeCtl.
 //
-// DNJ selection (minQpair) is a serial scan in the reference: row i is
-// rescanned iff its stale bound Q[i] is below the running minimum m(i) of
-// the rows above it.  Here, per join:
-//   k_dnj_top   rescans the top-B candidate rows S (Q[r] < m0) in 2048-cell
-//               units spread over the whole GPU; its last block derives
-//               U = min(m0, min_{k in S} max(fresh_k, Q_k)), an upper bound of
-//               m(i) for every row below S (a row k above i that the serial
-//               scan rescans gives m(i) <= fresh_k, one it skips gives
-//               m(i) <= m(k) <= Q_k);
-//   k_dnj_rest  rescans every row below S with Q[r] < U (any other row is
-//               provably skipped by the reference); its last block replays
-//               the reference's accept/reject decisions over S then C1 in
-//               descending row order.  When every fresh min is >= its stale
-//               bound the running minimum is exactly the prefix minimum of the
-//               fresh values, so the replay is a parallel scan; otherwise it
-//               runs serially.  Either way Q/P and the pair are minQpair's.
+// Pipeline without in-kernel grid synchronisation.  A dependent global round
+// trip costs ~1 us on MI355X (coherent traffic crosses XCDs), so no kernel
+// ends in a "last block" ticket: every kernel writes per-block partials, and
+// the NEXT kernel folds them redundantly in each of its blocks (identical,
+// fixed-order, hence deterministic), substituting locally the few values its
+// block 0 persists for the kernels after it.  Per DNJ join:
+//   k_dnj_select  folds the previous requeue (updateDNJ + DNJ_popArrange +
+//                 minPos), picks the top-B candidate rows S (Q[r] < m0,
+//                 scanning down from n-1) and rescans them in 16384-cell
+//                 units; each unit atomically lowers the key of
+//                 U = min(m0, min_k max(fresh_k, Q_k)), an upper bound of the
+//                 serial running min m(i) for every row below S (a row k that
+//                 the serial scan rescans gives m(i) <= fresh_k, one it skips
+//                 gives m(i) <= m(k) <= Q_k; max distributes over the units'
+//                 min, so one atomicMin per unit suffices);
+//   k_dnj_rest    rescans every row below S with Q[r] < U (any other row is
+//                 provably skipped by minQpair); one extra block folds the
+//                 units of S;
+//   k_dnj_join    replays minQpair's accept/reject decisions over S then the
+//                 rest in descending row order (a parallel prefix-min when
+//                 every fresh min is >= its stale bound, serial otherwise),
+//                 records the join and runs updateD;
+//   k_dnj_requeue folds the new row sum of j and runs updateDNJ's Q/P part
+//                 plus DNJ_popArrange.
+// NJ: k_nj_argmin (initQ over all cells), k_nj_join (fold + updateD),
+// k_nj_pop (row sum + ltdMatrix_popArrange).
 #include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include "ccg_internal.h"
 
-#define TB 256           // threads per block of the vector kernels
+#define TB 256           // threads per block
 #define DNJ_B 128        // |S|: top candidate rows rescanned speculatively
-#define SEG 2048         // cells per rescan unit (8 per thread)
-#define RPB 16           // rows per block slice in k_dnj_rest
-#define TOP_BLOCKS 1024  // grid of k_dnj_top
-#define REPLAY_CAP 2048  // entries replayed from LDS at once
+#define SEG 2048         // cells per rescan unit (TB threads x 8)
+#define SEL_BLOCKS 1024  // max grid of k_dnj_select
+#define SCAN_BLOCKS 1024 // max grid of k_dnj_scan
+#define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
+#define TBF 1024         // threads of k_dnj_find (one block)
+#define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
+#define REPLAY_CAP 2048  // rest entries staged in LDS
+#define CNT_CHUNK 2048   // slice counts staged in LDS at once
+#define NJ_BLOCKS 2048   // max grid of k_nj_argmin
+
+// one candidate row of minQpair: fresh (q, j) and its stale bound Q[row]
+struct Entry {
+	double f, bnd;
+	int row, j;
+};
 
 struct TreeCtl {
-	int n;               // current matrix size
 	int done;            // the reference loop stopped (pos == 0)
 	int final_n;
 	int njoins;
@@ -49,25 +69,28 @@ struct TreeCtl {
 	double Li, Lj, Dij;
 	int cand;            // minQpair's candidate row
 	int pos_i, pos_j;    // minQpair's initial pos
+	int nS, smin;        // |S| and its lowest row (1 when |S| < DNJ_B)
+	int T;               // rows found below S
 	double m0;           // minQpair's initial min
-	double U;            // bound for rows below S
-	int nS, nunits, smin;
-	int mi, mj;
-	int neg, exact, method;
+	unsigned tick;       // k_dnj_select's last-block ticket
+	int neg, exact, method, has_missing;
 	int serial_sums, serial_replays;
-	unsigned tick[4];    // last-block tickets (reset by their last block)
-	long long rows, cells;
-	long long cells_top, cells_rest;
-	int has_missing;
+	long long rows, cells, cells_top, cells_rest;
 };
 
 struct TreeBufs {
-	double *sD, *Q, *fq, *contrib;
-	int *N, *P, *fj;
+	double *sD, *Q, *contrib;
+	int *N, *P;
 	int *S, *uoff;       // DNJ_B rows, DNJ_B+1 unit offsets
-	double *uq;          // per-unit partial (q, j)
+	double *Sb;          // Q[S[t]] at selection time
+	double *uq;          // per-unit (q, j) of the S rescans, by unit (uoff[t]..uoff[t+1])
 	int *uj;
-	int *blk_rows, *blk_cnt;
+	Entry *Sent;         // folded S rows
+	int *crow;           // rows found below S with Q < U, descending (k_dnj_select)
+	double *cbnd;        // their bounds Q[row]
+	int *coff;           // and SEG-cell unit offsets (REPLAY_CAP + 1)
+	double *cq;          // per-unit (q, j) of the rest rescans, by unit (coff[e]..coff[e+1])
+	int *cj;
 	double *wsum, *wabs; // per-block partial sums / sum |c|
 	int *wcnt, *wexp;    // per-block count / min exponent of the contributions
 	double *qpart;       // 4 (q, idx) partials per block
@@ -75,32 +98,60 @@ struct TreeBufs {
 	long long *fpart;
 	ccg_join *joins;
 	TreeCtl *ctl;
+	int maxu;
 };
 
-// ------------------------------------------------------------------ helpers
-__device__ __forceinline__ double lds_min_reduce(double v, double *s) {
-	for(int off = 32; off > 0; off >>= 1) {
-		double o = __shfl_xor(v, off, 64);
-		v = o < v ? o : v;
-	}
-	__syncthreads();
-	if((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-	__syncthreads();
-	v = s[0];
-	for(int w = 1; w < (int) (blockDim.x >> 6); ++w) v = s[w] < v ? s[w] : v;
-	__syncthreads();
-	return v;
+
+// ---- diagnostic build only (make trace): s_memrealtime stamps (100 MHz) of
+// block 0's entry and phases and of the last block exit, for the joins at
+// n in (g_trace_hi - 256, g_trace_hi]; dumped to stderr by tree_run_t.
+#ifdef CCG_TRACE
+#define NKT 5
+__device__ unsigned long long g_trace[256 * NKT * 16];
+__device__ int g_trace_hi;
+__device__ __forceinline__ unsigned long long rt_stamp() {
+	unsigned long long t;
+	__builtin_amdgcn_sched_barrier(0);
+	asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+	__builtin_amdgcn_sched_barrier(0);
+	return t;
 }
+#define TS(kern, ph)                                                                  \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
+#define TS_ENTRY(kern)                                                                \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + 15] = ~rt_stamp(); \
+		}                                                                             \
+	} while(0)
+#define TS_EXIT(kern)                                                                 \
+	do {                                                                              \
+		if(threadIdx.x == 0) {                                                        \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) atomicMax(&g_trace[(s_ * NKT + (kern)) * 16 + 14], rt_stamp()); \
+		}                                                                             \
+	} while(0)
+#else
+#define TS_EXIT(kern)
+#define TS(kern, ph)
+#define TS_ENTRY(kern)
+#endif
+
+// ------------------------------------------------------------------ helpers
+__host__ __device__ static inline unsigned cdiv(long long a, long long b) { return (unsigned) ((a + b - 1) / b); }
+__device__ __forceinline__ int dcdiv(int a, int b) { return (a + b - 1) / b; }
 
 // block-wide exclusive prefix sum of a per-thread int; *total receives the sum
+// (two barriers; `s` holds blockDim/64 ints)
 __device__ __forceinline__ int block_excl_scan(int v, int *s, int *total) {
 	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	int x = v;
-	for(int off = 1; off < 64; off <<= 1) {
-		int y = __shfl_up(x, off, 64);
-		if(lane >= off) x += y;
-	}
-	__syncthreads();
+	const int x = wave_incl_sum(v);
 	if(lane == 63) s[wid] = x;
 	__syncthreads();
 	int pre = 0, tot = 0;
@@ -113,12 +164,37 @@ __device__ __forceinline__ int block_excl_scan(int v, int *s, int *total) {
 	return pre + x - v;
 }
 
+// ---- wave-level building blocks (no block barriers)
+// orders the wave's own LDS accesses (they complete in issue order per wave)
+__device__ __forceinline__ void wave_sync() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int *total) {
+	const int inc = wave_incl_sum(v);
+	*total = __builtin_amdgcn_readlane(inc, 63);
+	return inc - v;
+}
+
+// fixed-order wave sum (DPP scan order); the same value in every lane
+__device__ __forceinline__ double wave_sum_fixed(double x) {
+#define S_(C, R) x += dpp_d<C, R>(0.0, x);
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return readlane_d(x, 63);
+}
+
+__device__ __forceinline__ int wave_sum_int(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
+__device__ __forceinline__ long long wave_sum_int(long long v) { return readlane_l(wave_incl_sum_l(v), 63); }
+__device__ __forceinline__ int wave_min_int(int v) { return __builtin_amdgcn_readlane(wave_incl_min_i(v), 63); }
+
 // nj.c:42 limbLength / nj.c:81 limbLengthNeg
-__device__ void limb_length(double *Li, double *Lj, int i, int j, const double *sD, const int *N, double Dij,
-                            int neg) {
-	int Ni = N[i] - 2, Nj = N[j] - 2;
+__device__ void limb_length(double *Li, double *Lj, double sDi, double sDj, int Ni_, int Nj_, double Dij, int neg) {
+	int Ni = Ni_ - 2, Nj = Nj_ - 2;
 	if(0 < Ni && 0 < Nj) {
-		double delta = ((sD[i] - Dij) / Ni) - ((sD[j] - Dij) / Nj);
+		double delta = ((sDi - Dij) / Ni) - ((sDj - Dij) / Nj);
 		*Li = (Dij + delta) / 2;
 		*Lj = (Dij - delta) / 2;
 		if(!neg) {
@@ -141,53 +217,41 @@ __device__ void limb_length(double *Li, double *Lj, int i, int j, const double *
 	}
 }
 
-template <int ET>
-__device__ void record_join(const typename Elem<ET>::T *D, double bs, const TreeBufs &b, int i, int j) {
-	TreeCtl *ctl = b.ctl;
-	double Dij = Elem<ET>::get(D[tri(i) + j], bs), Li, Lj;
-	limb_length(&Li, &Lj, i, j, b.sD, b.N, Dij, ctl->neg);
-	ctl->i = i;
-	ctl->j = j;
-	ctl->Li = Li;
-	ctl->Lj = Lj;
-	ctl->Dij = Dij;
-	ccg_join J;
-	J.i = i;
-	J.j = j;
-	J.Li = Li;
-	J.Lj = Lj;
-	b.joins[ctl->njoins++] = J;
-}
-
-// (q, j) min of LT row r over columns [c0, c1), whole block, 8 loads in flight
-// per thread (dnj.c:99-112 with the `<=` last-wins rule)
-template <int ET, int UNR = 8>
+// (q, j) min of LT row r over columns [c0, c1), whole block of NT threads,
+// UNR cells in flight per thread (dnj.c:99-112, `<=` last-wins rule).  Column
+// isub (the row moved by the previous join, not yet persisted) reads (Nm, sDm).
+// Without missing entries (GEN = false) every N[k] equals the matrix size n
+// (initSummaD counts n - 1 entries + 1; updateD and the pop keep that), so
+// the N gathers are skipped and Nr = Nm = n is passed in.
+template <int ET, bool GEN, int NT, int UNR>
 __device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__restrict__ D, double bs,
                                                 const double *__restrict__ sD, const int *__restrict__ N, int r,
-                                                int c0, int c1, double &q, int &idx) {
+                                                int c0, int c1, int Nr, double sDr, int isub, int Nm, double sDm,
+                                                double &q, int &idx) {
 	const typename Elem<ET>::T *row = D + tri(r);
-	const int Nr = N[r];
-	const double sDr = sD[r];
-	for(int base = c0; base < c1; base += UNR * TB) {
+	for(int base = c0; base < c1; base += UNR * NT) {
 		typename Elem<ET>::T v[UNR];
 		int nk[UNR];
 		double sk[UNR];
 #pragma unroll
 		for(int m = 0; m < UNR; ++m) {
-			int c = base + m * TB + (int) threadIdx.x;
-			if(c < c1) {
-				v[m] = row[c];
-				nk[m] = N[c];
-				sk[m] = sD[c];
-			}
+			// clamped (always valid) addresses: no branches between the loads,
+			// so all of them are in flight before the first wait
+			int c = base + m * NT + (int) threadIdx.x;
+			c = c < c1 ? c : c1 - 1;
+			v[m] = row[c];
+			nk[m] = GEN ? N[c] : Nr;
+			sk[m] = sD[c];
 		}
 #pragma unroll
 		for(int m = 0; m < UNR; ++m) {
-			int c = base + m * TB + (int) threadIdx.x;
+			int c = base + m * NT + (int) threadIdx.x;
 			if(c < c1) {
 				double d = Elem<ET>::get(v[m], bs);
+				int Nc = c == isub ? Nm : nk[m];
+				double sc = c == isub ? sDm : sk[m];
 				if(0 <= d) {
-					double x = qcrit(Nr, nk[m], d, sDr, sk[m]);
+					double x = qcrit(Nr, Nc, d, sDr, sc);
 					if(qarg_better(x, c, q, idx)) {
 						q = x;
 						idx = c;
@@ -198,25 +262,94 @@ __device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__re
 	}
 }
 
+// fold of the (q, j) unit partials [ua, ub), 4 branch-free loads in flight
+__device__ __forceinline__ void fold_units(const double *__restrict__ uq, const int *__restrict__ uj, int ua, int ub,
+                                           double &q, int &idx) {
+	for(int u = ua; u < ub; u += 4) {
+		double oq[4];
+		int oi[4];
+#pragma unroll
+		for(int m = 0; m < 4; ++m) {
+			const int v = u + m < ub ? u + m : ub - 1;
+			oq[m] = uq[v];
+			oi[m] = uj[v];
+		}
+#pragma unroll
+		for(int m = 0; m < 4; ++m) {
+			if(u + m < ub && qarg_better(oq[m], oi[m], q, idx)) {
+				q = oq[m];
+				idx = oi[m];
+			}
+		}
+	}
+}
+
+// block (q, idx) reduce with one barrier; the result is valid in thread 0.
+// The caller separates two uses with a barrier.
+__device__ __forceinline__ void qarg_block_reduce1(double &q, int &idx, double *sq, int *si) {
+	qarg_wave_reduce(q, idx);
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if(lane == 0) {
+		sq[wid] = q;
+		si[wid] = idx;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int w = 1; w < nw; ++w) {
+			if(qarg_better(sq[w], si[w], q, idx)) {
+				q = sq[w];
+				idx = si[w];
+			}
+		}
+	}
+}
+
 // ------------------------------------------------------------------ init
+// nj.c:111 initSummaD: per row, the row part (m < k) then the column part
+// (m > k), each in increasing m, summed serially.  k_init_rows: one wave per
+// row stages 64 contiguous cells at a time and lane 0 accumulates them in
+// order; k_init_cols: one thread per row continues over the column part,
+// coalesced across the wave (threads k..k+63 read row m at columns k..k+63).
 template <int ET>
-__global__ void k_init_sums(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                            double *__restrict__ sD, int *__restrict__ N, TreeCtl *ctl) {
-	int k = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(TB) void k_init_rows(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
+                                                  double *__restrict__ sD, int *__restrict__ N, TreeCtl *ctl) {
+	__shared__ double buf[TB / 64][64];
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int k = blockIdx.x * (TB / 64) + wid;
 	if(k >= n) return;
 	double s = 0;
 	int c = 1, miss = 0;
 	const typename Elem<ET>::T *row = D + tri(k);
-	for(int m = 0; m < k; ++m) {        // row part: m < k, increasing m
-		double d = Elem<ET>::get(row[m], bs);
-		if(0 <= d) {
-			s += d;
-			++c;
-		} else {
-			miss = 1;
+	for(int m0 = 0; m0 < k; m0 += 64) {
+		int m = m0 + lane;
+		double d = m < k ? Elem<ET>::get(row[m], bs) : 0.0;
+		bool ok = m < k && 0 <= d;
+		miss |= m < k && !ok;
+		c += __popcll(__ballot(ok));
+		buf[wid][lane] = ok ? d : 0.0;
+		__builtin_amdgcn_wave_barrier();
+		if(lane == 0) {
+			int lim = k - m0 < 64 ? k - m0 : 64;
+			for(int u = 0; u < lim; ++u) s += buf[wid][u];
 		}
+		__builtin_amdgcn_wave_barrier();
 	}
-	for(int m = k + 1; m < n; ++m) {    // column part: m > k, increasing m
+	miss = __any(miss);
+	if(lane == 0) {
+		sD[k] = s;
+		N[k] = c;
+		if(miss) atomicOr(&ctl->has_missing, 1);
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(TB) void k_init_cols(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
+                                                  double *__restrict__ sD, int *__restrict__ N, TreeCtl *ctl) {
+	const int k = blockIdx.x * TB + threadIdx.x;
+	if(k >= n) return;
+	double s = sD[k];
+	int c = N[k], miss = 0;
+	for(int m = k + 1; m < n; ++m) {
 		double d = Elem<ET>::get(D[tri(m) + k], bs);
 		if(0 <= d) {
 			s += d;
@@ -270,64 +403,10 @@ __global__ void k_init_hnj(const typename Elem<ET>::T *__restrict__ D, int n, do
 	}
 }
 
-// ------------------------------------------------------------------ DNJ selection setup
-// Computes minQpair's starting point and the top-B candidate set S for the
-// current n; run by ONE block (the last block of k_dnj_requeue, or k_dnj_prep).
-__device__ void prepare_selection(const TreeBufs &b, int n, int cand) {
-	__shared__ int s_scan[TB / 64];
-	__shared__ int s_cnt;
-	TreeCtl *ctl = b.ctl;
-	double m0 = DBL_MAX;
-	if(cand && m0 != ld_wt(&b.Q[cand])) m0 = ld_wt(&b.Q[cand]);
-	if(threadIdx.x == 0) {
-		ctl->cand = cand;
-		ctl->m0 = m0;
-		ctl->pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
-		ctl->pos_j = (cand && m0 != DBL_MAX) ? ld_wt(&b.P[cand]) : 0;
-		s_cnt = 0;
-	}
-	__syncthreads();
-	// rows n-1, n-2, ... with Q[r] < m0, 4 rows per thread per step
-	for(int base = n - 1; base >= 1; base -= 4 * (int) blockDim.x) {
-		int cnt = s_cnt;
-		if(cnt >= DNJ_B) break;
-		int rows[4], k = 0;
-#pragma unroll
-		for(int m = 0; m < 4; ++m) {
-			int r = base - 4 * (int) threadIdx.x - m;
-			if(r >= 1 && ld_wt(&b.Q[r]) < m0) rows[k++] = r;
-		}
-		int tot;
-		int off = block_excl_scan(k, s_scan, &tot);
-		for(int m = 0; m < k; ++m) {
-			if(cnt + off + m < DNJ_B) b.S[cnt + off + m] = rows[m];
-		}
-		__syncthreads();
-		if(threadIdx.x == 0) s_cnt = cnt + tot;
-		__syncthreads();
-	}
-	__threadfence_block();
-	__syncthreads();
-	int nS = s_cnt < DNJ_B ? s_cnt : DNJ_B;
-	// rescan units per row of S
-	int t = threadIdx.x;
-	int u = 0;
-	if(t < nS) u = (b.S[t] + SEG - 1) / SEG;
-	int tot;
-	int off = block_excl_scan(u, s_scan, &tot);
-	if(t < nS) b.uoff[t] = off;
-	if(t == 0) {
-		b.uoff[nS] = tot;
-		ctl->nS = nS;
-		ctl->nunits = tot;
-	}
-}
-
-// hclust.c:353 minQ -> the first candidate (dnj.c:997-998), then selection setup
-__global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b) {
+// hclust.c:353 minQ -> the first candidate row (dnj.c:997-998)
+__global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
-	const int n = b.ctl->n;
 	double q = DBL_MAX;
 	int idx = 0;
 	for(int i = 1 + threadIdx.x; i < n; i += blockDim.x) {
@@ -337,424 +416,412 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b) {
 		}
 	}
 	qarg_block_reduce(q, idx, sq, si);
-	prepare_selection(b, n, idx);
+	if(threadIdx.x == 0) b.ctl->cand = idx;
 }
 
-// ------------------------------------------------------------------ DNJ rescans
-template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_top(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+// ------------------------------------------------------------------ DNJ select
+// Prologue, wave 0 only (no block barriers): the previous join's
+// updateDNJ/DNJ_popArrange fold (dnj.c:619-709, :817-975), minPos
+// (dnj.c:1026-1032), minQpair's start (dnj.c:55-60) and the top-B rows S
+// (rows n-1, n-2, ... with Q[r] < m0).  Then the whole block rescans units.
+template <int ET, bool GEN>
+__global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                    int n, int first) {
 	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
+	__shared__ double sQS[DNJ_B];
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
+	__shared__ int s_nS, s_isub, s_Nm, s_done;
+	__shared__ double s_sDm;
 	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int nS = ctl->nS, nunits = ctl->nunits;
-	for(int t = threadIdx.x; t <= nS; t += blockDim.x) {
-		if(t < nS) sS[t] = b.S[t];
-		so[t] = b.uoff[t];
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	TS_ENTRY(0);
+	TS(0, 0);
+	if(wid == 0) {
+		// ---- loads that do not depend on the previous join's outcome
+		const int done = ctl->done;
+		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
+		const int cand0 = first ? ctl->cand : 0;
+		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
+		int ix[4] = {0, -1, 0, -1};
+		if(!first) {
+			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
+			for(int w = lane; w < G; w += 64) {
+#pragma unroll
+				for(int t = 0; t < 4; ++t) {
+					double oq = b.qpart[4 * w + t];
+					int oi = b.ipart[4 * w + t];
+					if(qarg_better(oq, oi, q[t], ix[t])) {
+						q[t] = oq;
+						ix[t] = oi;
+					}
+				}
+			}
+		}
+		double topQ[SEL_RPL];
+#pragma unroll
+		for(int m = 0; m < SEL_RPL; ++m) {
+			int r = n - 1 - (m * 64 + lane);   // coalesced; descending = (m, lane) order
+			topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+		}
+		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
+		const int Nm = first ? 0 : b.N[n];
+		if(done) {
+			if(lane == 0) s_done = 1;
+		} else {
+#pragma unroll
+			for(int t = 0; t < 4; ++t) qarg_wave_reduce(q[t], ix[t]);
+			const int nn = n;
+			const bool move = !first && i != nn;
+			const int isub = move ? i : -1, jsub = first ? -1 : j;
+			const double Qj = q[0], Qi = q[2];
+			const int Pj = ix[0], Pi = ix[2];
+#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : b.Q[(r)])
+#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : b.P[(r)])
+			int cand;
+			if(first) {
+				cand = cand0;
+			} else {
+				int p = j;
+				if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
+				int p2 = 0;
+				if(move) {
+					p2 = i;
+					if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
+				}
+				if(p2 == nn) {
+					cand = p;
+				} else if(p == nn) {
+					cand = p2;
+				} else {
+					double Qp = QSUB(p), Qp2 = QSUB(p2);
+					cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
+				}
+			}
+			const double Qc = cand ? QSUB(cand) : DBL_MAX;
+			double m0 = DBL_MAX;
+			if(cand && m0 != Qc) m0 = Qc;
+			const int pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
+			const int pos_j = (cand && m0 != DBL_MAX) ? PSUB(cand) : 0;
+#undef QSUB
+#undef PSUB
+			TS(0, 1);
+			// ---- S: 64*SEL_RPL rows per step; row base - (m*64 + lane), so the
+			// descending order is (m, lane) and ballots give the positions
+			int cnt = 0;
+			for(int base = n - 1, step = 0; base >= 1 && cnt < DNJ_B; base -= 64 * SEL_RPL, ++step) {
+#pragma unroll
+				for(int m = 0; m < SEL_RPL; ++m) {
+					const int r = base - (m * 64 + lane);
+					if(step) topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+					const double v = r == jsub ? Qj : r == isub ? Qi : topQ[m];
+					const bool f = r >= 1 && v < m0;
+					const unsigned long long bm = __ballot(f);
+					const int pos = cnt + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm >> 32),
+					                                                     __builtin_amdgcn_mbcnt_lo((unsigned) bm, 0));
+					if(f && pos < DNJ_B) {
+						sS[pos] = r;
+						sQS[pos] = v;
+					}
+					cnt += __popcll(bm);
+				}
+			}
+			const int nS = cnt < DNJ_B ? cnt : DNJ_B;
+			wave_sync();
+			// ---- units of SEG cells per row of S (lane: rows 2*lane, 2*lane+1)
+			const int t0 = 2 * lane, t1 = 2 * lane + 1;
+			const int r0 = t0 < nS ? sS[t0] : 0, r1 = t1 < nS ? sS[t1] : 0;
+			const int u0 = dcdiv(r0, SEG), u1 = dcdiv(r1, SEG);
+			int utot;
+			const int upre = wave_excl_scan(u0 + u1, &utot);
+			if(t0 < nS) so[t0] = upre;
+			if(t1 < nS) so[t1] = upre + u0;
+			if(lane == 0) so[nS] = utot;
+			TS(0, 2);
+			if(blockIdx.x == 0) {
+				// persist the fold and the selection for the kernels that follow
+				if(t0 < nS) {
+					b.S[t0] = r0;
+					b.Sb[t0] = sQS[t0];
+					b.uoff[t0] = upre;
+				}
+				if(t1 < nS) {
+					b.S[t1] = r1;
+					b.Sb[t1] = sQS[t1];
+					b.uoff[t1] = upre + u0;
+				}
+				const long long cells = wave_sum_int((long long) r0 + r1);
+				if(lane == 0) {
+					b.uoff[nS] = utot;
+					if(!first) {
+						b.Q[j] = Qj;
+						b.P[j] = Pj;
+						if(move) {
+							b.Q[i] = Qi;
+							b.P[i] = Pi;
+							b.sD[i] = sDm;
+							b.N[i] = Nm;
+						}
+					}
+					ctl->cand = cand;
+					ctl->m0 = m0;
+					ctl->pos_i = pos_i;
+					ctl->pos_j = pos_j;
+					ctl->nS = nS;
+					ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
+					ctl->rows += nS;
+					ctl->cells += cells;
+					ctl->cells_top += cells;
+				}
+			}
+			if(lane == 0) {
+				s_done = 0;
+				s_nS = nS;
+				s_isub = isub;
+				s_Nm = Nm;
+				s_sDm = sDm;
+			}
+		}
 	}
 	__syncthreads();
+	if(s_done) return;
+	TS(0, 3);
+	const int nS = s_nS, isub = s_isub, Nm = s_Nm;
+	const double sDm = s_sDm;
+	const int nunits = so[nS];
+	// ---- rescans, one unit of SEG cells per block iteration
 	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
 		int lo = 0, hi = nS - 1;   // last t with so[t] <= u
 		while(lo < hi) {
 			int mid = (lo + hi + 1) >> 1;
 			if(so[mid] <= u) lo = mid; else hi = mid - 1;
 		}
-		int r = sS[lo];
-		int c0 = (u - so[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
-		double q = DBL_MAX;
+		const int r = sS[lo];
+		const int c0 = (u - so[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int Nr = GEN ? (r == isub ? Nm : b.N[r]) : n;
+		const double sDr = r == isub ? sDm : b.sD[r];
+		double qq = DBL_MAX;
 		int idx = 0;
-		row_segment_min<ET>(D, bs, b.sD, b.N, r, c0, c1, q, idx);
-		qarg_block_reduce(q, idx, sq, si);
-		if(threadIdx.x == 0) {
-			st_wt(&b.uq[u], q);
-			st_wt(&b.uj[u], idx);
+		row_segment_min<ET, GEN, TB, SEG / TB>(D, bs, b.sD, b.N, r, c0, c1, Nr, sDr, isub, GEN ? Nm : n, sDm, qq, idx);
+		qarg_block_reduce1(qq, idx, sq, si);
+		TS(0, 4);
+		if(tid == 0) {
+			b.uq[lo * b.maxu + (u - so[lo])] = qq;
+			b.uj[lo * b.maxu + (u - so[lo])] = idx;
 		}
+		if(u + (int) gridDim.x < nunits) __syncthreads();
 	}
-	if(!last_block_arrive(&ctl->tick[0])) return;
-	// fold the units of every row of S; derive U
-	double U = ctl->m0;
-	long long cells = 0;
-	for(int t = threadIdx.x; t < nS; t += blockDim.x) {
-		double q = DBL_MAX;
-		int idx = 0;
-		for(int u = so[t]; u < so[t + 1]; ++u) {
-			double uq = ld_wt(&b.uq[u]);
-			int uj = ld_wt(&b.uj[u]);
-			if(qarg_better(uq, uj, q, idx)) {
-				q = uq;
-				idx = uj;
-			}
-		}
-		int r = sS[t];
-		b.fq[r] = q;
-		b.fj[r] = idx;
-		double Qr = b.Q[r];
-		double v = q > Qr ? q : Qr;
-		U = v < U ? v : U;
-		cells += r;
-	}
-	U = lds_min_reduce(U, sq);
-	for(int off = 32; off > 0; off >>= 1) cells += __shfl_xor(cells, off, 64);
-	if((threadIdx.x & 63) == 0 && cells) {
-		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
-		atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) cells);
-	}
-	if(threadIdx.x == 0) {
-		ctl->U = U;
-		ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
-		ctl->rows += nS;
-		ctl->tick[0] = 0;
-	}
+	TS(0, 5);
+	TS_EXIT(0);
 }
 
-template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_rest(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+// ------------------------------------------------------------------ DNJ find
+// One block: the fresh mins of S (fold of k_dnj_select's units), the bound
+// U = min(m0, min_k max(fresh_k, Q_k)) and the rows below S with Q[r] < U in
+// descending order (any other row is provably skipped by minQpair, see the
+// file comment) with their SEG-cell unit offsets, for k_dnj_scan/k_dnj_join.
+__global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
+	constexpr int NW = TBF / 64, FR = FIND_RPT;
+	__shared__ double sq[NW];
+	__shared__ double s_U;
+	__shared__ int s_mw[FR * NW], s_cnt, s_scan[NW];
+	__shared__ int lrow[REPLAY_CAP];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	TS_ENTRY(1);
+	TS(1, 0);
+	// ---- loads that do not depend on U (rows n-2 down; rows >= smin masked)
+	const int done = ctl->done, nS = ctl->nS, smin = ctl->smin;
+	const double m0 = ctl->m0;
+	int sr = 0, su = 0;
+	double sb = DBL_MAX;
+	if(tid < DNJ_B) {
+		sr = b.S[tid];
+		sb = b.Sb[tid];
+		su = b.uoff[tid + 1] - b.uoff[tid];
+	}
+	const int top = n - 2;
+	double qv[FR];
+#pragma unroll
+	for(int m = 0; m < FR; ++m) {
+		const int r = top - (m * TBF + tid);   // coalesced; descending = (m, tid) order
+		qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+	}
+	if(done) return;
+	// ---- fresh mins of S and U
+	double fq = DBL_MAX;
+	int fj = 0;
+	if(tid < nS) {
+		fold_units(b.uq + tid * b.maxu, b.uj + tid * b.maxu, 0, su, fq, fj);
+		Entry e;
+		e.f = fq;
+		e.bnd = sb;
+		e.row = sr;
+		e.j = fj;
+		b.Sent[tid] = e;
+	}
+	{
+		double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
+		v = readlane_d(wave_incl_min(v), 63);
+		if(lane == 0) sq[wid] = v;
+		__syncthreads();
+		if(tid == 0) {
+			double U = m0;
+			for(int w = 0; w < NW; ++w) U = sq[w] < U ? sq[w] : U;
+			s_U = U;
+		}
+		__syncthreads();
+	}
+	const double U = s_U;
+	TS(1, 1);
+	// ---- rows [1, smin) with Q[r] < U, descending: per (m, wave) ballot
+	// counts, one prefix over them, then mbcnt within the wave
+	int T = 0;
+	if(nS == DNJ_B) {
+		for(int base = top; base >= 1; base -= TBF * FR) {
+			if(base != top) {
+#pragma unroll
+				for(int m = 0; m < FR; ++m) {
+					const int r = base - (m * TBF + tid);
+					qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+				}
+			}
+			unsigned long long bm[FR];
+#pragma unroll
+			for(int m = 0; m < FR; ++m) {
+				const int r = base - (m * TBF + tid);
+				bm[m] = __ballot(r >= 1 && r < smin && qv[m] < U);
+				if(lane == 0) s_mw[m * NW + wid] = __popcll(bm[m]);
+			}
+			__syncthreads();
+			if(wid == 0) {
+				// exclusive prefix over the FR*NW counts in (m, wave) order
+				constexpr int NC = FR * NW, PER = (NC + 63) / 64;
+				int c[PER], sum = 0;
+#pragma unroll
+				for(int k = 0; k < PER; ++k) {
+					const int x = lane * PER + k;
+					c[k] = x < NC ? s_mw[x] : 0;
+					sum += c[k];
+				}
+				int tot;
+				int pre = wave_excl_scan(sum, &tot);
+#pragma unroll
+				for(int k = 0; k < PER; ++k) {
+					const int x = lane * PER + k;
+					if(x < NC) s_mw[x] = pre;
+					pre += c[k];
+				}
+				if(lane == 0) s_cnt = tot;
+			}
+			__syncthreads();
+#pragma unroll
+			for(int m = 0; m < FR; ++m) {
+				if((bm[m] >> lane) & 1ull) {
+					const int r = base - (m * TBF + tid);
+					const int pos = T + s_mw[m * NW + wid] +
+					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
+					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
+					if(pos < REPLAY_CAP) lrow[pos] = r;
+					b.crow[pos] = r;
+					b.cbnd[pos] = qv[m];
+				}
+			}
+			T += s_cnt;
+			__syncthreads();
+			if(base - TBF * FR < 1) break;
+		}
+	}
+	if(tid == 0) ctl->T = T;
+	// more rows than LDS holds: k_dnj_join replays them alone (rare)
+	if(T == 0 || T > REPLAY_CAP) return;
+	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
+	const int K = dcdiv(T, TBF);
+	int mysum = 0;
+	long long cells = 0;
+	for(int k = 0; k < K; ++k) {
+		const int e = tid * K + k;
+		if(e < T) {
+			mysum += dcdiv(lrow[e], SEG);
+			cells += lrow[e];
+		}
+	}
+	int utot;
+	int pre = block_excl_scan(mysum, s_scan, &utot);
+	for(int k = 0; k < K; ++k) {
+		const int e = tid * K + k;
+		if(e < T) {
+			b.coff[e] = pre;
+			pre += dcdiv(lrow[e], SEG);
+		}
+	}
+	cells = wave_sum_int(cells);
+	if(lane == 0 && cells) {
+		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
+		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) cells);
+	}
+	if(tid == 0) {
+		b.coff[T] = utot;
+		ctl->rows += T;
+	}
+	TS(1, 2);
+	TS_EXIT(1);
+}
+
+// ------------------------------------------------------------------ DNJ scan
+// Rescans of the rows found by k_dnj_find, in SEG-cell units spread over the
+// whole grid.
+template <int ET, bool GEN>
+__global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                 int n) {
+	__shared__ int erow[REPLAY_CAP];
+	__shared__ int eoff[REPLAY_CAP + 1];
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
-	__shared__ int scan[TB / 64];
-	__shared__ double wmin[TB / 64];
-	__shared__ int list[RPB];
-	__shared__ int s_cnt;
-	__shared__ int e_row[REPLAY_CAP], e_j[REPLAY_CAP];
-	__shared__ double e_b[REPLAY_CAP], e_f[REPLAY_CAP];
-	__shared__ int s_pi, s_pj;
 	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int smin = ctl->smin;
-	const double U = ctl->U;
-	const int nblk = (smin - 1 + RPB - 1) / RPB;   // slices of rows [1, smin)
-	const int w = blockIdx.x;
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-	for(int sl = w; sl < nblk; sl += gridDim.x) {
-		int lo = 1 + sl * RPB, hi = lo + RPB < smin ? lo + RPB : smin;
-		if(threadIdx.x < 64) {
-			int r = hi - 1 - (int) threadIdx.x;
-			bool f = r >= lo && b.Q[r] < U;
-			unsigned long long m = __ballot(f);
-			if(f) list[__popcll(m & ((1ull << threadIdx.x) - 1))] = r;
-			if(threadIdx.x == 0) s_cnt = __popcll(m);
-		}
-		__syncthreads();
-		const int cnt = s_cnt;
-		long long cells = 0;
-		for(int t = 0; t < cnt; ++t) {
-			int r = list[t];
-			double q = DBL_MAX;
-			int idx = 0;
-			row_segment_min<ET, 16>(D, bs, b.sD, b.N, r, 0, r, q, idx);
-			qarg_block_reduce(q, idx, sq, si);
-			if(threadIdx.x == 0) {
-				st_wt(&b.fq[r], q);
-				st_wt(&b.fj[r], idx);
-				st_wt(&b.blk_rows[sl * RPB + t], r);
-			}
-			cells += r;
-		}
-		if(threadIdx.x == 0) {
-			st_wt(&b.blk_cnt[sl], cnt);
-			if(cnt) {
-				atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
-				atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) cells);
-				atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) cnt);
-			}
-		}
-		__syncthreads();
+	const int tid = threadIdx.x;
+	TS_ENTRY(2);
+	TS(2, 0);
+	// speculative first TB entries, then the rest once T is known
+	const int r0 = b.crow[tid], o0 = b.coff[tid];
+	const int done = ctl->done, T = ctl->T;
+	if(done || T == 0 || T > REPLAY_CAP) return;
+	if(tid < T) {
+		erow[tid] = r0;
+		eoff[tid] = o0;
 	}
-	if(!last_block_arrive(&ctl->tick[1])) return;
-
-	// ---- replay of minQpair's decisions: S (descending) then slices nblk-1 .. 0
-	const int nS = ctl->nS;
-	const double m0 = ctl->m0;
-	if(threadIdx.x == 0) {
-		s_pi = ctl->pos_i;
-		s_pj = ctl->pos_j;
+	for(int e = TB + tid; e < T; e += TB) {
+		erow[e] = b.crow[e];
+		eoff[e] = b.coff[e];
 	}
-	int carry = nS;
-	for(int c0 = 0; c0 < nblk; c0 += blockDim.x) {
-		int t = c0 + threadIdx.x;
-		int c = t < nblk ? ld_wt(&b.blk_cnt[nblk - 1 - t]) : 0;
-		int tot;
-		int off = block_excl_scan(c, scan, &tot);
-		for(int k = 0; k < c; ++k) {
-			int e = carry + off + k;
-			if(e < REPLAY_CAP) e_row[e] = ld_wt(&b.blk_rows[(nblk - 1 - t) * RPB + k]);
-		}
-		carry += tot;
-	}
-	for(int t = threadIdx.x; t < nS; t += blockDim.x) e_row[t] = b.S[t];
-	const int total = carry;
+	if(tid == 0) eoff[T] = b.coff[T];
 	__syncthreads();
-	if(total <= REPLAY_CAP) {
-		// gather (bound, fresh, j) and test the prefix-min condition fresh >= bound
-		int bad = 0;
-		for(int e = threadIdx.x; e < total; e += blockDim.x) {
-			int r = e_row[e];
-			double bq = b.Q[r], fq = ld_wt(&b.fq[r]);
-			e_b[e] = bq;
-			e_f[e] = fq;
-			e_j[e] = ld_wt(&b.fj[r]);
-			bad |= !(fq >= bq);
+	TS(2, 1);
+	const int nunits = eoff[T];
+	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
+		int lo = 0, hi = T - 1;   // last e with eoff[e] <= u
+		while(lo < hi) {
+			int mid = (lo + hi + 1) >> 1;
+			if(eoff[mid] <= u) lo = mid; else hi = mid - 1;
 		}
-		bad = __syncthreads_or(bad);
-		if(!bad) {
-			// running min before entry e = min(m0, f[0..e-1]); accepted iff bound < it
-			double carry_m = m0;
-			for(int c0 = 0; c0 < total; c0 += blockDim.x) {
-				int e = c0 + threadIdx.x;
-				double f = e < total ? e_f[e] : DBL_MAX;
-				double x = f;   // inclusive wave min-scan
-				for(int off = 1; off < 64; off <<= 1) {
-					double y = __shfl_up(x, off, 64);
-					if(lane >= off) x = y < x ? y : x;
-				}
-				if(lane == 63) wmin[wid] = x;
-				__syncthreads();
-				double pre = carry_m;
-				for(int k = 0; k < wid; ++k) pre = wmin[k] < pre ? wmin[k] : pre;
-				double excl = __shfl_up(x, 1, 64);
-				if(lane > 0) pre = excl < pre ? excl : pre;
-				double chunk_min = carry_m;
-				for(int k = 0; k < (int) (blockDim.x >> 6); ++k) chunk_min = wmin[k] < chunk_min ? wmin[k] : chunk_min;
-				if(e < total && e_b[e] < pre) {
-					int r = e_row[e];
-					b.Q[r] = f;
-					b.P[r] = e_j[e];
-				}
-				__syncthreads();
-				carry_m = chunk_min;
-			}
-			// the pair: first entry reaching the final minimum, if below m0
-			double q = DBL_MAX;
-			int idx = 0x7fffffff;
-			for(int e = threadIdx.x; e < total; e += blockDim.x) {
-				double f = e_f[e];
-				if(f < q || (f == q && e < idx)) {
-					q = f;
-					idx = e;
-				}
-			}
-			for(int off = 32; off > 0; off >>= 1) {
-				double oq = __shfl_xor(q, off, 64);
-				int oi = __shfl_xor(idx, off, 64);
-				if(oq < q || (oq == q && oi < idx)) {
-					q = oq;
-					idx = oi;
-				}
-			}
-			if(lane == 0) {
-				sq[wid] = q;
-				si[wid] = idx;
-			}
-			__syncthreads();
-			if(threadIdx.x == 0) {
-				for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
-					if(sq[k] < q || (sq[k] == q && si[k] < idx)) {
-						q = sq[k];
-						idx = si[k];
-					}
-				}
-				if(total && q < m0) {
-					s_pi = e_row[idx];
-					s_pj = e_j[idx];
-				}
-			}
-			__syncthreads();
-		} else {
-			if(threadIdx.x == 0) {
-				double m = m0;
-				int pi = s_pi, pj = s_pj;
-				for(int e = 0; e < total; ++e) {
-					if(e_b[e] < m) {
-						int r = e_row[e];
-						b.Q[r] = e_f[e];
-						b.P[r] = e_j[e];
-						if(e_f[e] < m) {
-							m = e_f[e];
-							pi = r;
-							pj = e_j[e];
-						}
-					}
-				}
-				s_pi = pi;
-				s_pj = pj;
-				ctl->serial_replays++;
-			}
-			__syncthreads();
+		const int r = erow[lo];
+		const int c0 = (u - eoff[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int Nr = GEN ? b.N[r] : n;
+		double qq = DBL_MAX;
+		int idx = 0;
+		row_segment_min<ET, GEN, TB, SEG / TB>(D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
+		qarg_block_reduce1(qq, idx, sq, si);
+		if(tid == 0) {
+			b.cq[u] = qq;
+			b.cj[u] = idx;
 		}
-	} else if(threadIdx.x == 0) {
-		// very large candidate sets: serial replay straight from global memory
-		double m = m0;
-		int pi = s_pi, pj = s_pj;
-		int t = 0, k = 0;
-		for(int e = 0; e < total; ++e) {
-			int r;
-			if(e < nS) {
-				r = b.S[e];
-			} else {
-				while(k >= ld_wt(&b.blk_cnt[nblk - 1 - t])) {
-					++t;
-					k = 0;
-				}
-				r = ld_wt(&b.blk_rows[(nblk - 1 - t) * RPB + k]);
-				++k;
-			}
-			if(b.Q[r] < m) {
-				double f = ld_wt(&b.fq[r]);
-				int fj = ld_wt(&b.fj[r]);
-				b.Q[r] = f;
-				b.P[r] = fj;
-				if(f < m) {
-					m = f;
-					pi = r;
-					pj = fj;
-				}
-			}
-		}
-		s_pi = pi;
-		s_pj = pj;
-		ctl->serial_replays++;
+		if(u + (int) gridDim.x < nunits) __syncthreads();
 	}
-	__syncthreads();
-	if(threadIdx.x == 0) {
-		ctl->tick[1] = 0;
-		if(s_pi == 0 && s_pj == 0) {
-			ctl->done = 1;
-			ctl->final_n = ctl->n;
-		} else {
-			record_join<ET>(D, bs, b, s_pi, s_pj);
-		}
-	}
+	TS(2, 2);
+	TS_EXIT(2);
 }
 
-// ------------------------------------------------------------------ NJ argmin
-// nj.c:182 initQ: min starts at 1, the last minimal cell in row-major order
-template <int ET>
-__global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
-	__shared__ double sq[TB / 64];
-	__shared__ long long sf[TB / 64];
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int n = ctl->n;
-	const long long cells = tri(n);
-	const long long chunk = (cells + gridDim.x - 1) / gridDim.x;
-	const long long f0 = (long long) blockIdx.x * chunk;
-	const long long f1 = f0 + chunk < cells ? f0 + chunk : cells;
-	double bq = 1.0;
-	long long bf = -1;
-	if(f0 < f1) {
-		long long f = f0 + threadIdx.x;
-		long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
-		while(r > 1 && tri(r) > f) --r;
-		while(tri(r + 1) <= f) ++r;
-		long long c = f - tri(r);
-		for(; f < f1; f += 4 * TB) {
-			// four cells of this thread: f, f+TB, f+2TB, f+3TB
-			typename Elem<ET>::T v[4];
-			int nr[4], nc[4];
-			double sr[4], sc[4];
-#pragma unroll
-			for(int m = 0; m < 4; ++m) {
-				if(f + m * TB < f1) {
-					v[m] = D[f + m * TB];
-					nr[m] = b.N[r];
-					sr[m] = b.sD[r];
-					nc[m] = b.N[c];
-					sc[m] = b.sD[c];
-				}
-				c += TB;
-				while(c >= r && r < n) {
-					c -= r;
-					++r;
-				}
-			}
-#pragma unroll
-			for(int m = 0; m < 4; ++m) {
-				long long fm = f + m * TB;
-				if(fm < f1) {
-					double d = Elem<ET>::get(v[m], bs);
-					if(0 <= d) {
-						double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
-						if(q < bq || (q == bq && fm > bf)) {
-							bq = q;
-							bf = fm;
-						}
-					}
-				}
-			}
-		}
-	}
-	// block reduce (min q, max f)
-	for(int off = 32; off > 0; off >>= 1) {
-		double oq = __shfl_xor(bq, off, 64);
-		long long of = __shfl_xor(bf, off, 64);
-		if(oq < bq || (oq == bq && of > bf)) {
-			bq = oq;
-			bf = of;
-		}
-	}
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-	if(lane == 0) {
-		sq[wid] = bq;
-		sf[wid] = bf;
-	}
-	__syncthreads();
-	if(threadIdx.x == 0) {
-		for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
-			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
-				bq = sq[k];
-				bf = sf[k];
-			}
-		}
-		st_wt(&b.qpart[blockIdx.x], bq);
-		st_wt(&b.fpart[blockIdx.x], bf);
-	}
-	if(!last_block_arrive(&ctl->tick[1])) return;
-	bq = 1.0;
-	bf = -1;
-	for(unsigned k = threadIdx.x; k < gridDim.x; k += blockDim.x) {
-		double oq = ld_wt(&b.qpart[k]);
-		long long of = ld_wt(&b.fpart[k]);
-		if(oq < bq || (oq == bq && of > bf)) {
-			bq = oq;
-			bf = of;
-		}
-	}
-	for(int off = 32; off > 0; off >>= 1) {
-		double oq = __shfl_xor(bq, off, 64);
-		long long of = __shfl_xor(bf, off, 64);
-		if(oq < bq || (oq == bq && of > bf)) {
-			bq = oq;
-			bf = of;
-		}
-	}
-	__syncthreads();
-	if(lane == 0) {
-		sq[wid] = bq;
-		sf[wid] = bf;
-	}
-	__syncthreads();
-	if(threadIdx.x == 0) {
-		for(int k = 1; k < (int) (blockDim.x >> 6); ++k) {
-			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
-				bq = sq[k];
-				bf = sf[k];
-			}
-		}
-		ctl->tick[1] = 0;
-		if(bf < 0) {
-			ctl->done = 1;
-			ctl->final_n = n;
-		} else {
-			long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) bf)) * 0.5);
-			while(r > 1 && tri(r) > bf) --r;
-			while(tri(r + 1) <= bf) ++r;
-			record_join<ET>(D, bs, b, (int) r, (int) (bf - tri(r)));
-		}
-	}
-}
-
-// ------------------------------------------------------------------ updateD
+// ------------------------------------------------------------------ updateD body
 // exponent e of the lowest set bit of x (x = odd * 2^e); INT32_MAX for 0,
 // INT32_MIN for inf / NaN
 __device__ __forceinline__ int low_exp(double x) {
@@ -771,45 +838,29 @@ __device__ __forceinline__ int low_exp(double x) {
 }
 
 // nj.c:836-1044 without missing entries: every k takes the (D_ik, D_kj >= 0)
-// branch, so the sD/N cursor never lags.  The new row sum sD[j] is the
-// reference's serial sum over k (exact mode) or a fixed-order tree sum; both
-// are the same number whenever every partial sum is exactly representable
-// (all terms multiples of 2^e and sum |c| < 2^53 * 2^e), e.g. integer SNP data.
+// branch, so the sD/N cursor never lags.  Writes the per-block partials of
+// the new row sum of j (sum, sum |c|, count, min exponent) and, in exact mode,
+// each contribution.
 template <int ET>
-__global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+__device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D, double bs, const TreeBufs &b, int n,
+                                            int i, int j, double Dij, bool exact, int k, double Dik, double Dkj,
+                                            double sDk, int Nk, int slot) {
 	__shared__ double ssum[TB / 64], sabs[TB / 64];
 	__shared__ int scnt[TB / 64], sexp[TB / 64];
-	__shared__ double buf[8 * TB];
-	__shared__ double red[1024];
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int n = ctl->n, i = ctl->i, j = ctl->j;
-	const double Dij = ctl->Dij;
-	const int k = blockIdx.x * blockDim.x + threadIdx.x;
 	double d = 0;
 	int cnt = 0;
 	if(k < n && k != i && k != j) {
-		long long fik = k < i ? tri(i) + k : tri(k) + i;
-		long long fkj = k < j ? tri(j) + k : tri(k) + j;
-		double Dik = Elem<ET>::get(D[fik], bs), Dkj = Elem<ET>::get(D[fkj], bs);
 		d = (Dik + Dkj - Dij) / 2;
 		d = d < 0 ? 0 : d;
-		D[fkj] = Elem<ET>::put(d, 0.25, bs);
-		b.sD[k] -= (Dik + Dkj - d);
-		b.N[k] -= 1;
+		D[k < j ? tri(j) + k : tri(k) + j] = Elem<ET>::put(d, 0.25, bs);
+		b.sD[k] = sDk - (Dik + Dkj - d);
+		b.N[k] = Nk - 1;
 		cnt = 1;
 	}
-	const bool exact = ctl->exact;
-	if(exact && k < n) st_wt(&b.contrib[k], d);
-	double s = d, a = fabs(d);
-	int e = low_exp(d);
-	for(int off = 32; off > 0; off >>= 1) {
-		s += __shfl_down(s, off, 64);
-		a += __shfl_down(a, off, 64);
-		cnt += __shfl_down(cnt, off, 64);
-		int oe = __shfl_down(e, off, 64);
-		e = oe < e ? oe : e;
-	}
+	if(exact && k < n) b.contrib[k] = d;
+	const double s = wave_sum_fixed(d), a = wave_sum_fixed(fabs(d));
+	cnt = wave_sum_int(cnt);
+	const int e = wave_min_int(low_exp(d));
 	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	if(lane == 0) {
 		ssum[wid] = s;
@@ -821,113 +872,416 @@ __global__ __launch_bounds__(TB) void k_update(typename Elem<ET>::T *__restrict_
 	if(threadIdx.x == 0) {
 		double t = 0, ta = 0;
 		int c = 0, te = INT32_MAX;
-		for(int w = 0; w < (int) (blockDim.x >> 6); ++w) {
+		for(int w = 0; w < TB / 64; ++w) {
 			t += ssum[w];
 			ta += sabs[w];
 			c += scnt[w];
 			te = sexp[w] < te ? sexp[w] : te;
 		}
-		st_wt(&b.wsum[blockIdx.x], t);
-		st_wt(&b.wabs[blockIdx.x], ta);
-		st_wt(&b.wcnt[blockIdx.x], c);
-		st_wt(&b.wexp[blockIdx.x], te);
-	}
-	if(!last_block_arrive(&ctl->tick[2])) return;
-	// fixed-order fold of the block partials: 1024 leaves (block g -> leaf
-	// g mod 1024, folded in order), then a pairwise tree
-	const int G = gridDim.x;
-	for(int leaf = threadIdx.x; leaf < 1024; leaf += blockDim.x) {
-		double v = 0;
-		for(int g = leaf; g < G; g += 1024) v += ld_wt(&b.wsum[g]);
-		red[leaf] = v;
-	}
-	double tabs = 0;
-	int tcnt = 0, texp = INT32_MAX;
-	for(int g = threadIdx.x; g < G; g += blockDim.x) {
-		tabs += ld_wt(&b.wabs[g]);
-		tcnt += ld_wt(&b.wcnt[g]);
-		int oe = ld_wt(&b.wexp[g]);
-		texp = oe < texp ? oe : texp;
-	}
-	__syncthreads();
-	for(int stride = 512; stride > 0; stride >>= 1) {
-		for(int leaf = threadIdx.x; leaf < stride; leaf += blockDim.x) red[leaf] += red[leaf + stride];
-		__syncthreads();
-	}
-	const double total = red[0];
-	for(int off = 32; off > 0; off >>= 1) {
-		tabs += __shfl_xor(tabs, off, 64);
-		tcnt += __shfl_xor(tcnt, off, 64);
-		int oe = __shfl_xor(texp, off, 64);
-		texp = oe < texp ? oe : texp;
-	}
-	__syncthreads();
-	if(lane == 0) {
-		sabs[wid] = tabs;
-		scnt[wid] = tcnt;
-		sexp[wid] = texp;
-	}
-	__syncthreads();
-	tabs = 0;
-	tcnt = 0;
-	texp = INT32_MAX;
-	for(int w = 0; w < (int) (blockDim.x >> 6); ++w) {
-		tabs += sabs[w];
-		tcnt += scnt[w];
-		texp = sexp[w] < texp ? sexp[w] : texp;
-	}
-	double sd = total;
-	if(exact) {
-		bool provable = texp != INT32_MIN &&
-		                (texp == INT32_MAX || (texp > -1000 && tabs * (1.0 + 1e-9) < ldexp(1.0, 53 + texp)));
-		if(!provable) {
-			// the reference's serial sum in increasing k (nj.c:911 / :1002)
-			sd = 0;
-			double nxt[4];
-#pragma unroll
-			for(int m = 0; m < 4; ++m) {
-				int kk = m * TB + threadIdx.x;
-				buf[m * TB + threadIdx.x] = kk < n ? ld_wt(&b.contrib[kk]) : 0.0;
-			}
-			__syncthreads();
-			for(int c0 = 0, p = 0; c0 < n; c0 += 4 * TB, p ^= 1) {
-				// fetch the next chunk while thread 0 runs the serial chain
-#pragma unroll
-				for(int m = 0; m < 4; ++m) {
-					int kk = c0 + 4 * TB + m * TB + threadIdx.x;
-					nxt[m] = kk < n ? ld_wt(&b.contrib[kk]) : 0.0;
-				}
-				if(threadIdx.x == 0) {
-					const double *cur = buf + p * 4 * TB;
-					int lim = n - c0 < 4 * TB ? n - c0 : 4 * TB;
-					for(int u = 0; u < lim; ++u) sd += cur[u];
-				}
-#pragma unroll
-				for(int m = 0; m < 4; ++m) buf[(p ^ 1) * 4 * TB + m * TB + threadIdx.x] = nxt[m];
-				__syncthreads();
-			}
-			if(threadIdx.x == 0) ctl->serial_sums++;
-		}
-	}
-	if(threadIdx.x == 0) {
-		b.N[j] = 1 + tcnt;
-		b.sD[j] = sd;
-		ctl->tick[2] = 0;
+		b.wsum[slot] = t;
+		b.wabs[slot] = ta;
+		b.wcnt[slot] = c;
+		b.wexp[slot] = te;
 	}
 }
 
-// nj.c:836-1044 general path (entries < 0 are "missing"): one block walks k
-// in chunks, reproducing the lagging sD/N cursor and the out-of-row read
-// D_j[k] of the D_kj-only column branch (nj.c:1022).
+// Wave 0: fold of the updateD partials of G blocks into the new row sum of j
+// and its count (fixed order: lane l sums blocks l, l+64, ... in order, then
+// a shfl_down tree), identical in every block.  In exact mode this is the
+// reference's serial sum whenever that is provable (all contributions
+// multiples of 2^e, sum |c| < 2^53 * 2^e, e.g. integer SNP distances);
+// otherwise *need_serial asks for serial_sum_block.  General (missing data):
+// k_update_general left the serial sum in wsum[0].
+__device__ void fold_update_wave(const TreeBufs &b, int G, bool exact, bool general, double *sd_out, int *nj_out,
+                                 bool *need_serial) {
+	const int lane = threadIdx.x & 63;
+	*need_serial = false;
+	if(general) {
+		*sd_out = b.wsum[0];
+		*nj_out = 1 + b.wcnt[0];
+		return;
+	}
+	double s = 0, a = 0;
+	int c = 0, e = INT32_MAX;
+	for(int g = lane; g < G; g += 64) {
+		s += b.wsum[g];
+		a += b.wabs[g];
+		c += b.wcnt[g];
+		int oe = b.wexp[g];
+		e = oe < e ? oe : e;
+	}
+	const double sd = wave_sum_fixed(s);
+	a = wave_sum_fixed(a);
+	c = wave_sum_int(c);
+	e = wave_min_int(e);
+	if(exact) {
+		bool provable = e != INT32_MIN && (e == INT32_MAX || (e > -1000 && a * (1.0 + 1e-9) < ldexp(1.0, 53 + e)));
+		*need_serial = !provable;
+	}
+	*sd_out = sd;
+	*nj_out = 1 + c;
+}
+
+// the reference's serial sum of the contributions in increasing k (nj.c:911 /
+// :1002); thread 0 runs the chain while the block stages the next chunk
+__device__ double serial_sum_block(const TreeBufs &b, int n) {
+	__shared__ double buf[8 * TB];
+	__shared__ double s_sd;
+	double sd = 0;
+	double nxt[4];
+#pragma unroll
+	for(int m = 0; m < 4; ++m) {
+		int kk = m * TB + threadIdx.x;
+		buf[m * TB + threadIdx.x] = kk < n ? b.contrib[kk] : 0.0;
+	}
+	__syncthreads();
+	for(int c0 = 0, p = 0; c0 < n; c0 += 4 * TB, p ^= 1) {
+#pragma unroll
+		for(int m = 0; m < 4; ++m) {
+			int kk = c0 + 4 * TB + m * TB + threadIdx.x;
+			nxt[m] = kk < n ? b.contrib[kk] : 0.0;
+		}
+		if(threadIdx.x == 0) {
+			const double *cur = buf + p * 4 * TB;
+			int lim = n - c0 < 4 * TB ? n - c0 : 4 * TB;
+			for(int u = 0; u < lim; ++u) sd += cur[u];
+		}
+#pragma unroll
+		for(int m = 0; m < 4; ++m) buf[(p ^ 1) * 4 * TB + m * TB + threadIdx.x] = nxt[m];
+		__syncthreads();
+	}
+	if(threadIdx.x == 0) s_sd = sd;
+	__syncthreads();
+	return s_sd;
+}
+
+// ------------------------------------------------------------------ minQpair replay
+// dnj.c:88-112 decisions over the candidate entries in scan order (S, then
+// the rest, descending rows), wave 0 only.  Entry e has its stale bound b_e
+// = Q[row] and fresh min (f_e, j_e); the serial running min m_e starts at m0,
+// entry e is accepted iff b_e < m_e, and then m_{e+1} = min(m_e, f_e).
+//   A "good" entry (f_e >= b_e) gives m_{e+1} = min(m_e, f_e) whether or not
+//   it is accepted (rejected means f_e >= b_e >= m_e), so over good entries
+//   m is a prefix min.  A "bad" entry (f_e < b_e) lowers m only if accepted.
+// So: prefix-min passes that treat the undecided bad entries as rejected;
+// the first bad entry found accepted (b_e < m_e) is certainly accepted, fixes
+// m_{e+1} = f_e, and the next pass starts after it.  Without bad entries this
+// is one pass.  Accepted (Q, P) updates are applied by the writer block only.
+__device__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
+                            const double *e_f, unsigned char *e_acc, bool writer, const TreeBufs &b, int &pi,
+                            int &pj, bool *had_bad) {
+	const int lane = threadIdx.x & 63;
+	int bad = 0;
+	for(int e = lane; e < total; e += 64) {
+		bad |= !(e_f[e] >= e_b[e]);
+		e_acc[e] = 0;
+	}
+	const bool any_bad = __any(bad);
+	*had_bad = any_bad;
+	wave_sync();
+	if(any_bad) {
+		double m = m0;
+		int start = 0;
+		for(;;) {
+			int hit = -1;
+			double cm = m;
+			for(int c0 = start; c0 < total; c0 += 64) {
+				const int e = c0 + lane;
+				const bool valid = e < total;
+				const double f = valid ? e_f[e] : DBL_MAX, bb = valid ? e_b[e] : DBL_MAX;
+				const bool good = valid && f >= bb;
+				const double x = wave_incl_min(good ? f : DBL_MAX);
+				double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
+				pre = pre < cm ? pre : cm;
+				const unsigned long long hm = __ballot(valid && !good && bb < pre);
+				if(hm) {
+					hit = c0 + __ffsll((long long) hm) - 1;
+					break;
+				}
+				const double last = readlane_d(x, 63);
+				cm = last < cm ? last : cm;
+			}
+			if(hit < 0) break;
+			if(lane == 0) e_acc[hit] = 1;
+			m = e_f[hit];
+			start = hit + 1;
+			wave_sync();
+		}
+	}
+	// final pass: decisions, writes and the pair (the first contributor that
+	// reaches the final minimum, if it is below m0)
+	double cm = m0;
+	for(int c0 = 0; c0 < total; c0 += 64) {
+		const int e = c0 + lane;
+		const bool valid = e < total;
+		const double f = valid ? e_f[e] : DBL_MAX, bb = valid ? e_b[e] : DBL_MAX;
+		const bool good = valid && f >= bb;
+		const bool contrib = good || (valid && e_acc[e]);
+		const double x = wave_incl_min(contrib ? f : DBL_MAX);
+		double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
+		pre = pre < cm ? pre : cm;
+		const bool accepted = good ? bb < pre : contrib;
+		if(writer && accepted) {
+			b.Q[e_row[e]] = f;
+			b.P[e_row[e]] = e_j[e];
+		}
+		const double last = readlane_d(x, 63);
+		cm = last < cm ? last : cm;
+	}
+	if(total && cm < m0) {
+		int first_e = 0x7fffffff;
+		for(int e = lane; e < total; e += 64) {
+			const bool contrib = e_f[e] >= e_b[e] || e_acc[e];
+			if(contrib && e_f[e] == cm && e < first_e) first_e = e;
+		}
+		first_e = wave_min_int(first_e);
+		pi = e_row[first_e];
+		pj = e_j[first_e];
+	}
+}
+
+// k_dnj_join when more rows qualified below S than LDS holds (rare): block 0
+// alone replays minQpair serially, rescanning a row only when the reference
+// would (bound below the running min), then runs updateD for the whole matrix
+// writing the partials of every block slot.  Other blocks exit at once, so
+// no row is read while it is being updated.
+template <int ET, bool GEN>
+__device__ void join_overflow(typename Elem<ET>::T *__restrict__ D, double bs, const TreeBufs &b, int n, int nS,
+                              int T, double m0, int pos_i, int pos_j, int njoins, int neg, bool exact) {
+	__shared__ double sq[TB / 64];
+	__shared__ int si[TB / 64];
+	__shared__ double s_m;
+	__shared__ int s_pi, s_pj;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x;
+	if(tid == 0) {
+		double m = m0;
+		int pi = pos_i, pj = pos_j;
+		for(int e = 0; e < nS; ++e) {
+			const Entry x = b.Sent[e];
+			if(x.bnd < m) {
+				b.Q[x.row] = x.f;
+				b.P[x.row] = x.j;
+				if(x.f < m) {
+					m = x.f;
+					pi = x.row;
+					pj = x.j;
+				}
+			}
+		}
+		s_m = m;
+		s_pi = pi;
+		s_pj = pj;
+		ctl->serial_replays++;
+	}
+	__syncthreads();
+	for(int e = 0; e < T; ++e) {
+		const int r = b.crow[e];
+		const double bnd = b.cbnd[e];
+		if(!(bnd < s_m)) continue;
+		double q = DBL_MAX;
+		int idx = 0;
+		row_segment_min<ET, GEN, TB, 8>(D, bs, b.sD, b.N, r, 0, r, GEN ? b.N[r] : n, b.sD[r], -1, 0, 0.0, q, idx);
+		qarg_block_reduce1(q, idx, sq, si);
+		if(tid == 0) {
+			b.Q[r] = q;
+			b.P[r] = idx;
+			if(q < s_m) {
+				s_m = q;
+				s_pi = r;
+				s_pj = idx;
+			}
+		}
+		__syncthreads();
+	}
+	const int i = s_pi, j = s_pj;
+	if(i == 0 && j == 0) {
+		if(tid == 0) {
+			ctl->done = 1;
+			ctl->final_n = n;
+		}
+		return;
+	}
+	const double Dij = Elem<ET>::get(D[tri(i) + j], bs);
+	if(tid == 0) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, neg);
+		ctl->i = i;
+		ctl->j = j;
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[njoins] = J;
+		ctl->njoins = njoins + 1;
+	}
+	if(GEN) return;   // k_update_general follows
+	for(int vb = 0; vb < (int) cdiv(n, TB); ++vb) {
+		const int k = vb * TB + tid;
+		double Dik = 0, Dkj = 0, sDk = 0;
+		int Nk = 0;
+		if(k < n && k != i && k != j) {
+			Dik = Elem<ET>::get(D[k < i ? tri(i) + k : tri(k) + i], bs);
+			Dkj = Elem<ET>::get(D[k < j ? tri(j) + k : tri(k) + j], bs);
+			sDk = b.sD[k];
+			Nk = b.N[k];
+		}
+		update_body<ET>(D, bs, b, n, i, j, Dij, exact, k, Dik, Dkj, sDk, Nk, vb);
+		__syncthreads();
+	}
+}
+
+// ------------------------------------------------------------------ DNJ join
+// Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
+// replay; then limbLength, the join record and updateD with the whole grid.
+template <int ET, bool GEN>
+__global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                                 int general) {
+	__shared__ int e_row[DNJ_B + REPLAY_CAP], e_j[DNJ_B + REPLAY_CAP];
+	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
+	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
+	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const bool writer = blockIdx.x == 0;
+	TS_ENTRY(3);
+	TS(3, 0);
+	if(wid == 0) {
+		// ---- loads independent of the outcome
+		const int done = ctl->done, nS = ctl->nS, T = ctl->T;
+		const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
+		const double m0 = ctl->m0;
+		Entry se0, se1;
+		se0 = b.Sent[lane];
+		se1 = b.Sent[lane + 64];
+		int rr[4], c0[4], c1[4];
+		double bb[4];
+#pragma unroll
+		for(int m = 0; m < 4; ++m) {
+			rr[m] = b.crow[lane + 64 * m];
+			bb[m] = b.cbnd[lane + 64 * m];
+			c0[m] = b.coff[lane + 64 * m];
+			c1[m] = b.coff[lane + 64 * m + 1];
+		}
+		if(lane == 0) {
+			s_nj = ctl->njoins;
+			s_neg = ctl->neg;
+			s_exact = ctl->exact;
+		}
+		if(done || T > REPLAY_CAP) {
+			if(lane == 0) s_stop = done ? 1 : 2;
+		} else {
+			TS(3, 1);
+			int pi = pos_i, pj = pos_j;
+			if(lane < nS) {
+				e_row[lane] = se0.row;
+				e_j[lane] = se0.j;
+				e_b[lane] = se0.bnd;
+				e_f[lane] = se0.f;
+			}
+			if(lane + 64 < nS) {
+				e_row[lane + 64] = se1.row;
+				e_j[lane + 64] = se1.j;
+				e_b[lane + 64] = se1.bnd;
+				e_f[lane + 64] = se1.f;
+			}
+			// fresh (q, j) of each rest entry: fold of its units
+			for(int e0 = 0; e0 < T; e0 += 256) {
+#pragma unroll
+				for(int m = 0; m < 4; ++m) {
+					const int e = e0 + lane + 64 * m;
+					if(e >= T) continue;
+					const int r = e0 ? b.crow[e] : rr[m];
+					const double bnd = e0 ? b.cbnd[e] : bb[m];
+					const int ua = e0 ? b.coff[e] : c0[m], ub = e0 ? b.coff[e + 1] : c1[m];
+					double q = DBL_MAX;
+					int idx = 0;
+					fold_units(b.cq, b.cj, ua, ub, q, idx);
+					e_row[nS + e] = r;
+					e_j[nS + e] = idx;
+					e_b[nS + e] = bnd;
+					e_f[nS + e] = q;
+				}
+			}
+			wave_sync();
+			TS(3, 2);
+			bool had_bad;
+			replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad);
+			if(writer && lane == 0 && had_bad) ctl->serial_replays++;
+			if(lane == 0) {
+				s_stop = 0;
+				s_pi = pi;
+				s_pj = pj;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) {
+		if(s_stop == 2 && blockIdx.x == 0)
+			join_overflow<ET, GEN>(D, bs, b, n, ctl->nS, ctl->T, ctl->m0, ctl->pos_i, ctl->pos_j, s_nj, s_neg, s_exact);
+		return;
+	}
+	TS(3, 3);
+	const int i = s_pi, j = s_pj;
+	if(i == 0 && j == 0) {
+		if(writer && tid == 0) {
+			ctl->done = 1;
+			ctl->final_n = n;
+		}
+		return;
+	}
+	// ---- join: limbLength (nj.c:42) and updateD (nj.c:836)
+	const int k = blockIdx.x * TB + tid;
+	const double Dij = Elem<ET>::get(D[tri(i) + j], bs);
+	double Dik = 0, Dkj = 0, sDk = 0;
+	int Nk = 0;
+	if(!general && k < n && k != i && k != j) {
+		Dik = Elem<ET>::get(D[k < i ? tri(i) + k : tri(k) + i], bs);
+		Dkj = Elem<ET>::get(D[k < j ? tri(j) + k : tri(k) + j], bs);
+		sDk = b.sD[k];
+		Nk = b.N[k];
+	}
+	if(writer && tid == 0) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, s_neg);
+		ctl->i = i;
+		ctl->j = j;
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[s_nj] = J;
+		ctl->njoins = s_nj + 1;
+	}
+	TS(3, 4);
+	if(general) return;
+	update_body<ET>(D, bs, b, n, i, j, Dij, s_exact, k, Dik, Dkj, sDk, Nk, blockIdx.x);
+	TS(3, 5);
+	TS_EXIT(3);
+}
+
+// ------------------------------------------------------------------ general updateD
+// nj.c:836-1044 with entries < 0 ("missing"): one block walks k in chunks,
+// reproducing the lagging sD/N cursor and the out-of-row read D_j[k] of the
+// D_kj-only column branch (nj.c:1022).  Leaves the serial row sum in wsum[0]
+// and the count in wcnt[0] for the fold that follows.
 template <int ET>
-__global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
+__global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                         int n) {
 	typedef typename Elem<ET>::T T;
 	__shared__ int wsc[16];
 	__shared__ double sbuf[1024];
 	__shared__ int s_carry, s_cnt;
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	const int n = ctl->n;
 	const int i = ctl->i, j = ctl->j;
 	const double Dij = ctl->Dij, Li = ctl->Li, Lj = ctl->Lj;
 	const long long rj = tri(j), ri = tri(i);
@@ -1041,48 +1395,94 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 		__syncthreads();
 	}
 	if(threadIdx.x == 0) {
-		b.N[j] = 1 + s_cnt;
-		b.sD[j] = sd;
+		b.wsum[0] = sd;
+		b.wcnt[0] = s_cnt;
 	}
 }
 
 // ------------------------------------------------------------------ DNJ requeue
-// updateDNJ's Q/P part (dnj.c:618-709) followed by DNJ_popArrange
-// (dnj.c:817-975) and minPos (dnj.c:1026-1032); the last block folds the four
-// (q, idx) reductions, shrinks n and prepares the next minQpair.
+// Row sum of j, then updateDNJ's Q/P part (dnj.c:618-709) and DNJ_popArrange
+// (dnj.c:817-975); the four (q, idx) reductions go to per-block partials that
+// the next k_dnj_select folds.
 template <int ET>
-__global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b) {
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	__shared__ int s_cand;
+__global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                    int n, int general) {
+	__shared__ double sq[4][TB / 64];
+	__shared__ int si[4][TB / 64];
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
 	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int n = ctl->n, i = ctl->i, j = ctl->j, nn = n - 1;
-	const int Nj = b.N[j];
-	const double sDj = b.sD[j];
+	const int nn = n - 1;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = blockIdx.x * TB + tid;
+	TS_ENTRY(4);
+	TS(4, 0);
+	int Nk = 0, pkk0 = 0;
+	double sDk = 0, qk0 = 0;
+	typename Elem<ET>::T vm = 0;
+	if(k < n) {
+		Nk = b.N[k];
+		sDk = b.sD[k];
+		qk0 = b.Q[k];
+		pkk0 = b.P[k];
+	}
+	if(k < nn) vm = D[tri(nn) + k];   // row nn, moved to i
+	const int Nm0 = b.N[nn];
+	const double sDm0 = b.sD[nn];
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need;
+			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j, Nj = s_nj;
+	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	TS(4, 1);
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = Nj;
+		if(s_serial) ctl->serial_sums++;
+	}
 	const bool move = i != nn;
-	const int Nm = move ? b.N[nn] : 0;
-	const double sDm = move ? b.sD[nn] : 0;
-	const int k = blockIdx.x * blockDim.x + threadIdx.x;
+	const int Nm = move ? Nm0 : 0;
+	const double sDm = move ? sDm0 : 0;
+	if(k == j) {
+		Nk = Nj;
+		sDk = sdj;
+	}
 	double rq = DBL_MAX, pq = DBL_MAX, r2q = DBL_MAX, p2q = DBL_MAX;
 	int rj = 0, pk = -1, r2j = 0, p2k = -1;
 	if(k < n) {
-		const int Nk = b.N[k];
-		const double sDk = b.sD[k];
 		if(k < j) {
 			double d = Elem<ET>::get(D[tri(j) + k], bs);
 			if(0 <= d) {
-				rq = qcrit(Nj, Nk, d, sDj, sDk);
+				rq = qcrit(Nj, Nk, d, sdj, sDk);
 				rj = k;
 			}
 		}
 		if(k > j && k != i) {
-			double qk = b.Q[k];
-			int pkk = b.P[k];
+			double qk = qk0;
+			int pkk = pkk0;
 			bool upd = false;
 			double d = Elem<ET>::get(D[tri(k) + j], bs);
 			if(0 <= d) {
-				double q = qcrit(Nj, Nk, d, sDj, sDk);
+				double q = qcrit(Nj, Nk, d, sdj, sDk);
 				if(q <= qk) {
 					qk = q;
 					pkk = j;
@@ -1092,9 +1492,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				}
 			}
 			if(move && k > i && k < nn) {
-				typename Elem<ET>::T v = D[tri(nn) + k];
-				D[tri(k) + i] = v;
-				double dm = Elem<ET>::get(v, bs);
+				D[tri(k) + i] = vm;
+				double dm = Elem<ET>::get(vm, bs);
 				if(0 <= dm) {
 					double q = qcrit(Nm, Nk, dm, sDm, sDk);
 					if(q <= qk) {
@@ -1107,111 +1506,276 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				}
 			}
 			if(upd) {
-				st_wt(&b.Q[k], qk);
-				st_wt(&b.P[k], pkk);
+				b.Q[k] = qk;
+				b.P[k] = pkk;
 			}
 		}
 		if(move && k < i) {
-			typename Elem<ET>::T v = D[tri(nn) + k];
-			D[tri(i) + k] = v;
-			double dm = Elem<ET>::get(v, bs);
+			D[tri(i) + k] = vm;
+			double dm = Elem<ET>::get(vm, bs);
 			if(0 <= dm) {
 				r2q = qcrit(Nm, Nk, dm, sDm, sDk);
 				r2j = k;
 			}
 		}
 	}
-	qarg_block_reduce(rq, rj, sq, si);
-	qarg_block_reduce(pq, pk, sq, si);
-	qarg_block_reduce(r2q, r2j, sq, si);
-	qarg_block_reduce(p2q, p2k, sq, si);
-	if(threadIdx.x == 0) {
-		double *qp = b.qpart + 4 * blockIdx.x;
-		int *ip = b.ipart + 4 * blockIdx.x;
-		st_wt(&qp[0], rq); st_wt(&ip[0], rj);
-		st_wt(&qp[1], pq); st_wt(&ip[1], pk);
-		st_wt(&qp[2], r2q); st_wt(&ip[2], r2j);
-		st_wt(&qp[3], p2q); st_wt(&ip[3], p2k);
+	qarg_wave_reduce(rq, rj);
+	qarg_wave_reduce(pq, pk);
+	qarg_wave_reduce(r2q, r2j);
+	qarg_wave_reduce(p2q, p2k);
+	if(lane == 0) {
+		sq[0][wid] = rq;
+		si[0][wid] = rj;
+		sq[1][wid] = pq;
+		si[1][wid] = pk;
+		sq[2][wid] = r2q;
+		si[2][wid] = r2j;
+		sq[3][wid] = p2q;
+		si[3][wid] = p2k;
 	}
-	if(!last_block_arrive(&ctl->tick[3])) return;
-	double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
-	int ix[4] = {0, -1, 0, -1};
-	for(unsigned w = threadIdx.x; w < gridDim.x; w += blockDim.x) {
+	__syncthreads();
+	if(tid < 4) {
+		double q = sq[tid][0];
+		int ix = si[tid][0];
+		for(int w = 1; w < TB / 64; ++w) {
+			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
+				q = sq[tid][w];
+				ix = si[tid][w];
+			}
+		}
+		b.qpart[4 * blockIdx.x + tid] = q;
+		b.ipart[4 * blockIdx.x + tid] = ix;
+	}
+	TS(4, 2);
+	TS_EXIT(4);
+}
+
+
+// (q, f) cells of initQ: smaller q wins, equal q -> larger flat index f
+__device__ __forceinline__ void qf_wave_reduce(double &q, long long &f) {
+#define S_(C, R)                                          \
+	{                                                     \
+		const double oq_ = dpp_d<C, R>(DBL_MAX, q);       \
+		const long long of_ = dpp_l<C, R>(-2, f);         \
+		if(oq_ < q || (oq_ == q && of_ > f)) {            \
+			q = oq_;                                      \
+			f = of_;                                      \
+		}                                                 \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	q = readlane_d(q, 63);
+	f = readlane_l(f, 63);
+}
+
+// ------------------------------------------------------------------ NJ argmin
+// nj.c:182 initQ: min starts at 1, the last minimal cell in row-major order
+template <int ET, bool GEN>
+__global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                  int n) {
+	__shared__ double sq[TB / 64];
+	__shared__ long long sf[TB / 64];
+	if(b.ctl->done) return;
+	const long long cells = tri(n);
+	const long long chunk = (cells + gridDim.x - 1) / gridDim.x;
+	const long long f0 = (long long) blockIdx.x * chunk;
+	const long long f1 = f0 + chunk < cells ? f0 + chunk : cells;
+	double bq = 1.0;
+	long long bf = -1;
+	if(f0 < f1) {
+		long long f = f0 + threadIdx.x;
+		long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
+		while(r > 1 && tri(r) > f) --r;
+		while(tri(r + 1) <= f) ++r;
+		long long c = f - tri(r);
+		for(; f < f1; f += 4 * TB) {
+			// four cells of this thread: f, f+TB, f+2TB, f+3TB
+			typename Elem<ET>::T v[4];
+			int nr[4], nc[4];
+			double sr[4], sc[4];
 #pragma unroll
-		for(int t = 0; t < 4; ++t) {
-			double oq = ld_wt(&b.qpart[4 * w + t]);
-			int oi = ld_wt(&b.ipart[4 * w + t]);
-			if(qarg_better(oq, oi, q[t], ix[t])) {
-				q[t] = oq;
-				ix[t] = oi;
+			for(int m = 0; m < 4; ++m) {
+				if(f + m * TB < f1) {
+					v[m] = D[f + m * TB];
+					nr[m] = GEN ? b.N[r] : n;
+					sr[m] = b.sD[r];
+					nc[m] = GEN ? b.N[c] : n;
+					sc[m] = b.sD[c];
+				}
+				c += TB;
+				while(c >= r && r < n) {
+					c -= r;
+					++r;
+				}
+			}
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				long long fm = f + m * TB;
+				if(fm < f1) {
+					double d = Elem<ET>::get(v[m], bs);
+					if(0 <= d) {
+						double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
+						if(q < bq || (q == bq && fm > bf)) {
+							bq = q;
+							bf = fm;
+						}
+					}
+				}
 			}
 		}
 	}
-#pragma unroll
-	for(int t = 0; t < 4; ++t) qarg_block_reduce(q[t], ix[t], sq, si);
-	if(threadIdx.x == 0) {
-		// row j (dnj.c:619-663) and p over the lowered column entries
-		st_wt(&b.Q[j], q[0]);
-		st_wt(&b.P[j], ix[0]);
-		int p = j;
-		if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
-		int p2 = 0;
-		if(move) {
-			b.sD[i] = sDm;
-			b.N[i] = Nm;
-			st_wt(&b.Q[i], q[2]);
-			st_wt(&b.P[i], ix[2]);
-			p2 = i;
-			if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
-		}
-		ctl->mi = p;
-		ctl->mj = p2;
-		ctl->n = nn;
-		ctl->tick[3] = 0;
-		// dnj.c:1026-1032: next candidate row
-		int cand;
-		if(p2 == nn) cand = p;
-		else if(p == nn) cand = p2;
-		else {
-			double Qp = ld_wt(&b.Q[p]), Qp2 = ld_wt(&b.Q[p2]);
-			cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
-		}
-		s_cand = cand;
+	qf_wave_reduce(bq, bf);
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	if(lane == 0) {
+		sq[wid] = bq;
+		sf[wid] = bf;
 	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	__syncthreads();
-	if(nn > 2) prepare_selection(b, nn, s_cand);
+	if(threadIdx.x == 0) {
+		for(int k = 1; k < TB / 64; ++k) {
+			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
+				bq = sq[k];
+				bf = sf[k];
+			}
+		}
+		b.qpart[blockIdx.x] = bq;
+		b.fpart[blockIdx.x] = bf;
+	}
 }
 
-// ------------------------------------------------------------------ NJ pop
-// matrix.c:518 ltdMatrix_popArrange + nj.c:1588-1589
+// fold of the argmin partials (wave 0), limbLength, the join record and updateD
 template <int ET>
-__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b) {
+__global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                                int G, int general) {
+	__shared__ long long s_bf;
+	__shared__ int s_stop, s_nj, s_neg, s_exact;
 	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int n = ctl->n, i = ctl->i, nn = n - 1;
-	const int k = blockIdx.x * blockDim.x + threadIdx.x;
-	if(i != nn) {
-		if(k < i) {
-			D[tri(i) + k] = D[tri(nn) + k];
-		} else if(k > i && k < nn) {
-			D[tri(k) + i] = D[tri(nn) + k];
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = blockIdx.x * TB + tid;
+	double sDk = 0;
+	int Nk = 0;
+	if(k < n) {
+		sDk = b.sD[k];
+		Nk = b.N[k];
+	}
+	if(wid == 0) {
+		const int done = ctl->done;
+		double bq = 1.0;
+		long long bf = -1;
+		for(int g = lane; g < G; g += 64) {
+			double oq = b.qpart[g];
+			long long of = b.fpart[g];
+			if(oq < bq || (oq == bq && of > bf)) {
+				bq = oq;
+				bf = of;
+			}
+		}
+		qf_wave_reduce(bq, bf);
+		if(lane == 0) {
+			s_stop = done;
+			s_bf = bf;
+			s_nj = ctl->njoins;
+			s_neg = ctl->neg;
+			s_exact = ctl->exact;
 		}
 	}
-	if(!last_block_arrive(&ctl->tick[3])) return;
-	if(threadIdx.x == 0) {
-		if(i != nn) {
-			b.sD[i] = b.sD[nn];
-			b.N[i] = b.N[nn];
+	__syncthreads();
+	if(s_stop) return;
+	const bool writer = blockIdx.x == 0 && tid == 0;
+	const long long bf = s_bf;
+	if(bf < 0) {
+		if(writer) {
+			ctl->done = 1;
+			ctl->final_n = n;
 		}
-		ctl->n = nn;
-		ctl->tick[3] = 0;
+		return;
+	}
+	long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) bf)) * 0.5);
+	while(r > 1 && tri(r) > bf) --r;
+	while(tri(r + 1) <= bf) ++r;
+	const int i = (int) r, j = (int) (bf - tri(r));
+	const double Dij = Elem<ET>::get(D[bf], bs);
+	double Dik = 0, Dkj = 0;
+	if(!general && k < n && k != i && k != j) {
+		Dik = Elem<ET>::get(D[k < i ? tri(i) + k : tri(k) + i], bs);
+		Dkj = Elem<ET>::get(D[k < j ? tri(j) + k : tri(k) + j], bs);
+	}
+	if(writer) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, s_neg);
+		ctl->i = i;
+		ctl->j = j;
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[s_nj] = J;
+		ctl->njoins = s_nj + 1;
+	}
+	if(general) return;
+	update_body<ET>(D, bs, b, n, i, j, Dij, s_exact, k, Dik, Dkj, sDk, Nk, blockIdx.x);
+}
+
+// row sum of j, then matrix.c:518 ltdMatrix_popArrange + nj.c:1588-1589
+template <int ET>
+__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, int general) {
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	TreeCtl *ctl = b.ctl;
+	const int nn = n - 1;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = blockIdx.x * TB + tid;
+	typename Elem<ET>::T vm = 0;
+	if(k < nn) vm = D[tri(nn) + k];
+	const double sDm = b.sD[nn];
+	const int Nm = b.N[nn];
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need;
+			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j;
+	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = s_nj;
+		if(i != nn) {
+			b.sD[i] = sDm;
+			b.N[i] = Nm;
+		}
+		if(s_serial) ctl->serial_sums++;
+	}
+	if(i != nn) {
+		if(k < i) {
+			D[tri(i) + k] = vm;
+		} else if(k > i && k < nn) {
+			D[tri(k) + i] = vm;
+		}
 	}
 }
 
 // ------------------------------------------------------------------ host
-static inline unsigned cdiv(long long a, long long b) { return (unsigned) ((a + b - 1) / b); }
-
 struct TreeWork {
 	TreeBufs b;
 	void *mem;
@@ -1219,20 +1783,24 @@ struct TreeWork {
 
 static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
-	const size_t maxunits = (size_t) DNJ_B * (cdiv(n, SEG) + 1);
-	const size_t nslices = (size_t) cdiv(n, RPB) + 1;
-	const size_t nq = 4096;
+	const size_t maxu = cdiv(n, SEG) + 1;
+	// every row below S may qualify: room for n entries and their units
+	const size_t ncand = (size_t) n + 257;
+	const size_t cunits = (size_t) n * ((size_t) n / SEG + 1) / 2 + (size_t) n + 256;
+	const size_t nq = NJ_BLOCKS;
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
 		size_t off = sz;
 		sz += (bytes + 255) & ~(size_t) 255;
 		return off;
 	};
-	size_t o_sD = take(n * 8), o_Q = take(n * 8), o_fq = take(n * 8), o_c = take(n * 8);
-	size_t o_N = take(n * 4), o_P = take(n * 4), o_fj = take(n * 4);
-	size_t o_S = take(DNJ_B * 4), o_uo = take((DNJ_B + 1) * 4);
-	size_t o_uq = take(maxunits * 8), o_uj = take(maxunits * 4);
-	size_t o_br = take(nslices * RPB * 4), o_bc = take(nslices * 4);
+	size_t o_sD = take((n + 1) * 8), o_Q = take((n + 1) * 8), o_c = take((n + 1) * 8);
+	size_t o_N = take((n + 1) * 4), o_P = take((n + 1) * 4);
+	size_t o_S = take(DNJ_B * 4), o_uo = take((DNJ_B + 1) * 4), o_Sb = take(DNJ_B * 8);
+	size_t o_uq = take(DNJ_B * maxu * 8), o_uj = take(DNJ_B * maxu * 4);
+	size_t o_Se = take(DNJ_B * sizeof(Entry));
+	size_t o_cr = take(ncand * 4), o_cb = take(ncand * 8), o_co = take(ncand * 4);
+	size_t o_cq = take(cunits * 8), o_cj = take(cunits * 4);
 	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
 	size_t o_qp = take((nb > nq ? nb : nq) * 4 * 8), o_ip = take((nb > nq ? nb : nq) * 4 * 4);
 	size_t o_fp = take(nq * 8);
@@ -1244,17 +1812,20 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	TreeBufs &b = w->b;
 	b.sD = (double *) (m + o_sD);
 	b.Q = (double *) (m + o_Q);
-	b.fq = (double *) (m + o_fq);
 	b.contrib = (double *) (m + o_c);
 	b.N = (int *) (m + o_N);
 	b.P = (int *) (m + o_P);
-	b.fj = (int *) (m + o_fj);
 	b.S = (int *) (m + o_S);
 	b.uoff = (int *) (m + o_uo);
+	b.Sb = (double *) (m + o_Sb);
 	b.uq = (double *) (m + o_uq);
 	b.uj = (int *) (m + o_uj);
-	b.blk_rows = (int *) (m + o_br);
-	b.blk_cnt = (int *) (m + o_bc);
+	b.Sent = (Entry *) (m + o_Se);
+	b.crow = (int *) (m + o_cr);
+	b.cbnd = (double *) (m + o_cb);
+	b.cq = (double *) (m + o_cq);
+	b.coff = (int *) (m + o_co);
+	b.cj = (int *) (m + o_cj);
 	b.wsum = (double *) (m + o_ws);
 	b.wabs = (double *) (m + o_wa);
 	b.wcnt = (int *) (m + o_wc);
@@ -1264,6 +1835,7 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.fpart = (long long *) (m + o_fp);
 	b.joins = (ccg_join *) (m + o_j);
 	b.ctl = (TreeCtl *) (m + o_ctl);
+	b.maxu = (int) maxu;
 	return CCG_OK;
 }
 
@@ -1314,38 +1886,41 @@ struct KTimer {
 	}
 };
 
-// One join's kernels, for a matrix of (at most) n taxa.
-template <int ET>
-static void enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n,
-                              int method, bool general, KTimer &kt) {
+// One join's kernels for a matrix of n taxa; returns the launch count.
+template <int ET, bool GEN>
+static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first,
+                             int method, KTimer &kt) {
+	const unsigned gn = cdiv(n, TB);
+	const int general = GEN;
 	if(method == CCG_TREE_DNJ) {
-		k_dnj_top<ET><<<TOP_BLOCKS, TB, 0, st>>>(D, bs, b);
+		unsigned gs = DNJ_B * cdiv(n - 1, SEG);
+		if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
+		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first);
 		kt.mark(CCG_K_TOP);
-		unsigned g2 = cdiv(n, RPB);
-		if(g2 > 2048) g2 = 2048;
-		k_dnj_rest<ET><<<g2, TB, 0, st>>>(D, bs, b);
+		unsigned gc = cdiv(n, 16);
+		if(gc > SCAN_BLOCKS) gc = SCAN_BLOCKS;
+		k_dnj_find<<<1, TBF, 0, st>>>(b, n);
+		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_REST);
-	} else {
-		long long cells = tri(n);
-		unsigned g = cdiv(cells, 8 * TB);
-		if(g > 2048) g = 2048;
-		if(g < 1) g = 1;
-		k_nj_argmin<ET><<<g, TB, 0, st>>>(D, bs, b);
-		kt.mark(CCG_K_ARGMIN);
-	}
-	if(general) {
-		k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b);
-	} else {
-		k_update<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
-	}
-	kt.mark(CCG_K_UPDATE);
-	if(method == CCG_TREE_DNJ) {
-		k_dnj_requeue<ET><<<cdiv(n, TB), TB, 0, st>>>(D, bs, b);
+		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+		kt.mark(CCG_K_UPDATE);
+		k_dnj_requeue<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
-	} else {
-		k_nj_pop<ET><<<cdiv(n, TB), TB, 0, st>>>(D, b);
-		kt.mark(CCG_K_POP);
+		return GEN ? 6 : 5;
 	}
+	long long cells = tri(n);
+	unsigned g = cdiv(cells, 8 * TB);
+	if(g > NJ_BLOCKS) g = NJ_BLOCKS;
+	if(g < 1) g = 1;
+	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
+	kt.mark(CCG_K_ARGMIN);
+	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general);
+	if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+	kt.mark(CCG_K_UPDATE);
+	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general);
+	kt.mark(CCG_K_POP);
+	return GEN ? 4 : 3;
 }
 
 template <int ET>
@@ -1362,7 +1937,6 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	TreeBufs b = w.b;
 	TreeCtl init;
 	memset(&init, 0, sizeof(init));
-	init.n = n0;
 	init.neg = (a->flags & 2) != 0;
 	init.exact = a->exact != 0;
 	init.method = a->method;
@@ -1371,11 +1945,12 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	static KTimer kt;
 	CCG_CHECK(hipEventRecord(ctx->ev0, st));
 	kt.init(st, a->profile != 0);
-	k_init_sums<ET><<<cdiv(n0, TB), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
-	++launches;
+	k_init_rows<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
+	k_init_cols<ET><<<cdiv(n0, TB), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
+	launches += 2;
 	if(a->method == CCG_TREE_DNJ) {
 		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.Q, b.P);
-		k_dnj_prep<<<1, TB, 0, st>>>(b);
+		k_dnj_prep<<<1, TB, 0, st>>>(b, n0);
 		launches += 2;
 	}
 	kt.mark(CCG_K_INIT);
@@ -1384,28 +1959,76 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 	CCG_CHECK(hipStreamSynchronize(st));
 	const bool general = h.has_missing != 0;
+#ifdef CCG_TRACE
+	const char *tn = getenv("CCG_TRACE_N");
+	int trace_hi = tn ? atoi(tn) : n0 / 2;
+	CCG_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_trace_hi), &trace_hi, sizeof(int), 0, hipMemcpyHostToDevice, st));
+	static unsigned long long zero_tr[256 * 4 * 16];
+	CCG_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_trace), zero_tr, sizeof(zero_tr), 0, hipMemcpyHostToDevice, st));
+#endif
 	int n = n0;
 	int since_check = 0;
-	while(n != 2) {
-		enqueue_iteration<ET>(st, D, bs, b, n, a->method, general, kt);
-		launches += a->method == CCG_TREE_DNJ ? 4 : 3;
+	bool stopped = false;
+	while(n > 2) {
+		launches += general ? enqueue_iteration<ET, true>(st, D, bs, b, n, n == n0, a->method, kt)
+		                    : enqueue_iteration<ET, false>(st, D, bs, b, n, n == n0, a->method, kt);
 		CCG_CHECK(hipGetLastError());
 		--n;
 		if(++since_check == 1024) {
 			since_check = 0;
 			CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 			CCG_CHECK(hipStreamSynchronize(st));
-			if(h.done) break;
+			if(h.done) {
+				stopped = true;
+				break;
+			}
 		}
 	}
+	(void) stopped;
 	CCG_CHECK(hipEventRecord(ctx->ev1, st));
 	kt.finish();
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 	CCG_CHECK(hipStreamSynchronize(st));
 	float ms = 0;
 	CCG_CHECK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+#ifdef CCG_TRACE
+	{
+		static unsigned long long tr[256 * NKT * 16];
+		CCG_CHECK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_trace), sizeof(tr), 0, hipMemcpyDeviceToHost));
+		const int nk = a->method == CCG_TREE_DNJ ? NKT : 0;   // NJ kernels are not stamped
+		// per kernel: min block entry (15, stored inverted), block-0 phases (0..8), max block exit (14);
+		// times in us relative to the kernel's first block entry, averaged over joins
+		double acc[NKT][16] = {{0}}, gap[NKT] = {0}, itv = 0;
+		int cnt = 0;
+		for(int s = 0; s < 256; ++s) {
+			const unsigned long long *e = tr + s * NKT * 16;
+			bool ok = true;
+			for(int k = 0; k < nk; ++k) ok = ok && e[k * 16 + 15] && e[k * 16 + 14];
+			if(!ok) continue;
+			++cnt;
+			for(int k = 0; k < nk; ++k) {
+				unsigned long long t0 = ~e[k * 16 + 15];
+				for(int p = 0; p < 15; ++p)
+					if(e[k * 16 + p]) acc[k][p] += ((double) e[k * 16 + p] - (double) t0) / 100.0;
+				if(k) gap[k] += ((double) t0 - (double) e[(k - 1) * 16 + 14]) / 100.0;
+			}
+			if(s + 1 < 256 && tr[(s + 1) * NKT * 16 + 15]) {
+				gap[0] += ((double) ~tr[(s + 1) * NKT * 16 + 15] - (double) e[(nk - 1) * 16 + 14]) / 100.0;
+				itv += ((double) ~tr[(s + 1) * NKT * 16 + 15] - (double) ~e[15]) / 100.0;
+			}
+		}
+		const char *kn[NKT] = {"select", "find", "scan", "join", "requeue"};
+		fprintf(stderr, "trace: %d joins at n <= %d; iteration %.2f us; serial replays %d, serial sums %d\n", cnt,
+		        trace_hi, cnt ? itv / (cnt - 1) : 0, h.serial_replays, h.serial_sums);
+		for(int k = 0; k < nk && cnt; ++k) {
+			fprintf(stderr, "  %-14s gap-before %6.2f  span %6.2f  block0:", kn[k], gap[k] / cnt, acc[k][14] / cnt);
+			for(int p = 0; p < 9; ++p) fprintf(stderr, " %6.2f", acc[k][p] / cnt);
+			fprintf(stderr, "\n");
+		}
+	}
+#endif
 	*njoins = h.njoins;
-	*final_n = h.done ? h.final_n : h.n;
+	*final_n = h.done ? h.final_n : 2;
 	if(h.njoins) {
 		CCG_CHECK(hipMemcpyAsync(joins, b.joins, (size_t) h.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
 	}

@@ -18,7 +18,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(HERE, "lib")
-ENGINE_PATH = os.path.join(LIBDIR, "libccphylo_amd.so")
+# CCPHYLO_AMD_ENGINE: alternative engine build (e.g. the phase-stamp diagnostic one)
+ENGINE_PATH = os.environ.get("CCPHYLO_AMD_ENGINE") or os.path.join(LIBDIR, "libccphylo_amd.so")
 HOST_PATH = os.path.join(LIBDIR, "libccphylo_host.so")
 CLI_PATH = os.path.join(HERE, "bin", "ccphylo")
 

@@ -3,15 +3,8 @@ import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import ccphylo_amd as cg
+from tools.synth import euclid
 
-def euclid(n, seed=1, dim=8):
-    rng = np.random.default_rng(seed)
-    pts = rng.random((n, dim))
-    D = np.empty(n * (n - 1) // 2)
-    for i in range(1, n):
-        o = i * (i - 1) // 2
-        D[o:o + i] = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
-    return np.round(D * 1e9) / 1e9
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 what = sys.argv[2] if len(sys.argv) > 2 else "all"
@@ -24,6 +17,12 @@ for method, exact in [(1, True), (1, False), (0, True)]:
     t = time.time()
     joins, fn, fd, st = dev.tree(D, n, method=method, exact=exact)
     w = time.time() - t
+    _, _, _, sp = dev.tree(D, n, method=method, exact=exact, profile=True)
+    parts = []
+    for c, name in enumerate(cg.native.KSTAT_NAMES):
+        if sp[4 + 2 * c]:
+            parts.append(f"{name} {sp[5 + 2 * c] / sp[4 + 2 * c] / 1e3:.2f}us x{sp[4 + 2 * c]}")
+    print("   per-kernel avg: " + ", ".join(parts), flush=True)
     print(f"{'dnj' if method else 'nj'} exact={exact}: wall {w:.3f}s device {st[3]/1e6:.3f}s joins {len(joins)} "
           f"-> {len(joins)/(st[3]/1e6):.0f} joins/s; rows {st[0]} cells {st[1]} launches {st[2]}", flush=True)
 # dist
