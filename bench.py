@@ -15,8 +15,10 @@ divided by the max over ranks of the timed span.
 
 Also reported: the dominant kernel's roofline (HIP-event timing of every
 kernel in one profiled extra step on the engine stream; algorithmic bytes as
-defined in DESIGN.md), the reference CPU path on the same matrix (rank 0,
-N=1), and extras (exact-row-sum mode, -m nj, and SNP `dist` throughput).
+defined in DESIGN.md; `traffic` from the committed rocprofv3 PMC summary of
+the same kernel, profiles/r01_pmc.json, when present), the reference CPU path
+on the same matrix (rank 0, N=1), and extras (exact-row-sum mode, -m nj, and
+SNP `dist` throughput).
 """
 import argparse
 import json
@@ -34,31 +36,48 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
-KNAMES = ["init", "dnj_top", "dnj_rest", "nj_argmin", "update", "dnj_requeue", "nj_pop"]
+KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
 
 
-def euclid_ltd(n, seed=1, dim=8):
-    """Distances of n points U[0,1)^dim, quantized like a %.9f Phylip."""
-    rng = np.random.default_rng(seed)
-    pts = rng.random((n, dim))
-    D = np.empty(n * (n - 1) // 2)
-    for i in range(1, n):
-        o = i * (i - 1) // 2
-        D[o:o + i] = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
-    return np.round(D * 1e9) / 1e9
+from tools.synth import euclid as euclid_ltd  # noqa: E402
 
 
-def algorithmic_bytes(kernel, n_join, s, cells):
-    """Compulsory HBM bytes of one launch ('Roofline accounting')."""
-    if kernel in ("dnj_top", "dnj_rest"):
-        return s * cells + 12.0 * n_join          # rescanned D cells + N/sD once
-    if kernel == "nj_argmin":
-        return s * n_join * (n_join - 1) / 2 + 12.0 * n_join
-    if kernel in ("update", "dnj_requeue"):
-        return 3.0 * s * n_join + 24.0 * n_join   # rows/cols i, j (+ moved row) and the n-vectors
-    if kernel == "nj_pop":
-        return 2.0 * s * n_join
+def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan):
+    """Compulsory HBM bytes of all launches of one class over a whole tree
+    (joins at matrix sizes n .. 3); DESIGN.md, 'Roofline accounting'.
+    s = bytes per D element; the n-vectors are f64 (sD, Q) and i32 (N, P)."""
+    sizes = range(3, n + 1)
+    sn = float(sum(sizes))
+    if kernel == "dnj_select":      # rescanned D cells of S + the sD vector once
+        return s * cells_select + 8.0 * sn
+    if kernel == "dnj_scan":        # rescanned D cells below S + the sD vector once
+        return s * cells_scan + 8.0 * sn
+    if kernel == "dnj_find":        # Q below S
+        return 8.0 * sn
+    if kernel == "nj_argmin":       # every LT cell + sD
+        return sum(s * k * (k - 1) / 2 + 8.0 * k for k in sizes)
+    if kernel == "update":          # D_ik, D_kj read, D_kj written; sD, N read+written
+        return (3.0 * s + 24.0) * sn
+    if kernel == "dnj_requeue":     # row/col j, row n-1 read; row/col i written; Q, P, sD, N
+        return (4.0 * s + 36.0) * sn
+    if kernel == "nj_pop":          # row n-1 read, row/col i written
+        return 2.0 * s * sn
+    if kernel == "init":            # two passes over the LT
+        return 2.0 * s * n * (n - 1) / 2
     return 0.0
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (FETCH_SIZE and WRITE_SIZE passes, corrected as MI355X_MICROARCH.md says)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        k = d["kernels"].get(kernel)
+        return (k["hbm_bytes_per_launch"], d["source"]) if k else (None, None)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def roofline(stats, n, s):
@@ -70,46 +89,55 @@ def roofline(stats, n, s):
             per[name] = (cnt, ns)
     name = max(per, key=lambda k: per[k][1])
     cnt, ns = per[name]
-    cells = stats[4 + 2 * len(KNAMES)] if name == "dnj_top" else stats[5 + 2 * len(KNAMES)]
-    # mean n over the joins (n runs from N down to 3)
-    if name == "nj_argmin":
-        tot = sum(algorithmic_bytes(name, k, s, 0) for k in range(3, n + 1))
-    elif name in ("dnj_top", "dnj_rest"):
-        tot = s * cells + 12.0 * sum(range(3, n + 1))
-    elif name == "init":
-        tot = 2 * s * n * (n - 1) / 2
-    else:
-        tot = sum(algorithmic_bytes(name, k, s, 0) for k in range(3, n + 1))
+    tot = algorithmic_bytes_total(name, n, s, stats[4 + 2 * len(KNAMES)], stats[5 + 2 * len(KNAMES)])
     avg_s = ns / cnt / 1e9
     achieved = tot / cnt / avg_s / 1e9
     shares = {k: round(v[1] / sum(x[1] for x in per.values()), 4) for k, v in per.items()}
-    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-            "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
-            "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares}
+    traffic, src = pmc_traffic(name)
+    out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+           "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
+           "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares}
+    if src:
+        out["traffic_source"] = src
+    return out
 
 
-def cpu_baseline(D, n, tmpdir):
+def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
     """The reference binary (oracle/_ref, built from /root/reference by
-    oracle/Makefile) on the same matrix written as Phylip, 1 thread; falls back
-    to the oracle's C restatement in-process."""
+    oracle/Makefile) on the same matrix written as Phylip, with 1 and 16
+    pthreads (`-t`, the box's CPU share); the faster is the baseline.  Falls
+    back to the oracle's C restatement in-process."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
     if os.path.exists(ref):
         from ccphylo_amd import native
         path = os.path.join(tmpdir, "bench_ref.phy")
         native.write_phylip(path, D, n, [f"t{k}" for k in range(n)])
-        t0 = time.perf_counter()
-        p = subprocess.run([ref, "tree", "-i", path, "-m", "dnj", "-t", "1", "-o", os.path.join(tmpdir, "ref.nwk")],
-                           capture_output=True, text=True, timeout=900)
-        wall = time.perf_counter() - t0
-        m = re.search(r"Constructing tree: ([0-9.]+) s", p.stderr)
-        ld = re.search(r"loading matrix: ([0-9.]+) s", p.stderr)
-        cons = float(m.group(1)) if m else wall
+        runs = {}
+        for t in threads:
+            t0 = time.perf_counter()
+            p = subprocess.run([ref, "tree", "-i", path, "-m", "dnj", "-t", str(t), "-o",
+                                os.path.join(tmpdir, "ref.nwk")], capture_output=True, text=True, timeout=900)
+            wall = time.perf_counter() - t0
+            # the reference reports clock() (CPU time summed over threads), so
+            # the construction rate uses the process wall clock minus its load
+            ld = re.search(r"loading matrix: ([0-9.]+) s", p.stderr)
+            load = float(ld.group(1)) if ld else 0.0
+            cons = max(wall - load, 1e-9) if t > 1 else None
+            m = re.search(r"Constructing tree: ([0-9.]+) s", p.stderr)
+            if cons is None:
+                cons = float(m.group(1)) if m else wall
+            runs[t] = (cons, wall, load)
         os.unlink(path)
-        return {"value": round((n - 2) / cons, 2), "unit": "NJ joins/s", "cores": 1, "kind": "reference",
-                "sample": f"full N={n} DNJ tree, reference ccphylo 0.8.5 `tree -m dnj -t 1` on the same matrix "
-                          f"(Phylip %.9f); construction {cons:.2f} s (its own clock() report), "
-                          f"Phylip load {float(ld.group(1)) if ld else -1:.2f} s, process wall {wall:.2f} s"}
+        best = min(runs, key=lambda t: runs[t][0])
+        cons, wall, load = runs[best]
+        desc = "; ".join(f"-t {t}: construction {c:.2f} s, load {l:.2f} s, wall {w:.2f} s"
+                         for t, (c, w, l) in sorted(runs.items()))
+        return {"value": round((n - 2) / cons, 2), "unit": "NJ joins/s", "cores": best, "kind": "reference",
+                "sample": f"full N={n} DNJ tree, reference ccphylo 0.8.5 `tree -m dnj` on the same matrix "
+                          f"(Phylip %.9f), best of {list(threads)} pthreads ({desc}); 1-thread time is the "
+                          f"reference's own 'Constructing tree' report, multi-thread time is process wall "
+                          f"minus its 'loading matrix' report"}
     from oracle import pyoracle
     t0 = time.perf_counter()
     j, _, _ = pyoracle.tree(D, n, method=1)

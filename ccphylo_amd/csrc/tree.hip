@@ -1900,6 +1900,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		unsigned gc = cdiv(n, 16);
 		if(gc > SCAN_BLOCKS) gc = SCAN_BLOCKS;
 		k_dnj_find<<<1, TBF, 0, st>>>(b, n);
+		kt.mark(CCG_K_FIND);
 		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_REST);
 		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general);

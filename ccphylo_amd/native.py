@@ -27,8 +27,8 @@ ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
 
 CCG_TREE_NJ = 0
 CCG_TREE_DNJ = 1
-NKSTAT = 7
-KSTAT_NAMES = ["init", "dnj_top", "dnj_rest", "nj_argmin", "update", "dnj_requeue", "nj_pop"]
+NKSTAT = 8
+KSTAT_NAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
 
 
 class CcgError(RuntimeError):

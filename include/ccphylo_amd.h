@@ -102,13 +102,14 @@ typedef struct {
  * [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT] cells rescanned by
  * CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST.  Classes: */
 #define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
-#define CCG_K_TOP      1   /* DNJ: rescans of the top candidate rows */
-#define CCG_K_REST     2   /* DNJ: bounded rescans + replay of minQpair */
+#define CCG_K_TOP      1   /* DNJ k_dnj_select: requeue fold, top rows S, their rescans */
+#define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the rows below S with Q < U */
 #define CCG_K_ARGMIN   3   /* NJ: full Q argmin (initQ) */
-#define CCG_K_UPDATE   4   /* updateD */
+#define CCG_K_UPDATE   4   /* updateD (DNJ: after minQpair's replay; NJ: after the argmin fold) */
 #define CCG_K_REQUEUE  5   /* DNJ: updateDNJ Q/P + DNJ_popArrange */
 #define CCG_K_POP      6   /* NJ: ltdMatrix_popArrange */
-#define CCG_NKSTAT     7
+#define CCG_K_FIND     7   /* DNJ k_dnj_find: bound U and the rows below S under it */
+#define CCG_NKSTAT     8
 
 /* D: host LT (n(n-1)/2 elements), left unmodified.  joins: room for n-2.
  * On return *njoins joins were made; *final_n is the matrix size at exit

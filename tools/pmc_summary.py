@@ -1,0 +1,65 @@
+"""Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE),
+corrected as MI355X_MICROARCH.md's HBM section prescribes, written to a JSON
+summary that bench.py reads for roofline.traffic.
+
+    python tools/pmc_summary.py gpurun_out/prof_r01 profiles/r01_pmc.json
+
+FETCH_SIZE/WRITE_SIZE are in KiB per dispatch.  FETCH_SIZE counts 64 B per
+128-B memory request on gfx950 (half the bytes of a coalesced streaming
+read); the factor 2 was re-checked for this engine's 8-byte-per-lane loads
+with tools/micro/rescan.hip (known D bytes: 256 rows x 9000 x 8 B = 18000 KiB
+-> FETCH_SIZE 9063 KiB), see the 'calibration' entry.  WRITE_SIZE is taken
+as reported (exact for streaming stores; this engine's scattered 8-byte
+column stores are uncalibrated)."""
+import csv
+import json
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+NAMES = {"k_dnj_select": "dnj_select", "k_dnj_find": "dnj_find", "k_dnj_scan": "dnj_scan",
+         "k_dnj_join": "update", "k_dnj_requeue": "dnj_requeue", "k_nj_argmin": "nj_argmin",
+         "k_nj_join": "update", "k_nj_pop": "nj_pop"}
+
+
+def per_kernel(path):
+    d = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        m = re.match(r"(?:void )?(\w+)", r["Kernel_Name"])
+        d[m.group(1)].append(float(r["Counter_Value"]) * 1024.0)
+    return d
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    fetch = per_kernel(f"{src}/pmc_fetch/run_counter_collection.csv")
+    write = per_kernel(f"{src}/pmc_write/run_counter_collection.csv")
+    kernels = {}
+    for k, label in NAMES.items():
+        if k not in fetch:
+            continue
+        f = 2.0 * statistics.mean(fetch[k])
+        w = statistics.mean(write.get(k, [0.0]))
+        kernels[label] = {"kernel": k, "launches": len(fetch[k]), "fetch_bytes_per_launch": round(f, 1),
+                          "write_bytes_per_launch": round(w, 1), "hbm_bytes_per_launch": round(f + w, 1)}
+    cal = {}
+    for r in csv.DictReader(open(f"{src}/pmc_cal/run_counter_collection.csv")):
+        if "k_rescan<256, 8, false>" in r["Kernel_Name"] and r["Grid_Size"] == "327680":
+            cal.setdefault("fetch_kib", []).append(float(r["Counter_Value"]))
+    calib = None
+    if cal:
+        kib = statistics.mean(cal["fetch_kib"])
+        calib = {"kernel": "tools/micro/rescan.hip k_rescan<256,8,false>, 256 rows x 9000 f64",
+                 "known_read_kib": 256 * 9000 * 8 / 1024.0, "fetch_size_kib": round(kib, 1),
+                 "ratio": round(kib / (256 * 9000 * 8 / 1024.0), 4)}
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                     f"tools/perf_dnj.py 10000 dnj (fast sums); FETCH_SIZE x2 per MI355X_MICROARCH.md",
+           "kernels": kernels, "calibration": calib}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
