@@ -195,6 +195,29 @@ __device__ __forceinline__ void qarg_wave_reduce(double &q, int &idx) {
 	idx = __builtin_amdgcn_readlane(idx, 63);
 }
 
+// the same, carrying a payload (cq, cp) of the winning element
+__device__ __forceinline__ void qarg_wave_reduce_carry(double &q, int &idx, double &cq, int &cp) {
+#define S_(C, R)                                          \
+	{                                                     \
+		const double oq_ = dpp_d<C, R>(DBL_MAX, q);       \
+		const int oi_ = dpp_i<C, R>(INT32_MIN, idx);      \
+		const double ocq_ = dpp_d<C, R>(DBL_MAX, cq);     \
+		const int ocp_ = dpp_i<C, R>(0, cp);              \
+		if(qarg_better(oq_, oi_, q, idx)) {               \
+			q = oq_;                                      \
+			idx = oi_;                                    \
+			cq = ocq_;                                    \
+			cp = ocp_;                                    \
+		}                                                 \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	q = readlane_d(q, 63);
+	idx = __builtin_amdgcn_readlane(idx, 63);
+	cq = readlane_d(cq, 63);
+	cp = __builtin_amdgcn_readlane(cp, 63);
+}
+
 // block-wide (q, idx) reduce; result valid in every thread.  `sq`/`si` are
 // LDS scratch of blockDim/64 entries.
 __device__ __forceinline__ void qarg_block_reduce(double &q, int &idx, double *sq, int *si) {

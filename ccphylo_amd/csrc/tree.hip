@@ -52,7 +52,7 @@
 #define TBF 1024         // threads of k_dnj_find (one block)
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
-#define CNT_CHUNK 2048   // slice counts staged in LDS at once
+#define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
 #define NJ_BLOCKS 2048   // max grid of k_nj_argmin
 
 // one candidate row of minQpair: fresh (q, j) and its stale bound Q[row]
@@ -68,6 +68,8 @@ struct TreeCtl {
 	int i, j;            // current join
 	double Li, Lj, Dij;
 	int cand;            // minQpair's candidate row
+	double cand_q;       // Q/P of the first candidate (k_dnj_prep)
+	int cand_p;
 	int pos_i, pos_j;    // minQpair's initial pos
 	int nS, smin;        // |S| and its lowest row (1 when |S| < DNJ_B)
 	int T;               // rows found below S
@@ -95,6 +97,8 @@ struct TreeBufs {
 	int *wcnt, *wexp;    // per-block count / min exponent of the contributions
 	double *qpart;       // 4 (q, idx) partials per block
 	int *ipart;
+	double *cfq;         // requeue: final (Q, P) of the row of each block's
+	int *cfp;            // column-j (q, idx) partial, carried to the fold
 	long long *fpart;
 	ccg_join *joins;
 	TreeCtl *ctl;
@@ -243,21 +247,18 @@ __device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__re
 			nk[m] = GEN ? N[c] : Nr;
 			sk[m] = sD[c];
 		}
+		// branch-free (no use of a loaded value under a condition, so the
+		// compiler cannot sink a load behind the first wait)
 #pragma unroll
 		for(int m = 0; m < UNR; ++m) {
-			int c = base + m * NT + (int) threadIdx.x;
-			if(c < c1) {
-				double d = Elem<ET>::get(v[m], bs);
-				int Nc = c == isub ? Nm : nk[m];
-				double sc = c == isub ? sDm : sk[m];
-				if(0 <= d) {
-					double x = qcrit(Nr, Nc, d, sDr, sc);
-					if(qarg_better(x, c, q, idx)) {
-						q = x;
-						idx = c;
-					}
-				}
-			}
+			const int c = base + m * NT + (int) threadIdx.x;
+			const double d = Elem<ET>::get(v[m], bs);
+			const int Nc = c == isub ? Nm : nk[m];
+			const double sc = c == isub ? sDm : sk[m];
+			const double x = qcrit(Nr, Nc, d, sDr, sc);
+			const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+			q = take ? x : q;
+			idx = take ? c : idx;
 		}
 	}
 }
@@ -416,7 +417,11 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 		}
 	}
 	qarg_block_reduce(q, idx, sq, si);
-	if(threadIdx.x == 0) b.ctl->cand = idx;
+	if(threadIdx.x == 0) {
+		b.ctl->cand = idx;
+		b.ctl->cand_q = b.Q[idx];
+		b.ctl->cand_p = b.P[idx];
+	}
 }
 
 // ------------------------------------------------------------------ DNJ select
@@ -442,8 +447,10 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 		const int done = ctl->done;
 		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
 		const int cand0 = first ? ctl->cand : 0;
-		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX};
-		int ix[4] = {0, -1, 0, -1};
+		const double cand0_q = first ? ctl->cand_q : 0.0;
+		const int cand0_p = first ? ctl->cand_p : 0;
+		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, cq1 = DBL_MAX;
+		int ix[4] = {0, -1, 0, -1}, cp1 = 0;
 		if(!first) {
 			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
 			for(int w = lane; w < G; w += 64) {
@@ -454,6 +461,10 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 					if(qarg_better(oq, oi, q[t], ix[t])) {
 						q[t] = oq;
 						ix[t] = oi;
+						if(t == 1) {
+							cq1 = b.cfq[w];
+							cp1 = b.cfp[w];
+						}
 					}
 				}
 			}
@@ -469,15 +480,21 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 		if(done) {
 			if(lane == 0) s_done = 1;
 		} else {
-#pragma unroll
-			for(int t = 0; t < 4; ++t) qarg_wave_reduce(q[t], ix[t]);
+			qarg_wave_reduce(q[0], ix[0]);
+			qarg_wave_reduce_carry(q[1], ix[1], cq1, cp1);
+			qarg_wave_reduce(q[2], ix[2]);
+			qarg_wave_reduce(q[3], ix[3]);
 			const int nn = n;
 			const bool move = !first && i != nn;
 			const int isub = move ? i : -1, jsub = first ? -1 : j;
 			const double Qj = q[0], Qi = q[2];
 			const int Pj = ix[0], Pi = ix[2];
-#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : b.Q[(r)])
-#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : b.P[(r)])
+			// Q/P of the rows minPos can pick, all known without loads: j and
+			// the moved i from the fold; the row lowered through column j with
+			// its final (Q, P) carried by the requeue partials; the row lowered
+			// through the moved row keeps (q[3], i); row 0 keeps DBL_MAX.
+#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : (r) == ix[1] ? cq1 : (r) == ix[3] ? q[3] : DBL_MAX)
+#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : (r) == ix[1] ? cp1 : (r) == ix[3] ? i : 0)
 			int cand;
 			if(first) {
 				cand = cand0;
@@ -498,11 +515,11 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 					cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
 				}
 			}
-			const double Qc = cand ? QSUB(cand) : DBL_MAX;
+			const double Qc = !cand ? DBL_MAX : first ? cand0_q : QSUB(cand);
 			double m0 = DBL_MAX;
 			if(cand && m0 != Qc) m0 = Qc;
 			const int pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
-			const int pos_j = (cand && m0 != DBL_MAX) ? PSUB(cand) : 0;
+			const int pos_j = (cand && m0 != DBL_MAX) ? (first ? cand0_p : PSUB(cand)) : 0;
 #undef QSUB
 #undef PSUB
 			TS(0, 1);
@@ -635,10 +652,21 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
 	const double m0 = ctl->m0;
 	int sr = 0, su = 0;
 	double sb = DBL_MAX;
+	// the first UPRE units of each S row, loaded before their count is known
+	constexpr int UPRE = 8;
+	double uqv[UPRE];
+	int ujv[UPRE];
 	if(tid < DNJ_B) {
 		sr = b.S[tid];
 		sb = b.Sb[tid];
 		su = b.uoff[tid + 1] - b.uoff[tid];
+		const int lim = b.maxu < UPRE ? b.maxu : UPRE;
+#pragma unroll
+		for(int u = 0; u < UPRE; ++u) {
+			const int v = u < lim ? u : lim - 1;
+			uqv[u] = b.uq[tid * b.maxu + v];
+			ujv[u] = b.uj[tid * b.maxu + v];
+		}
 	}
 	const int top = n - 2;
 	double qv[FR];
@@ -652,7 +680,14 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
 	double fq = DBL_MAX;
 	int fj = 0;
 	if(tid < nS) {
-		fold_units(b.uq + tid * b.maxu, b.uj + tid * b.maxu, 0, su, fq, fj);
+#pragma unroll
+		for(int u = 0; u < UPRE; ++u) {
+			if(u < su && qarg_better(uqv[u], ujv[u], fq, fj)) {
+				fq = uqv[u];
+				fj = ujv[u];
+			}
+		}
+		if(su > UPRE) fold_units(b.uq + tid * b.maxu, b.uj + tid * b.maxu, UPRE, su, fq, fj);
 		Entry e;
 		e.f = fq;
 		e.bnd = sb;
@@ -1145,11 +1180,20 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
 	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
 	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact;
+	__shared__ double lq[JOIN_UPRE];
+	__shared__ int lj[JOIN_UPRE];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 	const bool writer = blockIdx.x == 0;
 	TS_ENTRY(3);
 	TS(3, 0);
+	// every thread prefetches rest-unit partials (their count is not known yet)
+#pragma unroll
+	for(int m = 0; m < JOIN_UPRE / TB; ++m) {
+		lq[tid + m * TB] = b.cq[tid + m * TB];
+		lj[tid + m * TB] = b.cj[tid + m * TB];
+	}
+	__syncthreads();
 	if(wid == 0) {
 		// ---- loads independent of the outcome
 		const int done = ctl->done, nS = ctl->nS, T = ctl->T;
@@ -1200,7 +1244,16 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 					const int ua = e0 ? b.coff[e] : c0[m], ub = e0 ? b.coff[e + 1] : c1[m];
 					double q = DBL_MAX;
 					int idx = 0;
-					fold_units(b.cq, b.cj, ua, ub, q, idx);
+					if(ub <= JOIN_UPRE) {
+						for(int u = ua; u < ub; ++u) {
+							if(qarg_better(lq[u], lj[u], q, idx)) {
+								q = lq[u];
+								idx = lj[u];
+							}
+						}
+					} else {
+						fold_units(b.cq, b.cj, ua, ub, q, idx);
+					}
 					e_row[nS + e] = r;
 					e_j[nS + e] = idx;
 					e_b[nS + e] = bnd;
@@ -1407,8 +1460,8 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 template <int ET>
 __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, int general) {
-	__shared__ double sq[4][TB / 64];
-	__shared__ int si[4][TB / 64];
+	__shared__ double sq[4][TB / 64], sfq[TB / 64];
+	__shared__ int si[4][TB / 64], sfp[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
 	TreeCtl *ctl = b.ctl;
@@ -1466,8 +1519,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		Nk = Nj;
 		sDk = sdj;
 	}
-	double rq = DBL_MAX, pq = DBL_MAX, r2q = DBL_MAX, p2q = DBL_MAX;
-	int rj = 0, pk = -1, r2j = 0, p2k = -1;
+	double rq = DBL_MAX, pq = DBL_MAX, r2q = DBL_MAX, p2q = DBL_MAX, fq = DBL_MAX;
+	int rj = 0, pk = -1, r2j = 0, p2k = -1, fp = 0;
 	if(k < n) {
 		if(k < j) {
 			double d = Elem<ET>::get(D[tri(j) + k], bs);
@@ -1509,6 +1562,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				b.Q[k] = qk;
 				b.P[k] = pkk;
 			}
+			fq = qk;    // the row's final (Q, P), carried with (pq, pk)
+			fp = pkk;
 		}
 		if(move && k < i) {
 			D[tri(i) + k] = vm;
@@ -1520,7 +1575,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		}
 	}
 	qarg_wave_reduce(rq, rj);
-	qarg_wave_reduce(pq, pk);
+	qarg_wave_reduce_carry(pq, pk, fq, fp);
 	qarg_wave_reduce(r2q, r2j);
 	qarg_wave_reduce(p2q, p2k);
 	if(lane == 0) {
@@ -1528,6 +1583,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		si[0][wid] = rj;
 		sq[1][wid] = pq;
 		si[1][wid] = pk;
+		sfq[wid] = fq;
+		sfp[wid] = fp;
 		sq[2][wid] = r2q;
 		si[2][wid] = r2j;
 		sq[3][wid] = p2q;
@@ -1535,16 +1592,22 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	}
 	__syncthreads();
 	if(tid < 4) {
-		double q = sq[tid][0];
-		int ix = si[tid][0];
+		double q = sq[tid][0], cq = sfq[0];
+		int ix = si[tid][0], cp = sfp[0];
 		for(int w = 1; w < TB / 64; ++w) {
 			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
 				q = sq[tid][w];
 				ix = si[tid][w];
+				cq = sfq[w];
+				cp = sfp[w];
 			}
 		}
 		b.qpart[4 * blockIdx.x + tid] = q;
 		b.ipart[4 * blockIdx.x + tid] = ix;
+		if(tid == 1) {
+			b.cfq[blockIdx.x] = cq;
+			b.cfp[blockIdx.x] = cp;
+		}
 	}
 	TS(4, 2);
 	TS_EXIT(4);
@@ -1588,39 +1651,36 @@ __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__
 		while(r > 1 && tri(r) > f) --r;
 		while(tri(r + 1) <= f) ++r;
 		long long c = f - tri(r);
-		for(; f < f1; f += 4 * TB) {
-			// four cells of this thread: f, f+TB, f+2TB, f+3TB
-			typename Elem<ET>::T v[4];
-			int nr[4], nc[4];
-			double sr[4], sc[4];
+		constexpr int UNR = 8;
+		for(; f < f1; f += UNR * TB) {
+			// UNR cells of this thread: f, f+TB, ...; clamped addresses and a
+			// branch-free compute keep every load in flight before the first wait
+			typename Elem<ET>::T v[UNR];
+			int nr[UNR], nc[UNR];
+			double sr[UNR], sc[UNR];
 #pragma unroll
-			for(int m = 0; m < 4; ++m) {
-				if(f + m * TB < f1) {
-					v[m] = D[f + m * TB];
-					nr[m] = GEN ? b.N[r] : n;
-					sr[m] = b.sD[r];
-					nc[m] = GEN ? b.N[c] : n;
-					sc[m] = b.sD[c];
-				}
+			for(int m = 0; m < UNR; ++m) {
+				const long long fm = f + m * TB < f1 ? f + m * TB : f1 - 1;
+				const long long cl = c < r ? c : r - 1;   // in bounds past f1 (masked below)
+				v[m] = D[fm];
+				nr[m] = GEN ? b.N[r] : n;
+				sr[m] = b.sD[r];
+				nc[m] = GEN ? b.N[cl] : n;
+				sc[m] = b.sD[cl];
 				c += TB;
-				while(c >= r && r < n) {
+				while(c >= r && r < n - 1) {
 					c -= r;
 					++r;
 				}
 			}
 #pragma unroll
-			for(int m = 0; m < 4; ++m) {
-				long long fm = f + m * TB;
-				if(fm < f1) {
-					double d = Elem<ET>::get(v[m], bs);
-					if(0 <= d) {
-						double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
-						if(q < bq || (q == bq && fm > bf)) {
-							bq = q;
-							bf = fm;
-						}
-					}
-				}
+			for(int m = 0; m < UNR; ++m) {
+				const long long fm = f + m * TB;
+				const double d = Elem<ET>::get(v[m], bs);
+				const double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
+				const bool take = fm < f1 && 0 <= d && (q < bq || (q == bq && fm > bf));
+				bq = take ? q : bq;
+				bf = take ? fm : bf;
 			}
 		}
 	}
@@ -1786,7 +1846,8 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t maxu = cdiv(n, SEG) + 1;
 	// every row below S may qualify: room for n entries and their units
 	const size_t ncand = (size_t) n + 257;
-	const size_t cunits = (size_t) n * ((size_t) n / SEG + 1) / 2 + (size_t) n + 256;
+	size_t cunits = (size_t) n * ((size_t) n / SEG + 1) / 2 + (size_t) n + 256;
+	if(cunits < JOIN_UPRE) cunits = JOIN_UPRE;
 	const size_t nq = NJ_BLOCKS;
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
@@ -1803,7 +1864,7 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_cq = take(cunits * 8), o_cj = take(cunits * 4);
 	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
 	size_t o_qp = take((nb > nq ? nb : nq) * 4 * 8), o_ip = take((nb > nq ? nb : nq) * 4 * 4);
-	size_t o_fp = take(nq * 8);
+	size_t o_fp = take(nq * 8), o_cfq = take(nb * 8), o_cfp = take(nb * 4);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
@@ -1833,6 +1894,8 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.qpart = (double *) (m + o_qp);
 	b.ipart = (int *) (m + o_ip);
 	b.fpart = (long long *) (m + o_fp);
+	b.cfq = (double *) (m + o_cfq);
+	b.cfp = (int *) (m + o_cfp);
 	b.joins = (ccg_join *) (m + o_j);
 	b.ctl = (TreeCtl *) (m + o_ctl);
 	b.maxu = (int) maxu;
