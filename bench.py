@@ -35,7 +35,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+# dist roofline: 32-bit integer VALU, 256 CU x 64 lanes/clk x 2.4 GHz; a
+# 32-position word pair costs 3 instructions (v_xor, v_bitop3, v_bcnt);
+# tools/micro/popc_rate.hip reaches this rate from registers.
+VALU_INT_LANE_OPS = 256 * 64 * 2.4e9
+OPS_PER_WORD_PAIR = 3.0
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
 
@@ -168,11 +172,13 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3):
         times.append(time.perf_counter() - t0)
     dt = min(times)
     words = (L + 31) // 32
-    ops = m * words * 4.0
+    ops = m * words * OPS_PER_WORD_PAIR
     del seqs, incs, Dd
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA (non-pair, double), input in HBM",
-            "valu_frac": round(ops / dt / VALU_LANE_OPS, 4)}
+            "roofline": {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": VALU_INT_LANE_OPS / 1e12,
+                         "unit": "T int lane-ops/s", "frac": round(ops / dt / VALU_INT_LANE_OPS, 4),
+                         "ops_per_word_pair": OPS_PER_WORD_PAIR}}
 
 
 def main():

@@ -10,7 +10,8 @@
 //   hi[t][w] = high code bits, lo[t][w] = low code bits, MSB = first position
 // (the include-mask bit order of fsacmp.c:200).  Non-pair mode pre-applies
 // the global include mask to both planes, so a pair's count is
-//   sum_w popc((hi_a ^ hi_b) | (lo_a ^ lo_b))        -- 4 VALU ops / 32 nt.
+//   sum_w popc((hi_a ^ hi_b) | (lo_a ^ lo_b))        -- 3 VALU ops / 32 nt
+// (v_xor, v_bitop3, v_bcnt with accumulate).
 // Pair mode keeps each taxon's mask m beside its planes:
 //   d += popc(((hi_a ^ hi_b) | (lo_a ^ lo_b)) & m_a & m_b), n += popc(m_a & m_b).
 // This is VALU-integer-bound (no dense contraction, MFMA not used): 128x128
@@ -23,6 +24,12 @@
 #define KCP 8          // words per LDS chunk (pair)
 #define RS 130         // LDS row stride in 8-byte units: 16-byte aligned, 2-way write conflicts at most
 #define RSP 130        // pair: stride in 16-byte units
+
+// (a ^ b) | c in one v_bitop3_b32 (truth table 0xBE, checked on gfx950 by
+// tools/micro/bitop3_check.hip): a word pair costs xor + bitop3 + bcnt
+__device__ __forceinline__ uint32_t xor_or(uint32_t a, uint32_t b, uint32_t c) {
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0xBE);
+}
 
 __device__ __forceinline__ uint32_t compress_even(uint64_t x) {
 	x &= 0x5555555555555555ull;
@@ -78,14 +85,26 @@ __device__ __forceinline__ void tile_ij(long long t, int &I, int &J) {
 	J = (int) (t - r * (r + 1) / 2);
 }
 
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8
+// XCDs, so give XCD x a contiguous run of row-major tiles (tiles (I, J),
+// (I, J+1), ... share the I panel in that XCD's L2).  Bijective on [0, cnt).
+__device__ __forceinline__ long long xcd_tile(long long b, long long cnt) {
+	const long long x = b & 7, k = b >> 3, q = cnt >> 3, r = cnt & 7;
+	return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
+// Non-pair tiles: double-buffered KC-word chunks of both 128-row panels; the
+// next chunk's global loads are in flight while the current one is consumed
+// from LDS, one barrier per chunk.
 template <int ET>
 __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P, int Wp, int n, long long t0,
-                                                     double nFactor, double bs, typename Elem<ET>::T *__restrict__ D,
-                                                     long long rowBegin, long long rowEnd) {
-	__shared__ __attribute__((aligned(16))) uint2 As[KC * RS];
-	__shared__ __attribute__((aligned(16))) uint2 Bs[KC * RS];
+                                                     long long cnt, double nFactor, double bs,
+                                                     typename Elem<ET>::T *__restrict__ D, long long rowBegin,
+                                                     long long rowEnd) {
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
 	int I, J;
-	tile_ij(t0 + blockIdx.x, I, J);
+	tile_ij(t0 + xcd_tile(blockIdx.x, cnt), I, J);
 	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
 	const uint2 *Ap = P + (size_t) I * TILE * Wp;
 	const uint2 *Bp = P + (size_t) J * TILE * Wp;
@@ -94,37 +113,63 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P
 	for(int a = 0; a < 8; ++a)
 #pragma unroll
 		for(int c = 0; c < 8; ++c) acc[a][c] = 0;
-
-	for(int w0 = 0; w0 < Wp; w0 += KC) {
+	// this thread's staging slots: rows e>>3, word pairs 2*(e&7), e = q*256 + tid
+	uint4 va[4], vb[4];
 #pragma unroll
-		for(int q = 0; q < 4; ++q) {
-			int e = q * 256 + threadIdx.x;
-			int row = e >> 3, wp = e & 7;
-			uint4 va = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + 2 * wp);
-			uint4 vb = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + 2 * wp);
-			As[(2 * wp) * RS + row] = make_uint2(va.x, va.y);
-			As[(2 * wp + 1) * RS + row] = make_uint2(va.z, va.w);
-			Bs[(2 * wp) * RS + row] = make_uint2(vb.x, vb.y);
-			Bs[(2 * wp + 1) * RS + row] = make_uint2(vb.z, vb.w);
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + 2 * wp);
+		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+		As[0][(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+		Bs[0][(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+		Bs[0][(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+	}
+	__syncthreads();
+	int buf = 0;
+	for(int w0 = 0; w0 < Wp; w0 += KC, buf ^= 1) {
+		const bool more = w0 + KC < Wp;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + KC + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
+			}
 		}
-		__syncthreads();
-#pragma unroll 2
+		const uint2 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 1
 		for(int w = 0; w < KC; ++w) {
 			uint4 a[4], b[4];
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
-				a[q] = *(const uint4 *) &As[w * RS + 2 * ty + 32 * q];
-				b[q] = *(const uint4 *) &Bs[w * RS + 2 * tx + 32 * q];
+				a[q] = *(const uint4 *) &Ac[w * RS + 2 * ty + 32 * q];
+				b[q] = *(const uint4 *) &Bc[w * RS + 2 * tx + 32 * q];
 			}
 #pragma unroll
 			for(int qa = 0; qa < 4; ++qa) {
 #pragma unroll
 				for(int qb = 0; qb < 4; ++qb) {
-					acc[2 * qa][2 * qb] += __popc((a[qa].x ^ b[qb].x) | (a[qa].y ^ b[qb].y));
-					acc[2 * qa][2 * qb + 1] += __popc((a[qa].x ^ b[qb].z) | (a[qa].y ^ b[qb].w));
-					acc[2 * qa + 1][2 * qb] += __popc((a[qa].z ^ b[qb].x) | (a[qa].w ^ b[qb].y));
-					acc[2 * qa + 1][2 * qb + 1] += __popc((a[qa].z ^ b[qb].z) | (a[qa].w ^ b[qb].w));
+					acc[2 * qa][2 * qb] += __popc(xor_or(a[qa].x, b[qb].x, a[qa].y ^ b[qb].y));
+					acc[2 * qa][2 * qb + 1] += __popc(xor_or(a[qa].x, b[qb].z, a[qa].y ^ b[qb].w));
+					acc[2 * qa + 1][2 * qb] += __popc(xor_or(a[qa].z, b[qb].x, a[qa].w ^ b[qb].y));
+					acc[2 * qa + 1][2 * qb + 1] += __popc(xor_or(a[qa].z, b[qb].z, a[qa].w ^ b[qb].w));
 				}
+			}
+		}
+		if(more) {
+			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+				Bn[(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
 			}
 		}
 		__syncthreads();
@@ -230,7 +275,7 @@ __global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restric
 #pragma unroll
 				for(int y = 0; y < 8; ++y) {
 					uint32_t m = a[x].z & b[y].z;
-					ad[x][y] += __popc(((a[x].x ^ b[y].x) | (a[x].y ^ b[y].y)) & m);
+					ad[x][y] += __popc(xor_or(a[x].x, b[y].x, a[x].y ^ b[y].y) & m);
 					an[x][y] += __popc(m);
 				}
 			}
@@ -268,7 +313,7 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 			k_snp_tile_pair<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>(
 			    (const uint4 *) planes, Wp, a->n, t, a->norm, a->minLength, a->byteScale, (T *) D, (T *) N, rb, re);
 		} else {
-			k_snp_tile<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, nFactor,
+			k_snp_tile<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, cnt, nFactor,
 			                                                       a->byteScale, (T *) D, rb, re);
 		}
 		CCG_CHECK(hipGetLastError());
