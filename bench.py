@@ -35,10 +35,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-# dist roofline: 32-bit integer VALU, 256 CU x 64 lanes/clk x 2.4 GHz; a
-# 32-position word pair costs 3 instructions (v_xor, v_bitop3, v_bcnt);
-# tools/micro/popc_rate.hip reaches this rate from registers.
-VALU_INT_LANE_OPS = 256 * 64 * 2.4e9
+# dist roofline: 32-bit integer VALU issue.  A 32-position word pair costs 3
+# instructions (v_xor, v_bitop3, v_bcnt with accumulate).  Peak = the
+# register-only issue rate of that mix measured by tools/micro/popc_rate.hip
+# on MI355X: 5.31e13 "4-op" lane-ops/s over 208 real instructions per 256
+# counted = 4.31e13 instruction-lanes/s (the nominal 256 CU x 64 lanes x
+# 2.4 GHz = 3.93e13 is exceeded, i.e. the engine clock runs above 2.4 GHz).
+VALU_INT_LANE_OPS = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")

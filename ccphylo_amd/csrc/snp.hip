@@ -95,19 +95,25 @@ __device__ __forceinline__ long long xcd_tile(long long b, long long cnt) {
 
 // Non-pair tiles: double-buffered KC-word chunks of both 128-row panels; the
 // next chunk's global loads are in flight while the current one is consumed
-// from LDS, one barrier per chunk.
-template <int ET>
+// from LDS, one barrier per chunk.  Work item = (tile, word slice): with
+// S > 1 slices (split-K, so small tile counts still fill the chip) the
+// partial counts are summed exactly with u32 atomics into `cnt` and
+// k_snp_finish writes D.
+template <int ET, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P, int Wp, int n, long long t0,
-                                                     long long cnt, double nFactor, double bs,
+                                                     long long items, int S, int Wk, double nFactor, double bs,
                                                      typename Elem<ET>::T *__restrict__ D, long long rowBegin,
-                                                     long long rowEnd) {
+                                                     long long rowEnd, unsigned *__restrict__ cnt, long long cbase) {
 	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
 	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
 	int I, J;
-	tile_ij(t0 + xcd_tile(blockIdx.x, cnt), I, J);
+	const long long item = t0 + xcd_tile(blockIdx.x, items);
+	tile_ij(item / S, I, J);
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
 	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-	const uint2 *Ap = P + (size_t) I * TILE * Wp;
-	const uint2 *Bp = P + (size_t) J * TILE * Wp;
+	const uint2 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint2 *Bp = P + (size_t) J * TILE * Wp + wb;
+	const int Wl = we - wb;   // words of this slice (a multiple of KC)
 	uint32_t acc[8][8];
 #pragma unroll
 	for(int a = 0; a < 8; ++a)
@@ -131,8 +137,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P
 	}
 	__syncthreads();
 	int buf = 0;
-	for(int w0 = 0; w0 < Wp; w0 += KC, buf ^= 1) {
-		const bool more = w0 + KC < Wp;
+	for(int w0 = 0; w0 < Wl; w0 += KC, buf ^= 1) {
+		const bool more = w0 + KC < Wl;
 		if(more) {
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
@@ -184,10 +190,24 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P
 		for(int c = 0; c < 8; ++c) {
 			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
 			if(j < i) {
-				double v = nFactor * (double) acc[a][c];
-				D[base + j] = Elem<ET>::put(v, 0.5, bs);
+				if(SPLIT) {
+					atomicAdd(&cnt[base + j - cbase], acc[a][c]);
+				} else {
+					double v = nFactor * (double) acc[a][c];
+					D[base + j] = Elem<ET>::put(v, 0.5, bs);
+				}
 			}
 		}
+	}
+}
+
+// split-K epilogue: D[f] = nFactor * count (fsacmpthrd.c:247-255)
+template <int ET>
+__global__ void k_snp_finish(const unsigned *__restrict__ cnt, long long cbase, long long f0, long long f1,
+                             double nFactor, double bs, typename Elem<ET>::T *__restrict__ D) {
+	for(long long f = f0 + (long long) blockIdx.x * blockDim.x + threadIdx.x; f < f1;
+	    f += (long long) gridDim.x * blockDim.x) {
+		D[f] = Elem<ET>::put(nFactor * (double) cnt[f - cbase], 0.5, bs);
 	}
 }
 
@@ -302,21 +322,60 @@ template <int ET>
 static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D, void *N,
                       long long rb, long long re) {
 	typedef typename Elem<ET>::T T;
-	int nb = (int) cdivll(a->n, TILE);
 	long long Ilo = rb / TILE, Ihi = (re - 1) / TILE;   // tile rows touching [rb, re)
 	long long t_begin = Ilo * (Ilo + 1) / 2, t_end = (Ihi + 1) * (Ihi + 2) / 2;
-	(void) nb;
 	const long long batch = 1 << 14;
-	for(long long t = t_begin; t < t_end; t += batch) {
-		long long cnt = t_end - t < batch ? t_end - t : batch;
-		if(a->pair) {
+	if(a->pair) {
+		for(long long t = t_begin; t < t_end; t += batch) {
+			long long cnt = t_end - t < batch ? t_end - t : batch;
 			k_snp_tile_pair<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>(
 			    (const uint4 *) planes, Wp, a->n, t, a->norm, a->minLength, a->byteScale, (T *) D, (T *) N, rb, re);
+			CCG_CHECK(hipGetLastError());
+		}
+		return CCG_OK;
+	}
+	// split-K: enough (tile, slice) items that the tail round of resident
+	// blocks (2 per CU) is small; each slice keeps >= 4 chunks
+	hipDeviceProp_t prop;
+	CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+	const long long slots = 2LL * prop.multiProcessorCount;
+	const long long tiles = t_end - t_begin;
+	const int chunks = Wp / KC;
+	int S = 1;
+	if(tiles < 16 * slots) {
+		S = (int) cdivll(16 * slots, tiles);
+		if(S > chunks / 4) S = chunks / 4;
+		if(S < 1) S = 1;
+	}
+	const int Wk = (int) cdivll(chunks, S) * KC;
+	S = (int) cdivll(Wp, Wk);
+	unsigned *cnt = NULL;
+	const long long f0 = tri(rb), f1 = tri(re);
+	if(S > 1) {
+		CCG_CHECK(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)));
+		CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
+	}
+	const long long i_begin = t_begin * S, i_end = t_end * S;
+	for(long long t = i_begin; t < i_end; t += batch) {
+		long long items = i_end - t < batch ? i_end - t : batch;
+		if(S > 1) {
+			k_snp_tile<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, items, S,
+			                                                             Wk, nFactor, a->byteScale, (T *) D, rb, re,
+			                                                             cnt, f0);
 		} else {
-			k_snp_tile<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, cnt, nFactor,
-			                                                       a->byteScale, (T *) D, rb, re);
+			k_snp_tile<ET, false><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, items,
+			                                                              1, Wp, nFactor, a->byteScale, (T *) D, rb,
+			                                                              re, cnt, f0);
 		}
 		CCG_CHECK(hipGetLastError());
+	}
+	if(S > 1) {
+		long long g = cdivll(f1 - f0, 256);
+		k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, f0, f0, f1, nFactor,
+		                                                                                a->byteScale, (T *) D);
+		CCG_CHECK(hipGetLastError());
+		CCG_CHECK(hipStreamSynchronize(ctx->stream));
+		CCG_CHECK(hipFree(cnt));
 	}
 	return CCG_OK;
 }
