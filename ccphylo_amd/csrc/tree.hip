@@ -53,7 +53,6 @@
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
 #define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
-#define NJ_BLOCKS 2048   // max grid of k_nj_argmin
 
 // one candidate row of minQpair: fresh (q, j) and its stale bound Q[row]
 struct Entry {
@@ -1633,54 +1632,76 @@ __device__ __forceinline__ void qf_wave_reduce(double &q, long long &f) {
 
 // ------------------------------------------------------------------ NJ argmin
 // nj.c:182 initQ: min starts at 1, the last minimal cell in row-major order
+// (larger flat index wins ties).  Blocks tile the triangle in NJ_SEG-column
+// segments x NJ_RB-row bands, enumerated segment-major: segment s holds the
+// bands from row s*NJ_SEG on, so block -> (s, band) is closed-form.  A thread
+// keeps its 8 columns' sD in registers for all the band's rows (sD[r] is one
+// scalar per row), so D is the only per-cell stream.
+#define NJ_RB 8
+#define NJ_SEG (TB * 8)
+__host__ __device__ __forceinline__ long long nj_prefix(long long s, long long nb) {
+	return s * nb - (long long) (NJ_SEG / NJ_RB) * s * (s - 1) / 2;
+}
+__host__ __device__ __forceinline__ long long nj_blocks(int n) {
+	const long long nb = (n + NJ_RB - 1) / NJ_RB, nseg = (n - 1 + NJ_SEG - 1) / NJ_SEG;
+	return nj_prefix(nseg, nb);
+}
+
 template <int ET, bool GEN>
 __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                   int n) {
 	__shared__ double sq[TB / 64];
 	__shared__ long long sf[TB / 64];
 	if(b.ctl->done) return;
-	const long long cells = tri(n);
-	const long long chunk = (cells + gridDim.x - 1) / gridDim.x;
-	const long long f0 = (long long) blockIdx.x * chunk;
-	const long long f1 = f0 + chunk < cells ? f0 + chunk : cells;
+	const long long nb = (n + NJ_RB - 1) / NJ_RB;
+	const long long idx = blockIdx.x;
+	long long s = 0;
+	while(nj_prefix(s + 1, nb) <= idx) ++s;
+	const int band = (int) ((NJ_SEG / NJ_RB) * s + (idx - nj_prefix(s, nb)));
+	const int c0 = (int) s * NJ_SEG;
+	constexpr int M = NJ_SEG / TB;
+	double sc[M];
+	int nc[M];
+#pragma unroll
+	for(int m = 0; m < M; ++m) {
+		int c = c0 + m * TB + (int) threadIdx.x;
+		c = c < n ? c : n - 1;
+		sc[m] = b.sD[c];
+		nc[m] = GEN ? b.N[c] : n;
+	}
 	double bq = 1.0;
 	long long bf = -1;
-	if(f0 < f1) {
-		long long f = f0 + threadIdx.x;
-		long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
-		while(r > 1 && tri(r) > f) --r;
-		while(tri(r + 1) <= f) ++r;
-		long long c = f - tri(r);
-		constexpr int UNR = 8;
-		for(; f < f1; f += UNR * TB) {
-			// UNR cells of this thread: f, f+TB, ...; clamped addresses and a
-			// branch-free compute keep every load in flight before the first wait
-			typename Elem<ET>::T v[UNR];
-			int nr[UNR], nc[UNR];
-			double sr[UNR], sc[UNR];
+	const int r0 = band * NJ_RB, r1 = r0 + NJ_RB < n ? r0 + NJ_RB : n;
+	constexpr int G = 4;   // rows per step: G*M loads in flight
+	for(int rg = r0; rg < r1; rg += G) {
+		typename Elem<ET>::T v[G][M];
+		double sr[G];
+		int nr[G];
 #pragma unroll
-			for(int m = 0; m < UNR; ++m) {
-				const long long fm = f + m * TB < f1 ? f + m * TB : f1 - 1;
-				const long long cl = c < r ? c : r - 1;   // in bounds past f1 (masked below)
-				v[m] = D[fm];
-				nr[m] = GEN ? b.N[r] : n;
-				sr[m] = b.sD[r];
-				nc[m] = GEN ? b.N[cl] : n;
-				sc[m] = b.sD[cl];
-				c += TB;
-				while(c >= r && r < n - 1) {
-					c -= r;
-					++r;
-				}
+		for(int g = 0; g < G; ++g) {
+			const int r = rg + g < r1 ? rg + g : r1 - 1;
+			const long long base = tri(r);
+			sr[g] = b.sD[r];
+			nr[g] = GEN ? b.N[r] : n;
+#pragma unroll
+			for(int m = 0; m < M; ++m) {
+				const int c = c0 + m * TB + (int) threadIdx.x;
+				v[g][m] = D[base + (c < r ? c : 0)];
 			}
+		}
 #pragma unroll
-			for(int m = 0; m < UNR; ++m) {
-				const long long fm = f + m * TB;
-				const double d = Elem<ET>::get(v[m], bs);
-				const double q = qcrit(nr[m], nc[m], d, sr[m], sc[m]);
-				const bool take = fm < f1 && 0 <= d && (q < bq || (q == bq && fm > bf));
+		for(int g = 0; g < G; ++g) {
+			const int r = rg + g;
+			const long long base = tri(r);
+#pragma unroll
+			for(int m = 0; m < M; ++m) {
+				const int c = c0 + m * TB + (int) threadIdx.x;
+				const double d = Elem<ET>::get(v[g][m], bs);
+				const double q = qcrit(nr[g], nc[m], d, sr[g], sc[m]);
+				const long long f = base + c;
+				const bool take = r < r1 && c < r && 0 <= d && (q < bq || (q == bq && f > bf));
 				bq = take ? q : bq;
-				bf = take ? fm : bf;
+				bf = take ? f : bf;
 			}
 		}
 	}
@@ -1707,7 +1728,8 @@ __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__
 template <int ET>
 __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
                                                 int G, int general) {
-	__shared__ long long s_bf;
+	__shared__ long long s_bf, s_wf[TB / 64];
+	__shared__ double s_wq[TB / 64];
 	__shared__ int s_stop, s_nj, s_neg, s_exact;
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1718,26 +1740,37 @@ __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict
 		sDk = b.sD[k];
 		Nk = b.N[k];
 	}
-	if(wid == 0) {
-		const int done = ctl->done;
-		double bq = 1.0;
-		long long bf = -1;
-		for(int g = lane; g < G; g += 64) {
-			double oq = b.qpart[g];
-			long long of = b.fpart[g];
-			if(oq < bq || (oq == bq && of > bf)) {
-				bq = oq;
-				bf = of;
+	// fold of the argmin partials by the whole block (G grows as n^2)
+	double fq = 1.0;
+	long long ff = -1;
+	for(int g = tid; g < G; g += TB) {
+		double oq = b.qpart[g];
+		long long of = b.fpart[g];
+		if(oq < fq || (oq == fq && of > ff)) {
+			fq = oq;
+			ff = of;
+		}
+	}
+	qf_wave_reduce(fq, ff);
+	if(lane == 0) {
+		s_wq[wid] = fq;
+		s_wf[wid] = ff;
+	}
+	if(tid == 0) {
+		s_stop = ctl->done;
+		s_nj = ctl->njoins;
+		s_neg = ctl->neg;
+		s_exact = ctl->exact;
+	}
+	__syncthreads();
+	if(tid == 0) {
+		for(int w = 1; w < TB / 64; ++w) {
+			if(s_wq[w] < fq || (s_wq[w] == fq && s_wf[w] > ff)) {
+				fq = s_wq[w];
+				ff = s_wf[w];
 			}
 		}
-		qf_wave_reduce(bq, bf);
-		if(lane == 0) {
-			s_stop = done;
-			s_bf = bf;
-			s_nj = ctl->njoins;
-			s_neg = ctl->neg;
-			s_exact = ctl->exact;
-		}
+		s_bf = ff;
 	}
 	__syncthreads();
 	if(s_stop) return;
@@ -1848,7 +1881,7 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t ncand = (size_t) n + 257;
 	size_t cunits = (size_t) n * ((size_t) n / SEG + 1) / 2 + (size_t) n + 256;
 	if(cunits < JOIN_UPRE) cunits = JOIN_UPRE;
-	const size_t nq = NJ_BLOCKS;
+	const size_t nq = (size_t) nj_blocks(n) + 1;
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
 		size_t off = sz;
@@ -1973,10 +2006,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_REQUEUE);
 		return GEN ? 6 : 5;
 	}
-	long long cells = tri(n);
-	unsigned g = cdiv(cells, 8 * TB);
-	if(g > NJ_BLOCKS) g = NJ_BLOCKS;
-	if(g < 1) g = 1;
+	const unsigned g = (unsigned) nj_blocks(n);
 	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
 	kt.mark(CCG_K_ARGMIN);
 	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general);
