@@ -153,8 +153,13 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
             "sample": f"full N={n} DNJ tree with the oracle's serial C restatement (reference binary absent)"}
 
 
-def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3):
-    """SNP distances (non-pair, double) with device-resident packed input."""
+def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=None):
+    """SNP distances (non-pair, double) with device-resident packed input.
+    With world > 1 the LT rows are sharded over the ranks (SURVEY 8(e):
+    pairs are independent, so no data-path collective): rank g computes rows
+    shard.lt_row_ranges(n, world)[g] of the same matrix; the rate is all
+    pairs over the max time over ranks (strong scaling of one matrix)."""
+    from ccphylo_amd import shard
     W = L // 32 + 1
     g = torch.Generator(device="cuda").manual_seed(3)
     seqs = torch.randint(-2**62, 2**62, (n, W), dtype=torch.int64, device="cuda", generator=g)
@@ -163,22 +168,26 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3):
     if L % 32:
         incs[(L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
     m = n * (n - 1) // 2
+    r0, r1 = shard.lt_row_ranges(n, world)[rank]
     Dd = torch.empty(m, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
-    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), row_range=(r0, r1))
     times = []
     for _ in range(reps):
         torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
         t0 = time.perf_counter()
-        dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
+        dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), row_range=(r0, r1))
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        times.append(shard.reduce_max(dt, dist) if dist is not None else dt)
     dt = min(times)
     words = (L + 31) // 32
-    ops = m * words * OPS_PER_WORD_PAIR
+    ops = m * words * OPS_PER_WORD_PAIR / world   # per GPU
     del seqs, incs, Dd
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
-            "config": f"N={n} x L={L} random MSA (non-pair, double), input in HBM",
+            "config": f"N={n} x L={L} random MSA (non-pair, double), input in HBM, LT rows sharded over {world} GPU(s)",
             "roofline": {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": VALU_INT_LANE_OPS / 1e12,
                          "unit": "T int lane-ops/s", "frac": round(ops / dt / VALU_INT_LANE_OPS, 4),
                          "ops_per_word_pair": OPS_PER_WORD_PAIR}}
@@ -285,11 +294,14 @@ def main():
         _, _, _, nst = dev.tree_dev(pb, n, method=cg.CCG_TREE_NJ, exact=exact, profile=True)
         extras["nj"]["roofline"] = roofline(nst, n, s)
         dev.free(pb)
-        try:
-            extras["dist"] = dist_extra(dev, torch)
-        except Exception as e:  # noqa: BLE001
-            extras["dist"] = {"error": str(e)}
         result["extras"] = extras
+    if not args.no_extras:
+        # every rank takes part (row-sharded dist); rank 0 reports
+        try:
+            d = dist_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None)
+        except Exception as e:  # noqa: BLE001
+            d = {"error": str(e)}
+        result.setdefault("extras", {})["dist"] = d
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)
