@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # 2.4 GHz = 3.93e13 is exceeded, i.e. the engine clock runs above 2.4 GHz).
 VALU_INT_LANE_OPS = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
-KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
+KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
 
 

@@ -1,0 +1,928 @@
+// tree_shard.hip -- NJ (nj.c:1560 loop, -t 1 semantics) over an LT matrix
+// whose rows are split across ranks, one process per GPU.
+//
+// Ownership: bands of CCG_SHARD_BAND (= NJ_RB) rows dealt round-robin; a rank
+// keeps its rows back to back (Shard::off).  sD and N are replicated and every
+// rank updates them identically, so the only exchanges per join are
+//   1. broadcast of row n-1 from its owner (it moves to slot i in the pop,
+//      matrix.c:518), issued first so it overlaps nothing it depends on;
+//   2. the per-rank argmin records (initQ nj.c:182): an allreduce of a
+//      world x 16-byte array in which each rank fills its own slot; every rank
+//      folds the records in rank order with initQ's total order (smaller q,
+//      then larger flat index), so all ranks pick the same (i, j);
+//   3. lines i and j (D_ik, D_jk for every k): each rank contributes the
+//      entries its rows hold and zeros elsewhere, so the bytewise sum is a
+//      gather.  Every rank then computes the whole updated line j
+//      (updateD nj.c:836) and the new row sum of j itself -- with the same
+//      fixed-order partials as the single-GPU engine (ccg_tree_common.h) --
+//      and stores the entries of its own rows.
+// The initial row sums (initSummaD nj.c:111, serial in increasing m) are
+// exact too: owners sum their rows' row parts, and the column parts are
+// continued serially from column chunks gathered the same way.  The joins are
+// therefore bit-identical to ccg_tree's for every world size.
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <rccl/rccl.h>
+#include "ccg_tree_common.h"
+
+#define SB CCG_SHARD_BAND
+static_assert(SB == NJ_RB, "a shard band is one NJ argmin row band");
+#define SH_GRID 2048         // max argmin blocks (grid-stride over the tiles)
+
+struct Shard {
+	int rank, world;
+	__host__ __device__ __forceinline__ bool owns(long long r) const { return (int) ((r / SB) % world) == rank; }
+	// elements before owned row r in the rank's buffer: full owned bands below
+	// r's band (band g holds SB*SB*g + SB*(SB-1)/2 elements), then r's
+	// predecessors in its band
+	__host__ __device__ __forceinline__ long long off(long long r) const {
+		const long long gb = r / SB, t = r - gb * SB, lb = gb / world;
+		return (long long) SB * SB * world * (lb * (lb - 1) / 2) + (long long) SB * SB * rank * lb +
+		       lb * (SB * (SB - 1) / 2) + SB * gb * t + t * (t - 1) / 2;
+	}
+};
+
+struct ShRec {   // one rank's argmin record (q, flat index); zeros in other ranks' slots
+	double q;
+	long long f;
+};
+
+__device__ __forceinline__ void rec_fold(const ShRec *__restrict__ rec, int world, double &bq, long long &bf) {
+	bq = 1.0;
+	bf = -1;
+	for(int w = 0; w < world; ++w) {
+		const double q = rec[w].q;
+		const long long f = rec[w].f;
+		if(f >= 0 && (q < bq || (q == bq && f > bf))) {
+			bq = q;
+			bf = f;
+		}
+	}
+}
+
+__device__ __forceinline__ void flat_to_ij(long long bf, int &i, int &j) {
+	long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) bf)) * 0.5);
+	while(r > 1 && tri(r) > bf) --r;
+	while(tri(r + 1) <= bf) ++r;
+	i = (int) r;
+	j = (int) (bf - tri(r));
+}
+
+// ------------------------------------------------------------------ init
+// initSummaD row parts of the owned rows (the same wave-serial sum as
+// tree.hip's k_init_rows); RP = [n f64 sums][n i32 counts][i32 missing]
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_init_rows(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
+                                                     Shard sh, double *__restrict__ rp, int *__restrict__ rc,
+                                                     int *__restrict__ miss_out) {
+	__shared__ double buf[TB / 64][64];
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int k = blockIdx.x * (TB / 64) + wid;
+	if(k >= n) return;
+	if(!sh.owns(k)) {
+		if(lane == 0) {
+			rp[k] = 0;
+			rc[k] = 0;
+		}
+		return;
+	}
+	double s = 0;
+	int c = 1, miss = 0;
+	const typename Elem<ET>::T *row = D + sh.off(k);
+	for(int m0 = 0; m0 < k; m0 += 64) {
+		int m = m0 + lane;
+		double d = m < k ? Elem<ET>::get(row[m], bs) : 0.0;
+		bool ok = m < k && 0 <= d;
+		miss |= m < k && !ok;
+		c += __popcll(__ballot(ok));
+		buf[wid][lane] = ok ? d : 0.0;
+		__builtin_amdgcn_wave_barrier();
+		if(lane == 0) {
+			int lim = k - m0 < 64 ? k - m0 : 64;
+			for(int u = 0; u < lim; ++u) s += buf[wid][u];
+		}
+		__builtin_amdgcn_wave_barrier();
+	}
+	miss = __any(miss);
+	if(lane == 0) {
+		rp[k] = s;
+		rc[k] = c;
+		if(miss) atomicOr(miss_out, 1);
+	}
+}
+
+// column chunk [c0, c0 + K): X[(m - c0 - 1) * K + (c - c0)] = D(m, c) for the
+// owned rows m > c, zero elsewhere
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_pack_cols(const typename Elem<ET>::T *__restrict__ D, int n, Shard sh,
+                                                     int c0, int K, typename Elem<ET>::T *__restrict__ X) {
+	const long long total = (long long) (n - c0 - 1) * K;
+	for(long long e = (long long) blockIdx.x * TB + threadIdx.x; e < total; e += (long long) gridDim.x * TB) {
+		const int m = c0 + 1 + (int) (e / K), c = c0 + (int) (e % K);
+		typename Elem<ET>::T v = 0;
+		if(c < m && sh.owns(m)) v = D[sh.off(m) + c];
+		X[e] = v;
+	}
+}
+
+// column parts, continued serially from the row parts in increasing m (the
+// same order as tree.hip's k_init_cols); 8 loads in flight per step
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_init_cols(const typename Elem<ET>::T *__restrict__ X, int n, double bs,
+                                                     int c0, int K, const double *__restrict__ rp,
+                                                     const int *__restrict__ rc, double *__restrict__ sD,
+                                                     int *__restrict__ N, TreeCtl *ctl) {
+	const int c = c0 + blockIdx.x * TB + threadIdx.x;
+	if(c >= c0 + K || c >= n) return;
+	double s = rp[c];
+	int cnt = rc[c], miss = 0;
+	const typename Elem<ET>::T *col = X + (c - c0);
+	constexpr int U = 8;
+	for(int m = c + 1; m < n; m += U) {
+		typename Elem<ET>::T v[U];
+#pragma unroll
+		for(int u = 0; u < U; ++u) {
+			const int mm = m + u < n ? m + u : n - 1;
+			v[u] = col[(long long) (mm - c0 - 1) * K];
+		}
+#pragma unroll
+		for(int u = 0; u < U; ++u) {
+			if(m + u < n) {
+				const double d = Elem<ET>::get(v[u], bs);
+				if(0 <= d) {
+					s += d;
+					++cnt;
+				} else {
+					miss = 1;
+				}
+			}
+		}
+	}
+	sD[c] = s;
+	N[c] = cnt;
+	if(miss) atomicOr(&ctl->has_missing, 1);
+}
+
+// ------------------------------------------------------------------ per join
+// initQ over the rank's tiles: NJ_SEG-column segments x one band, segment-
+// major.  Segment s holds the local bands from global band 256 s on:
+// first(s) = ceil((256 s - rank) / world), F = prefix sums of first, so the
+// tiles before segment s number P(s) = s * nlb - F[s].
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_argmin(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                  int n, Shard sh, const long long *__restrict__ F, int nlb,
+                                                  int sstar, long long tiles) {
+	__shared__ double sq[TB / 64];
+	__shared__ long long sf[TB / 64];
+	if(b.ctl->done) return;
+	constexpr int M = NJ_SEG / TB;
+	double bq = 1.0;
+	long long bf = -1;
+	for(long long idx = blockIdx.x; idx < tiles; idx += gridDim.x) {
+		int lo = 0, hi = sstar - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if((long long) mid * nlb - F[mid] <= idx) lo = mid;
+			else hi = mid - 1;
+		}
+		const int s = lo;
+		const long long lb = (F[s + 1] - F[s]) + (idx - ((long long) s * nlb - F[s]));
+		const int r0 = (int) ((lb * sh.world + sh.rank) * SB), r1 = r0 + SB < n ? r0 + SB : n;
+		const int c0 = s * NJ_SEG;
+		double sc[M];
+#pragma unroll
+		for(int m = 0; m < M; ++m) {
+			int c = c0 + m * TB + (int) threadIdx.x;
+			c = c < n ? c : n - 1;
+			sc[m] = b.sD[c];
+		}
+		constexpr int G = 4;
+		for(int rg = r0; rg < r1; rg += G) {
+			typename Elem<ET>::T v[G][M];
+			double sr[G];
+#pragma unroll
+			for(int g = 0; g < G; ++g) {
+				const int r = rg + g < r1 ? rg + g : r1 - 1;
+				const long long base = sh.off(r);
+				sr[g] = b.sD[r];
+#pragma unroll
+				for(int m = 0; m < M; ++m) {
+					const int c = c0 + m * TB + (int) threadIdx.x;
+					v[g][m] = D[base + (c < r ? c : 0)];
+				}
+			}
+#pragma unroll
+			for(int g = 0; g < G; ++g) {
+				const int r = rg + g;
+				const long long fb = tri(r);
+#pragma unroll
+				for(int m = 0; m < M; ++m) {
+					const int c = c0 + m * TB + (int) threadIdx.x;
+					const double d = Elem<ET>::get(v[g][m], bs);
+					const double q = qcrit(n, n, d, sr[g], sc[m]);
+					const long long f = fb + c;
+					const bool take = r < r1 && c < r && 0 <= d && (q < bq || (q == bq && f > bf));
+					bq = take ? q : bq;
+					bf = take ? f : bf;
+				}
+			}
+		}
+	}
+	qf_wave_reduce(bq, bf);
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	if(lane == 0) {
+		sq[wid] = bq;
+		sf[wid] = bf;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int k = 1; k < TB / 64; ++k) {
+			if(sq[k] < bq || (sq[k] == bq && sf[k] > bf)) {
+				bq = sq[k];
+				bf = sf[k];
+			}
+		}
+		b.qpart[blockIdx.x] = bq;
+		b.fpart[blockIdx.x] = bf;
+	}
+}
+
+// this rank's record (G argmin partials; G = 0 when it owns no tile)
+__global__ __launch_bounds__(TB) void k_sh_fold(TreeBufs b, int G, Shard sh, ShRec *__restrict__ rec) {
+	__shared__ double sq[TB / 64];
+	__shared__ long long sf[TB / 64];
+	double fq = 1.0;
+	long long ff = -1;
+	for(int g = threadIdx.x; g < G; g += TB) {
+		const double oq = b.qpart[g];
+		const long long of = b.fpart[g];
+		if(oq < fq || (oq == fq && of > ff)) {
+			fq = oq;
+			ff = of;
+		}
+	}
+	qf_wave_reduce(fq, ff);
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	if(lane == 0) {
+		sq[wid] = fq;
+		sf[wid] = ff;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int w = 1; w < TB / 64; ++w) {
+			if(sq[w] < fq || (sq[w] == fq && sf[w] > ff)) {
+				fq = sq[w];
+				ff = sf[w];
+			}
+		}
+	}
+	ShRec z;
+	z.q = 0;
+	z.f = 0;
+	for(int w = threadIdx.x; w < sh.world; w += TB) {
+		if(w != sh.rank) rec[w] = z;
+	}
+	if(threadIdx.x == 0) {
+		ShRec r = z;
+		if(!b.ctl->done) {
+			r.q = fq;
+			r.f = ff;
+		}
+		rec[sh.rank] = r;
+	}
+}
+
+// the pieces of lines i and j this rank's rows hold: X[k] = D(i, k),
+// X[n + k] = D(j, k) (raw elements; zeros where another rank owns the cell)
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_lines(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
+                                                 Shard sh, const ShRec *__restrict__ rec,
+                                                 typename Elem<ET>::T *__restrict__ X) {
+	const int k = blockIdx.x * TB + threadIdx.x;
+	if(b.ctl->done) return;
+	double bq;
+	long long bf;
+	rec_fold(rec, sh.world, bq, bf);
+	if(bf < 0) {
+		if(blockIdx.x == 0 && threadIdx.x == 0) {
+			b.ctl->done = 1;
+			b.ctl->final_n = n;
+		}
+		return;
+	}
+	int i, j;
+	flat_to_ij(bf, i, j);
+	if(k >= n) return;
+	typename Elem<ET>::T xi = 0, xj = 0;
+	if(k > i) {
+		if(sh.owns(k)) xi = D[sh.off(k) + i];
+	} else if(k < i && sh.owns(i)) {
+		xi = D[sh.off(i) + k];
+	}
+	if(k > j) {
+		if(sh.owns(k)) xj = D[sh.off(k) + j];
+	} else if(k < j && sh.owns(j)) {
+		xj = D[sh.off(j) + k];
+	}
+	X[k] = xi;
+	X[n + k] = xj;
+}
+
+// limbLength, the join record and updateD (nj.c:836) over the gathered lines;
+// every rank computes the whole new line j and stores its own cells
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                                Shard sh, const ShRec *__restrict__ rec,
+                                                const typename Elem<ET>::T *__restrict__ X,
+                                                typename Elem<ET>::T *__restrict__ Xm) {
+	__shared__ int s_stop, s_nj, s_neg, s_exact;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x;
+	const int k = blockIdx.x * TB + tid;
+	double sDk = 0, Dik = 0, Dkj = 0;
+	int Nk = 0;
+	if(k < n) {
+		sDk = b.sD[k];
+		Nk = b.N[k];
+		Dik = Elem<ET>::get(X[k], bs);
+		Dkj = Elem<ET>::get(X[n + k], bs);
+	}
+	if(tid == 0) {
+		s_stop = ctl->done;
+		s_nj = ctl->njoins;
+		s_neg = ctl->neg;
+		s_exact = ctl->exact;
+	}
+	__syncthreads();
+	if(s_stop) return;
+	double bq;
+	long long bf;
+	rec_fold(rec, sh.world, bq, bf);
+	int i, j;
+	flat_to_ij(bf, i, j);
+	const double Dij = Elem<ET>::get(X[j], bs);
+	if(blockIdx.x == 0 && tid == 0) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, s_neg);
+		ctl->i = i;
+		ctl->j = j;
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[s_nj] = J;
+		ctl->njoins = s_nj + 1;
+	}
+	double d = 0;
+	int cnt = 0;
+	if(k < n && k != i && k != j) {
+		d = (Dik + Dkj - Dij) / 2;
+		d = d < 0 ? 0 : d;
+		const typename Elem<ET>::T v = Elem<ET>::put(d, 0.25, bs);
+		if(k > j) {
+			if(sh.owns(k)) D[sh.off(k) + j] = v;
+		} else if(sh.owns(j)) {
+			D[sh.off(j) + k] = v;
+		}
+		if(k == n - 1) Xm[j] = v;   // row n-1 moves to slot i in the pop
+		b.sD[k] = sDk - (Dik + Dkj - d);
+		b.N[k] = Nk - 1;
+		cnt = 1;
+	}
+	update_partials(b, n, s_exact, k, d, cnt, blockIdx.x);
+}
+
+// row sum of j, then ltdMatrix_popArrange (matrix.c:518) + nj.c:1588-1589:
+// row n-1 (broadcast into Xm) becomes row/column i
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, Shard sh,
+                                               const typename Elem<ET>::T *__restrict__ Xm) {
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	TreeCtl *ctl = b.ctl;
+	const int nn = n - 1;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = blockIdx.x * TB + tid;
+	typename Elem<ET>::T vm = 0;
+	if(k < nn) vm = Xm[k];
+	const double sDm = b.sD[nn];
+	const int Nm = b.N[nn];
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need;
+			fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j;
+	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = s_nj;
+		if(i != nn) {
+			b.sD[i] = sDm;
+			b.N[i] = Nm;
+		}
+		if(s_serial) ctl->serial_sums++;
+	}
+	if(i != nn) {
+		if(k < i) {
+			if(sh.owns(i)) D[sh.off(i) + k] = vm;
+		} else if(k > i && k < nn && sh.owns(k)) {
+			D[sh.off(k) + i] = vm;
+		}
+	}
+}
+
+// ------------------------------------------------------------------ transports
+static int coll_fail(const char *what) {
+	hipError_t e = hipErrorUnknown;
+	ccg_set_last_error(e, what, __FILE__, __LINE__);
+	return CCG_EHIP;
+}
+
+// world == 1 without a transport: nothing to reduce, the broadcast is a copy
+static int self_allreduce(void *, void *, size_t, void *) { return 0; }
+static int self_bcast(void *, const void *send, void *recv, size_t bytes, int, void *stream) {
+	if(send != recv && bytes) {
+		if(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, (hipStream_t) stream) != hipSuccess) return -1;
+	}
+	return 0;
+}
+
+struct CollRun {
+	const ccg_coll *c;
+	hipStream_t st;
+	unsigned char *h;   // pinned staging buffer (host_staged transports)
+	KTimer *kt;
+	int allreduce(void *d, size_t bytes) {
+		if(!c->host_staged) {
+			if(c->allreduce_sum_u8(c->user, d, bytes, (void *) st)) return coll_fail("allreduce");
+			kt->mark(CCG_K_COLL);
+			return CCG_OK;
+		}
+		CCG_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st));
+		CCG_CHECK(hipStreamSynchronize(st));
+		if(c->allreduce_sum_u8(c->user, h, bytes, (void *) st)) return coll_fail("allreduce");
+		CCG_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+		kt->mark(CCG_K_COLL);
+		return CCG_OK;
+	}
+	int bcast(const void *dsend, void *drecv, size_t bytes, int root) {
+		if(!c->host_staged) {
+			if(c->broadcast(c->user, dsend, drecv, bytes, root, (void *) st)) return coll_fail("broadcast");
+			kt->mark(CCG_K_COLL);
+			return CCG_OK;
+		}
+		if(root == c->rank) CCG_CHECK(hipMemcpyAsync(h, dsend, bytes, hipMemcpyDeviceToHost, st));
+		CCG_CHECK(hipStreamSynchronize(st));
+		if(c->broadcast(c->user, h, h, bytes, root, (void *) st)) return coll_fail("broadcast");
+		CCG_CHECK(hipMemcpyAsync(drecv, h, bytes, hipMemcpyHostToDevice, st));
+		kt->mark(CCG_K_COLL);
+		return CCG_OK;
+	}
+};
+
+// RCCL, resolved with dlopen so the engine has no link-time dependency on it
+struct RcclApi {
+	void *h;
+	ncclResult_t (*get_id)(ncclUniqueId *);
+	ncclResult_t (*init_rank)(ncclComm_t *, int, ncclUniqueId, int);
+	ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+	ncclResult_t (*bcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+	ncclResult_t (*destroy)(ncclComm_t);
+	const char *(*err)(ncclResult_t);
+};
+static RcclApi g_rccl;
+
+static int rccl_load() {
+	if(g_rccl.h) return CCG_OK;
+	const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+	void *h = NULL;
+	for(int k = 0; k < 3 && !h; ++k) h = dlopen(names[k], RTLD_NOW | RTLD_GLOBAL);
+	if(!h) return CCG_EUNSUP;
+	RcclApi a;
+	a.h = h;
+	a.get_id = (decltype(a.get_id)) dlsym(h, "ncclGetUniqueId");
+	a.init_rank = (decltype(a.init_rank)) dlsym(h, "ncclCommInitRank");
+	a.all_reduce = (decltype(a.all_reduce)) dlsym(h, "ncclAllReduce");
+	a.bcast = (decltype(a.bcast)) dlsym(h, "ncclBroadcast");
+	a.destroy = (decltype(a.destroy)) dlsym(h, "ncclCommDestroy");
+	a.err = (decltype(a.err)) dlsym(h, "ncclGetErrorString");
+	if(!a.get_id || !a.init_rank || !a.all_reduce || !a.bcast || !a.destroy || !a.err) return CCG_EUNSUP;
+	g_rccl = a;
+	return CCG_OK;
+}
+
+struct RcclUser {
+	ncclComm_t comm;
+};
+
+// widest element that tiles the byte range (the sum is a gather either way)
+static void rccl_type(const void *p, size_t bytes, ncclDataType_t *t, size_t *count) {
+	const uintptr_t a = (uintptr_t) p;
+	if(bytes % 8 == 0 && a % 8 == 0) {
+		*t = ncclUint64;
+		*count = bytes / 8;
+	} else if(bytes % 4 == 0 && a % 4 == 0) {
+		*t = ncclUint32;
+		*count = bytes / 4;
+	} else {
+		*t = ncclUint8;
+		*count = bytes;
+	}
+}
+
+static int rccl_allreduce(void *user, void *buf, size_t bytes, void *stream) {
+	ncclDataType_t t;
+	size_t cnt;
+	rccl_type(buf, bytes, &t, &cnt);
+	ncclResult_t r = g_rccl.all_reduce(buf, buf, cnt, t, ncclSum, ((RcclUser *) user)->comm, (hipStream_t) stream);
+	if(r != ncclSuccess) fprintf(stderr, "ccphylo_amd: ncclAllReduce: %s\n", g_rccl.err(r));
+	return r != ncclSuccess;
+}
+
+static int rccl_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
+	ncclResult_t r = g_rccl.bcast(send ? send : recv, recv, bytes, ncclUint8, root, ((RcclUser *) user)->comm,
+	                              (hipStream_t) stream);
+	if(r != ncclSuccess) fprintf(stderr, "ccphylo_amd: ncclBroadcast: %s\n", g_rccl.err(r));
+	return r != ncclSuccess;
+}
+
+// ------------------------------------------------------------------ host driver
+static long long sh_first(int s, const Shard &sh) {
+	if(s == 0) return 0;
+	const long long a = (long long) (NJ_SEG / NJ_RB) * s - sh.rank;
+	return (a + sh.world - 1) / sh.world;
+}
+
+static int sh_nlb(int n, const Shard &sh) {
+	const int nb = (n + SB - 1) / SB;
+	return nb > sh.rank ? (nb - sh.rank + sh.world - 1) / sh.world : 0;
+}
+
+template <int ET>
+static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll_in, void *Dd,
+                            ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	typedef typename Elem<ET>::T T;
+	T *D = (T *) Dd;
+	const int n0 = a->n;
+	const double bs = a->byteScale;
+	hipStream_t st = ctx->stream;
+	ccg_coll self;
+	if(!coll_in) {
+		memset(&self, 0, sizeof(self));
+		self.world = 1;
+		self.allreduce_sum_u8 = self_allreduce;
+		self.broadcast = self_bcast;
+		coll_in = &self;
+	}
+	const Shard sh = {coll_in->rank, coll_in->world};
+	// device state: the single-GPU TreeBufs subset this loop uses
+	const size_t nb = (size_t) cdiv(n0, TB) + 1;
+	const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
+	size_t free_b = 0, total_b = 0;
+	CCG_CHECK(hipMemGetInfo(&free_b, &total_b));
+	// init column chunk: wide enough to keep the serial column sums parallel
+	size_t budget = coll_in->host_staged ? ((size_t) 64 << 20) : (free_b / 4 < ((size_t) 16 << 30) ? free_b / 4 : ((size_t) 16 << 30));
+	long long K = (long long) (budget / ((size_t) n0 * ET));
+	if(K < 256) K = 256;
+	if(K > n0) K = n0;
+	const size_t xc_bytes = (size_t) K * (size_t) n0 * ET;
+	const size_t rp_bytes = (size_t) n0 * 12 + 16;
+	size_t sz = 0;
+	auto take = [&](size_t bytes) {
+		size_t off = sz;
+		sz += (bytes + 255) & ~(size_t) 255;
+		return off;
+	};
+	size_t o_sD = take((n0 + 1) * 8), o_c = take((n0 + 1) * 8), o_N = take((n0 + 1) * 4);
+	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
+	size_t o_qp = take(SH_GRID * 8), o_fp = take(SH_GRID * 8);
+	size_t o_j = take((size_t) n0 * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
+	size_t o_F = take((size_t) (nseg0 + 2) * 8), o_rec = take((size_t) coll_in->world * sizeof(ShRec));
+	size_t o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
+	char *m;
+	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
+	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
+	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
+	unsigned char *h = NULL;
+	if(coll_in->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
+		hipFree(m);
+		return CCG_ENOMEM;
+	}
+	int rc = CCG_OK;
+	static KTimer kt;
+	CollRun cr = {coll_in, st, h, &kt};
+	TreeBufs b;
+	memset(&b, 0, sizeof(b));
+	b.sD = (double *) (m + o_sD);
+	b.contrib = (double *) (m + o_c);
+	b.N = (int *) (m + o_N);
+	b.wsum = (double *) (m + o_ws);
+	b.wabs = (double *) (m + o_wa);
+	b.wcnt = (int *) (m + o_wc);
+	b.wexp = (int *) (m + o_we);
+	b.qpart = (double *) (m + o_qp);
+	b.fpart = (long long *) (m + o_fp);
+	b.joins = (ccg_join *) (m + o_j);
+	b.ctl = (TreeCtl *) (m + o_ctl);
+	long long *F = (long long *) (m + o_F);
+	ShRec *rec = (ShRec *) (m + o_rec);
+	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xc = (T *) (m + o_xc);
+	double *rp = (double *) (m + o_rp);
+	int *rcnt = (int *) (m + o_rp + (size_t) n0 * 8);
+	int *rmiss = rcnt + n0;
+	long long *hF = (long long *) malloc((size_t) (nseg0 + 2) * 8);
+	TreeCtl init, hc;
+	long long launches = 0;
+	int n = n0;
+	float ms = 0;
+	memset(&init, 0, sizeof(init));
+	init.neg = (a->flags & 2) != 0;
+	init.exact = a->exact != 0;
+	init.method = a->method;
+#define SH_TRY(x)                    \
+	do {                             \
+		if((rc = (x)) != CCG_OK) goto out; \
+	} while(0)
+#define SH_HIP(x)                                                     \
+	do {                                                              \
+		hipError_t e_ = (x);                                          \
+		if(e_ != hipSuccess) {                                        \
+			ccg_set_last_error(e_, #x, __FILE__, __LINE__);          \
+			rc = e_ == hipErrorOutOfMemory ? CCG_ENOMEM : CCG_EHIP;  \
+			goto out;                                                 \
+		}                                                             \
+	} while(0)
+	if(!hF) {
+		rc = CCG_ENOMEM;
+		goto out;
+	}
+	hF[0] = 0;
+	for(int s = 0; s <= nseg0; ++s) hF[s + 1] = hF[s] + sh_first(s, sh);
+	SH_HIP(hipMemsetAsync(m, 0, sz - xc_bytes, st));
+	SH_HIP(hipMemcpyAsync(F, hF, (size_t) (nseg0 + 2) * 8, hipMemcpyHostToDevice, st));
+	SH_HIP(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
+	SH_HIP(hipEventRecord(ctx->ev0, st));
+	kt.init(st, a->profile != 0);
+	// initSummaD: owned row parts, gathered; then the column parts chunk by chunk
+	k_sh_init_rows<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, sh, rp, rcnt, rmiss);
+	SH_HIP(hipGetLastError());
+	kt.mark(CCG_K_INIT);
+	SH_TRY(cr.allreduce(rp, rp_bytes));
+	for(int c0 = 0; c0 < n0 - 1; c0 += (int) K) {
+		const int Kc = (int) (n0 - c0 < K ? n0 - c0 : K);
+		const long long cells = (long long) (n0 - c0 - 1) * Kc;
+		long long g = (cells + TB - 1) / TB;
+		if(g > 65536) g = 65536;
+		k_sh_pack_cols<ET><<<(unsigned) g, TB, 0, st>>>(D, n0, sh, c0, Kc, Xc);
+		kt.mark(CCG_K_INIT);
+		SH_TRY(cr.allreduce(Xc, (size_t) cells * ET));
+		k_sh_init_cols<ET><<<cdiv(Kc, TB), TB, 0, st>>>(Xc, n0, bs, c0, Kc, rp, rcnt, b.sD, b.N, b.ctl);
+		kt.mark(CCG_K_INIT);
+		launches += 2;
+	}
+	// the last column (n0 - 1) has no column part
+	{
+		const int c = n0 - 1;
+		SH_HIP(hipMemcpyAsync(b.sD + c, rp + c, 8, hipMemcpyDeviceToDevice, st));
+		SH_HIP(hipMemcpyAsync(b.N + c, rcnt + c, 4, hipMemcpyDeviceToDevice, st));
+	}
+	SH_HIP(hipGetLastError());
+	launches += 1;
+	{
+		int hm = 0;
+		SH_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
+		SH_HIP(hipMemcpyAsync(&hm, rmiss, 4, hipMemcpyDeviceToHost, st));
+		SH_HIP(hipStreamSynchronize(st));
+		if(hc.has_missing || hm) {
+			rc = CCG_EUNSUP;   // the missing-entry quirks of updateD run on one GPU only
+			goto out;
+		}
+	}
+	{
+		int since_check = 0;
+		while(n > 2) {
+			const int root = ccg_shard_owner(n - 1, sh.world);
+			SH_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
+			                root));
+			const int nlb = sh_nlb(n, sh), nseg = (int) cdiv(n - 1, NJ_SEG);
+			int sstar = 0;
+			while(sstar < nseg && hF[sstar + 1] - hF[sstar] < nlb) ++sstar;
+			const long long tiles = (long long) sstar * nlb - hF[sstar];
+			const int G = (int) (tiles < SH_GRID ? tiles : SH_GRID);
+			if(G > 0) k_sh_argmin<ET><<<G, TB, 0, st>>>(D, bs, b, n, sh, F, nlb, sstar, tiles);
+			k_sh_fold<<<1, TB, 0, st>>>(b, G, sh, rec);
+			kt.mark(CCG_K_ARGMIN);
+			SH_TRY(cr.allreduce(rec, (size_t) sh.world * sizeof(ShRec)));
+			const unsigned gn = cdiv(n, TB);
+			k_sh_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, rec, X);
+			kt.mark(CCG_K_UPDATE);
+			SH_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
+			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xm);
+			kt.mark(CCG_K_UPDATE);
+			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xm);
+			kt.mark(CCG_K_POP);
+			SH_HIP(hipGetLastError());
+			launches += (G > 0) + 5;
+			--n;
+			if(++since_check == 1024) {
+				since_check = 0;
+				SH_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
+				SH_HIP(hipStreamSynchronize(st));
+				if(hc.done) break;
+			}
+		}
+	}
+	SH_HIP(hipEventRecord(ctx->ev1, st));
+	kt.finish();
+	SH_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
+	SH_HIP(hipStreamSynchronize(st));
+	SH_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+	*njoins = hc.njoins;
+	*final_n = hc.done ? hc.final_n : 2;
+	if(hc.njoins) {
+		SH_HIP(hipMemcpyAsync(joins, b.joins, (size_t) hc.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
+	}
+	*final_d = -1.0;
+	if(*final_n == 2) {
+		// D(1, 0): row 1 is in band 0, owned by rank 0
+		SH_TRY(cr.bcast(sh.rank == 0 ? (const void *) (D + sh.off(1)) : NULL, Xm, ET, 0));
+		T v;
+		SH_HIP(hipMemcpyAsync(&v, Xm, sizeof(T), hipMemcpyDeviceToHost, st));
+		SH_HIP(hipStreamSynchronize(st));
+		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
+	}
+	if(stats) {
+		stats[0] = 0;
+		stats[1] = 0;
+		stats[2] = launches;
+		stats[3] = (int64_t) (ms * 1000.0);
+		if(a->profile) {
+			for(int c = 0; c < CCG_NKSTAT; ++c) {
+				stats[4 + 2 * c] = kt.cnt[c];
+				stats[5 + 2 * c] = kt.ns[c];
+			}
+			stats[4 + 2 * CCG_NKSTAT] = 0;
+			stats[5 + 2 * CCG_NKSTAT] = 0;
+		}
+	}
+out:
+#undef SH_TRY
+#undef SH_HIP
+	if(rc != CCG_OK) kt.on = false;
+	hipStreamSynchronize(st);
+	free(hF);
+	if(h) hipHostFree(h);
+	hipFree(m);
+	return rc;
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int ccg_shard_owner(int64_t row, int world) { return world > 0 ? (int) ((row / SB) % world) : -1; }
+
+int64_t ccg_shard_row_offset(int64_t row, int rank, int world) {
+	const Shard sh = {rank, world};
+	return sh.off(row);
+}
+
+int64_t ccg_shard_elems(int64_t n, int rank, int world) {
+	if(n <= 0 || world <= 0 || rank < 0 || rank >= world) return 0;
+	const Shard sh = {rank, world};
+	const int64_t gb = n / SB;
+	if(n % SB && sh.owns(n)) return sh.off(n);   // n falls inside an owned band
+	// first owned band at or above ceil(n / SB)
+	int64_t g = (n + SB - 1) / SB;
+	g += ((rank - g % world) % world + world) % world;
+	(void) gb;
+	return sh.off(g * SB);
+}
+
+int ccg_rccl_unique_id(void *id) {
+	if(!id) return CCG_EINVAL;
+	int rc = rccl_load();
+	if(rc) return rc;
+	ncclUniqueId u;
+	if(g_rccl.get_id(&u) != ncclSuccess) return CCG_EHIP;
+	memcpy(id, &u, sizeof(u));
+	return CCG_OK;
+}
+
+int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *out) {
+	if(!ctx || !id || !out || world < 1 || rank < 0 || rank >= world) return CCG_EINVAL;
+	int rc = rccl_load();
+	if(rc) return rc;
+	CCG_CHECK(hipSetDevice(ctx->device));
+	RcclUser *u = (RcclUser *) calloc(1, sizeof(RcclUser));
+	if(!u) return CCG_ENOMEM;
+	ncclUniqueId uid;
+	memcpy(&uid, id, sizeof(uid));
+	ncclResult_t r = g_rccl.init_rank(&u->comm, world, uid, rank);
+	if(r != ncclSuccess) {
+		fprintf(stderr, "ccphylo_amd: ncclCommInitRank: %s\n", g_rccl.err(r));
+		free(u);
+		return CCG_EHIP;
+	}
+	memset(out, 0, sizeof(*out));
+	out->user = u;
+	out->rank = rank;
+	out->world = world;
+	out->host_staged = 0;
+	out->allreduce_sum_u8 = rccl_allreduce;
+	out->broadcast = rccl_bcast;
+	return CCG_OK;
+}
+
+int ccg_rccl_close(ccg_coll *c) {
+	if(!c || !c->user) return CCG_EINVAL;
+	RcclUser *u = (RcclUser *) c->user;
+	ncclResult_t r = g_rccl.destroy(u->comm);
+	free(u);
+	c->user = NULL;
+	return r == ncclSuccess ? CCG_OK : CCG_EHIP;
+}
+
+static int shard_check(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll) {
+	if(!c || !a) return CCG_EINVAL;
+	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ)) return CCG_EINVAL;
+	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
+	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
+	if(coll && (coll->world < 1 || coll->rank < 0 || coll->rank >= coll->world || !coll->allreduce_sum_u8 ||
+	            !coll->broadcast))
+		return CCG_EINVAL;
+	if(a->method != CCG_TREE_NJ) return CCG_EUNSUP;
+	return CCG_OK;
+}
+
+int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
+                       int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	int rc = shard_check(c, a, coll);
+	if(rc) return rc;
+	if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	switch(a->etype) {
+		case 8: return tree_shard_run_t<8>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		case 4: return tree_shard_run_t<4>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		case 2: return tree_shard_run_t<2>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		default: return tree_shard_run_t<1>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+	}
+}
+
+int ccg_tree_shard(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, const void *D, ccg_join *joins,
+                   int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	int rc = shard_check(c, a, coll);
+	if(rc) return rc;
+	if(!D) return CCG_EINVAL;
+	const int rank = coll ? coll->rank : 0, world = coll ? coll->world : 1;
+	const int64_t n = a->n, es = a->etype;
+	const int64_t elems = ccg_shard_elems(n, rank, world);
+	// the rank's bands are contiguous row runs of the full LT: copy band by band
+	char *hbuf = (char *) malloc((size_t) (elems ? elems : 1) * es);
+	if(!hbuf) return CCG_ENOMEM;
+	const char *src = (const char *) D;
+	for(int64_t g = rank; g * SB < n; g += world) {
+		const int64_t r0 = g * SB, r1 = r0 + SB < n ? r0 + SB : n;
+		memcpy(hbuf + ccg_shard_row_offset(r0, rank, world) * es, src + tri(r0) * es, (size_t) (tri(r1) - tri(r0)) * es);
+	}
+	CCG_CHECK(hipSetDevice(c->device));
+	void *d = NULL;
+	if(hipMalloc(&d, (size_t) (elems ? elems : 1) * es) != hipSuccess) {
+		free(hbuf);
+		return CCG_ENOMEM;
+	}
+	if(hipMemcpy(d, hbuf, (size_t) elems * es, hipMemcpyHostToDevice) != hipSuccess) {
+		rc = CCG_EHIP;
+	} else {
+		rc = ccg_tree_shard_dev(c, a, coll, d, joins, njoins, final_n, final_d, stats);
+	}
+	free(hbuf);
+	hipStreamSynchronize(c->stream);
+	hipFree(d);
+	return rc;
+}
+
+}   // extern "C"

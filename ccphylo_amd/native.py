@@ -27,8 +27,10 @@ ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
 
 CCG_TREE_NJ = 0
 CCG_TREE_DNJ = 1
-NKSTAT = 8
-KSTAT_NAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find"]
+NKSTAT = 9
+KSTAT_NAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
+SHARD_BAND = 8
+RCCL_ID_BYTES = 128
 
 
 class CcgError(RuntimeError):
@@ -56,6 +58,16 @@ class Join(C.Structure):
     _fields_ = [("i", C.c_int32), ("j", C.c_int32), ("Li", C.c_double), ("Lj", C.c_double)]
 
 
+# ccg_coll (include/ccphylo_amd.h): the sharded tree loop's collectives
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+BROADCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p)
+
+
+class Coll(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("rank", C.c_int), ("world", C.c_int), ("host_staged", C.c_int),
+                ("allreduce_sum_u8", ALLREDUCE_FN), ("broadcast", BROADCAST_FN)]
+
+
 JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("Lj", np.float64)])
 
 # every symbol of include/ccphylo_amd.h
@@ -63,6 +75,8 @@ ENGINE_SYMBOLS = [
     "ccg_init", "ccg_destroy", "ccg_strerror", "ccg_device_info",
     "ccg_snp_ltd", "ccg_snp_ltd_dev", "ccg_tree", "ccg_tree_dev",
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
+    "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
+    "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -101,6 +115,18 @@ def engine_lib():
         lib.ccg_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         lib.ccg_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         lib.ccg_synchronize.argtypes = [C.c_void_p]
+        lib.ccg_shard_owner.argtypes = [C.c_int64, C.c_int]
+        lib.ccg_shard_row_offset.argtypes = [C.c_int64, C.c_int, C.c_int]
+        lib.ccg_shard_row_offset.restype = C.c_int64
+        lib.ccg_shard_elems.argtypes = [C.c_int64, C.c_int, C.c_int]
+        lib.ccg_shard_elems.restype = C.c_int64
+        lib.ccg_rccl_unique_id.argtypes = [C.c_void_p]
+        lib.ccg_rccl_open.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(Coll)]
+        lib.ccg_rccl_close.argtypes = [C.POINTER(Coll)]
+        lib.ccg_tree_shard.argtypes = [C.c_void_p, C.POINTER(TreeArgs), C.POINTER(Coll), C.c_void_p, C.c_void_p,
+                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int64)]
+        lib.ccg_tree_shard_dev.argtypes = lib.ccg_tree_shard.argtypes
         _engine = lib
     return _engine
 
@@ -234,6 +260,34 @@ class Device:
         self._check(rc, "ccg_tree")
         return joins[:nj.value], fn.value, fd.value, list(st)
 
+    def tree_shard(self, D, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
+                   profile=False):
+        """Sharded NJ from the full host LT (ccg_tree_shard): this rank uploads
+        its own row bands only.  `coll`: a HostColl / RcclColl (None = world 1)."""
+        D = np.ascontiguousarray(D, dtype=ETYPES[etype])
+        assert D.size == n * (n - 1) // 2
+        return self._tree_shard(self.lib.ccg_tree_shard, D.ctypes.data, n, coll, etype, byte_scale, method, flags,
+                                exact, profile)
+
+    def tree_shard_dev(self, dptr, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
+                       profile=False):
+        """Sharded NJ on this rank's device row bands (ccg_tree_shard_dev; consumed)."""
+        return self._tree_shard(self.lib.ccg_tree_shard_dev, dptr, n, coll, etype, byte_scale, method, flags,
+                                exact, profile)
+
+    def _tree_shard(self, fn_, ptr, n, coll, etype, byte_scale, method, flags, exact, profile):
+        joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
+        nj = C.c_int(0)
+        fn = C.c_int(0)
+        fd = C.c_double(0)
+        st = (C.c_int64 * (6 + 2 * NKSTAT))()
+        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile))
+        cp = C.byref(coll.c) if coll is not None else None
+        rc = fn_(self.h, C.byref(a), cp, C.c_void_p(ptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd),
+                 st)
+        self._check(rc, "ccg_tree_shard")
+        return joins[:nj.value], fn.value, fd.value, list(st)
+
     # ---- device memory (ccg_malloc & co.) for HBM-resident inputs
     def malloc(self, nbytes):
         p = C.c_void_p()
@@ -262,6 +316,114 @@ class Device:
         self._check(self.lib.ccg_snp_ltd_dev(self.h, C.byref(a), C.c_void_p(D_ptr),
                                              C.c_void_p(N_ptr) if N_ptr else None, C.byref(inc)), "ccg_snp_ltd_dev")
         return inc.value
+
+
+# ---------------------------------------------------------------- sharding
+def shard_owner(row, world):
+    """Rank owning LT row `row`: bands of SHARD_BAND rows dealt round-robin."""
+    return (row // SHARD_BAND) % world
+
+
+def shard_row_offset(row, rank, world):
+    """Element offset of owned row `row` in its rank's buffer (ccg_shard_row_offset)."""
+    return engine_lib().ccg_shard_row_offset(int(row), int(rank), int(world))
+
+
+def shard_elems(n, rank, world):
+    """Elements of a rank's rows below n (ccg_shard_elems)."""
+    return engine_lib().ccg_shard_elems(int(n), int(rank), int(world))
+
+
+def shard_extract(D, n, rank, world):
+    """This rank's rows of a full packed LT, back to back (the layout of
+    ccg_tree_shard_dev's buffer)."""
+    D = np.asarray(D)
+    out = np.empty(shard_elems(n, rank, world), dtype=D.dtype)
+    for g in range(rank, (n + SHARD_BAND - 1) // SHARD_BAND, world):
+        r0, r1 = g * SHARD_BAND, min(g * SHARD_BAND + SHARD_BAND, n)
+        o = shard_row_offset(r0, rank, world)
+        out[o:o + (r1 * (r1 - 1) - r0 * (r0 - 1)) // 2] = D[r0 * (r0 - 1) // 2:r1 * (r1 - 1) // 2]
+    return out
+
+
+class HostColl:
+    """Host-staged ccg_coll over torch.distributed (gloo): the engine copies
+    each exchange to host memory and calls back here.  For tests and for
+    transports without GPU-direct collectives."""
+
+    def __init__(self, dist, group=None):
+        import torch
+        self._torch = torch
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.calls = 0
+        self.bytes = 0
+        self.errors = []
+
+        def _arr(buf, nbytes):
+            return torch.from_numpy(np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(buf)))
+
+        def allreduce(user, buf, nbytes, stream):
+            try:
+                self.calls += 1
+                self.bytes += nbytes
+                if nbytes:
+                    t = _arr(buf, nbytes)
+                    # gloo sums uint8 elementwise; only one rank is non-zero per byte
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+                return 0
+            except Exception as e:  # never unwind through C
+                self.errors.append(repr(e))
+                return 1
+
+        def broadcast(user, send, recv, nbytes, root, stream):
+            try:
+                self.calls += 1
+                self.bytes += nbytes
+                if nbytes:
+                    t = _arr(recv, nbytes)
+                    if self.rank == root and send != recv:
+                        C.memmove(recv, send, nbytes)
+                    dist.broadcast(t, src=dist.get_global_rank(group, root) if group is not None else root,
+                                   group=group)
+                return 0
+            except Exception as e:
+                self.errors.append(repr(e))
+                return 1
+
+        self._ar = ALLREDUCE_FN(allreduce)   # keep the thunks alive
+        self._bc = BROADCAST_FN(broadcast)
+        self.c = Coll(None, self.rank, self.world, 1, self._ar, self._bc)
+
+
+class RcclColl:
+    """ccg_coll over RCCL (ccg_rccl_open): device buffers, enqueued on the
+    engine stream.  Rank 0 makes the id; it travels over `dist` (any backend)."""
+
+    def __init__(self, dev, dist, group=None):
+        import torch
+        lib = engine_lib()
+        self.lib = lib
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        ident = (C.c_uint8 * RCCL_ID_BYTES)()
+        if rank == 0:
+            rc = lib.ccg_rccl_unique_id(ident)
+            if rc != 0:
+                raise CcgError(f"ccg_rccl_unique_id: {lib.ccg_strerror(rc).decode()}")
+        obj = [bytes(ident)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        C.memmove(ident, obj[0], RCCL_ID_BYTES)
+        self.c = Coll()
+        rc = lib.ccg_rccl_open(dev.h, ident, rank, world, C.byref(self.c))
+        if rc != 0:
+            raise CcgError(f"ccg_rccl_open: {lib.ccg_strerror(rc).decode()}")
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if self.c.user:
+            self.lib.ccg_rccl_close(C.byref(self.c))
 
 
 # ---------------------------------------------------------------- host API

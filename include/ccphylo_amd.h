@@ -10,6 +10,9 @@
  *   ccg_snp_ltd   replaces fsaCmpThreadOut(tnum, &cmpFsaThrd | &cmpairFsaThrd, D, N, ...)
  *                 declared fsacmpthrd.h:49, impl fsacmpthrd.c:76-106,
  *                 called from cdist.c:351/:354 (MSA) and cdist.c:181/:184.
+ *   ccg_tree_shard  the same loop with the LT rows split over ranks
+ *                 (SURVEY.md 8(e)), one process per GPU, collectives over
+ *                 RCCL (ccg_rccl_open) or a caller-supplied transport.
  *   ccg_tree      replaces dnj_thread(D, sD, Q, N, names, t) (dnj.c:1054,
  *                 called tree.c:89) and nj_thread(D, sD, N, names, t)
  *                 (nj.c:1612, called tree.c:91).  It returns the join list;
@@ -109,7 +112,9 @@ typedef struct {
 #define CCG_K_REQUEUE  5   /* DNJ: updateDNJ Q/P + DNJ_popArrange */
 #define CCG_K_POP      6   /* NJ: ltdMatrix_popArrange */
 #define CCG_K_FIND     7   /* DNJ k_dnj_find: bound U and the rows below S under it */
-#define CCG_NKSTAT     8
+#define CCG_K_COLL     8   /* sharded engine: collectives (enqueue time, or the
+                              host round trip of a host-staged transport) */
+#define CCG_NKSTAT     9
 
 /* D: host LT (n(n-1)/2 elements), left unmodified.  joins: room for n-2.
  * On return *njoins joins were made; *final_n is the matrix size at exit
@@ -123,6 +128,60 @@ int ccg_tree(ccg_ctx *ctx, const ccg_tree_args *a, const void *D,
 /* Same on a DEVICE LT buffer, which is consumed (overwritten). */
 int ccg_tree_dev(ccg_ctx *ctx, const ccg_tree_args *a, void *D_dev,
                  ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
+
+/* ------------------------------------------------------------------ */
+/* sharded tree: one LT matrix split over `world` ranks  */
+/* ------------------------------------------------------------------ */
+/* Row ownership: bands of CCG_SHARD_BAND consecutive LT rows are dealt
+ * round-robin, band b = rows [8b, 8b+8) to rank b % world, so the rows the
+ * join loop drops from the end (ltdMatrix_popArrange, matrix.c:518) drain
+ * every rank evenly.  A rank stores its rows in increasing order, back to
+ * back, row r holding its r elements (columns 0..r-1) as in the reference's
+ * LT buffer (matrix.c:74-83). */
+#define CCG_SHARD_BAND 8
+int ccg_shard_owner(int64_t row, int world);
+/* element offset of an owned row in its rank's buffer */
+int64_t ccg_shard_row_offset(int64_t row, int rank, int world);
+/* elements of a rank's rows below n (the size of its buffer for n taxa) */
+int64_t ccg_shard_elems(int64_t n, int rank, int world);
+
+/* The collectives of the sharded loop; every rank makes the same calls in the
+ * same order.  host_staged = 0: buffers are device pointers and each call is
+ * enqueued on `stream` (a hipStream_t), as RCCL does; host_staged = 1: they
+ * are host memory and the engine has synchronised its stream first (test
+ * transports, e.g. torch.distributed gloo).
+ *   allreduce_sum_u8: bytewise sum in place.  The engine only reduces arrays
+ *     in which at most one rank holds a non-zero byte, so the sum is a gather
+ *     of owned pieces, exact for every element type.
+ *   broadcast: `bytes` from `send` on rank `root` into `recv` on every rank
+ *     (root included); `send` is ignored elsewhere. */
+typedef struct {
+	void *user;
+	int rank, world;
+	int host_staged;
+	int (*allreduce_sum_u8)(void *user, void *buf, size_t bytes, void *stream);
+	int (*broadcast)(void *user, const void *send, void *recv, size_t bytes, int root, void *stream);
+} ccg_coll;
+
+/* RCCL transport (librccl.so.1 is loaded on first use).  Rank 0 makes the
+ * 128-byte id and the caller ships it to the other ranks (e.g. through the
+ * torch.distributed TCP store); ccg_rccl_open blocks until all ranks joined. */
+#define CCG_RCCL_ID_BYTES 128
+int ccg_rccl_unique_id(void *id);
+int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *out);
+int ccg_rccl_close(ccg_coll *coll);
+
+/* NJ (a->method = CCG_TREE_NJ) on the rank's rows.  Every rank returns the
+ * full join list, identical on all ranks and bit-identical to ccg_tree with
+ * the same `exact` flag for any world size.  Dloc_dev holds the rank's
+ * ccg_shard_elems(n, rank, world) elements and is consumed.  CCG_EUNSUP for
+ * DNJ and for matrices with missing (negative) entries. */
+int ccg_tree_shard_dev(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc_dev,
+                       ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
+/* Same from the full host LT (every rank passes the whole matrix; only the
+ * rank's own rows are uploaded). */
+int ccg_tree_shard(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, const void *D,
+                   ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
 
 /* ------------------------------------------------------------------ */
 /* device memory helpers (for callers that keep the pipeline in HBM)   */

@@ -1,0 +1,143 @@
+"""GPU parity of the row-sharded NJ engine (ccg_tree_shard).
+
+Its joins must be bit-identical to the single-GPU engine's (and so, in exact
+mode, to the reference's) for every world size:
+- world 1 without a transport;
+- world 2 / 3 as separate processes on the one GPU, exchanging over the
+  host-staged gloo transport (HostColl);
+- world 1 over RCCL (the production transport; more ranks need more GPUs).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ROOT, golden_bytes, golden_cases, parse_tree_args
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import ccphylo_amd as cg
+    d = cg.Device(0)
+    yield d
+    d.close()
+
+
+def _euclid(n, seed, dim=8):
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n, dim))
+    i, j = np.tril_indices(n, -1)
+    return np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
+
+
+def _snp(n, seed, L=3000):
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, 4, (n, L))
+    X[rng.random((n, L)) < 0.7] = 0        # shared sites: many equal distances
+    i, j = np.tril_indices(n, -1)
+    return (X[i] != X[j]).sum(1).astype(np.float64)
+
+
+def _typed(D, et):
+    bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 1.0}[et]
+    if et == 8:
+        return D, bs
+    if et == 4:
+        return D.astype(np.float32), bs
+    return np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16), bs
+
+
+def _same(a, b):
+    (ja, fa, da), (jb, fb, db) = a, b
+    assert (fa, da) == (fb, db)
+    assert len(ja) == len(jb)
+    assert (ja == jb).all()
+
+
+@pytest.mark.parametrize("n,kind,et,exact", [(600, "euc", 8, True), (600, "euc", 8, False), (1100, "snp", 8, True),
+                                             (700, "snp", 4, True), (700, "snp", 2, False), (500, "snp", 1, True),
+                                             (2100, "euc", 8, False)])
+def test_shard_world1_matches_single(dev, n, kind, et, exact):
+    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
+    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=0, exact=exact)[:3]
+    got = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=0, exact=exact)[:3]
+    _same(got, ref)
+
+
+@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if "nj" in c["args"] and not c["name"].startswith("miss")], ids=lambda c: c["name"])
+def test_shard_golden_nj(dev, case):
+    import ccphylo_amd as cg
+    path, method, et, bs, flags, prec = parse_tree_args(case["args"])
+
+    def run(D, n):
+        joins, fn, fd, _ = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=method, flags=flags)
+        return joins, fn, fd
+    trees = cg.newick_from_phylip(path, run, etype=et, byte_scale=bs, flags=flags, precision=prec)
+    assert ("\n".join(trees) + "\n").encode() == golden_bytes(case)
+
+
+def test_shard_refuses_dnj_and_missing(dev):
+    import ccphylo_amd as cg
+    n = 50
+    D = _euclid(n, 1)
+    with pytest.raises(cg.CcgError, match="not supported"):
+        dev.tree_shard(D, n, None, method=1)
+    D[17] = -1.0
+    with pytest.raises(cg.CcgError, match="not supported"):
+        dev.tree_shard(D, n, None, method=0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, n, kind, et, exact, transport, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
+    dev = cg.Device(0)
+    coll = nt.HostColl(dist) if transport == "gloo" else nt.RcclColl(dev, dist)
+    if transport == "gloo":
+        joins, fn, fd, st = dev.tree_shard(D, n, coll, etype=et, byte_scale=bs, method=0, exact=exact)
+    else:
+        loc = nt.shard_extract(D, n, rank, world)
+        p = dev.malloc(max(loc.nbytes, 1))
+        dev.h2d(p, loc)
+        joins, fn, fd, st = dev.tree_shard_dev(p, n, coll, etype=et, byte_scale=bs, method=0, exact=exact)
+        dev.free(p)
+        coll.close()
+    np.save(os.path.join(out_dir, f"j{rank}.npy"), joins)
+    np.save(os.path.join(out_dir, f"f{rank}.npy"), np.array([fn, fd]))
+    dev.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,kind,et,exact,transport", [(2, 700, "euc", 8, True, "gloo"),
+                                                             (3, 450, "snp", 8, True, "gloo"),
+                                                             (2, 400, "snp", 2, False, "gloo"),
+                                                             (1, 900, "euc", 8, True, "rccl")])
+def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport):
+    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
+    ref_j, ref_fn, ref_fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=0, exact=exact)
+    mp.start_processes(_rank_main, args=(world, _free_port(), n, kind, et, exact, transport, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        j = np.load(tmp_path / f"j{r}.npy")
+        fn, fd = np.load(tmp_path / f"f{r}.npy")
+        assert (int(fn), fd) == (ref_fn, ref_fd)
+        assert len(j) == len(ref_j) and (j == ref_j).all()
