@@ -193,6 +193,63 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
                          "ops_per_word_pair": OPS_PER_WORD_PAIR}}
 
 
+def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64):
+    """NJ with the LT rows sharded over the ranks (ccg_tree_shard_dev; SURVEY
+    8(e)): rank g holds the row bands g, g + world, ... of ONE n-taxon matrix
+    (n = 100k, double: 40 GB in all), collectives over RCCL (world > 1) --
+    strong scaling of one tree.  Timed: the first `joins` joins (each a full
+    initQ scan of the whole matrix), as time(joins + 1) - time(1) so the exact
+    initSummaD and the setup are excluded.  Every rank takes part."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    from tools.synth import euclid_shard_dev
+    coll = nt.RcclColl(dev, dist) if world > 1 else None
+    loc = euclid_shard_dev(torch, n, rank, world)
+    work = torch.empty_like(loc)
+
+    def run(k, profile=False):
+        work.copy_(loc)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        j, fn, fd, st = dev.tree_shard_dev(work.data_ptr(), n, coll, method=cg.CCG_TREE_NJ, exact=False,
+                                           profile=profile, max_joins=k)
+        dt = time.perf_counter() - t0
+        assert len(j) == k, (len(j), k)
+        dt = shard_max(dt, dist)
+        return dt, st
+
+    try:
+        t1, _ = run(1)
+        tk, _ = run(joins + 1)
+        _, pst = run(joins + 1, profile=True)
+    finally:
+        if coll is not None:
+            coll.close()
+    dt = tk - t1
+    # algorithmic bytes of the argmin of the timed joins: every LT cell once (s = 8) + sD
+    cells = sum((m * (m - 1) // 2) for m in range(n - joins, n))
+    gb = (8.0 * cells + 8.0 * n * joins) / dt / 1e9
+    cnt, ns = pst[4 + 2 * 3], pst[5 + 2 * 3]
+    kern_gb = (8.0 * cells / world + 8.0 * n * joins) / (ns / 1e9) / 1e9 if ns else None
+    del loc, work
+    return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 3), "joins": joins,
+            "n": n, "world": world, "seconds": round(dt, 4),
+            "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, 40 GB) with its LT row bands dealt over "
+                      f"{world} GPU(s); first {joins} joins; fast row sums",
+            "hbm_GBps_aggregate": round(gb, 1), "hbm_frac_aggregate": round(gb / (HBM_PEAK_GBS * world), 4),
+            "argmin_kernel_GBps_per_gpu": round(kern_gb, 1) if kern_gb else None,
+            "coll_us_per_join": round(pst[5 + 2 * 8] / 1e3 / (joins + 1), 2) if pst[4 + 2 * 8] else 0.0}
+
+
+def shard_max(x, dist):
+    if dist is None:
+        return x
+    from ccphylo_amd import shard
+    return shard.reduce_max(x, dist)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -302,6 +359,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             d = {"error": str(e)}
         result.setdefault("extras", {})["dist"] = d
+        try:
+            d = nj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None)
+        except Exception as e:  # noqa: BLE001
+            d = {"error": str(e)}
+        result["extras"]["nj_sharded"] = d
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)

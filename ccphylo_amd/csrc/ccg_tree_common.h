@@ -321,6 +321,7 @@ struct KTimer {
 		if(!on) return;
 		harvest();
 		for(int k = 0; k < 1025; ++k) hipEventDestroy(ev[k]);
+		on = false;   // later marks (e.g. a final collective) are not timed
 	}
 };
 

@@ -1759,7 +1759,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	int n = n0;
 	int since_check = 0;
 	bool stopped = false;
-	while(n > 2) {
+	const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
+	while(n > stop_n) {
 		launches += general ? enqueue_iteration<ET, true>(st, D, bs, b, n, n == n0, a->method, kt)
 		                    : enqueue_iteration<ET, false>(st, D, bs, b, n, n == n0, a->method, kt);
 		CCG_CHECK(hipGetLastError());
@@ -1818,7 +1819,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	}
 #endif
 	*njoins = h.njoins;
-	*final_n = h.done ? h.final_n : 2;
+	*final_n = h.done ? h.final_n : n;
 	if(h.njoins) {
 		CCG_CHECK(hipMemcpyAsync(joins, b.joins, (size_t) h.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
 	}

@@ -28,7 +28,7 @@
 
 #define SB CCG_SHARD_BAND
 static_assert(SB == NJ_RB, "a shard band is one NJ argmin row band");
-#define SH_GRID 2048         // max argmin blocks (grid-stride over the tiles)
+#define SH_GRID 8192         // max argmin blocks (grid-stride over the tiles)
 
 struct Shard {
 	int rank, world;
@@ -724,7 +724,8 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	}
 	{
 		int since_check = 0;
-		while(n > 2) {
+		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
+		while(n > stop_n) {
 			const int root = ccg_shard_owner(n - 1, sh.world);
 			SH_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
 			                root));
@@ -762,7 +763,7 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	SH_HIP(hipStreamSynchronize(st));
 	SH_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
 	*njoins = hc.njoins;
-	*final_n = hc.done ? hc.final_n : 2;
+	*final_n = hc.done ? hc.final_n : n;
 	if(hc.njoins) {
 		SH_HIP(hipMemcpyAsync(joins, b.joins, (size_t) hc.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
 	}

@@ -231,7 +231,7 @@ static int main_tree(int argc, char **argv) {
 				jcap = n;
 				joins = realloc(joins, jcap * sizeof(ccg_join));
 			}
-			ccg_tree_args ta = {n, et, bs, m, flag, !fast, 0};
+			ccg_tree_args ta = {n, et, bs, m, flag, !fast, 0, 0};
 			int nj = 0, fn = 0;
 			double fd = 0;
 			int64_t st[6 + 2 * CCG_NKSTAT];

@@ -51,6 +51,7 @@ class TreeArgs(C.Structure):
     _fields_ = [
         ("n", C.c_int), ("etype", C.c_int), ("byteScale", C.c_double),
         ("method", C.c_int), ("flags", C.c_int), ("exact", C.c_int), ("profile", C.c_int),
+        ("max_joins", C.c_int),
     ]
 
 
@@ -239,49 +240,53 @@ class Device:
         self._check(rc, "ccg_snp_ltd")
         return D[:m], (N[:m] if N is not None else None), inc.value
 
-    def tree(self, D, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False):
+    def tree(self, D, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False,
+             max_joins=0):
         """NJ/DNJ on a packed host LT (ccg_tree).  Returns (joins, final_n, final_d, stats)."""
         D = np.ascontiguousarray(D, dtype=ETYPES[etype])
         assert D.size == n * (n - 1) // 2
-        return self._tree(self.lib.ccg_tree, D.ctypes.data, n, etype, byte_scale, method, flags, exact, profile)
+        return self._tree(self.lib.ccg_tree, D.ctypes.data, n, etype, byte_scale, method, flags, exact, profile,
+                          max_joins)
 
-    def tree_dev(self, dptr, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False):
+    def tree_dev(self, dptr, n, etype=8, byte_scale=1.0, method=CCG_TREE_DNJ, flags=0, exact=True, profile=False,
+                 max_joins=0):
         """Same on a device LT (ccg_tree_dev); the buffer is consumed."""
-        return self._tree(self.lib.ccg_tree_dev, dptr, n, etype, byte_scale, method, flags, exact, profile)
+        return self._tree(self.lib.ccg_tree_dev, dptr, n, etype, byte_scale, method, flags, exact, profile,
+                          max_joins)
 
-    def _tree(self, fn_, dptr, n, etype, byte_scale, method, flags, exact, profile):
+    def _tree(self, fn_, dptr, n, etype, byte_scale, method, flags, exact, profile, max_joins=0):
         joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
         st = (C.c_int64 * (6 + 2 * NKSTAT))()
-        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile))
+        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         rc = fn_(self.h, C.byref(a), C.c_void_p(dptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd), st)
         self._check(rc, "ccg_tree")
         return joins[:nj.value], fn.value, fd.value, list(st)
 
     def tree_shard(self, D, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
-                   profile=False):
+                   profile=False, max_joins=0):
         """Sharded NJ from the full host LT (ccg_tree_shard): this rank uploads
         its own row bands only.  `coll`: a HostColl / RcclColl (None = world 1)."""
         D = np.ascontiguousarray(D, dtype=ETYPES[etype])
         assert D.size == n * (n - 1) // 2
         return self._tree_shard(self.lib.ccg_tree_shard, D.ctypes.data, n, coll, etype, byte_scale, method, flags,
-                                exact, profile)
+                                exact, profile, max_joins)
 
     def tree_shard_dev(self, dptr, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
-                       profile=False):
+                       profile=False, max_joins=0):
         """Sharded NJ on this rank's device row bands (ccg_tree_shard_dev; consumed)."""
         return self._tree_shard(self.lib.ccg_tree_shard_dev, dptr, n, coll, etype, byte_scale, method, flags,
-                                exact, profile)
+                                exact, profile, max_joins)
 
-    def _tree_shard(self, fn_, ptr, n, coll, etype, byte_scale, method, flags, exact, profile):
+    def _tree_shard(self, fn_, ptr, n, coll, etype, byte_scale, method, flags, exact, profile, max_joins):
         joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
         st = (C.c_int64 * (6 + 2 * NKSTAT))()
-        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile))
+        a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         cp = C.byref(coll.c) if coll is not None else None
         rc = fn_(self.h, C.byref(a), cp, C.c_void_p(ptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd),
                  st)

@@ -97,6 +97,8 @@ typedef struct {
 	                          may differ from the reference in the last ulp) */
 	int profile;           /* 1: time every kernel with HIP events on the engine
 	                          stream; per-kernel totals go to stats[4..] */
+	int max_joins;         /* > 0: stop after this many joins (benchmarks time a
+	                          prefix of a large tree); 0: run to n = 2 */
 } ccg_tree_args;
 
 /* stats layout (ccg_tree / ccg_tree_dev, 6 + 2*CCG_NKSTAT entries when

@@ -141,3 +141,16 @@ def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport)
         fn, fd = np.load(tmp_path / f"f{r}.npy")
         assert (int(fn), fd) == (ref_fn, ref_fd)
         assert len(j) == len(ref_j) and (j == ref_j).all()
+
+
+def test_max_joins_prefix(dev):
+    """max_joins stops both engines after a prefix of the same join list."""
+    n, k = 500, 37
+    D = _euclid(n, 5)
+    full = dev.tree(D, n, method=0)[0]
+    for fn in (lambda: dev.tree(D, n, method=0, max_joins=k), lambda: dev.tree(D, n, method=1, max_joins=k),
+               lambda: dev.tree_shard(D, n, None, method=0, max_joins=k)):
+        j, fin, fd, _ = fn()
+        assert len(j) == k and fin == n - k and fd == -1.0
+    j = dev.tree_shard(D, n, None, method=0, max_joins=k)[0]
+    assert (j == full[:k]).all()

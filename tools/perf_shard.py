@@ -21,12 +21,15 @@ def report(tag, n, st, wall):
 
 
 def main():
-    sizes = [int(a) for a in sys.argv[1:]] or [4000, 10000]
+    import faulthandler
+    faulthandler.enable()
+    prof = "--noprof" not in sys.argv
+    sizes = [int(a) for a in sys.argv[1:] if not a.startswith("-")] or [4000, 10000]
     dev = cg.Device(0)
     for n in sizes:
         D = euclid(n, 1)
-        for tag, fn in (("single", lambda: dev.tree(D, n, method=0, exact=False, profile=True)),
-                        ("shard-w1", lambda: dev.tree_shard(D, n, None, method=0, exact=False, profile=True))):
+        for tag, fn in (("single", lambda: dev.tree(D, n, method=0, exact=False, profile=prof)),
+                        ("shard-w1", lambda: dev.tree_shard(D, n, None, method=0, exact=False, profile=prof))):
             t = time.perf_counter()
             j, fnn, fd, st = fn()
             report(tag, n, st, time.perf_counter() - t)

@@ -12,3 +12,31 @@ def euclid(n, seed=1, dim=8):
         o = i * (i - 1) // 2
         D[o:o + i] = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
     return np.round(D * 1e9) / 1e9
+
+
+def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=512):
+    """This rank's row bands (ccg_tree_shard_dev layout: bands of `band` rows
+    dealt round-robin, owned rows back to back, row r = D(r, 0..r-1)) of the
+    Euclidean distances between n points of U[0,1)^dim, computed on the GPU.
+    Every rank draws the same points (CPU generator, fixed seed)."""
+    g = torch.Generator().manual_seed(seed)
+    pts = torch.rand((n, dim), generator=g, dtype=torch.float64).cuda()
+    nb = (n + band - 1) // band
+    mine = list(range(rank, nb, world))
+    sizes = [sum(range(b * band, min(b * band + band, n))) for b in mine]
+    out = torch.empty(max(sum(sizes), 1), dtype=torch.float64, device="cuda")
+    per = max(1, chunk_rows // band)
+    pos = 0
+    for c in range(0, len(mine), per):
+        bands = mine[c:c + per]
+        rows = torch.cat([torch.arange(b * band, min(b * band + band, n), device="cuda") for b in bands])
+        rmax = int(rows[-1])
+        if rmax == 0:
+            continue
+        d = torch.cdist(pts[rows], pts[:rmax], compute_mode="donot_use_mm_for_euclid_dist")
+        mask = torch.arange(rmax, device="cuda")[None, :] < rows[:, None]
+        vals = d[mask]                       # row-major: each row's prefix, rows in order
+        out[pos:pos + vals.numel()] = vals
+        pos += vals.numel()
+    assert pos == sum(sizes)
+    return out
