@@ -8,10 +8,13 @@ configs[1]: an N=10,000-taxon distance matrix, one full tree per step, the
 packed LT already resident in HBM when the timed region starts (one fresh
 device copy per step; the engine consumes its input).
 
-Multi-GPU (torchrun, one process per GPU): every rank builds its own tree on
-its own GPU ("replicas": the NJ loop is a strict dependency chain; the sharded
-DNJ of SURVEY 8(e) is later work) -> scaling "weak", value = all ranks' joins
-divided by the max over ranks of the timed span.
+Multi-GPU (torchrun, one process per GPU): every rank builds its own N=10k
+tree on its own GPU ("replicas") -> scaling "weak", value = all ranks' joins
+divided by the max over ranks of the timed span.  One N=10k tree does not
+gain from more GPUs (a join is ~35 us of dependent steps); the sharded path is
+measured where it pays, in extras.nj_sharded: ONE N=100k matrix (40 GB) with
+its LT row bands dealt over all ranks, NJ joins with RCCL exchanges
+(ccg_tree_shard_dev), strong scaling.
 
 Also reported: the dominant kernel's roofline (HIP-event timing of every
 kernel in one profiled extra step on the engine stream; algorithmic bytes as
@@ -45,6 +48,7 @@ VALU_INT_LANE_OPS = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
+SHARD_LEG_TIMEOUT_S = 300
 
 
 from tools.synth import euclid as euclid_ltd  # noqa: E402
@@ -193,7 +197,7 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
                          "ops_per_word_pair": OPS_PER_WORD_PAIR}}
 
 
-def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64):
+def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, transport="rccl"):
     """NJ with the LT rows sharded over the ranks (ccg_tree_shard_dev; SURVEY
     8(e)): rank g holds the row bands g, g + world, ... of ONE n-taxon matrix
     (n = 100k, double: 40 GB in all), collectives over RCCL (world > 1) --
@@ -203,7 +207,9 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64):
     import ccphylo_amd as cg
     from ccphylo_amd import native as nt
     from tools.synth import euclid_shard_dev
-    coll = nt.RcclColl(dev, dist) if world > 1 else None
+    coll = None
+    if world > 1:
+        coll = nt.RcclColl(dev, dist) if transport == "rccl" else nt.HostColl(dist)
     loc = euclid_shard_dev(torch, n, rank, world)
     work = torch.empty_like(loc)
 
@@ -225,7 +231,7 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64):
         tk, _ = run(joins + 1)
         _, pst = run(joins + 1, profile=True)
     finally:
-        if coll is not None:
+        if coll is not None and transport == "rccl":
             coll.close()
     dt = tk - t1
     # algorithmic bytes of the argmin of the timed joins: every LT cell once (s = 8) + sD
@@ -236,8 +242,9 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64):
     del loc, work
     return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 3), "joins": joins,
             "n": n, "world": world, "seconds": round(dt, 4),
-            "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, 40 GB) with its LT row bands dealt over "
-                      f"{world} GPU(s); first {joins} joins; fast row sums",
+            "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, {8 * n * (n - 1) / 2 / 1e9:.1f} GB) with "
+                      f"its LT row bands dealt over {world} GPU(s) ({transport if world > 1 else 'no'} transport); "
+                      f"first {joins} joins; fast row sums",
             "hbm_GBps_aggregate": round(gb, 1), "hbm_frac_aggregate": round(gb / (HBM_PEAK_GBS * world), 4),
             "argmin_kernel_GBps_per_gpu": round(kern_gb, 1) if kern_gb else None,
             "coll_us_per_join": round(pst[5 + 2 * 8] / 1e3 / (joins + 1), 2) if pst[4 + 2 * 8] else 0.0}
@@ -259,6 +266,10 @@ def main():
     ap.add_argument("--sums", choices=["fast", "exact"], default="fast")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--shard-n", type=int, default=100_000)
+    ap.add_argument("--shard-joins", type=int, default=64)
+    ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
+                    help="gloo: host-staged (rehearsal of several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,13 +280,15 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
+    # one GPU per rank; on a smaller box (rehearsals) ranks share the devices
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     import ccphylo_amd as cg
 
     n = args.n
     s = 8
     D = euclid_ltd(n, seed=1)
-    dev = cg.Device(local)
+    dev = cg.Device(gpu)
     exact = args.sums == "exact"
     nbytes = D.nbytes
     bufs = [dev.malloc(nbytes) for _ in range(args.steps + args.warmup)]
@@ -359,14 +372,29 @@ def main():
         except Exception as e:  # noqa: BLE001
             d = {"error": str(e)}
         result.setdefault("extras", {})["dist"] = d
-        try:
-            d = nj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None)
-        except Exception as e:  # noqa: BLE001
-            d = {"error": str(e)}
-        result["extras"]["nj_sharded"] = d
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)
+    if not args.no_extras:
+        # last, under a watchdog: a collective that never completes (e.g. an
+        # RCCL bootstrap failure on one rank) must not cost the whole line
+        import threading
+
+        def _timeout():
+            if rank == 0:
+                result["extras"]["nj_sharded"] = {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"}
+                print(json.dumps(result), flush=True)
+            os._exit(0)
+        wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
+        wd.daemon = True
+        wd.start()
+        try:
+            d = nj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None, n=args.shard_n,
+                               joins=args.shard_joins, transport=args.shard_transport)
+        except Exception as e:  # noqa: BLE001
+            d = {"error": str(e)}
+        wd.cancel()
+        result["extras"]["nj_sharded"] = d
     dev.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -16,6 +16,11 @@ void ccg_set_last_error(hipError_t e, const char *what, const char *file, int li
 	fprintf(stderr, "ccphylo_amd: HIP error: %s\n", g_last_error);
 }
 
+void ccg_set_last_msg(const char *msg) {
+	snprintf(g_last_error, sizeof(g_last_error), "%s", msg);
+	fprintf(stderr, "ccphylo_amd: %s\n", g_last_error);
+}
+
 extern "C" {
 
 const char *ccg_strerror(int code) {

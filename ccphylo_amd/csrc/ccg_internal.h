@@ -23,6 +23,8 @@
 	} while(0)
 
 void ccg_set_last_error(hipError_t e, const char *what, const char *file, int line);
+// free-form text for ccg_strerror(CCG_EHIP) (collective transports)
+void ccg_set_last_msg(const char *msg);
 
 struct ccg_ctx {
 	int device;

@@ -456,8 +456,9 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 
 // ------------------------------------------------------------------ transports
 static int coll_fail(const char *what) {
-	hipError_t e = hipErrorUnknown;
-	ccg_set_last_error(e, what, __FILE__, __LINE__);
+	char m[128];
+	snprintf(m, sizeof(m), "collective transport failed in %s", what);
+	ccg_set_last_msg(m);
 	return CCG_EHIP;
 }
 
@@ -558,14 +559,22 @@ static int rccl_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 	size_t cnt;
 	rccl_type(buf, bytes, &t, &cnt);
 	ncclResult_t r = g_rccl.all_reduce(buf, buf, cnt, t, ncclSum, ((RcclUser *) user)->comm, (hipStream_t) stream);
-	if(r != ncclSuccess) fprintf(stderr, "ccphylo_amd: ncclAllReduce: %s\n", g_rccl.err(r));
+	if(r != ncclSuccess) {
+		char m[160];
+		snprintf(m, sizeof(m), "ncclAllReduce: %s", g_rccl.err(r));
+		ccg_set_last_msg(m);
+	}
 	return r != ncclSuccess;
 }
 
 static int rccl_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
 	ncclResult_t r = g_rccl.bcast(send ? send : recv, recv, bytes, ncclUint8, root, ((RcclUser *) user)->comm,
 	                              (hipStream_t) stream);
-	if(r != ncclSuccess) fprintf(stderr, "ccphylo_amd: ncclBroadcast: %s\n", g_rccl.err(r));
+	if(r != ncclSuccess) {
+		char m[160];
+		snprintf(m, sizeof(m), "ncclBroadcast: %s", g_rccl.err(r));
+		ccg_set_last_msg(m);
+	}
 	return r != ncclSuccess;
 }
 
@@ -844,7 +853,9 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 	memcpy(&uid, id, sizeof(uid));
 	ncclResult_t r = g_rccl.init_rank(&u->comm, world, uid, rank);
 	if(r != ncclSuccess) {
-		fprintf(stderr, "ccphylo_amd: ncclCommInitRank: %s\n", g_rccl.err(r));
+		char m[160];
+		snprintf(m, sizeof(m), "ncclCommInitRank: %s", g_rccl.err(r));
+		ccg_set_last_msg(m);
 		free(u);
 		return CCG_EHIP;
 	}
