@@ -56,6 +56,32 @@ int orc_snp_ltd(int n, int len, const uint64_t *seqs, const uint32_t *incs, int 
 int orc_tree(int n, int etype, double byteScale, void *D, int method, int flags,
              orc_join *joins, int *final_n, double *final_d, int64_t *stats);
 
+/* B1/B2: distances between KMA count matrices (*.mat[.gz]) of template
+ * `tmpl` (ltdmatrixthrd.c:376 ltdMatrixThrd, matcmp.c:448 cmpMats, metrics
+ * matcmp.c:63-446; kma_oracle.c).  D/N receive the packed LT of the *n_out
+ * included samples (room for nfiles(nfiles-1)/2 elements; N may be NULL);
+ * include[nfiles] the inclusion flags.  Returns 0; -2 where the reference
+ * exits(1) ("did not exceed threshold", ltdmatrixthrd.c:337); -3 when a file
+ * cannot be read. */
+#define ORC_KMA_COS    0
+#define ORC_KMA_CHI2   2
+#define ORC_KMA_NCHI2  3
+#define ORC_KMA_NC     4
+#define ORC_KMA_C      5
+#define ORC_KMA_NBC    8
+#define ORC_KMA_BC     9
+#define ORC_KMA_NL1   10
+#define ORC_KMA_NL2   11
+#define ORC_KMA_NLINF 12
+#define ORC_KMA_L1    13
+#define ORC_KMA_L2    14
+#define ORC_KMA_LINF  15
+#define ORC_KMA_LN    16
+#define ORC_KMA_NLN   17
+int orc_kma_dist(int nfiles, const char **files, const char *tmpl, int metric, unsigned lnorm, unsigned norm,
+                 unsigned minDepth, unsigned minLength, double minCov, int etype, double bs, void *D, void *N,
+                 unsigned char *include, int *n_out);
+
 /* initSummaD (nj.c:111) on its own, for unit tests */
 void orc_init_sums(int n, int etype, double byteScale, const void *D, double *sD, int32_t *N);
 

@@ -44,6 +44,9 @@ def lib():
         L.orc_fsacmpair.restype = C.c_uint64
         L.orc_code_table.argtypes = [C.c_uint, C.c_void_p]
         L.orc_init_sums.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_kma_dist.argtypes = [C.c_int, C.c_void_p, C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint,
+                                   C.c_double, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -74,3 +77,39 @@ def snp_ltd(seqs, incs, n, length, pair=False, norm=0, min_length=1, min_cov=0.0
     inc = lib().orc_snp_ltd(n, length, seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length, min_cov,
                             proxi, etype, byte_scale, D.ctypes.data, N.ctypes.data if N is not None else None)
     return D[:m], (N[:m] if N is not None else None), inc
+
+
+KMA_METRICS = {"cos": 0, "chi2": 2, "nchi2": 3, "nc": 4, "c": 5, "nbc": 8, "bc": 9, "nl1": 10, "nl2": 11,
+               "nlinf": 12, "l1": 13, "l2": 14, "linf": 15}
+
+
+def kma_metric(name):
+    """-d name -> (metric id, n of ln / nln) as dist.c:736-790 parses it."""
+    if name in KMA_METRICS:
+        return KMA_METRICS[name], 0
+    if name.startswith("nl") and name[2:].isdigit():
+        return 17, int(name[2:])
+    if name.startswith("l") and name[1:].isdigit():
+        return 16, int(name[1:])
+    raise ValueError(name)
+
+
+def kma_dist(files, tmpl, metric="cos", norm=0, min_depth=15, min_length=1, min_cov=0.5, etype=8,
+             byte_scale=1.0, want_n=False):
+    """KMA *.mat distances (ltdMatrixThrd).  Returns (D, N, include, n) or
+    raises RuntimeError where the reference exits."""
+    mid, ln = kma_metric(metric)
+    nf = len(files)
+    arr = (C.c_char_p * nf)(*[f.encode() for f in files])
+    m = max(nf * (nf - 1) // 2, 1)
+    D = np.zeros(m, dtype=ETYPES[etype])
+    N = np.zeros(m, dtype=ETYPES[etype]) if want_n else None
+    inc = np.zeros(nf, dtype=np.uint8)
+    n = C.c_int(0)
+    rc = lib().orc_kma_dist(nf, arr, tmpl.encode(), mid, ln, norm, min_depth, min_length, min_cov, etype,
+                            byte_scale, D.ctypes.data, N.ctypes.data if N is not None else None, inc.ctypes.data,
+                            C.byref(n))
+    if rc:
+        raise RuntimeError(f"orc_kma_dist: {rc}")
+    k = n.value * (n.value - 1) // 2
+    return D[:k], (N[:k] if N is not None else None), inc, n.value

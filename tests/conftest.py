@@ -68,8 +68,10 @@ def parse_tree_args(args):
     return os.path.join(GOLDEN, inp), method, et, bs, flags, prec
 
 
-def print_phylip(D, n, names, flag, precision, etype=8, bs=1.0):
-    """Formats a packed LT with the product host writer (ccq_print_phy)."""
+def print_phylip(D, n, names, flag, precision, etype=8, bs=1.0, include=None, comment=None):
+    """Formats a packed LT with the product host writer (ccq_print_phy).
+    `include` (one flag per name) selects the printed names; `comment` is
+    the '#' line of format flag 4 (the template name)."""
     import tempfile
     from ccphylo_amd import native
     lib = native.host_lib()
@@ -80,11 +82,15 @@ def print_phylip(D, n, names, flag, precision, etype=8, bs=1.0):
     lib.ccq_print_phy.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_char_p), C.c_void_p, C.c_char_p,
                                   C.c_uint, C.c_int]
     ltd = native._Ltd(n, n, etype, bs, D.ctypes.data if D.size else None)
-    arr = (C.c_char_p * max(n, 1))(*[s.encode() for s in names])
+    arr = (C.c_char_p * max(len(names), 1))(*[s.encode() for s in names])
+    inc = None
+    if include is not None:
+        inc = np.ascontiguousarray(include, dtype=np.uint8)
     with tempfile.NamedTemporaryFile(delete=False) as t:
         path = t.name
     fp = libc.fopen(path.encode(), b"wb")
-    lib.ccq_print_phy(fp, C.byref(ltd), arr, None, None, flag, precision)
+    lib.ccq_print_phy(fp, C.byref(ltd), arr, inc.ctypes.data if inc is not None else None,
+                      comment.encode() if comment is not None else None, flag, precision)
     libc.fclose(fp)
     with open(path, "rb") as f:
         data = f.read()
@@ -105,6 +111,36 @@ def parse_dist_args(args):
         elif a == "-L": o["minLength"] = int(nxt); k += 1
         elif a == "-C": o["minCov"] = float(nxt) / 100; k += 1
         elif a == "-P": o["proxi"] = int(nxt); k += 1
+        elif a == "-x": o["prec"] = int(nxt); k += 1
+        elif a == "-n": o["nout"] = True; k += 1
+        elif a == "-p": o["et"] = 4
+        elif a in ("-s", "-b"):
+            o["et"] = 2 if a == "-s" else 1
+            if nxt is not None and not nxt.startswith("-"):
+                o["bs"] = float(nxt); k += 1
+        k += 1
+    return o
+
+
+def parse_kma_args(args):
+    """dist CLI args of a KMA (*.mat) golden case -> dict (dist.c:508-690 option meanings)."""
+    o = dict(files=[], tmpl=None, metric="cos", flag=1, norm=0, minDepth=15, minLength=1, minCov=0.5, et=8, bs=1.0,
+             prec=9, nout=False)
+    k = 1
+    while k < len(args):
+        a = args[k]
+        nxt = args[k + 1] if k + 1 < len(args) else None
+        if a == "-i":
+            while k + 1 < len(args) and not args[k + 1].startswith("-"):
+                o["files"].append(os.path.join(GOLDEN, args[k + 1]))
+                k += 1
+        elif a == "-r": o["tmpl"] = nxt; k += 1
+        elif a == "-d": o["metric"] = nxt; k += 1
+        elif a == "-f": o["flag"] = int(nxt); k += 1
+        elif a == "-W": o["norm"] = int(nxt); k += 1
+        elif a == "-E": o["minDepth"] = int(float(nxt)); k += 1
+        elif a == "-L": o["minLength"] = int(nxt); k += 1
+        elif a == "-C": o["minCov"] = float(nxt) / 100; k += 1
         elif a == "-x": o["prec"] = int(nxt); k += 1
         elif a == "-n": o["nout"] = True; k += 1
         elif a == "-p": o["et"] = 4

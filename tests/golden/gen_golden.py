@@ -78,6 +78,41 @@ def euclid_phy(path, n, seed, dim=8, fmt="%.9f", gz=False):
             f.write("\t".join(row) + "\n")
 
 
+def kma_sample(path, templates, seed, depth=30, ins=0.0, gz=True, skip=(), trunc=None):
+    """A KMA count matrix (*.mat[.gz]): per template "#name", one row per
+    position "ref A C G T N -" (tab separated), a blank line at the end.
+    `ins` adds insertion rows (ref '-'); `trunc` cuts a template short."""
+    rng = random.Random(seed)
+    op = gzip.open if gz else open
+    with op(path, "wt") as f:
+        for name, ref in templates:
+            if name in skip:
+                continue
+            f.write(f"#{name}\n")
+            rows = ref if not trunc or name not in trunc else ref[:trunc[name]]
+            for b in rows:
+                dep = max(0, int(rng.gauss(depth, depth / 3)))
+                c = [0] * 6
+                base = "ACGT".index(b) if rng.random() > 0.02 else rng.randrange(4)
+                for _ in range(dep):
+                    r = rng.random()
+                    if r < 0.9:
+                        c[base] += 1
+                    elif r < 0.97:
+                        c[rng.randrange(4)] += 1
+                    elif r < 0.985:
+                        c[4] += 1
+                    else:
+                        c[5] += 1
+                f.write(b + "\t" + "\t".join(map(str, c)) + "\n")
+                if ins and rng.random() < ins:
+                    c = [0] * 6
+                    c[rng.randrange(4)] = rng.randrange(1, 20)
+                    c[5] = rng.randrange(0, 10)
+                    f.write("-\t" + "\t".join(map(str, c)) + "\n")
+            f.write("\n")
+
+
 def run(args, out):
     p = subprocess.run([REF] + args, capture_output=True, check=True)
     with open(out, "wb") as f:
@@ -158,6 +193,33 @@ def main():
             f.write(f"#matrix{k}\n")
             f.write(open(fn).read())
     case("multi_dnj", ["tree", "-i", "multi.phy"], "multi_dnj.out", "tree")
+
+    # (v) KMA count matrices (B1/B2): 9 samples x 2 templates -- insertion rows
+    # (s2, s5: stripMat's 7-short stride), a low-depth sample (s3), a missing
+    # template (s4), a truncated one (s7: cmpMats' early -1), a plain file (s8)
+    rng = random.Random(8)
+    t1 = "".join(rng.choice("ACGT") for _ in range(3000))
+    t2 = "".join(rng.choice("ACGT") for _ in range(1500))
+    kfiles = []
+    for k in range(9):
+        fn = f"kma{k}.mat" + ("" if k == 8 else ".gz")
+        kma_sample(fn, [("tmpl_one", t1), ("tmpl_two", t2)], seed=k + 10, depth=8 if k == 3 else 30,
+                   ins=0.01 if k in (2, 5) else 0.0, skip=("tmpl_two",) if k == 4 else (), gz=k != 8,
+                   trunc={"tmpl_one": 2900} if k == 7 else None)
+        kfiles.append(fn)
+    for m in ("cos", "c", "l1", "l2", "linf", "chi2", "nchi2", "nc", "bc", "nbc", "nl1", "nl2", "nlinf", "l3",
+              "nl3"):
+        case(f"kma_{m}", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-d", m], f"kma_{m}.out", "kma")
+    case("kma_t2", ["dist", "-i"] + kfiles + ["-r", "tmpl_two"], "kma_t2.out", "kma")
+    case("kma_t2_c", ["dist", "-i"] + kfiles + ["-r", "tmpl_two", "-d", "c"], "kma_t2_c.out", "kma")
+    case("kma_W", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-W", "1000"], "kma_W.out", "kma")
+    case("kma_p", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-p"], "kma_p.out", "kma")
+    case("kma_s", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-s", "100"], "kma_s.out", "kma")
+    case("kma_b", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-b", "0.5"], "kma_b.out", "kma")
+    case("kma_E5", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-E", "5"], "kma_E5.out", "kma")
+    case("kma_CL", ["dist", "-i"] + kfiles + ["-r", "tmpl_two", "-C", "10", "-L", "100"], "kma_CL.out", "kma")
+    case("kma_n", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-n", "-", "-d", "l1"], "kma_n.out", "kma")
+    case("kma_f5", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-f", "5", "-x", "4"], "kma_f5.out", "kma")
 
     with open("golden.json", "w") as f:
         json.dump({"reference": "ccphylo 0.8.5 (oracle/_ref/ccphylo, built by oracle/Makefile)",

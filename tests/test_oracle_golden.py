@@ -2,7 +2,7 @@
 golden vector the reference binary produced (tests/golden/golden.json)."""
 import pytest
 
-from conftest import golden_bytes, golden_cases, parse_dist_args, parse_tree_args, print_phylip
+from conftest import golden_bytes, golden_cases, parse_dist_args, parse_kma_args, parse_tree_args, print_phylip
 
 
 @pytest.mark.parametrize("case", golden_cases("tree"), ids=lambda c: c["name"])
@@ -33,3 +33,25 @@ def test_dist_oracle_matches_reference(case):
         if N is not None:
             out += print_phylip(N, n, heads, o["flag"], o["prec"], o["et"], o["bs"])
     assert out == golden_bytes(case)
+
+
+def kma_phylip(o, D, N, include, n):
+    """The bytes `ccphylo dist` prints for a KMA run (dist.c:175-179)."""
+    names = [f for f in o["files"]]
+    out = b""
+    if n > 1:
+        out = print_phylip(D, n, names, o["flag"], o["prec"], o["et"], o["bs"], include=include, comment=o["tmpl"])
+        if N is not None:
+            out += print_phylip(N, n, names, o["flag"], o["prec"], o["et"], o["bs"], include=include,
+                                comment=o["tmpl"])
+    return out
+
+
+@pytest.mark.parametrize("case", golden_cases("kma"), ids=lambda c: c["name"])
+def test_kma_oracle_matches_reference(case):
+    from oracle import pyoracle
+    o = parse_kma_args(case["args"])
+    D, N, inc, n = pyoracle.kma_dist(o["files"], o["tmpl"], metric=o["metric"], norm=o["norm"],
+                                     min_depth=o["minDepth"], min_length=o["minLength"], min_cov=o["minCov"],
+                                     etype=o["et"], byte_scale=o["bs"], want_n=o["nout"])
+    assert kma_phylip(o, D, N, inc, n) == golden_bytes(case)
