@@ -289,13 +289,140 @@ static int dist_help(FILE *out) {
 	return out == stderr;
 }
 
+/* dist.c:736-790: -d name -> metric; z, p, np -> -1 (not on the GPU engine) */
+static int kma_metric_id(const char *m, int *id, unsigned *lnorm) {
+	static const struct {
+		const char *name;
+		int id;
+	} tab[] = {{"cos", CCG_KMA_COS}, {"z", -1}, {"chi2", CCG_KMA_CHI2}, {"nchi2", CCG_KMA_NCHI2},
+	           {"nc", CCG_KMA_NC}, {"c", CCG_KMA_C}, {"np", -1}, {"p", -1}, {"nbc", CCG_KMA_NBC},
+	           {"bc", CCG_KMA_BC}, {"nl1", CCG_KMA_NL1}, {"nl2", CCG_KMA_NL2}, {"nlinf", CCG_KMA_NLINF},
+	           {"l1", CCG_KMA_L1}, {"l2", CCG_KMA_L2}, {"linf", CCG_KMA_LINF}};
+	for(size_t k = 0; k < sizeof(tab) / sizeof(tab[0]); ++k) {
+		if(!strcmp(m, tab[k].name)) {
+			*id = tab[k].id;
+			return 0;
+		}
+	}
+	char *e;
+	if(m[0] == 'l') {
+		*lnorm = (unsigned) strtoul(m + 1, &e, 10);
+		*id = CCG_KMA_LN;
+		return *e != 0;
+	}
+	if(!strncmp(m, "nl", 2)) {
+		*lnorm = (unsigned) strtoul(m + 2, &e, 10);
+		*id = CCG_KMA_NLN;
+		return *e != 0;
+	}
+	return 1;
+}
+
+/* filebuff.c:26 fileExist: the format is the file's first raw byte */
+static int first_byte(const char *path) {
+	FILE *f = fopen(path, "rb");
+	if(!f) return EOF;
+	int c = fgetc(f);
+	fclose(f);
+	return c;
+}
+
+/* dist.c:138-180 with count matrices: ltdMatrixThrd's samples, cmpMats per
+ * pair on the GPU (ccg_kma_ltd), printphy of D (and N) */
+static int dist_kma(char **files, int nfiles, const char *tmpl, const char *outname, const char *noutname,
+                    int metric, unsigned lnorm, unsigned norm, unsigned minDepth, unsigned minLength, double minCov,
+                    unsigned flag, int precision, int et, double bs, unsigned threads, int device) {
+	if(metric < 0) {
+		fprintf(stderr, "ccphylo_amd: distance method is not implemented by the GPU engine (z, p, np).\n");
+		return 1;
+	}
+	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
+	if(!out) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	FILE *nout = NULL;
+	if(noutname) {
+		if(!strcmp(noutname, outname)) nout = out;
+		else if(noutname[0] == '-' && noutname[1] == 0) nout = stdout;
+		else nout = fopen(noutname, "wb");
+		if(!nout) {
+			fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+			return 1;
+		}
+	}
+	ccq_kma *K = ccq_load_kma(files, nfiles, tmpl, minDepth, minLength, minCov, threads > 16 ? (int) threads : 16,
+	                          stderr);
+	if(K->status) return 1;
+	const int n = K->n;
+	ccq_ltd *D = ccq_ltd_new(n > 1 ? n : 2, et, bs), *N = ccq_ltd_new(n > 1 ? n : 2, et, bs);
+	D->n = N->n = 0;
+	if(n > 1) {
+		ccg_ctx *ctx = open_gpu(device);
+		ccg_kma_args a;
+		memset(&a, 0, sizeof(a));
+		a.n = n;
+		a.metric = metric;
+		a.lnorm = lnorm;
+		a.norm = norm;
+		a.minDepth = minDepth;
+		a.minLength = minLength;
+		a.minCov = minCov;
+		a.etype = et;
+		a.byteScale = bs;
+		a.stride1 = K->stride1;
+		a.rec1 = K->rec1;
+		a.len1 = K->len1;
+		a.stride2 = K->stride2;
+		a.rec2 = K->rec2;
+		a.len2 = K->len2;
+		int64_t fatal = -1;
+		int rc = ccg_kma_ltd(ctx, &a, D->mat, N->mat, &fatal);
+		ccg_destroy(ctx);
+		if(rc) {
+			fprintf(stderr, "ccphylo_amd: distance computation failed: %s\n", ccg_strerror(rc));
+			return 1;
+		}
+		if(fatal >= 0) {
+			int64_t i = 1;
+			while((i + 1) * i / 2 <= fatal) ++i;
+			const int64_t j = fatal - i * (i - 1) / 2;
+			fprintf(stderr, "Template (\"%s\") did not exceed threshold for inclusion:\t%s\n", tmpl,
+			        files[K->file_of[j]]);
+			return 1;
+		}
+		if(et >= 4) {   /* cmpMatThrd's warning (it names files[row]) */
+			for(int64_t i = 1, f = 0; i < n; ++i) {
+				for(int64_t j = 0; j < i; ++j, ++f) {
+					if(ccq_ltd_get(D, f) == -1.0) {
+						fprintf(stderr, "No sufficient overlap between samples:\t%s\t%s\n", files[i],
+						        files[K->file_of[j]]);
+					}
+				}
+			}
+		}
+		D->n = N->n = n;
+	}
+	if(1 < D->n) {
+		ccq_print_phy(out, D, files, K->include, tmpl, flag, precision);
+		if(nout && 1 < N->n) ccq_print_phy(nout, N, files, K->include, tmpl, flag, precision);
+	}
+	if(out != stdout) fclose(out);
+	else fflush(stdout);
+	if(nout && nout != out && nout != stdout) fclose(nout);
+	ccq_ltd_free(D);
+	ccq_ltd_free(N);
+	ccq_kma_free(K);
+	return 0;
+}
+
 static int main_dist(int argc, char **argv) {
 	const char *outname = "-", *noutname = NULL;
 	char **files = NULL;
 	int nfiles = 0, precision = 9, et = 8, device = 0;
-	unsigned flag = 1, norm = 0, minLength = 1, proxi = 0;
+	unsigned flag = 1, norm = 0, minLength = 1, proxi = 0, minDepth = 15, threads = 1;
 	double minCov = 0.5, bs = 1.0;
-	const char *unsup = NULL;
+	const char *unsup = NULL, *tmpl = NULL, *method = "cos";
 	Args A = {argc, 0, argv};
 	for(A.k = 1; A.k < argc; ++A.k) {
 		char *a = argv[A.k];
@@ -335,15 +462,19 @@ static int main_dist(int argc, char **argv) {
 			else if(!strcmp(name, "proximity")) proxi = (unsigned) opt_num(&A, att, "proximity");
 			else if(!strcmp(name, "flag")) flag = (unsigned) opt_num(&A, att, "flag");
 			else if(!strcmp(name, "flag_help")) flag = (unsigned) -1;
-			else if(!strcmp(name, "threads")) (void) opt_num(&A, att, "threads");
+			else if(!strcmp(name, "threads")) threads = (unsigned) opt_num(&A, att, "threads");
 			else if(!strcmp(name, "float_precision")) et = 4;
 			else if(!strcmp(name, "short_precision")) { et = 2; bs = opt_dvalue_def(&A, att, bs, "short_precision"); }
 			else if(!strcmp(name, "byte_precision")) { et = 1; bs = opt_dvalue_def(&A, att, bs, "byte_precision"); }
 			else if(!strcmp(name, "mmap")) { }
 			else if(!strcmp(name, "tmp")) (void) opt_value(&A, att, "tmp");
 			else if(!strcmp(name, "device")) device = (int) opt_num(&A, att, "device");
-			else if(!strcmp(name, "distance") || !strcmp(name, "min_depth") || !strcmp(name, "significance_lvl")) (void) opt_value(&A, att, name);
-			else if(!strcmp(name, "reference") || !strcmp(name, "add") || !strcmp(name, "methylation_motifs") ||
+			else if(!strcmp(name, "distance")) method = opt_value(&A, att, name);
+			else if(!strcmp(name, "distance_help")) method = NULL;
+			else if(!strcmp(name, "min_depth")) minDepth = (unsigned) strtod(opt_value(&A, att, name), NULL);
+			else if(!strcmp(name, "significance_lvl")) (void) opt_value(&A, att, name);
+			else if(!strcmp(name, "reference")) tmpl = opt_value(&A, att, name);
+			else if(!strcmp(name, "add") || !strcmp(name, "methylation_motifs") ||
 			        !strcmp(name, "nucleotide_variations")) { (void) opt_value(&A, att, name); unsup = name; }
 			else if(!strcmp(name, "help")) return dist_help(stdout);
 			else die_opt("Unknown", a);
@@ -376,10 +507,13 @@ static int main_dist(int argc, char **argv) {
 				case 'W': norm = (unsigned) opt_num(&A, att, "W"); break;
 				case 'P': proxi = (unsigned) opt_num(&A, att, "P"); break;
 				case 'f': flag = (unsigned) opt_num(&A, att, "f"); break;
-				case 't': (void) opt_num(&A, att, "t"); break;
+				case 't': threads = (unsigned) opt_num(&A, att, "t"); break;
 				case 'T': (void) opt_value(&A, att, "T"); break;
-				case 'd': case 'E': case 'l': (void) opt_value(&A, att, "d"); break;
-				case 'r': case 'a': case 'y': case 'V': {
+				case 'd': method = opt_value(&A, att, "d"); break;
+				case 'E': minDepth = (unsigned) strtod(opt_value(&A, att, "E"), NULL); break;
+				case 'l': (void) opt_value(&A, att, "l"); break;
+				case 'r': tmpl = opt_value(&A, att, "r"); break;
+				case 'a': case 'y': case 'V': {
 					static char nm[2];
 					nm[0] = o;
 					(void) opt_value(&A, att, nm);
@@ -390,7 +524,8 @@ static int main_dist(int argc, char **argv) {
 				case 'b': et = 1; bs = opt_dvalue_def(&A, att, bs, "b"); break;
 				case 'p': et = 4; took = 0; break;
 				case 'F': flag = (unsigned) -1; took = 0; break;
-				case 'D': case 'H': took = 0; break;
+				case 'D': method = NULL; took = 0; break;
+				case 'H': took = 0; break;
 				case 'h': return dist_help(stdout);
 				default: {
 					char bad[3] = {'-', o, 0};
@@ -414,8 +549,37 @@ static int main_dist(int argc, char **argv) {
 		fprintf(stdout, "#\n");
 		return 0;
 	}
+	if(!method) {
+		fprintf(stdout, "# Distance calculation methods:\n");
+		fprintf(stdout, "#\n");
+		fprintf(stdout, "# cos:\tCalculate distance between positions as the angle between the count vectors.\n");
+		fprintf(stdout, "# z:\tMake consensus comparison if vectors passes a McNemar test\n");
+		fprintf(stdout, "# chi2:\tCalculate the chi square distance\n");
+		fprintf(stdout, "# nchi2:\tCalculate the normalized chi square distance\n");
+		fprintf(stdout, "# c:\tCalculate the Clausen distance between the count vectors. d(A,B) = (||A-B||_1 / sum(max{Ai, Bi}))\n");
+		fprintf(stdout, "# nc:\tCalculate the normalized Clausen distance between the count vectors.\n");
+		fprintf(stdout, "# bc:\tCalculate the Bray-Curtis dissimilarity between the count vectors.\n");
+		fprintf(stdout, "# nbc:\tCalculate the normalized Bray-Curtis dissimilarity between the count vectors.\n");
+		fprintf(stdout, "# ln:\tCalculate distance between positions as the n-norm distance between the count vectors. Replace \"n\" with the waned norm\n");
+		fprintf(stdout, "# linf:\tCalculate distance between positions as the l_infinity distance between the count vectors.\n");
+		fprintf(stdout, "# nln:\tCalculate distance between positions as the normalized n-norm distance between the count vectors. Replace last \"n\" with the waned norm\n");
+		fprintf(stdout, "# nlinf:\tCalculate distance between positions as the normalized l_infinity distance between the count vectors.\n");
+		fprintf(stdout, "#\n");
+		return 0;
+	}
+	int metric;
+	unsigned lnorm = 0;
+	if(kma_metric_id(method, &metric, &lnorm)) die_opt("Invalid", "\"-d\"");
 	if(unsup) {
 		fprintf(stderr, "ccphylo_amd: dist option \"%s\" is not implemented by the GPU engine.\n", unsup);
+		return 1;
+	}
+	if(tmpl && nfiles > 1 && !(flag & 16) && first_byte(files[0]) != '>') {
+		return dist_kma(files, nfiles, tmpl, outname, noutname, metric, lnorm, norm, minDepth, minLength, minCov,
+		                flag, precision, et, bs, threads, device);
+	}
+	if(metric < 0) {
+		fprintf(stderr, "ccphylo_amd: distance method \"%s\" is not implemented by the GPU engine.\n", method);
 		return 1;
 	}
 	if(nfiles > 1) {

@@ -47,6 +47,31 @@ class SnpArgs(C.Structure):
     ]
 
 
+class KmaArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int), ("metric", C.c_int), ("lnorm", C.c_uint), ("norm", C.c_uint), ("minDepth", C.c_uint),
+        ("minLength", C.c_uint), ("minCov", C.c_double), ("etype", C.c_int), ("byteScale", C.c_double),
+        ("stride1", C.c_int64), ("rec1", C.c_void_p), ("len1", C.c_void_p),
+        ("stride2", C.c_int64), ("rec2", C.c_void_p), ("len2", C.c_void_p),
+    ]
+
+
+# -d names of `ccphylo dist` on count matrices (dist.c:736-790) -> CCG_KMA_*
+KMA_METRICS = {"cos": 0, "chi2": 2, "nchi2": 3, "nc": 4, "c": 5, "nbc": 8, "bc": 9, "nl1": 10, "nl2": 11,
+               "nlinf": 12, "l1": 13, "l2": 14, "linf": 15}
+
+
+def kma_metric(name):
+    """-d name -> (CCG_KMA_* id, n of l<n> / nl<n>)."""
+    if name in KMA_METRICS:
+        return KMA_METRICS[name], 0
+    if name.startswith("nl") and name[2:].isdigit():
+        return 17, int(name[2:])
+    if name.startswith("l") and name[1:].isdigit():
+        return 16, int(name[1:])
+    raise ValueError(f"distance method {name!r} is not on the GPU engine")
+
+
 class TreeArgs(C.Structure):
     _fields_ = [
         ("n", C.c_int), ("etype", C.c_int), ("byteScale", C.c_double),
@@ -78,6 +103,7 @@ ENGINE_SYMBOLS = [
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
+    "ccg_kma_ltd", "ccg_kma_ltd_dev",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -86,7 +112,7 @@ HOST_SYMBOLS = [
     "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
     "ccq_replay_newick", "ccq_newick_pair",
     "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
-    "ccq_load_msa", "ccq_msa_free",
+    "ccq_load_msa", "ccq_msa_free", "ccq_load_kma", "ccq_kma_free",
 ]
 
 _engine = None
@@ -128,6 +154,8 @@ def engine_lib():
                                        C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int64)]
         lib.ccg_tree_shard_dev.argtypes = lib.ccg_tree_shard.argtypes
+        lib.ccg_kma_ltd.argtypes = [C.c_void_p, C.POINTER(KmaArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
+        lib.ccg_kma_ltd_dev.argtypes = lib.ccg_kma_ltd.argtypes
         _engine = lib
     return _engine
 
@@ -160,6 +188,10 @@ def host_lib():
         lib.ccq_load_msa.restype = C.c_void_p
         lib.ccq_load_msa.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_double, C.c_uint, C.c_void_p]
         lib.ccq_msa_free.argtypes = [C.c_void_p]
+        lib.ccq_load_kma.restype = C.c_void_p
+        lib.ccq_load_kma.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_uint, C.c_uint, C.c_double, C.c_int,
+                                     C.c_void_p]
+        lib.ccq_kma_free.argtypes = [C.c_void_p]
         _host = lib
     return _host
 
@@ -181,6 +213,13 @@ class _Msa(C.Structure):
     _fields_ = [("n", C.c_int), ("len", C.c_int), ("W", C.c_int), ("pair", C.c_int),
                 ("headers", C.POINTER(C.c_char_p)), ("seqs", C.POINTER(C.c_uint64)),
                 ("incs", C.POINTER(C.c_uint32)), ("minLength", C.c_uint)]
+
+
+class _Kma(C.Structure):
+    _fields_ = [("nfiles", C.c_int), ("n", C.c_int), ("status", C.c_int), ("include", C.POINTER(C.c_uint8)),
+                ("file_of", C.POINTER(C.c_int)), ("stride1", C.c_int64), ("stride2", C.c_int64),
+                ("rec1", C.POINTER(C.c_uint16)), ("rec2", C.POINTER(C.c_uint16)),
+                ("len1", C.POINTER(C.c_int32)), ("len2", C.POINTER(C.c_int32))]
 
 
 # ---------------------------------------------------------------- engine API
@@ -292,6 +331,25 @@ class Device:
                  st)
         self._check(rc, "ccg_tree_shard")
         return joins[:nj.value], fn.value, fd.value, list(st)
+
+    def kma_ltd(self, K, metric="cos", norm=0, min_depth=15, min_length=1, min_cov=0.5, etype=8, byte_scale=1.0,
+                want_n=False):
+        """Count-matrix distances (ccg_kma_ltd) of the samples of a
+        load_kma() result.  Returns (D, N, fatal) with fatal the flat index of
+        the first pair where the reference would exit(1), or -1."""
+        mid, ln = kma_metric(metric)
+        n = K["n"]
+        m = n * (n - 1) // 2
+        D = np.zeros(max(m, 1), dtype=ETYPES[etype])
+        N = np.zeros(max(m, 1), dtype=ETYPES[etype]) if want_n else None
+        a = KmaArgs(n, mid, ln, norm, min_depth, min_length, min_cov, etype, byte_scale,
+                    K["stride1"], K["rec1"].ctypes.data, K["len1"].ctypes.data,
+                    K["stride2"], K["rec2"].ctypes.data, K["len2"].ctypes.data)
+        fatal = C.c_int64(-1)
+        rc = self.lib.ccg_kma_ltd(self.h, C.byref(a), D.ctypes.data, N.ctypes.data if N is not None else None,
+                                  C.byref(fatal))
+        self._check(rc, "ccg_kma_ltd")
+        return D[:m], (N[:m] if N is not None else None), fatal.value
 
     # ---- device memory (ccg_malloc & co.) for HBM-resident inputs
     def malloc(self, nbytes):
@@ -529,6 +587,40 @@ def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0):
     res = (heads, seqs, incs, M.len, M.minLength)
     lib.ccq_msa_free(Mp)
     return res
+
+
+def load_kma(files, tmpl, min_depth=15, min_length=1, min_cov=0.5, threads=16):
+    """KMA count matrices -> the engine's sample views (ccq_load_kma): a dict
+    with n, include (per file), file_of, rec1 (n, stride1, 8), len1, rec2,
+    len2 as numpy arrays."""
+    lib = host_lib()
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    log = libc.fopen(b"/dev/null", b"w")
+    arr = (C.c_char_p * max(len(files), 1))(*[f.encode() for f in files])
+    try:
+        p = lib.ccq_load_kma(arr, len(files), tmpl.encode(), min_depth, min_length, min_cov, threads, log)
+    finally:
+        libc.fclose(log)
+    K = _Kma.from_address(p)
+    try:
+        if K.status:
+            raise CcgError(f"ccq_load_kma: cannot read the inputs ({K.status})")
+        n, s1, s2 = K.n, K.stride1, K.stride2
+
+        def take(ptr, count, dtype):
+            return np.ctypeslib.as_array(ptr, shape=(max(count, 1),))[:count].copy().astype(dtype)
+        out = {"n": n, "stride1": s1, "stride2": s2,
+               "include": take(K.include, len(files), np.uint8),
+               "file_of": take(K.file_of, n, np.int32),
+               "rec1": take(K.rec1, n * s1 * 8, np.uint16).reshape(n, s1, 8),
+               "rec2": take(K.rec2, n * s2 * 8, np.uint16).reshape(n, s2, 8),
+               "len1": take(K.len1, n, np.int32), "len2": take(K.len2, n, np.int32)}
+    finally:
+        lib.ccq_kma_free(p)
+    return out
 
 
 def write_phylip(path, D, n, names, flag=1, precision=9, etype=8, byte_scale=1.0):

@@ -10,6 +10,10 @@
  *   ccg_snp_ltd   replaces fsaCmpThreadOut(tnum, &cmpFsaThrd | &cmpairFsaThrd, D, N, ...)
  *                 declared fsacmpthrd.h:49, impl fsacmpthrd.c:76-106,
  *                 called from cdist.c:351/:354 (MSA) and cdist.c:181/:184.
+ *   ccg_kma_ltd   replaces the per-pair cmpMats (matcmp.c:448) calls of
+ *                 ltdMatrixThrd (ltdmatrixthrd.h:52, called dist.c:168):
+ *                 distances between KMA count matrices (*.mat); the host
+ *                 loader (ccq_load_kma) reads every sample once.
  *   ccg_tree_shard  the same loop with the LT rows split over ranks
  *                 (SURVEY.md 8(e)), one process per GPU, collectives over
  *                 RCCL (ccg_rccl_open) or a caller-supplied transport.
@@ -73,6 +77,57 @@ int ccg_snp_ltd(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_
 /* Same, with a->seqs / a->incs and D / N all DEVICE pointers (HBM-resident
  * pipeline: dist writes the LT that ccg_tree_dev consumes in place). */
 int ccg_snp_ltd_dev(ccg_ctx *ctx, const ccg_snp_args *a, void *D_dev, void *N_dev, int *inc_out);
+
+/* ------------------------------------------------------------------ */
+/* dist on KMA count matrices (matcmp.c:448 cmpMats per pair)          */
+/* ------------------------------------------------------------------ */
+/* -d metrics (dist.c:736-790 names -> these ids) */
+#define CCG_KMA_COS    0   /* cos (default)  matcmp.c:420 */
+#define CCG_KMA_CHI2   2   /* chi2   :381 */
+#define CCG_KMA_NCHI2  3   /* nchi2  :396 */
+#define CCG_KMA_NC     4   /* nc     :243 */
+#define CCG_KMA_C      5   /* c      :278 */
+#define CCG_KMA_NBC    8   /* nbc    :206 */
+#define CCG_KMA_BC     9   /* bc     :227 */
+#define CCG_KMA_NL1   10   /* nl1    :63 */
+#define CCG_KMA_NL2   11   /* nl2    :81 */
+#define CCG_KMA_NLINF 12   /* nlinf  :122 */
+#define CCG_KMA_L1    13   /* l1     :143 */
+#define CCG_KMA_L2    14   /* l2     :158 */
+#define CCG_KMA_LINF  15   /* linf   :193 */
+#define CCG_KMA_LN    16   /* l<n>   :173 (pow: parity within 1e-12 relative) */
+#define CCG_KMA_NLN   17   /* nl<n>  :98  (pow: parity within 1e-12 relative) */
+
+/* One position of a sample: 8 u16 = counts A C G T - N, then the u32 depth
+ * total (little endian), the row layout of FileBuffLoadMat (matparse.c:213). */
+typedef struct {
+	int n;                  /* included samples, in LT row order */
+	int metric;             /* CCG_KMA_* */
+	unsigned lnorm;         /* n of l<n> / nl<n> */
+	unsigned norm;          /* -W */
+	unsigned minDepth;      /* -E */
+	unsigned minLength;     /* -L */
+	double minCov;          /* -C / 100 */
+	int etype;              /* 8, 4, 2, 1 */
+	double byteScale;
+	int64_t stride1;        /* rows per sample in rec1 */
+	const uint16_t *rec1;   /* n x stride1 x 8: a sample as the row sample (mat1,
+	                           after stripMat matcmp.c:27), zero past len1 */
+	const int32_t *len1;    /* mat1->len after stripMat */
+	int64_t stride2;        /* rows per sample in rec2 */
+	const uint16_t *rec2;   /* n x stride2 x 8: a sample as the column sample
+	                           (its rows with ref != '-', in order) */
+	const int32_t *len2;    /* rows in rec2 */
+} ccg_kma_args;
+
+/* Host buffers.  D / N (N may be NULL) receive the packed LT of n elements
+ * of `etype` in reference cell order: cell (i, j) = cmpMats(sample i as mat1,
+ * sample j as mat2).  *fatal (may be NULL) receives the flat index of the
+ * first cell where cmpMats returns -2 -- the reference then exits(1)
+ * ("did not exceed threshold", ltdmatrixthrd.c:337) -- or -1. */
+int ccg_kma_ltd(ccg_ctx *ctx, const ccg_kma_args *a, void *D, void *N, int64_t *fatal);
+/* Same with rec1/len1/rec2/len2 and D/N all device pointers. */
+int ccg_kma_ltd_dev(ccg_ctx *ctx, const ccg_kma_args *a, void *D_dev, void *N_dev, int64_t *fatal);
 
 /* ------------------------------------------------------------------ */
 /* tree: NJ / DNJ on an HBM-resident packed LT matrix                  */

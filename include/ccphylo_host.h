@@ -113,6 +113,22 @@ ccq_msa *ccq_load_msa(ccq_reader *r, unsigned flag, unsigned minLength, double m
                       unsigned proxi, FILE *log);
 void ccq_msa_free(ccq_msa *M);
 
+/* KMA count matrices (*.mat[.gz]) of template `tmpl` for ccg_kma_ltd
+ * (ltdmatrixthrd.c:376 ltdMatrixThrd's inclusion rules; every file read once,
+ * `threads` at a time).  Exclusions are logged like the reference. */
+typedef struct {
+	int nfiles, n;             /* files given, samples included */
+	int status;                /* 0, or -3 when a file cannot be read */
+	unsigned char *include;    /* per file */
+	int *file_of;              /* included sample -> file index */
+	int64_t stride1, stride2;  /* rows per sample in rec1 / rec2 */
+	uint16_t *rec1, *rec2;     /* n x stride x 8 (see ccg_kma_args) */
+	int32_t *len1, *len2;
+} ccq_kma;
+ccq_kma *ccq_load_kma(char **files, int nfiles, const char *tmpl, unsigned minDepth, unsigned minLength,
+                      double minCov, int threads, FILE *log);
+void ccq_kma_free(ccq_kma *K);
+
 #ifdef __cplusplus
 }
 #endif
