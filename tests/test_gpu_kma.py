@@ -1,8 +1,11 @@
 """GPU parity of count-matrix (KMA *.mat) distances, ccg_kma_ltd:
 bit-exact against the reference's golden vectors and the oracle, through the
 C-ABI and through the CLI.  l<n> / nl<n> go through pow(), which the GPU
-math library does not round like glibc: those compare within 1e-12 relative
-(parity of pow itself is unpinned)."""
+math library does not round like glibc (parity of pow itself is unpinned):
+l<n> compares within 1e-12 relative.  nl<n> raises the FIRST difference
+without |.| (matcmp.c:113), so a position's sum can cancel to about +-1e-20,
+where a one-ulp difference of pow decides between a cube root of ~1e-7 and
+NaN (excluded): nl<n> compares within 1e-6 relative."""
 import os
 import subprocess
 import sys
@@ -18,6 +21,10 @@ sys.path.insert(0, GOLDEN)
 
 def _pow_metric(m):
     return m[0] == "l" and m[1:].isdigit() or m.startswith("nl") and m[2:].isdigit()
+
+
+def _pow_rtol(m):
+    return 1e-6 if m.startswith("nl") else 1e-12
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +55,8 @@ def test_kma_golden_engine(dev, case):
     assert fatal == -1
     got = kma_phylip(o, D, N, K["include"], K["n"])
     if _pow_metric(o["metric"]):
-        np.testing.assert_allclose(_phylip_values(got), _phylip_values(golden_bytes(case)), rtol=1e-12)
+        np.testing.assert_allclose(_phylip_values(got), _phylip_values(golden_bytes(case)),
+                                   rtol=_pow_rtol(o["metric"]))
     else:
         assert got == golden_bytes(case)
 
@@ -58,8 +66,9 @@ def test_kma_golden_cli(case):
     import ccphylo_amd as cg
     p = subprocess.run([cg.CLI_PATH] + case["args"], cwd=GOLDEN, capture_output=True, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
-    if _pow_metric(parse_kma_args(case["args"])["metric"]):
-        np.testing.assert_allclose(_phylip_values(p.stdout), _phylip_values(golden_bytes(case)), rtol=1e-12)
+    m = parse_kma_args(case["args"])["metric"]
+    if _pow_metric(m):
+        np.testing.assert_allclose(_phylip_values(p.stdout), _phylip_values(golden_bytes(case)), rtol=_pow_rtol(m))
     else:
         assert p.stdout == golden_bytes(case)
 
