@@ -263,3 +263,114 @@ void ccq_msa_free(ccq_msa *M) {
 		free(M);
 	}
 }
+
+/* cdist.c:36-194 ltdFsaMatrix_get: the entry `tmpl` of every file.  All files
+ * keep their slot (n = nfiles, stride W): cmpFsaThrd enumerates pairs over the
+ * file indices (fsacmpthrd.c:192-218).  Files without the entry keep zero
+ * sequences (the reference leaves them uninitialised).  Returns NULL where
+ * the reference exits(1) (not FASTA, lengths differ), after its message. */
+ccq_msa *ccq_load_fsa_files(char **files, int nfiles, const char *tmpl, unsigned flag, unsigned minLength,
+                            double minCov, unsigned proxi, unsigned char *include, FILE *log) {
+	unsigned char table[256];
+	const int variant = (flag & 32) ? 32 : (flag & 8) ? 8 : 0;
+	ccq_code_table(flag, table);
+	ccq_msa *M = ccq_xmalloc(sizeof(ccq_msa));
+	memset(M, 0, sizeof(*M));
+	M->pair = (flag & 2) != 0;
+	M->n = nfiles;
+	M->headers = ccq_xmalloc((nfiles > 0 ? nfiles : 1) * sizeof(char *));
+	ccq_str *hdr = ccq_new(64), *seq = ccq_new(1 << 20), *ref = ccq_new(1 << 20);
+	int len = 0, W = 0, have_ref = 0;
+	for(int f = 0; f < nfiles; ++f) {
+		M->headers[f] = strdup(files[f]);
+		include[f] = 1;
+	}
+	for(int f = 0; f < nfiles; ++f) {
+		ccq_reader *r = ccq_open(files[f]);
+		if(!r || ccq_peek(r) != '>') {
+			fprintf(stderr, "\"%s\" is not fasta.\n", files[f]);
+			if(r) ccq_close(r);
+			goto fail;
+		}
+		int found = 0;
+		while(ccq_read_fasta(r, hdr, seq, table)) {
+			if(!strcmp((const char *) hdr->seq + 1, tmpl)) {
+				found = 1;
+				break;
+			}
+		}
+		ccq_close(r);
+		if(!found) {
+			fprintf(log, "Missing template entry (\"%s\") in file:\t%s\n", tmpl, files[f]);
+			include[f] = 0;
+			continue;
+		}
+		if(!have_ref) {
+			/* the first usable file: length, minCov, reference (cdist.c:116-163);
+			 * rows packed for earlier (excluded) files are kept */
+			len = (int) seq->len;
+			if(minLength < minCov * len) minLength = (unsigned) (minCov * len);
+			const int W2 = len / 32 + 1;
+			if(W2 != W) {
+				uint64_t *s2 = calloc((size_t) nfiles * W2, sizeof(uint64_t));
+				uint32_t *i2 = calloc((size_t) (M->pair ? nfiles : 1) * W2, sizeof(uint32_t));
+				if(!s2 || !i2) abort();
+				for(int q = 0; W && q < nfiles; ++q) {
+					memcpy(s2 + (size_t) q * W2, M->seqs + (size_t) q * W, (size_t) (W < W2 ? W : W2) * 8);
+				}
+				free(M->seqs);
+				free(M->incs);
+				M->seqs = s2;
+				M->incs = i2;
+				W = W2;
+			}
+		} else if((int) seq->len != len) {
+			fprintf(stderr, "Sequences does not match: %s\n", files[f]);
+			goto fail;
+		}
+		uint64_t *dst = M->seqs + (size_t) f * W;
+		uint32_t *m = M->incs + (M->pair ? (size_t) f * W : 0);
+		int inc;
+		if(!have_ref || M->pair) {
+			ccq_init_inc(m, len);
+			ccq_pack(seq->seq, len, dst);
+			ccq_inc_update(m, seq->seq, seq->seq, len, proxi, variant);
+			inc = ccq_npos(m, len);
+		} else {
+			inc = len - ccq_pack(seq->seq, len, dst);
+		}
+		if((unsigned) inc < minLength) {
+			fprintf(log, "# Excluded:\t%s\t( %d / %d )\n", files[f], inc, len);
+			include[f] = 0;
+			continue;
+		}
+		fprintf(log, "# Included:\t%s\t( %d / %d )\n", files[f], inc, len);
+		if(!have_ref) {
+			ccq_str *t = ref;
+			ref = seq;
+			seq = t;
+			have_ref = 1;
+		} else if(!M->pair) {
+			ccq_inc_update(M->incs, seq->seq, ref->seq, len, proxi, variant);
+		}
+	}
+	M->len = len;
+	M->W = W > 0 ? W : 1;
+	M->minLength = minLength;
+	if(!M->seqs) {
+		M->seqs = ccq_xmalloc(8);
+		M->incs = ccq_xmalloc(4);
+		M->seqs[0] = 0;
+		M->incs[0] = 0;
+	}
+	ccq_free(hdr);
+	ccq_free(seq);
+	ccq_free(ref);
+	return M;
+fail:
+	ccq_free(hdr);
+	ccq_free(seq);
+	ccq_free(ref);
+	ccq_msa_free(M);
+	return NULL;
+}

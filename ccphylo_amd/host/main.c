@@ -416,6 +416,132 @@ static int dist_kma(char **files, int nfiles, const char *tmpl, const char *outn
 	return 0;
 }
 
+/* cmpFsaThrd's pair order over file indices (fsacmpthrd.c:192-218): the
+ * skip condition is `&&`, so a pair with one excluded file is not skipped;
+ * cells (pi, pj) get these pairs in turn */
+static void fsa_cell_pairs(const unsigned char *include, int n, int64_t cells, int *pi_, int *pj_) {
+	int first = 0;
+	while(first < n && !include[first]) ++first;
+	int si = first + 1, sj = 0;
+	for(int64_t c = 0; c < cells; ++c) {
+		int i = si, j = sj;
+		while(!include[i] && !include[j]) {
+			while(i < n && !include[i]) ++i;
+			while(j < i && !include[j]) ++j;
+			if(i == j) {
+				++i;
+				j = 0;
+			}
+		}
+		pi_[c] = i;
+		pj_[c] = j;
+		si = i;
+		sj = j + 1;
+		if(si == sj) {
+			++si;
+			sj = 0;
+		}
+	}
+}
+
+/* dist.c:138-180 with FASTA files and -r: ltdFsaMatrix_get (cdist.c:36) */
+static int dist_fsa_files(char **files, int nfiles, const char *tmpl, const char *outname, const char *noutname,
+                          unsigned flag, unsigned norm, unsigned minLength, double minCov, unsigned proxi,
+                          int precision, int et, double bs, int device) {
+	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
+	if(!out) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	FILE *nout = NULL;
+	if(noutname) {
+		if(!strcmp(noutname, outname)) nout = out;
+		else if(noutname[0] == '-' && noutname[1] == 0) nout = stdout;
+		else nout = fopen(noutname, "wb");
+	}
+	unsigned char *include = calloc((size_t) nfiles, 1);
+	ccq_msa *M = ccq_load_fsa_files(files, nfiles, tmpl, flag, minLength, minCov, proxi, include, stderr);
+	if(!M) return 1;
+	int Dn = 0;
+	for(int f = 0; f < nfiles; ++f) Dn += include[f] != 0;
+	ccq_ltd *D = ccq_ltd_new(Dn > 1 ? Dn : 2, et, bs), *N = ccq_ltd_new(Dn > 1 ? Dn : 2, et, bs);
+	D->n = N->n = 0;
+	const int W = M->W;
+	if(!Dn) {
+		fprintf(stderr, "All sequences were trimmed away.\n");
+	} else {
+		ccg_ctx *ctx = open_gpu(device);
+		ccg_snp_args sa;
+		memset(&sa, 0, sizeof(sa));
+		sa.len = M->len;
+		sa.stride = W;
+		sa.pair = M->pair;
+		sa.norm = norm;
+		sa.minLength = M->minLength;
+		sa.proxi = M->pair ? proxi : 0;
+		sa.etype = et;
+		sa.byteScale = bs;
+		int rc = CCG_OK;
+		if(!M->pair) {
+			fprintf(stderr, "# %d / %d bases included in distance matrix.\n", ccq_npos(M->incs, M->len), M->len);
+		}
+		if(M->pair || Dn == nfiles) {
+			/* pairs of included files in order (cmpairFsaThrd skips with `||`) */
+			uint64_t *sq = malloc((size_t) Dn * W * 8);
+			uint32_t *ic = malloc((size_t) (M->pair ? Dn : 1) * W * 4);
+			for(int f = 0, r = 0; f < nfiles; ++f) {
+				if(!include[f]) continue;
+				memcpy(sq + (size_t) r * W, M->seqs + (size_t) f * W, (size_t) W * 8);
+				if(M->pair) memcpy(ic + (size_t) r * W, M->incs + (size_t) f * W, (size_t) W * 4);
+				++r;
+			}
+			if(!M->pair) memcpy(ic, M->incs, (size_t) W * 4);
+			sa.n = Dn;
+			sa.seqs = sq;
+			sa.incs = ic;
+			if(Dn > 1) rc = ccg_snp_ltd(ctx, &sa, D->mat, (M->pair && nout) ? N->mat : NULL, NULL);
+			free(sq);
+			free(ic);
+		} else if(Dn > 1) {
+			/* all files, then the cells in cmpFsaThrd's quirky pair order */
+			ccq_ltd *F = ccq_ltd_new(nfiles, et, bs);
+			sa.n = nfiles;
+			sa.seqs = M->seqs;
+			sa.incs = M->incs;
+			rc = ccg_snp_ltd(ctx, &sa, F->mat, NULL, NULL);
+			const int64_t cells = (int64_t) Dn * (Dn - 1) / 2;
+			int *pi_ = malloc((size_t) cells * sizeof(int)), *pj_ = malloc((size_t) cells * sizeof(int));
+			fsa_cell_pairs(include, nfiles, cells, pi_, pj_);
+			for(int64_t c = 0; c < cells; ++c) {
+				const int64_t src = (int64_t) pi_[c] * (pi_[c] - 1) / 2 + pj_[c];
+				memcpy((char *) D->mat + c * et, (char *) F->mat + src * et, (size_t) et);
+			}
+			free(pi_);
+			free(pj_);
+			ccq_ltd_free(F);
+		}
+		ccg_destroy(ctx);
+		if(rc) {
+			fprintf(stderr, "ccphylo_amd: distance computation failed: %s\n", ccg_strerror(rc));
+			return 1;
+		}
+		D->n = Dn;
+		if(M->pair) N->n = Dn;
+	}
+	if(1 < D->n) {
+		ccq_print_phy(out, D, files, include, tmpl, flag, precision);
+		if(nout && 1 < N->n) ccq_print_phy(nout, N, files, include, tmpl, flag, precision);
+	}
+	if(out != stdout) fclose(out);
+	else fflush(stdout);
+	if(nout && nout != out && nout != stdout) fclose(nout);
+	ccq_ltd_free(D);
+	ccq_ltd_free(N);
+	ccq_msa_free(M);
+	free(include);
+	return 0;
+}
+
 static int main_dist(int argc, char **argv) {
 	const char *outname = "-", *noutname = NULL;
 	char **files = NULL;
@@ -574,13 +700,17 @@ static int main_dist(int argc, char **argv) {
 		fprintf(stderr, "ccphylo_amd: dist option \"%s\" is not implemented by the GPU engine.\n", unsup);
 		return 1;
 	}
-	if(tmpl && nfiles > 1 && !(flag & 16) && first_byte(files[0]) != '>') {
+	if(tmpl && nfiles > 1 && !(flag & 16) && first_byte(files[0]) != '>') {   /* dist.c:99-108 */
 		return dist_kma(files, nfiles, tmpl, outname, noutname, metric, lnorm, norm, minDepth, minLength, minCov,
 		                flag, precision, et, bs, threads, device);
 	}
-	if(metric < 0) {
-		fprintf(stderr, "ccphylo_amd: distance method \"%s\" is not implemented by the GPU engine.\n", method);
-		return 1;
+	if(tmpl && nfiles > 1) {
+		if((flag & 2) && proxi) {
+			fprintf(stderr, "ccphylo_amd: pairwise proximity masking (-f 2 with -P) is not implemented by the GPU engine.\n");
+			return 1;
+		}
+		return dist_fsa_files(files, nfiles, tmpl, outname, noutname, flag, norm, minLength, minCov, proxi,
+		                      precision, et, bs, device);
 	}
 	if(nfiles > 1) {
 		fprintf(stderr, "ccphylo_amd: multi-file dist input is not implemented by the GPU engine (use one MSA).\n");

@@ -113,6 +113,12 @@ ccq_msa *ccq_load_msa(ccq_reader *r, unsigned flag, unsigned minLength, double m
                       unsigned proxi, FILE *log);
 void ccq_msa_free(ccq_msa *M);
 
+/* Multi-file FASTA with -r (cdist.c:36 ltdFsaMatrix_get): entry `tmpl` of
+ * every file; n = nfiles (every file keeps its slot), include[nfiles] the
+ * inclusion flags.  NULL where the reference exits(1). */
+ccq_msa *ccq_load_fsa_files(char **files, int nfiles, const char *tmpl, unsigned flag, unsigned minLength,
+                            double minCov, unsigned proxi, unsigned char *include, FILE *log);
+
 /* KMA count matrices (*.mat[.gz]) of template `tmpl` for ccg_kma_ltd
  * (ltdmatrixthrd.c:376 ltdMatrixThrd's inclusion rules; every file read once,
  * `threads` at a time).  Exclusions are logged like the reference. */

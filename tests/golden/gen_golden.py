@@ -221,6 +221,39 @@ def main():
     case("kma_n", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-n", "-", "-d", "l1"], "kma_n.out", "kma")
     case("kma_f5", ["dist", "-i"] + kfiles + ["-r", "tmpl_one", "-f", "5", "-x", "4"], "kma_f5.out", "kma")
 
+    # (vi) multi-file FASTA with -r (cdist.c:36 ltdFsaMatrix_get): one file
+    # per sample holding two template entries; ff3 lacks "gene_b", ff5's
+    # gene_b is mostly N (excluded), so cmpFsaThrd's `&&` pair order shows
+    rng = random.Random(9)
+    ga = [rng.choice("ACGT") for _ in range(2500)]
+    gb = [rng.choice("ACGT") for _ in range(1337)]
+    ffiles = []
+    for k in range(7):
+        fn = f"ff{k}.fsa"
+        with open(fn, "w") as f:
+            for name, base in (("gene_a", ga), ("gene_b", gb)):
+                if name == "gene_b" and k == 3:
+                    continue
+                s_ = list(base)
+                for p_ in range(len(s_)):
+                    r_ = rng.random()
+                    if r_ < 0.02:
+                        s_[p_] = rng.choice("ACGT")
+                    elif r_ < 0.025:
+                        s_[p_] = "N"
+                    elif (name == "gene_b" and k == 5) and r_ < 0.7:
+                        s_[p_] = "N"
+                f.write(f">{name}\n")
+                txt = "".join(s_)
+                for q in range(0, len(txt), 60):
+                    f.write(txt[q:q + 60] + "\n")
+        ffiles.append(fn)
+    case("ff_a", ["dist", "-i"] + ffiles + ["-r", "gene_a"], "ff_a.out", "fsafiles")
+    case("ff_b", ["dist", "-i"] + ffiles + ["-r", "gene_b"], "ff_b.out", "fsafiles")
+    case("ff_b_W", ["dist", "-i"] + ffiles + ["-r", "gene_b", "-W", "1000", "-f", "5"], "ff_b_W.out", "fsafiles")
+    case("ff_b_f3", ["dist", "-i"] + ffiles + ["-r", "gene_b", "-f", "3", "-n", "-"], "ff_b_f3.out", "fsafiles")
+    case("ff_a_f3s", ["dist", "-i"] + ffiles + ["-r", "gene_a", "-f", "3", "-s", "10"], "ff_a_f3s.out", "fsafiles")
+
     with open("golden.json", "w") as f:
         json.dump({"reference": "ccphylo 0.8.5 (oracle/_ref/ccphylo, built by oracle/Makefile)",
                    "cases": cases}, f, indent=1)

@@ -37,7 +37,8 @@ def test_tree_golden_engine(dev, case):
     assert ("\n".join(trees) + "\n").encode() == golden_bytes(case)
 
 
-@pytest.mark.parametrize("case", golden_cases("tree") + golden_cases("dist"), ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", golden_cases("tree") + golden_cases("dist") + golden_cases("fsafiles"),
+                         ids=lambda c: c["name"])
 def test_cli_golden(case):
     import ccphylo_amd as cg
     args = list(case["args"])
