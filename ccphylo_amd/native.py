@@ -112,7 +112,7 @@ HOST_SYMBOLS = [
     "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
     "ccq_replay_newick", "ccq_newick_pair",
     "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
-    "ccq_load_msa", "ccq_msa_free", "ccq_load_kma", "ccq_kma_free",
+    "ccq_load_msa", "ccq_msa_free", "ccq_load_fsa_files", "ccq_load_kma", "ccq_kma_free",
 ]
 
 _engine = None
