@@ -197,6 +197,42 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
                          "ops_per_word_pair": OPS_PER_WORD_PAIR}}
 
 
+def kma_extra(dev, torch, n=256, L=200_000, reps=3, metric="cos"):
+    """Count-matrix (KMA *.mat) distances, ccg_kma_ltd_dev: n samples x L
+    positions of synthetic depth-~30 counts (views built on the GPU; the
+    file loader is not timed).  Rate = sample pairs x positions / s."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    base = torch.randint(0, 4, (L,), device="cuda", generator=g)
+    cnt = torch.randint(0, 3, (n, L, 6), device="cuda", generator=g, dtype=torch.int32)
+    dom = torch.randint(15, 45, (n, L), device="cuda", generator=g, dtype=torch.int32)
+    cnt.scatter_add_(2, base.view(1, L, 1).expand(n, L, 1), dom.unsqueeze(2))
+    tot = cnt.sum(2)
+    rec = torch.zeros((n, L, 4), dtype=torch.int32, device="cuda")
+    rec[:, :, 0] = cnt[:, :, 0] | (cnt[:, :, 1] << 16)
+    rec[:, :, 1] = cnt[:, :, 2] | (cnt[:, :, 3] << 16)
+    rec[:, :, 2] = cnt[:, :, 4] | (cnt[:, :, 5] << 16)
+    rec[:, :, 3] = tot
+    rec1 = torch.zeros((n, L + 1, 4), dtype=torch.int32, device="cuda")
+    rec1[:, :L] = rec
+    len1 = torch.full((n,), L + 1, dtype=torch.int32, device="cuda")   # stripMat without insertions
+    len2 = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    m = n * (n - 1) // 2
+    D = torch.empty(m, dtype=torch.float64, device="cuda")
+    args = (n, rec1.data_ptr(), len1.data_ptr(), L + 1, rec.data_ptr(), len2.data_ptr(), L, D.data_ptr())
+    dev.kma_ltd_dev(*args, metric=metric)
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.kma_ltd_dev(*args, metric=metric)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    dt = min(times)
+    del rec, rec1, cnt, D
+    return {"sample_pairs_per_s": round(m / dt, 1), "position_pairs_per_s": m * L / dt, "seconds": round(dt, 4),
+            "config": f"{n} KMA count matrices x {L} positions, -d {metric}, double, views in HBM"}
+
+
 def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, transport="rccl"):
     """NJ with the LT rows sharded over the ranks (ccg_tree_shard_dev; SURVEY
     8(e)): rank g holds the row bands g, g + world, ... of ONE n-taxon matrix
@@ -372,6 +408,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             d = {"error": str(e)}
         result.setdefault("extras", {})["dist"] = d
+        if world == 1:
+            try:
+                result["extras"]["kma_cos"] = kma_extra(dev, torch)
+            except Exception as e:  # noqa: BLE001
+                result["extras"]["kma_cos"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)

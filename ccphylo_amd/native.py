@@ -351,6 +351,18 @@ class Device:
         self._check(rc, "ccg_kma_ltd")
         return D[:m], (N[:m] if N is not None else None), fatal.value
 
+    def kma_ltd_dev(self, n, rec1_ptr, len1_ptr, stride1, rec2_ptr, len2_ptr, stride2, D_ptr, N_ptr=None,
+                    metric="cos", norm=0, min_depth=15, min_length=1, min_cov=0.5, etype=8, byte_scale=1.0):
+        """ccg_kma_ltd_dev on device views; returns the fatal flat index or -1."""
+        mid, ln = kma_metric(metric)
+        a = KmaArgs(n, mid, ln, norm, min_depth, min_length, min_cov, etype, byte_scale,
+                    stride1, rec1_ptr, len1_ptr, stride2, rec2_ptr, len2_ptr)
+        fatal = C.c_int64(-1)
+        self._check(self.lib.ccg_kma_ltd_dev(self.h, C.byref(a), C.c_void_p(D_ptr),
+                                             C.c_void_p(N_ptr) if N_ptr else None, C.byref(fatal)),
+                    "ccg_kma_ltd_dev")
+        return fatal.value
+
     # ---- device memory (ccg_malloc & co.) for HBM-resident inputs
     def malloc(self, nbytes):
         p = C.c_void_p()
