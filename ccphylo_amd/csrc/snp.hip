@@ -44,21 +44,23 @@ __device__ __forceinline__ uint32_t compress_even(uint64_t x) {
 // qseq2nibble word (position p at bits 63-2p..62-2p) -> (hi, lo) planes
 __global__ void k_planes(const uint64_t *__restrict__ seqs, const uint32_t *__restrict__ incs, int n, int stride,
                          int W32, int Wp, int pair, uint2 *__restrict__ out2, uint4 *__restrict__ out4) {
-	long long e = (long long) blockIdx.x * blockDim.x + threadIdx.x;
-	long long total = (long long) n * Wp;
-	if(e >= total) return;
-	int t = (int) (e / Wp), w = (int) (e % Wp);
-	uint32_t hi = 0, lo = 0, m = 0;
-	if(w < W32) {
-		uint64_t x = seqs[(size_t) t * stride + w];
-		hi = compress_even(x >> 1);
-		lo = compress_even(x);
-		m = pair ? incs[(size_t) t * stride + w] : incs[w];
-	}
-	if(pair) {
-		out4[e] = make_uint4(hi, lo, m, 0);
-	} else {
-		out2[e] = make_uint2(hi & m, lo & m);
+	// grid-stride: n * Wp exceeds 2^32 work-items at config sizes (50k x 5M)
+	const long long total = (long long) n * Wp;
+	for(long long e = (long long) blockIdx.x * blockDim.x + threadIdx.x; e < total;
+	    e += (long long) gridDim.x * blockDim.x) {
+		const int t = (int) (e / Wp), w = (int) (e % Wp);
+		uint32_t hi = 0, lo = 0, m = 0;
+		if(w < W32) {
+			uint64_t x = seqs[(size_t) t * stride + w];
+			hi = compress_even(x >> 1);
+			lo = compress_even(x);
+			m = pair ? incs[(size_t) t * stride + w] : incs[w];
+		}
+		if(pair) {
+			out4[e] = make_uint4(hi, lo, m, 0);
+		} else {
+			out2[e] = make_uint2(hi & m, lo & m);
+		}
 	}
 }
 
@@ -406,7 +408,8 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 	CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
 	CCG_CHECK(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream));
 	long long total = (long long) a->n * Wp;
-	k_planes<<<(unsigned) cdivll(total, 256), 256, 0, ctx->stream>>>(a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair,
+	const long long pg = cdivll(total, 256);
+	k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair,
 	                                                                (uint2 *) planes, (uint4 *) planes);
 	CCG_CHECK(hipGetLastError());
 	int inc = 0;
