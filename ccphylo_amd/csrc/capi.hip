@@ -82,6 +82,7 @@ int ccg_device_info(ccg_ctx *c, char *buf, size_t len) {
 int ccg_snp_ltd_dev(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
 	if(!c || !a || !D) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
 	return ccg_snp_dev_impl(c, a, D, N, inc_out);
 }
 
@@ -140,6 +141,7 @@ int ccg_tree_dev(ccg_ctx *c, const ccg_tree_args *a, void *D, ccg_join *joins, i
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
 	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats);
 }
 

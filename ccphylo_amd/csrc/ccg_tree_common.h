@@ -43,6 +43,9 @@ struct TreeBufs {
 	double *uq;          // per-unit (q, j) of the S rescans, by unit (uoff[t]..uoff[t+1])
 	int *uj;
 	Entry *Sent;         // folded S rows
+	double *ef, *eb;     // replay entries in HBM when more than REPLAY_CAP rows
+	int *erow, *ej;      // qualified below S (S first, then the rest)
+	unsigned char *eacc;
 	int *crow;           // rows found below S with Q < U, descending (k_dnj_select)
 	double *cbnd;        // their bounds Q[row]
 	int *coff;           // and SEG-cell unit offsets (REPLAY_CAP + 1)

@@ -46,7 +46,8 @@
 #define DNJ_B 128        // |S|: top candidate rows rescanned speculatively
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
 #define SEL_BLOCKS 1024  // max grid of k_dnj_select
-#define SCAN_BLOCKS 1024 // max grid of k_dnj_scan
+#define SCAN_BLOCKS 1024 // max grid of k_dnj_scan (default; CCG_SCAN_MAX overrides)
+static int g_scan_div = 4, g_scan_max = 2048;   // grid of k_dnj_scan: min(n / div, max)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
 #define TBF 1024         // threads of k_dnj_find (one block)
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
@@ -642,8 +643,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
 		}
 	}
 	if(tid == 0) ctl->T = T;
-	// more rows than LDS holds: k_dnj_join replays them alone (rare)
-	if(T == 0 || T > REPLAY_CAP) return;
+	if(T == 0) return;
 	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
 	const int K = dcdiv(T, TBF);
 	int mysum = 0;
@@ -651,8 +651,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
 	for(int k = 0; k < K; ++k) {
 		const int e = tid * K + k;
 		if(e < T) {
-			mysum += dcdiv(lrow[e], SEG);
-			cells += lrow[e];
+			const int r = e < REPLAY_CAP ? lrow[e] : b.crow[e];   // past the LDS copy: HBM
+			mysum += dcdiv(r, SEG);
+			cells += r;
 		}
 	}
 	int utot;
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
 		const int e = tid * K + k;
 		if(e < T) {
 			b.coff[e] = pre;
-			pre += dcdiv(lrow[e], SEG);
+			pre += dcdiv(e < REPLAY_CAP ? lrow[e] : b.crow[e], SEG);
 		}
 	}
 	cells = wave_sum_int(cells);
@@ -694,27 +695,32 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	// speculative first TB entries, then the rest once T is known
 	const int r0 = b.crow[tid], o0 = b.coff[tid];
 	const int done = ctl->done, T = ctl->T;
-	if(done || T == 0 || T > REPLAY_CAP) return;
-	if(tid < T) {
-		erow[tid] = r0;
-		eoff[tid] = o0;
+	if(done || T == 0) return;
+	// the entry table in LDS when it fits, else searched in HBM (L2-resident)
+	const bool lds = T <= REPLAY_CAP;
+	if(lds) {
+		if(tid < T) {
+			erow[tid] = r0;
+			eoff[tid] = o0;
+		}
+		for(int e = TB + tid; e < T; e += TB) {
+			erow[e] = b.crow[e];
+			eoff[e] = b.coff[e];
+		}
+		if(tid == 0) eoff[T] = b.coff[T];
 	}
-	for(int e = TB + tid; e < T; e += TB) {
-		erow[e] = b.crow[e];
-		eoff[e] = b.coff[e];
-	}
-	if(tid == 0) eoff[T] = b.coff[T];
 	__syncthreads();
 	TS(2, 1);
-	const int nunits = eoff[T];
+	const int *off = lds ? eoff : b.coff;
+	const int nunits = off[T];
 	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
-		int lo = 0, hi = T - 1;   // last e with eoff[e] <= u
+		int lo = 0, hi = T - 1;   // last e with off[e] <= u
 		while(lo < hi) {
 			int mid = (lo + hi + 1) >> 1;
-			if(eoff[mid] <= u) lo = mid; else hi = mid - 1;
+			if(off[mid] <= u) lo = mid; else hi = mid - 1;
 		}
-		const int r = erow[lo];
-		const int c0 = (u - eoff[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int r = lds ? erow[lo] : b.crow[lo];
+		const int c0 = (u - off[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
 		const int Nr = GEN ? b.N[r] : n;
 		double qq = DBL_MAX;
 		int idx = 0;
@@ -763,7 +769,7 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 // the first bad entry found accepted (b_e < m_e) is certainly accepted, fixes
 // m_{e+1} = f_e, and the next pass starts after it.  Without bad entries this
 // is one pass.  Accepted (Q, P) updates are applied by the writer block only.
-__device__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
+__device__ __forceinline__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
                             const double *e_f, unsigned char *e_acc, bool writer, const TreeBufs &b, int &pi,
                             int &pj, bool *had_bad) {
 	const int lane = threadIdx.x & 63;
@@ -836,101 +842,6 @@ __device__ void replay_wave(int total, double m0, const int *e_row, const int *e
 	}
 }
 
-// k_dnj_join when more rows qualified below S than LDS holds (rare): block 0
-// alone replays minQpair serially, rescanning a row only when the reference
-// would (bound below the running min), then runs updateD for the whole matrix
-// writing the partials of every block slot.  Other blocks exit at once, so
-// no row is read while it is being updated.
-template <int ET, bool GEN>
-__device__ void join_overflow(typename Elem<ET>::T *__restrict__ D, double bs, const TreeBufs &b, int n, int nS,
-                              int T, double m0, int pos_i, int pos_j, int njoins, int neg, bool exact) {
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	__shared__ double s_m;
-	__shared__ int s_pi, s_pj;
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x;
-	if(tid == 0) {
-		double m = m0;
-		int pi = pos_i, pj = pos_j;
-		for(int e = 0; e < nS; ++e) {
-			const Entry x = b.Sent[e];
-			if(x.bnd < m) {
-				b.Q[x.row] = x.f;
-				b.P[x.row] = x.j;
-				if(x.f < m) {
-					m = x.f;
-					pi = x.row;
-					pj = x.j;
-				}
-			}
-		}
-		s_m = m;
-		s_pi = pi;
-		s_pj = pj;
-		ctl->serial_replays++;
-	}
-	__syncthreads();
-	for(int e = 0; e < T; ++e) {
-		const int r = b.crow[e];
-		const double bnd = b.cbnd[e];
-		if(!(bnd < s_m)) continue;
-		double q = DBL_MAX;
-		int idx = 0;
-		row_segment_min<ET, GEN, TB, 8>(D, bs, b.sD, b.N, r, 0, r, GEN ? b.N[r] : n, b.sD[r], -1, 0, 0.0, q, idx);
-		qarg_block_reduce1(q, idx, sq, si);
-		if(tid == 0) {
-			b.Q[r] = q;
-			b.P[r] = idx;
-			if(q < s_m) {
-				s_m = q;
-				s_pi = r;
-				s_pj = idx;
-			}
-		}
-		__syncthreads();
-	}
-	const int i = s_pi, j = s_pj;
-	if(i == 0 && j == 0) {
-		if(tid == 0) {
-			ctl->done = 1;
-			ctl->final_n = n;
-		}
-		return;
-	}
-	const double Dij = Elem<ET>::get(D[tri(i) + j], bs);
-	if(tid == 0) {
-		double Li, Lj;
-		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, neg);
-		ctl->i = i;
-		ctl->j = j;
-		ctl->Li = Li;
-		ctl->Lj = Lj;
-		ctl->Dij = Dij;
-		ccg_join J;
-		J.i = i;
-		J.j = j;
-		J.Li = Li;
-		J.Lj = Lj;
-		b.joins[njoins] = J;
-		ctl->njoins = njoins + 1;
-	}
-	if(GEN) return;   // k_update_general follows
-	for(int vb = 0; vb < (int) cdiv(n, TB); ++vb) {
-		const int k = vb * TB + tid;
-		double Dik = 0, Dkj = 0, sDk = 0;
-		int Nk = 0;
-		if(k < n && k != i && k != j) {
-			Dik = Elem<ET>::get(D[k < i ? tri(i) + k : tri(k) + i], bs);
-			Dkj = Elem<ET>::get(D[k < j ? tri(j) + k : tri(k) + j], bs);
-			sDk = b.sD[k];
-			Nk = b.N[k];
-		}
-		update_body<ET>(D, bs, b, n, i, j, Dij, exact, k, Dik, Dkj, sDk, Nk, vb);
-		__syncthreads();
-	}
-}
-
 // ------------------------------------------------------------------ DNJ join
 // Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
 // replay; then limbLength, the join record and updateD with the whole grid.
@@ -977,22 +888,26 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			s_neg = ctl->neg;
 			s_exact = ctl->exact;
 		}
-		if(done || T > REPLAY_CAP) {
-			if(lane == 0) s_stop = done ? 1 : 2;
+		if(done) {
+			if(lane == 0) s_stop = 1;
 		} else {
 			TS(3, 1);
 			int pi = pos_i, pj = pos_j;
+			// entries in LDS, or in HBM when more rows qualified than LDS holds
+			const bool lds = T <= REPLAY_CAP;
+			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
+			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
 			if(lane < nS) {
-				e_row[lane] = se0.row;
-				e_j[lane] = se0.j;
-				e_b[lane] = se0.bnd;
-				e_f[lane] = se0.f;
+				x_row[lane] = se0.row;
+				x_j[lane] = se0.j;
+				x_b[lane] = se0.bnd;
+				x_f[lane] = se0.f;
 			}
 			if(lane + 64 < nS) {
-				e_row[lane + 64] = se1.row;
-				e_j[lane + 64] = se1.j;
-				e_b[lane + 64] = se1.bnd;
-				e_f[lane + 64] = se1.f;
+				x_row[lane + 64] = se1.row;
+				x_j[lane + 64] = se1.j;
+				x_b[lane + 64] = se1.bnd;
+				x_f[lane + 64] = se1.f;
 			}
 			// fresh (q, j) of each rest entry: fold of its units
 			for(int e0 = 0; e0 < T; e0 += 256) {
@@ -1015,16 +930,18 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 					} else {
 						fold_units(b.cq, b.cj, ua, ub, q, idx);
 					}
-					e_row[nS + e] = r;
-					e_j[nS + e] = idx;
-					e_b[nS + e] = bnd;
-					e_f[nS + e] = q;
+					x_row[nS + e] = r;
+					x_j[nS + e] = idx;
+					x_b[nS + e] = bnd;
+					x_f[nS + e] = q;
 				}
 			}
 			wave_sync();
 			TS(3, 2);
 			bool had_bad;
-			replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad);
+			// two calls so the LDS case keeps ds_* accesses (no flat addressing)
+			if(lds) replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad);
+			else replay_wave(nS + T, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, writer, b, pi, pj, &had_bad);
 			if(writer && lane == 0 && had_bad) ctl->serial_replays++;
 			if(lane == 0) {
 				s_stop = 0;
@@ -1034,11 +951,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		}
 	}
 	__syncthreads();
-	if(s_stop) {
-		if(s_stop == 2 && blockIdx.x == 0)
-			join_overflow<ET, GEN>(D, bs, b, n, ctl->nS, ctl->T, ctl->m0, ctl->pos_i, ctl->pos_j, s_nj, s_neg, s_exact);
-		return;
-	}
+	if(s_stop) return;
 	TS(3, 3);
 	const int i = s_pi, j = s_pj;
 	if(i == 0 && j == 0) {
@@ -1636,6 +1549,9 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_S = take(DNJ_B * 4), o_uo = take((DNJ_B + 1) * 4), o_Sb = take(DNJ_B * 8);
 	size_t o_uq = take(DNJ_B * maxu * 8), o_uj = take(DNJ_B * maxu * 4);
 	size_t o_Se = take(DNJ_B * sizeof(Entry));
+	const size_t nent = (size_t) DNJ_B + ncand;
+	size_t o_ef = take(nent * 8), o_eb = take(nent * 8), o_er = take(nent * 4), o_ej = take(nent * 4);
+	size_t o_ea = take(nent);
 	size_t o_cr = take(ncand * 4), o_cb = take(ncand * 8), o_co = take(ncand * 4);
 	size_t o_cq = take(cunits * 8), o_cj = take(cunits * 4);
 	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
@@ -1658,6 +1574,11 @@ static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.uq = (double *) (m + o_uq);
 	b.uj = (int *) (m + o_uj);
 	b.Sent = (Entry *) (m + o_Se);
+	b.ef = (double *) (m + o_ef);
+	b.eb = (double *) (m + o_eb);
+	b.erow = (int *) (m + o_er);
+	b.ej = (int *) (m + o_ej);
+	b.eacc = (unsigned char *) (m + o_ea);
 	b.crow = (int *) (m + o_cr);
 	b.cbnd = (double *) (m + o_cb);
 	b.cq = (double *) (m + o_cq);
@@ -1689,8 +1610,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
 		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first);
 		kt.mark(CCG_K_TOP);
-		unsigned gc = cdiv(n, 16);
-		if(gc > SCAN_BLOCKS) gc = SCAN_BLOCKS;
+		unsigned gc = cdiv(n, g_scan_div);
+		if(gc > (unsigned) g_scan_max) gc = g_scan_max;
 		k_dnj_find<<<1, TBF, 0, st>>>(b, n);
 		kt.mark(CCG_K_FIND);
 		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n);
@@ -1722,6 +1643,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	const double bs = a->byteScale;
 	hipStream_t st = ctx->stream;
 	TreeWork w;
+	if(const char *e = getenv("CCG_SCAN_DIV")) g_scan_div = atoi(e) > 0 ? atoi(e) : 4;
+	if(const char *e = getenv("CCG_SCAN_MAX")) g_scan_max = atoi(e) > 0 ? atoi(e) : 2048;
 	int rc = tree_alloc(&w, n0, st);
 	if(rc) return rc;
 	TreeBufs b = w.b;

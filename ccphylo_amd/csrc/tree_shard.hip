@@ -896,6 +896,7 @@ int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll,
 	if(rc) return rc;
 	if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
 	switch(a->etype) {
 		case 8: return tree_shard_run_t<8>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
 		case 4: return tree_shard_run_t<4>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);

@@ -2,7 +2,9 @@
  * ccphylo_amd.h -- C-ABI of the MI355X (gfx950) hot-path engine.
  *
  * Plain pointers and sizes only.  Every entry point is synchronous to the
- * caller and returns 0 or a negative CCG_E* code (never exit()s, unlike the
+ * caller; the *_dev ones first wait for all prior work on the device, so
+ * their inputs may be produced on any stream (e.g. PyTorch's).  Each returns
+ * 0 or a negative CCG_E* code (never exit()s, unlike the
  * reference's ERROR(), pherror.h:28).  There is no CPU fallback: if the HIP
  * runtime or a gfx950 device is missing, ccg_init fails with CCG_ENODEV.
  *

@@ -25,6 +25,9 @@ def main():
     D = torch.empty(m, dtype=torch.float64, device="cuda")
     dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
     Dh = D.cpu().numpy().copy()
+    import hashlib
+    print("D md5", hashlib.md5(Dh.tobytes()).hexdigest(), "seqs md5",
+          hashlib.md5(seqs.cpu().numpy().tobytes()).hexdigest(), flush=True)
     for exact in (False, True):
         D.copy_(torch.from_numpy(Dh).cuda())
         t = time.perf_counter()

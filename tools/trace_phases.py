@@ -19,8 +19,21 @@ import numpy as np  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 method = cg.CCG_TREE_NJ if (len(sys.argv) > 2 and sys.argv[2] == "nj") else cg.CCG_TREE_DNJ
-D = euclid(n)
 dev = cg.Device(0)
+if "--clade" in sys.argv:   # config-3-like clade data (tools/config3.py) through the GPU dist
+    import torch
+    from tools.config3 import make_packed
+    L = 1_000_000
+    W = L // 32 + 1
+    seqs = make_packed(torch, n, W)
+    incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
+    incs[(L + 31) // 32:] = 0
+    Dd = torch.empty(n * (n - 1) // 2, dtype=torch.float64, device="cuda")
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
+    D = Dd.cpu().numpy()
+    del seqs, Dd
+else:
+    D = euclid(n)
 for exact in (False, True):
     joins, fn, fd, st = dev.tree(D, n, method=method, exact=exact)
     print(f"exact={exact}: {len(joins)} joins, device {st[3] / 1e3:.1f} ms", flush=True)
