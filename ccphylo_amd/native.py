@@ -119,12 +119,29 @@ _engine = None
 _host = None
 
 
+def _preload_torch_hip():
+    """PyTorch ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded by
+    libtorch_hip as "libamdhip64.so").  Loading it first makes the engine bind
+    to the same HIP runtime, whichever of torch / the engine comes first in the
+    process: one runtime, so device pointers, streams and
+    hipDeviceSynchronize are shared with torch (two runtimes in one process
+    leave torch without a device)."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(p):
+        C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
 def engine_lib():
     """Loads libccphylo_amd.so (raises if it was not built)."""
     global _engine
     if _engine is None:
         if not os.path.exists(ENGINE_PATH):
             raise CcgError(f"{ENGINE_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+        _preload_torch_hip()
         lib = C.CDLL(ENGINE_PATH)
         lib.ccg_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         lib.ccg_destroy.argtypes = [C.c_void_p]
