@@ -771,16 +771,31 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 // is one pass.  Accepted (Q, P) updates are applied by the writer block only.
 __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
                             const double *e_f, unsigned char *e_acc, bool writer, const TreeBufs &b, int &pi,
-                            int &pj, bool *had_bad) {
+                            int &pj, bool *had_bad, int n) {
+	(void) n;   // trace stamps only
 	const int lane = threadIdx.x & 63;
 	int bad = 0;
-	for(int e = lane; e < total; e += 64) {
-		bad |= !(e_f[e] >= e_b[e]);
-		e_acc[e] = 0;
+	// 4 chunks of loads in flight (the entries may live in HBM)
+	for(int e0 = lane; e0 < total; e0 += 256) {
+		double f[4], bb[4];
+#pragma unroll
+		for(int k = 0; k < 4; ++k) {
+			const int e = e0 + 64 * k < total ? e0 + 64 * k : total - 1;
+			f[k] = e_f[e];
+			bb[k] = e_b[e];
+		}
+#pragma unroll
+		for(int k = 0; k < 4; ++k) {
+			if(e0 + 64 * k < total) {
+				bad |= !(f[k] >= bb[k]);
+				e_acc[e0 + 64 * k] = 0;
+			}
+		}
 	}
 	const bool any_bad = __any(bad);
 	*had_bad = any_bad;
 	wave_sync();
+	TS(3, 6);
 	if(any_bad) {
 		double m = m0;
 		int start = 0;
@@ -813,28 +828,57 @@ __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_r
 	// final pass: decisions, writes and the pair (the first contributor that
 	// reaches the final minimum, if it is below m0)
 	double cm = m0;
-	for(int c0 = 0; c0 < total; c0 += 64) {
-		const int e = c0 + lane;
-		const bool valid = e < total;
-		const double f = valid ? e_f[e] : DBL_MAX, bb = valid ? e_b[e] : DBL_MAX;
-		const bool good = valid && f >= bb;
-		const bool contrib = good || (valid && e_acc[e]);
-		const double x = wave_incl_min(contrib ? f : DBL_MAX);
-		double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
-		pre = pre < cm ? pre : cm;
-		const bool accepted = good ? bb < pre : contrib;
-		if(writer && accepted) {
-			b.Q[e_row[e]] = f;
-			b.P[e_row[e]] = e_j[e];
+	for(int g0 = 0; g0 < total; g0 += 256) {
+		double fv[4], bv[4];
+		int rv[4], jv[4], av[4];
+#pragma unroll
+		for(int k = 0; k < 4; ++k) {
+			const int e = g0 + 64 * k + lane < total ? g0 + 64 * k + lane : total - 1;
+			fv[k] = e_f[e];
+			bv[k] = e_b[e];
+			rv[k] = e_row[e];
+			jv[k] = e_j[e];
+			av[k] = e_acc[e];
 		}
-		const double last = readlane_d(x, 63);
-		cm = last < cm ? last : cm;
+#pragma unroll
+		for(int k = 0; k < 4; ++k) {
+			const int c0 = g0 + 64 * k;
+			if(c0 >= total) break;
+			const bool valid = c0 + lane < total;
+			const double f = valid ? fv[k] : DBL_MAX, bb = valid ? bv[k] : DBL_MAX;
+			const bool good = valid && f >= bb;
+			const bool contrib = good || (valid && av[k]);
+			const double x = wave_incl_min(contrib ? f : DBL_MAX);
+			double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
+			pre = pre < cm ? pre : cm;
+			const bool accepted = good ? bb < pre : contrib;
+			if(writer && accepted) {
+				b.Q[rv[k]] = f;
+				b.P[rv[k]] = jv[k];
+			}
+			const double last = readlane_d(x, 63);
+			cm = last < cm ? last : cm;
+		}
 	}
+	TS(3, 7);
 	if(total && cm < m0) {
 		int first_e = 0x7fffffff;
-		for(int e = lane; e < total; e += 64) {
-			const bool contrib = e_f[e] >= e_b[e] || e_acc[e];
-			if(contrib && e_f[e] == cm && e < first_e) first_e = e;
+		for(int e0 = lane; e0 < total; e0 += 256) {
+			double f[4], bb[4];
+			int a[4];
+#pragma unroll
+			for(int k = 0; k < 4; ++k) {
+				const int e = e0 + 64 * k < total ? e0 + 64 * k : total - 1;
+				f[k] = e_f[e];
+				bb[k] = e_b[e];
+				a[k] = e_acc[e];
+			}
+#pragma unroll
+			for(int k = 0; k < 4; ++k) {
+				const int e = e0 + 64 * k;
+				const bool contrib = f[k] >= bb[k] || a[k];
+				if(e < total && contrib && f[k] == cm && e < first_e) first_e = e;
+			}
 		}
 		first_e = wave_min_int(first_e);
 		pi = e_row[first_e];
@@ -851,7 +895,8 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	__shared__ int e_row[DNJ_B + REPLAY_CAP], e_j[DNJ_B + REPLAY_CAP];
 	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
 	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
-	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact;
+	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact, s_nS;
+	__shared__ double s_m0;
 	__shared__ double lq[JOIN_UPRE];
 	__shared__ int lj[JOIN_UPRE];
 	TreeCtl *ctl = b.ctl;
@@ -870,7 +915,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		// ---- loads independent of the outcome
 		const int done = ctl->done, nS = ctl->nS, T = ctl->T;
 		const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
-		const double m0 = ctl->m0;
+		const double m0 = ctl->m0;   // read early (independent of the outcome)
 		Entry se0, se1;
 		se0 = b.Sent[lane];
 		se1 = b.Sent[lane + 64];
@@ -909,49 +954,89 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				x_b[lane + 64] = se1.bnd;
 				x_f[lane + 64] = se1.f;
 			}
-			// fresh (q, j) of each rest entry: fold of its units
-			for(int e0 = 0; e0 < T; e0 += 256) {
+			// fresh (q, j) of the first 256 rest entries: fold of their units
+			// (entries past 256 are folded by the whole block below)
 #pragma unroll
-				for(int m = 0; m < 4; ++m) {
-					const int e = e0 + lane + 64 * m;
-					if(e >= T) continue;
-					const int r = e0 ? b.crow[e] : rr[m];
-					const double bnd = e0 ? b.cbnd[e] : bb[m];
-					const int ua = e0 ? b.coff[e] : c0[m], ub = e0 ? b.coff[e + 1] : c1[m];
-					double q = DBL_MAX;
-					int idx = 0;
-					if(ub <= JOIN_UPRE) {
-						for(int u = ua; u < ub; ++u) {
-							if(qarg_better(lq[u], lj[u], q, idx)) {
-								q = lq[u];
-								idx = lj[u];
-							}
+			for(int m = 0; m < 4; ++m) {
+				const int e = lane + 64 * m;
+				if(e >= T) continue;
+				const int ua = c0[m], ub = c1[m];
+				double q = DBL_MAX;
+				int idx = 0;
+				if(ub <= JOIN_UPRE) {
+					for(int u = ua; u < ub; ++u) {
+						if(qarg_better(lq[u], lj[u], q, idx)) {
+							q = lq[u];
+							idx = lj[u];
 						}
-					} else {
-						fold_units(b.cq, b.cj, ua, ub, q, idx);
 					}
-					x_row[nS + e] = r;
-					x_j[nS + e] = idx;
-					x_b[nS + e] = bnd;
-					x_f[nS + e] = q;
+				} else {
+					fold_units(b.cq, b.cj, ua, ub, q, idx);
 				}
+				x_row[nS + e] = rr[m];
+				x_j[nS + e] = idx;
+				x_b[nS + e] = bb[m];
+				x_f[nS + e] = q;
 			}
 			wave_sync();
-			TS(3, 2);
-			bool had_bad;
-			// two calls so the LDS case keeps ds_* accesses (no flat addressing)
-			if(lds) replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad);
-			else replay_wave(nS + T, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, writer, b, pi, pj, &had_bad);
-			if(writer && lane == 0 && had_bad) ctl->serial_replays++;
 			if(lane == 0) {
 				s_stop = 0;
 				s_pi = pi;
 				s_pj = pj;
+				s_nS = nS;
+				s_m0 = m0;
+			}
+		}
+	}
+	// entries past the first 256: the whole block folds them (T is uniform)
+	const int T = ctl->T;
+	if(T > 256) {
+		__syncthreads();
+		if(!s_stop) {
+			const int nS = s_nS;
+			const bool lds = T <= REPLAY_CAP;
+			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
+			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
+			for(int e = 256 + tid; e < T; e += TB) {
+				const int r = b.crow[e], ua = b.coff[e], ub = b.coff[e + 1];
+				const double bnd = b.cbnd[e];
+				double q = DBL_MAX;
+				int idx = 0;
+				if(ub <= JOIN_UPRE) {
+					for(int u = ua; u < ub; ++u) {
+						if(qarg_better(lq[u], lj[u], q, idx)) {
+							q = lq[u];
+							idx = lj[u];
+						}
+					}
+				} else {
+					fold_units(b.cq, b.cj, ua, ub, q, idx);
+				}
+				x_row[nS + e] = r;
+				x_j[nS + e] = idx;
+				x_b[nS + e] = bnd;
+				x_f[nS + e] = q;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
+	if(wid == 0) {
+		TS(3, 2);
+		const int nS = s_nS;
+		const double m0 = s_m0;
+		int pi = s_pi, pj = s_pj;
+		bool had_bad;
+		// two calls so the LDS case keeps ds_* accesses (no flat addressing)
+		if(T <= REPLAY_CAP) replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad, n);
+		else replay_wave(nS + T, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, writer, b, pi, pj, &had_bad, n);
+		if(writer && lane == 0 && had_bad) ctl->serial_replays++;
+		if(lane == 0) {
+			s_pi = pi;
+			s_pj = pj;
+		}
+	}
+	__syncthreads();
 	TS(3, 3);
 	const int i = s_pi, j = s_pj;
 	if(i == 0 && j == 0) {
