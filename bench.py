@@ -302,6 +302,7 @@ def main():
     ap.add_argument("--sums", choices=["fast", "exact"], default="fast")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-config3", action="store_true", help="skip the 50k x 5M dist+tree leg (~40 s)")
     ap.add_argument("--shard-n", type=int, default=100_000)
     ap.add_argument("--shard-joins", type=int, default=64)
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
@@ -413,6 +414,19 @@ def main():
                 result["extras"]["kma_cos"] = kma_extra(dev, torch)
             except Exception as e:  # noqa: BLE001
                 result["extras"]["kma_cos"] = {"error": str(e)}
+            if not args.no_config3:
+                # configs[2]: N=50k x L=5M tree-like alignment -> dist -> DNJ, all in HBM
+                try:
+                    from tools.config3 import run as config3_run
+                    torch.cuda.empty_cache()
+                    c3 = config3_run(dev, torch)
+                    c3["config"] = ("configs[2]: 50k taxa x 5 Mbp synthetic tree-like alignment (512 clades, ~0.8% "
+                                    "codes flipped per taxon), packed in HBM -> ccg_snp_ltd_dev (double LT, 10 GB) "
+                                    "-> ccg_tree_dev DNJ with fast row sums")
+                    result["extras"]["config3_dist_tree"] = c3
+                except Exception as e:  # noqa: BLE001
+                    result["extras"]["config3_dist_tree"] = {"error": str(e)}
+                torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)
