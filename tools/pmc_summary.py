@@ -19,8 +19,9 @@ import sys
 from collections import defaultdict
 
 NAMES = {"k_dnj_select": "dnj_select", "k_dnj_find": "dnj_find", "k_dnj_scan": "dnj_scan",
-         "k_dnj_join": "update", "k_dnj_requeue": "dnj_requeue", "k_nj_argmin": "nj_argmin",
-         "k_nj_join": "update", "k_nj_pop": "nj_pop"}
+         "k_dnj_join": "update", "k_dnj_requeue": "dnj_requeue"}
+# the NJ passes (tools/perf_dnj.py 10000 nj), when present
+NJ_NAMES = {"k_nj_argmin": "nj_argmin", "k_nj_join": "nj_update", "k_nj_pop": "nj_pop"}
 
 
 def per_kernel(path):
@@ -36,13 +37,20 @@ def main():
     fetch = per_kernel(f"{src}/pmc_fetch/run_counter_collection.csv")
     write = per_kernel(f"{src}/pmc_write/run_counter_collection.csv")
     kernels = {}
-    for k, label in NAMES.items():
-        if k not in fetch:
-            continue
-        f = 2.0 * statistics.mean(fetch[k])
-        w = statistics.mean(write.get(k, [0.0]))
-        kernels[label] = {"kernel": k, "launches": len(fetch[k]), "fetch_bytes_per_launch": round(f, 1),
-                          "write_bytes_per_launch": round(w, 1), "hbm_bytes_per_launch": round(f + w, 1)}
+
+    def add(names, fetch, write):
+        for k, label in names.items():
+            if k not in fetch:
+                continue
+            f = 2.0 * statistics.mean(fetch[k])
+            w = statistics.mean(write.get(k, [0.0]))
+            kernels[label] = {"kernel": k, "launches": len(fetch[k]), "fetch_bytes_per_launch": round(f, 1),
+                              "write_bytes_per_launch": round(w, 1), "hbm_bytes_per_launch": round(f + w, 1)}
+    add(NAMES, fetch, write)
+    import os
+    if os.path.exists(f"{src}/pmc_fetch_nj/run_counter_collection.csv"):
+        add(NJ_NAMES, per_kernel(f"{src}/pmc_fetch_nj/run_counter_collection.csv"),
+            per_kernel(f"{src}/pmc_write_nj/run_counter_collection.csv"))
     cal = {}
     for r in csv.DictReader(open(f"{src}/pmc_cal/run_counter_collection.csv")):
         if "k_rescan<256, 8, false>" in r["Kernel_Name"] and r["Grid_Size"] == "327680":
@@ -54,7 +62,7 @@ def main():
                  "known_read_kib": 256 * 9000 * 8 / 1024.0, "fetch_size_kib": round(kib, 1),
                  "ratio": round(kib / (256 * 9000 * 8 / 1024.0), 4)}
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     f"tools/perf_dnj.py 10000 dnj (fast sums); FETCH_SIZE x2 per MI355X_MICROARCH.md",
+                     f"tools/perf_dnj.py 10000 dnj|nj (fast sums); FETCH_SIZE x2 per MI355X_MICROARCH.md",
            "kernels": kernels, "calibration": calib}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
