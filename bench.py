@@ -197,7 +197,7 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
                          "ops_per_word_pair": OPS_PER_WORD_PAIR}}
 
 
-def kma_extra(dev, torch, n=256, L=200_000, reps=3, metric="cos"):
+def kma_extra(dev, torch, n=1024, L=50_000, reps=3, metric="cos"):
     """Count-matrix (KMA *.mat) distances, ccg_kma_ltd_dev: n samples x L
     positions of synthetic depth-~30 counts (views built on the GPU; the
     file loader is not timed).  Rate = sample pairs x positions / s."""
