@@ -15,7 +15,7 @@ D = euclid(n, seed=1)
 with tempfile.TemporaryDirectory(dir="/tmp") as td:
     path = os.path.join(td, "m.phy")
     t = time.perf_counter()
-    cg.write_phylip(path, D, n, [f"t{k}" for k in range(n)])
+    cg.native.write_phylip(path, D, n, [f"t{k}" for k in range(n)])
     print(f"write {time.perf_counter() - t:.2f} s, {os.path.getsize(path) / 1e6:.0f} MB", flush=True)
     runs = [("gpu", [cg.CLI_PATH, "tree", "-i", path]), ("gpu-fast", [cg.CLI_PATH, "tree", "-i", path, "--fast_sums"])]
     ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "ccphylo")
