@@ -64,6 +64,12 @@ struct TreeBufs {
 };
 
 
+// the device state of one tree run (one hipMalloc), sized for n taxa
+struct TreeWork {
+	TreeBufs b;
+	void *mem;
+};
+int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st);
 
 // ------------------------------------------------------------------ helpers
 __host__ __device__ static inline unsigned cdiv(long long a, long long b) { return (unsigned) ((a + b - 1) / b); }

@@ -43,142 +43,9 @@
 #include <stdlib.h>
 #include "ccg_tree_common.h"
 
-#define DNJ_B 128        // |S|: top candidate rows rescanned speculatively
-#define SEG 2048         // cells per rescan unit (TB threads x 8)
-#define SEL_BLOCKS 1024  // max grid of k_dnj_select
-#define SCAN_BLOCKS 1024 // max grid of k_dnj_scan (default; CCG_SCAN_MAX overrides)
+#include "ccg_dnj_search.h"
+
 static int g_scan_div = 4, g_scan_max = 2048;   // grid of k_dnj_scan: min(n / div, max)
-#define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
-#define TBF 1024         // threads of k_dnj_find (one block)
-#define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
-#define REPLAY_CAP 2048  // rest entries staged in LDS
-#define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
-
-// ---- diagnostic build only (make trace): s_memrealtime stamps (100 MHz) of
-// block 0's entry and phases and of the last block exit, for the joins at
-// n in (g_trace_hi - 256, g_trace_hi]; dumped to stderr by tree_run_t.
-#ifdef CCG_TRACE
-#define NKT 5
-__device__ unsigned long long g_trace[256 * NKT * 16];
-__device__ int g_trace_hi;
-__device__ __forceinline__ unsigned long long rt_stamp() {
-	unsigned long long t;
-	__builtin_amdgcn_sched_barrier(0);
-	asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-	__builtin_amdgcn_sched_barrier(0);
-	return t;
-}
-#define TS(kern, ph)                                                                  \
-	do {                                                                              \
-		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
-		}                                                                             \
-	} while(0)
-#define TS_ENTRY(kern)                                                                \
-	do {                                                                              \
-		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + 15] = ~rt_stamp(); \
-		}                                                                             \
-	} while(0)
-#define TS_EXIT(kern)                                                                 \
-	do {                                                                              \
-		if(threadIdx.x == 0) {                                                        \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) atomicMax(&g_trace[(s_ * NKT + (kern)) * 16 + 14], rt_stamp()); \
-		}                                                                             \
-	} while(0)
-#else
-#define TS_EXIT(kern)
-#define TS(kern, ph)
-#define TS_ENTRY(kern)
-#endif
-
-// ------------------------------------------------------------------ helpers
-// (q, j) min of LT row r over columns [c0, c1), whole block of NT threads,
-// UNR cells in flight per thread (dnj.c:99-112, `<=` last-wins rule).  Column
-// isub (the row moved by the previous join, not yet persisted) reads (Nm, sDm).
-// Without missing entries (GEN = false) every N[k] equals the matrix size n
-// (initSummaD counts n - 1 entries + 1; updateD and the pop keep that), so
-// the N gathers are skipped and Nr = Nm = n is passed in.
-template <int ET, bool GEN, int NT, int UNR>
-__device__ __forceinline__ void row_segment_min(const typename Elem<ET>::T *__restrict__ D, double bs,
-                                                const double *__restrict__ sD, const int *__restrict__ N, int r,
-                                                int c0, int c1, int Nr, double sDr, int isub, int Nm, double sDm,
-                                                double &q, int &idx) {
-	const typename Elem<ET>::T *row = D + tri(r);
-	for(int base = c0; base < c1; base += UNR * NT) {
-		typename Elem<ET>::T v[UNR];
-		int nk[UNR];
-		double sk[UNR];
-#pragma unroll
-		for(int m = 0; m < UNR; ++m) {
-			// clamped (always valid) addresses: no branches between the loads,
-			// so all of them are in flight before the first wait
-			int c = base + m * NT + (int) threadIdx.x;
-			c = c < c1 ? c : c1 - 1;
-			v[m] = row[c];
-			nk[m] = GEN ? N[c] : Nr;
-			sk[m] = sD[c];
-		}
-		// branch-free (no use of a loaded value under a condition, so the
-		// compiler cannot sink a load behind the first wait)
-#pragma unroll
-		for(int m = 0; m < UNR; ++m) {
-			const int c = base + m * NT + (int) threadIdx.x;
-			const double d = Elem<ET>::get(v[m], bs);
-			const int Nc = c == isub ? Nm : nk[m];
-			const double sc = c == isub ? sDm : sk[m];
-			const double x = qcrit(Nr, Nc, d, sDr, sc);
-			const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
-			q = take ? x : q;
-			idx = take ? c : idx;
-		}
-	}
-}
-
-// fold of the (q, j) unit partials [ua, ub), 4 branch-free loads in flight
-__device__ __forceinline__ void fold_units(const double *__restrict__ uq, const int *__restrict__ uj, int ua, int ub,
-                                           double &q, int &idx) {
-	for(int u = ua; u < ub; u += 4) {
-		double oq[4];
-		int oi[4];
-#pragma unroll
-		for(int m = 0; m < 4; ++m) {
-			const int v = u + m < ub ? u + m : ub - 1;
-			oq[m] = uq[v];
-			oi[m] = uj[v];
-		}
-#pragma unroll
-		for(int m = 0; m < 4; ++m) {
-			if(u + m < ub && qarg_better(oq[m], oi[m], q, idx)) {
-				q = oq[m];
-				idx = oi[m];
-			}
-		}
-	}
-}
-
-// block (q, idx) reduce with one barrier; the result is valid in thread 0.
-// The caller separates two uses with a barrier.
-__device__ __forceinline__ void qarg_block_reduce1(double &q, int &idx, double *sq, int *si) {
-	qarg_wave_reduce(q, idx);
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	if(lane == 0) {
-		sq[wid] = q;
-		si[wid] = idx;
-	}
-	__syncthreads();
-	if(threadIdx.x == 0) {
-		for(int w = 1; w < nw; ++w) {
-			if(qarg_better(sq[w], si[w], q, idx)) {
-				q = sq[w];
-				idx = si[w];
-			}
-		}
-	}
-}
 
 // ------------------------------------------------------------------ init
 // nj.c:111 initSummaD: per row, the row part (m < k) then the column part
@@ -239,503 +106,6 @@ __global__ __launch_bounds__(TB) void k_init_cols(const typename Elem<ET>::T *__
 	if(miss) atomicOr(&ctl->has_missing, 1);
 }
 
-// hclust.c:56-130: per-row min with ties -> smaller D, then later j
-template <int ET>
-__global__ void k_init_hnj(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                           const double *__restrict__ sD, const int *__restrict__ N,
-                           double *__restrict__ Q, int *__restrict__ P) {
-	int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-	int lane = threadIdx.x & 63;
-	if(i >= n) return;
-	double bq = DBL_MAX, bd = DBL_MAX;
-	int bj = 0;
-	const typename Elem<ET>::T *row = D + tri(i);
-	int Ni = N[i];
-	double sDi = sD[i];
-	for(int j = lane; j < i; j += 64) {
-		double d = Elem<ET>::get(row[j], bs);
-		if(0 <= d) {
-			double q = qcrit(Ni, N[j], d, sDi, sD[j]);
-			if(q < bq || (q == bq && (d < bd || (d == bd && j > bj)))) {
-				bq = q;
-				bd = d;
-				bj = j;
-			}
-		}
-	}
-#pragma unroll
-	for(int off = 32; off > 0; off >>= 1) {
-		double oq = __shfl_xor(bq, off, 64), od = __shfl_xor(bd, off, 64);
-		int oj = __shfl_xor(bj, off, 64);
-		if(oq < bq || (oq == bq && (od < bd || (od == bd && oj > bj)))) {
-			bq = oq;
-			bd = od;
-			bj = oj;
-		}
-	}
-	if(lane == 0) {
-		Q[i] = bq;
-		P[i] = bj;
-	}
-}
-
-// hclust.c:353 minQ -> the first candidate row (dnj.c:997-998)
-__global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	double q = DBL_MAX;
-	int idx = 0;
-	for(int i = 1 + threadIdx.x; i < n; i += blockDim.x) {
-		if(qarg_better(b.Q[i], i, q, idx)) {
-			q = b.Q[i];
-			idx = i;
-		}
-	}
-	qarg_block_reduce(q, idx, sq, si);
-	if(threadIdx.x == 0) {
-		b.ctl->cand = idx;
-		b.ctl->cand_q = b.Q[idx];
-		b.ctl->cand_p = b.P[idx];
-	}
-}
-
-// ------------------------------------------------------------------ DNJ select
-// Prologue, wave 0 only (no block barriers): the previous join's
-// updateDNJ/DNJ_popArrange fold (dnj.c:619-709, :817-975), minPos
-// (dnj.c:1026-1032), minQpair's start (dnj.c:55-60) and the top-B rows S
-// (rows n-1, n-2, ... with Q[r] < m0).  Then the whole block rescans units.
-template <int ET, bool GEN>
-__global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                    int n, int first) {
-	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
-	__shared__ double sQS[DNJ_B];
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	__shared__ int s_nS, s_isub, s_Nm, s_done;
-	__shared__ double s_sDm;
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-	TS_ENTRY(0);
-	TS(0, 0);
-	if(wid == 0) {
-		// ---- loads that do not depend on the previous join's outcome
-		const int done = ctl->done;
-		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
-		const int cand0 = first ? ctl->cand : 0;
-		const double cand0_q = first ? ctl->cand_q : 0.0;
-		const int cand0_p = first ? ctl->cand_p : 0;
-		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, cq1 = DBL_MAX;
-		int ix[4] = {0, -1, 0, -1}, cp1 = 0;
-		if(!first) {
-			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
-			for(int w = lane; w < G; w += 64) {
-#pragma unroll
-				for(int t = 0; t < 4; ++t) {
-					double oq = b.qpart[4 * w + t];
-					int oi = b.ipart[4 * w + t];
-					if(qarg_better(oq, oi, q[t], ix[t])) {
-						q[t] = oq;
-						ix[t] = oi;
-						if(t == 1) {
-							cq1 = b.cfq[w];
-							cp1 = b.cfp[w];
-						}
-					}
-				}
-			}
-		}
-		double topQ[SEL_RPL];
-#pragma unroll
-		for(int m = 0; m < SEL_RPL; ++m) {
-			int r = n - 1 - (m * 64 + lane);   // coalesced; descending = (m, lane) order
-			topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-		}
-		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
-		const int Nm = first ? 0 : b.N[n];
-		if(done) {
-			if(lane == 0) s_done = 1;
-		} else {
-			qarg_wave_reduce(q[0], ix[0]);
-			qarg_wave_reduce_carry(q[1], ix[1], cq1, cp1);
-			qarg_wave_reduce(q[2], ix[2]);
-			qarg_wave_reduce(q[3], ix[3]);
-			const int nn = n;
-			const bool move = !first && i != nn;
-			const int isub = move ? i : -1, jsub = first ? -1 : j;
-			const double Qj = q[0], Qi = q[2];
-			const int Pj = ix[0], Pi = ix[2];
-			// Q/P of the rows minPos can pick, all known without loads: j and
-			// the moved i from the fold; the row lowered through column j with
-			// its final (Q, P) carried by the requeue partials; the row lowered
-			// through the moved row keeps (q[3], i); row 0 keeps DBL_MAX.
-#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : (r) == ix[1] ? cq1 : (r) == ix[3] ? q[3] : DBL_MAX)
-#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : (r) == ix[1] ? cp1 : (r) == ix[3] ? i : 0)
-			int cand;
-			if(first) {
-				cand = cand0;
-			} else {
-				int p = j;
-				if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
-				int p2 = 0;
-				if(move) {
-					p2 = i;
-					if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
-				}
-				if(p2 == nn) {
-					cand = p;
-				} else if(p == nn) {
-					cand = p2;
-				} else {
-					double Qp = QSUB(p), Qp2 = QSUB(p2);
-					cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
-				}
-			}
-			const double Qc = !cand ? DBL_MAX : first ? cand0_q : QSUB(cand);
-			double m0 = DBL_MAX;
-			if(cand && m0 != Qc) m0 = Qc;
-			const int pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
-			const int pos_j = (cand && m0 != DBL_MAX) ? (first ? cand0_p : PSUB(cand)) : 0;
-#undef QSUB
-#undef PSUB
-			TS(0, 1);
-			// ---- S: 64*SEL_RPL rows per step; row base - (m*64 + lane), so the
-			// descending order is (m, lane) and ballots give the positions
-			int cnt = 0;
-			for(int base = n - 1, step = 0; base >= 1 && cnt < DNJ_B; base -= 64 * SEL_RPL, ++step) {
-#pragma unroll
-				for(int m = 0; m < SEL_RPL; ++m) {
-					const int r = base - (m * 64 + lane);
-					if(step) topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-					const double v = r == jsub ? Qj : r == isub ? Qi : topQ[m];
-					const bool f = r >= 1 && v < m0;
-					const unsigned long long bm = __ballot(f);
-					const int pos = cnt + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm >> 32),
-					                                                     __builtin_amdgcn_mbcnt_lo((unsigned) bm, 0));
-					if(f && pos < DNJ_B) {
-						sS[pos] = r;
-						sQS[pos] = v;
-					}
-					cnt += __popcll(bm);
-				}
-			}
-			const int nS = cnt < DNJ_B ? cnt : DNJ_B;
-			wave_sync();
-			// ---- units of SEG cells per row of S (lane: rows 2*lane, 2*lane+1)
-			const int t0 = 2 * lane, t1 = 2 * lane + 1;
-			const int r0 = t0 < nS ? sS[t0] : 0, r1 = t1 < nS ? sS[t1] : 0;
-			const int u0 = dcdiv(r0, SEG), u1 = dcdiv(r1, SEG);
-			int utot;
-			const int upre = wave_excl_scan(u0 + u1, &utot);
-			if(t0 < nS) so[t0] = upre;
-			if(t1 < nS) so[t1] = upre + u0;
-			if(lane == 0) so[nS] = utot;
-			TS(0, 2);
-			if(blockIdx.x == 0) {
-				// persist the fold and the selection for the kernels that follow
-				if(t0 < nS) {
-					b.S[t0] = r0;
-					b.Sb[t0] = sQS[t0];
-					b.uoff[t0] = upre;
-				}
-				if(t1 < nS) {
-					b.S[t1] = r1;
-					b.Sb[t1] = sQS[t1];
-					b.uoff[t1] = upre + u0;
-				}
-				const long long cells = wave_sum_int((long long) r0 + r1);
-				if(lane == 0) {
-					b.uoff[nS] = utot;
-					if(!first) {
-						b.Q[j] = Qj;
-						b.P[j] = Pj;
-						if(move) {
-							b.Q[i] = Qi;
-							b.P[i] = Pi;
-							b.sD[i] = sDm;
-							b.N[i] = Nm;
-						}
-					}
-					ctl->cand = cand;
-					ctl->m0 = m0;
-					ctl->pos_i = pos_i;
-					ctl->pos_j = pos_j;
-					ctl->nS = nS;
-					ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
-					ctl->rows += nS;
-					ctl->cells += cells;
-					ctl->cells_top += cells;
-				}
-			}
-			if(lane == 0) {
-				s_done = 0;
-				s_nS = nS;
-				s_isub = isub;
-				s_Nm = Nm;
-				s_sDm = sDm;
-			}
-		}
-	}
-	__syncthreads();
-	if(s_done) return;
-	TS(0, 3);
-	const int nS = s_nS, isub = s_isub, Nm = s_Nm;
-	const double sDm = s_sDm;
-	const int nunits = so[nS];
-	// ---- rescans, one unit of SEG cells per block iteration
-	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
-		int lo = 0, hi = nS - 1;   // last t with so[t] <= u
-		while(lo < hi) {
-			int mid = (lo + hi + 1) >> 1;
-			if(so[mid] <= u) lo = mid; else hi = mid - 1;
-		}
-		const int r = sS[lo];
-		const int c0 = (u - so[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
-		const int Nr = GEN ? (r == isub ? Nm : b.N[r]) : n;
-		const double sDr = r == isub ? sDm : b.sD[r];
-		double qq = DBL_MAX;
-		int idx = 0;
-		row_segment_min<ET, GEN, TB, SEG / TB>(D, bs, b.sD, b.N, r, c0, c1, Nr, sDr, isub, GEN ? Nm : n, sDm, qq, idx);
-		qarg_block_reduce1(qq, idx, sq, si);
-		TS(0, 4);
-		if(tid == 0) {
-			b.uq[lo * b.maxu + (u - so[lo])] = qq;
-			b.uj[lo * b.maxu + (u - so[lo])] = idx;
-		}
-		if(u + (int) gridDim.x < nunits) __syncthreads();
-	}
-	TS(0, 5);
-	TS_EXIT(0);
-}
-
-// ------------------------------------------------------------------ DNJ find
-// One block: the fresh mins of S (fold of k_dnj_select's units), the bound
-// U = min(m0, min_k max(fresh_k, Q_k)) and the rows below S with Q[r] < U in
-// descending order (any other row is provably skipped by minQpair, see the
-// file comment) with their SEG-cell unit offsets, for k_dnj_scan/k_dnj_join.
-__global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n) {
-	constexpr int NW = TBF / 64, FR = FIND_RPT;
-	__shared__ double sq[NW];
-	__shared__ double s_U;
-	__shared__ int s_mw[FR * NW], s_cnt, s_scan[NW];
-	__shared__ int lrow[REPLAY_CAP];
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-	TS_ENTRY(1);
-	TS(1, 0);
-	// ---- loads that do not depend on U (rows n-2 down; rows >= smin masked)
-	const int done = ctl->done, nS = ctl->nS, smin = ctl->smin;
-	const double m0 = ctl->m0;
-	int sr = 0, su = 0;
-	double sb = DBL_MAX;
-	// the first UPRE units of each S row, loaded before their count is known
-	constexpr int UPRE = 8;
-	double uqv[UPRE];
-	int ujv[UPRE];
-	if(tid < DNJ_B) {
-		sr = b.S[tid];
-		sb = b.Sb[tid];
-		su = b.uoff[tid + 1] - b.uoff[tid];
-		const int lim = b.maxu < UPRE ? b.maxu : UPRE;
-#pragma unroll
-		for(int u = 0; u < UPRE; ++u) {
-			const int v = u < lim ? u : lim - 1;
-			uqv[u] = b.uq[tid * b.maxu + v];
-			ujv[u] = b.uj[tid * b.maxu + v];
-		}
-	}
-	const int top = n - 2;
-	double qv[FR];
-#pragma unroll
-	for(int m = 0; m < FR; ++m) {
-		const int r = top - (m * TBF + tid);   // coalesced; descending = (m, tid) order
-		qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-	}
-	if(done) return;
-	// ---- fresh mins of S and U
-	double fq = DBL_MAX;
-	int fj = 0;
-	if(tid < nS) {
-#pragma unroll
-		for(int u = 0; u < UPRE; ++u) {
-			if(u < su && qarg_better(uqv[u], ujv[u], fq, fj)) {
-				fq = uqv[u];
-				fj = ujv[u];
-			}
-		}
-		if(su > UPRE) fold_units(b.uq + tid * b.maxu, b.uj + tid * b.maxu, UPRE, su, fq, fj);
-		Entry e;
-		e.f = fq;
-		e.bnd = sb;
-		e.row = sr;
-		e.j = fj;
-		b.Sent[tid] = e;
-	}
-	{
-		double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
-		v = readlane_d(wave_incl_min(v), 63);
-		if(lane == 0) sq[wid] = v;
-		__syncthreads();
-		if(tid == 0) {
-			double U = m0;
-			for(int w = 0; w < NW; ++w) U = sq[w] < U ? sq[w] : U;
-			s_U = U;
-		}
-		__syncthreads();
-	}
-	const double U = s_U;
-	TS(1, 1);
-	// ---- rows [1, smin) with Q[r] < U, descending: per (m, wave) ballot
-	// counts, one prefix over them, then mbcnt within the wave
-	int T = 0;
-	if(nS == DNJ_B) {
-		for(int base = top; base >= 1; base -= TBF * FR) {
-			if(base != top) {
-#pragma unroll
-				for(int m = 0; m < FR; ++m) {
-					const int r = base - (m * TBF + tid);
-					qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-				}
-			}
-			unsigned long long bm[FR];
-#pragma unroll
-			for(int m = 0; m < FR; ++m) {
-				const int r = base - (m * TBF + tid);
-				bm[m] = __ballot(r >= 1 && r < smin && qv[m] < U);
-				if(lane == 0) s_mw[m * NW + wid] = __popcll(bm[m]);
-			}
-			__syncthreads();
-			if(wid == 0) {
-				// exclusive prefix over the FR*NW counts in (m, wave) order
-				constexpr int NC = FR * NW, PER = (NC + 63) / 64;
-				int c[PER], sum = 0;
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					c[k] = x < NC ? s_mw[x] : 0;
-					sum += c[k];
-				}
-				int tot;
-				int pre = wave_excl_scan(sum, &tot);
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					if(x < NC) s_mw[x] = pre;
-					pre += c[k];
-				}
-				if(lane == 0) s_cnt = tot;
-			}
-			__syncthreads();
-#pragma unroll
-			for(int m = 0; m < FR; ++m) {
-				if((bm[m] >> lane) & 1ull) {
-					const int r = base - (m * TBF + tid);
-					const int pos = T + s_mw[m * NW + wid] +
-					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
-					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
-					if(pos < REPLAY_CAP) lrow[pos] = r;
-					b.crow[pos] = r;
-					b.cbnd[pos] = qv[m];
-				}
-			}
-			T += s_cnt;
-			__syncthreads();
-			if(base - TBF * FR < 1) break;
-		}
-	}
-	if(tid == 0) ctl->T = T;
-	if(T == 0) return;
-	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
-	const int K = dcdiv(T, TBF);
-	int mysum = 0;
-	long long cells = 0;
-	for(int k = 0; k < K; ++k) {
-		const int e = tid * K + k;
-		if(e < T) {
-			const int r = e < REPLAY_CAP ? lrow[e] : b.crow[e];   // past the LDS copy: HBM
-			mysum += dcdiv(r, SEG);
-			cells += r;
-		}
-	}
-	int utot;
-	int pre = block_excl_scan(mysum, s_scan, &utot);
-	for(int k = 0; k < K; ++k) {
-		const int e = tid * K + k;
-		if(e < T) {
-			b.coff[e] = pre;
-			pre += dcdiv(e < REPLAY_CAP ? lrow[e] : b.crow[e], SEG);
-		}
-	}
-	cells = wave_sum_int(cells);
-	if(lane == 0 && cells) {
-		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
-		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) cells);
-	}
-	if(tid == 0) {
-		b.coff[T] = utot;
-		ctl->rows += T;
-	}
-	TS(1, 2);
-	TS_EXIT(1);
-}
-
-// ------------------------------------------------------------------ DNJ scan
-// Rescans of the rows found by k_dnj_find, in SEG-cell units spread over the
-// whole grid.
-template <int ET, bool GEN>
-__global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                 int n) {
-	__shared__ int erow[REPLAY_CAP];
-	__shared__ int eoff[REPLAY_CAP + 1];
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x;
-	TS_ENTRY(2);
-	TS(2, 0);
-	// speculative first TB entries, then the rest once T is known
-	const int r0 = b.crow[tid], o0 = b.coff[tid];
-	const int done = ctl->done, T = ctl->T;
-	if(done || T == 0) return;
-	// the entry table in LDS when it fits, else searched in HBM (L2-resident)
-	const bool lds = T <= REPLAY_CAP;
-	if(lds) {
-		if(tid < T) {
-			erow[tid] = r0;
-			eoff[tid] = o0;
-		}
-		for(int e = TB + tid; e < T; e += TB) {
-			erow[e] = b.crow[e];
-			eoff[e] = b.coff[e];
-		}
-		if(tid == 0) eoff[T] = b.coff[T];
-	}
-	__syncthreads();
-	TS(2, 1);
-	const int *off = lds ? eoff : b.coff;
-	const int nunits = off[T];
-	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
-		int lo = 0, hi = T - 1;   // last e with off[e] <= u
-		while(lo < hi) {
-			int mid = (lo + hi + 1) >> 1;
-			if(off[mid] <= u) lo = mid; else hi = mid - 1;
-		}
-		const int r = lds ? erow[lo] : b.crow[lo];
-		const int c0 = (u - off[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
-		const int Nr = GEN ? b.N[r] : n;
-		double qq = DBL_MAX;
-		int idx = 0;
-		row_segment_min<ET, GEN, TB, SEG / TB>(D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
-		qarg_block_reduce1(qq, idx, sq, si);
-		if(tid == 0) {
-			b.cq[u] = qq;
-			b.cj[u] = idx;
-		}
-		if(u + (int) gridDim.x < nunits) __syncthreads();
-	}
-	TS(2, 2);
-	TS_EXIT(2);
-}
-
 // nj.c:836-1044 without missing entries: every k takes the (D_ik, D_kj >= 0)
 // branch, so the sD/N cursor never lags.  Writes the per-block partials of
 // the new row sum of j (sum, sum |c|, count, min exponent) and, in exact mode,
@@ -757,134 +127,6 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 	update_partials(b, n, exact, k, d, cnt, slot);
 }
 
-// ------------------------------------------------------------------ minQpair replay
-// dnj.c:88-112 decisions over the candidate entries in scan order (S, then
-// the rest, descending rows), wave 0 only.  Entry e has its stale bound b_e
-// = Q[row] and fresh min (f_e, j_e); the serial running min m_e starts at m0,
-// entry e is accepted iff b_e < m_e, and then m_{e+1} = min(m_e, f_e).
-//   A "good" entry (f_e >= b_e) gives m_{e+1} = min(m_e, f_e) whether or not
-//   it is accepted (rejected means f_e >= b_e >= m_e), so over good entries
-//   m is a prefix min.  A "bad" entry (f_e < b_e) lowers m only if accepted.
-// So: prefix-min passes that treat the undecided bad entries as rejected;
-// the first bad entry found accepted (b_e < m_e) is certainly accepted, fixes
-// m_{e+1} = f_e, and the next pass starts after it.  Without bad entries this
-// is one pass.  Accepted (Q, P) updates are applied by the writer block only.
-__device__ __forceinline__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
-                            const double *e_f, unsigned char *e_acc, bool writer, const TreeBufs &b, int &pi,
-                            int &pj, bool *had_bad, int n) {
-	(void) n;   // trace stamps only
-	const int lane = threadIdx.x & 63;
-	int bad = 0;
-	// 4 chunks of loads in flight (the entries may live in HBM)
-	for(int e0 = lane; e0 < total; e0 += 256) {
-		double f[4], bb[4];
-#pragma unroll
-		for(int k = 0; k < 4; ++k) {
-			const int e = e0 + 64 * k < total ? e0 + 64 * k : total - 1;
-			f[k] = e_f[e];
-			bb[k] = e_b[e];
-		}
-#pragma unroll
-		for(int k = 0; k < 4; ++k) {
-			if(e0 + 64 * k < total) {
-				bad |= !(f[k] >= bb[k]);
-				e_acc[e0 + 64 * k] = 0;
-			}
-		}
-	}
-	const bool any_bad = __any(bad);
-	*had_bad = any_bad;
-	wave_sync();
-	TS(3, 6);
-	if(any_bad) {
-		double m = m0;
-		int start = 0;
-		for(;;) {
-			int hit = -1;
-			double cm = m;
-			for(int c0 = start; c0 < total; c0 += 64) {
-				const int e = c0 + lane;
-				const bool valid = e < total;
-				const double f = valid ? e_f[e] : DBL_MAX, bb = valid ? e_b[e] : DBL_MAX;
-				const bool good = valid && f >= bb;
-				const double x = wave_incl_min(good ? f : DBL_MAX);
-				double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
-				pre = pre < cm ? pre : cm;
-				const unsigned long long hm = __ballot(valid && !good && bb < pre);
-				if(hm) {
-					hit = c0 + __ffsll((long long) hm) - 1;
-					break;
-				}
-				const double last = readlane_d(x, 63);
-				cm = last < cm ? last : cm;
-			}
-			if(hit < 0) break;
-			if(lane == 0) e_acc[hit] = 1;
-			m = e_f[hit];
-			start = hit + 1;
-			wave_sync();
-		}
-	}
-	// final pass: decisions, writes and the pair (the first contributor that
-	// reaches the final minimum, if it is below m0)
-	double cm = m0;
-	for(int g0 = 0; g0 < total; g0 += 256) {
-		double fv[4], bv[4];
-		int rv[4], jv[4], av[4];
-#pragma unroll
-		for(int k = 0; k < 4; ++k) {
-			const int e = g0 + 64 * k + lane < total ? g0 + 64 * k + lane : total - 1;
-			fv[k] = e_f[e];
-			bv[k] = e_b[e];
-			rv[k] = e_row[e];
-			jv[k] = e_j[e];
-			av[k] = e_acc[e];
-		}
-#pragma unroll
-		for(int k = 0; k < 4; ++k) {
-			const int c0 = g0 + 64 * k;
-			if(c0 >= total) break;
-			const bool valid = c0 + lane < total;
-			const double f = valid ? fv[k] : DBL_MAX, bb = valid ? bv[k] : DBL_MAX;
-			const bool good = valid && f >= bb;
-			const bool contrib = good || (valid && av[k]);
-			const double x = wave_incl_min(contrib ? f : DBL_MAX);
-			double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
-			pre = pre < cm ? pre : cm;
-			const bool accepted = good ? bb < pre : contrib;
-			if(writer && accepted) {
-				b.Q[rv[k]] = f;
-				b.P[rv[k]] = jv[k];
-			}
-			const double last = readlane_d(x, 63);
-			cm = last < cm ? last : cm;
-		}
-	}
-	TS(3, 7);
-	if(total && cm < m0) {
-		int first_e = 0x7fffffff;
-		for(int e0 = lane; e0 < total; e0 += 256) {
-			double f[4], bb[4];
-			int a[4];
-#pragma unroll
-			for(int k = 0; k < 4; ++k) {
-				const int e = e0 + 64 * k < total ? e0 + 64 * k : total - 1;
-				f[k] = e_f[e];
-				bb[k] = e_b[e];
-				a[k] = e_acc[e];
-			}
-#pragma unroll
-			for(int k = 0; k < 4; ++k) {
-				const int e = e0 + 64 * k;
-				const bool contrib = f[k] >= bb[k] || a[k];
-				if(e < total && contrib && f[k] == cm && e < first_e) first_e = e;
-			}
-		}
-		first_e = wave_min_int(first_e);
-		pi = e_row[first_e];
-		pj = e_j[first_e];
-	}
-}
 
 // ------------------------------------------------------------------ DNJ join
 // Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
@@ -1610,12 +852,7 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 }
 
 // ------------------------------------------------------------------ host
-struct TreeWork {
-	TreeBufs b;
-	void *mem;
-};
-
-static int tree_alloc(TreeWork *w, int n, hipStream_t st) {
+int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
 	const size_t maxu = cdiv(n, SEG) + 1;
 	// every row below S may qualify: room for n entries and their units
@@ -1693,13 +930,13 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	if(method == CCG_TREE_DNJ) {
 		unsigned gs = DNJ_B * cdiv(n - 1, SEG);
 		if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
-		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first);
+		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows());
 		kt.mark(CCG_K_TOP);
 		unsigned gc = cdiv(n, g_scan_div);
 		if(gc > (unsigned) g_scan_max) gc = g_scan_max;
-		k_dnj_find<<<1, TBF, 0, st>>>(b, n);
+		k_dnj_find<<<1, TBF, 0, st>>>(b, n, DenseRows());
 		kt.mark(CCG_K_FIND);
-		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n);
+		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows());
 		kt.mark(CCG_K_REST);
 		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
@@ -1730,7 +967,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	TreeWork w;
 	if(const char *e = getenv("CCG_SCAN_DIV")) g_scan_div = atoi(e) > 0 ? atoi(e) : 4;
 	if(const char *e = getenv("CCG_SCAN_MAX")) g_scan_max = atoi(e) > 0 ? atoi(e) : 2048;
-	int rc = tree_alloc(&w, n0, st);
+	int rc = ccg_tree_alloc(&w, n0, st);
 	if(rc) return rc;
 	TreeBufs b = w.b;
 	TreeCtl init;
@@ -1747,8 +984,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	k_init_cols<ET><<<cdiv(n0, TB), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
 	launches += 2;
 	if(a->method == CCG_TREE_DNJ) {
-		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.Q, b.P);
-		k_dnj_prep<<<1, TB, 0, st>>>(b, n0);
+		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(DenseRows(), D, n0, bs, b.sD, b.N, b.Q, b.P);
+		k_dnj_prep<><<<1, TB, 0, st>>>(b, n0);
 		launches += 2;
 	}
 	kt.mark(CCG_K_INIT);

@@ -25,144 +25,10 @@
 #include <stdlib.h>
 #include <rccl/rccl.h>
 #include "ccg_tree_common.h"
+#include "ccg_shard.h"
 
-#define SB CCG_SHARD_BAND
-static_assert(SB == NJ_RB, "a shard band is one NJ argmin row band");
 #define SH_GRID 8192         // max argmin blocks (grid-stride over the tiles)
 
-struct Shard {
-	int rank, world;
-	__host__ __device__ __forceinline__ bool owns(long long r) const { return (int) ((r / SB) % world) == rank; }
-	// elements before owned row r in the rank's buffer: full owned bands below
-	// r's band (band g holds SB*SB*g + SB*(SB-1)/2 elements), then r's
-	// predecessors in its band
-	__host__ __device__ __forceinline__ long long off(long long r) const {
-		const long long gb = r / SB, t = r - gb * SB, lb = gb / world;
-		return (long long) SB * SB * world * (lb * (lb - 1) / 2) + (long long) SB * SB * rank * lb +
-		       lb * (SB * (SB - 1) / 2) + SB * gb * t + t * (t - 1) / 2;
-	}
-};
-
-struct ShRec {   // one rank's argmin record (q, flat index); zeros in other ranks' slots
-	double q;
-	long long f;
-};
-
-__device__ __forceinline__ void rec_fold(const ShRec *__restrict__ rec, int world, double &bq, long long &bf) {
-	bq = 1.0;
-	bf = -1;
-	for(int w = 0; w < world; ++w) {
-		const double q = rec[w].q;
-		const long long f = rec[w].f;
-		if(f >= 0 && (q < bq || (q == bq && f > bf))) {
-			bq = q;
-			bf = f;
-		}
-	}
-}
-
-__device__ __forceinline__ void flat_to_ij(long long bf, int &i, int &j) {
-	long long r = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) bf)) * 0.5);
-	while(r > 1 && tri(r) > bf) --r;
-	while(tri(r + 1) <= bf) ++r;
-	i = (int) r;
-	j = (int) (bf - tri(r));
-}
-
-// ------------------------------------------------------------------ init
-// initSummaD row parts of the owned rows (the same wave-serial sum as
-// tree.hip's k_init_rows); RP = [n f64 sums][n i32 counts][i32 missing]
-template <int ET>
-__global__ __launch_bounds__(TB) void k_sh_init_rows(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
-                                                     Shard sh, double *__restrict__ rp, int *__restrict__ rc,
-                                                     int *__restrict__ miss_out) {
-	__shared__ double buf[TB / 64][64];
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-	const int k = blockIdx.x * (TB / 64) + wid;
-	if(k >= n) return;
-	if(!sh.owns(k)) {
-		if(lane == 0) {
-			rp[k] = 0;
-			rc[k] = 0;
-		}
-		return;
-	}
-	double s = 0;
-	int c = 1, miss = 0;
-	const typename Elem<ET>::T *row = D + sh.off(k);
-	for(int m0 = 0; m0 < k; m0 += 64) {
-		int m = m0 + lane;
-		double d = m < k ? Elem<ET>::get(row[m], bs) : 0.0;
-		bool ok = m < k && 0 <= d;
-		miss |= m < k && !ok;
-		c += __popcll(__ballot(ok));
-		buf[wid][lane] = ok ? d : 0.0;
-		__builtin_amdgcn_wave_barrier();
-		if(lane == 0) {
-			int lim = k - m0 < 64 ? k - m0 : 64;
-			for(int u = 0; u < lim; ++u) s += buf[wid][u];
-		}
-		__builtin_amdgcn_wave_barrier();
-	}
-	miss = __any(miss);
-	if(lane == 0) {
-		rp[k] = s;
-		rc[k] = c;
-		if(miss) atomicOr(miss_out, 1);
-	}
-}
-
-// column chunk [c0, c0 + K): X[(m - c0 - 1) * K + (c - c0)] = D(m, c) for the
-// owned rows m > c, zero elsewhere
-template <int ET>
-__global__ __launch_bounds__(TB) void k_sh_pack_cols(const typename Elem<ET>::T *__restrict__ D, int n, Shard sh,
-                                                     int c0, int K, typename Elem<ET>::T *__restrict__ X) {
-	const long long total = (long long) (n - c0 - 1) * K;
-	for(long long e = (long long) blockIdx.x * TB + threadIdx.x; e < total; e += (long long) gridDim.x * TB) {
-		const int m = c0 + 1 + (int) (e / K), c = c0 + (int) (e % K);
-		typename Elem<ET>::T v = 0;
-		if(c < m && sh.owns(m)) v = D[sh.off(m) + c];
-		X[e] = v;
-	}
-}
-
-// column parts, continued serially from the row parts in increasing m (the
-// same order as tree.hip's k_init_cols); 8 loads in flight per step
-template <int ET>
-__global__ __launch_bounds__(TB) void k_sh_init_cols(const typename Elem<ET>::T *__restrict__ X, int n, double bs,
-                                                     int c0, int K, const double *__restrict__ rp,
-                                                     const int *__restrict__ rc, double *__restrict__ sD,
-                                                     int *__restrict__ N, TreeCtl *ctl) {
-	const int c = c0 + blockIdx.x * TB + threadIdx.x;
-	if(c >= c0 + K || c >= n) return;
-	double s = rp[c];
-	int cnt = rc[c], miss = 0;
-	const typename Elem<ET>::T *col = X + (c - c0);
-	constexpr int U = 8;
-	for(int m = c + 1; m < n; m += U) {
-		typename Elem<ET>::T v[U];
-#pragma unroll
-		for(int u = 0; u < U; ++u) {
-			const int mm = m + u < n ? m + u : n - 1;
-			v[u] = col[(long long) (mm - c0 - 1) * K];
-		}
-#pragma unroll
-		for(int u = 0; u < U; ++u) {
-			if(m + u < n) {
-				const double d = Elem<ET>::get(v[u], bs);
-				if(0 <= d) {
-					s += d;
-					++cnt;
-				} else {
-					miss = 1;
-				}
-			}
-		}
-	}
-	sD[c] = s;
-	N[c] = cnt;
-	if(miss) atomicOr(&ctl->has_missing, 1);
-}
 
 // ------------------------------------------------------------------ per join
 // initQ over the rank's tiles: NJ_SEG-column segments x one band, segment-
@@ -454,55 +320,6 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 	}
 }
 
-// ------------------------------------------------------------------ transports
-static int coll_fail(const char *what) {
-	char m[128];
-	snprintf(m, sizeof(m), "collective transport failed in %s", what);
-	ccg_set_last_msg(m);
-	return CCG_EHIP;
-}
-
-// world == 1 without a transport: nothing to reduce, the broadcast is a copy
-static int self_allreduce(void *, void *, size_t, void *) { return 0; }
-static int self_bcast(void *, const void *send, void *recv, size_t bytes, int, void *stream) {
-	if(send != recv && bytes) {
-		if(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, (hipStream_t) stream) != hipSuccess) return -1;
-	}
-	return 0;
-}
-
-struct CollRun {
-	const ccg_coll *c;
-	hipStream_t st;
-	unsigned char *h;   // pinned staging buffer (host_staged transports)
-	KTimer *kt;
-	int allreduce(void *d, size_t bytes) {
-		if(!c->host_staged) {
-			if(c->allreduce_sum_u8(c->user, d, bytes, (void *) st)) return coll_fail("allreduce");
-			kt->mark(CCG_K_COLL);
-			return CCG_OK;
-		}
-		CCG_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st));
-		CCG_CHECK(hipStreamSynchronize(st));
-		if(c->allreduce_sum_u8(c->user, h, bytes, (void *) st)) return coll_fail("allreduce");
-		CCG_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
-		kt->mark(CCG_K_COLL);
-		return CCG_OK;
-	}
-	int bcast(const void *dsend, void *drecv, size_t bytes, int root) {
-		if(!c->host_staged) {
-			if(c->broadcast(c->user, dsend, drecv, bytes, root, (void *) st)) return coll_fail("broadcast");
-			kt->mark(CCG_K_COLL);
-			return CCG_OK;
-		}
-		if(root == c->rank) CCG_CHECK(hipMemcpyAsync(h, dsend, bytes, hipMemcpyDeviceToHost, st));
-		CCG_CHECK(hipStreamSynchronize(st));
-		if(c->broadcast(c->user, h, h, bytes, root, (void *) st)) return coll_fail("broadcast");
-		CCG_CHECK(hipMemcpyAsync(drecv, h, bytes, hipMemcpyHostToDevice, st));
-		kt->mark(CCG_K_COLL);
-		return CCG_OK;
-	}
-};
 
 // RCCL, resolved with dlopen so the engine has no link-time dependency on it
 struct RcclApi {
@@ -600,25 +417,20 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	hipStream_t st = ctx->stream;
 	ccg_coll self;
 	if(!coll_in) {
-		memset(&self, 0, sizeof(self));
-		self.world = 1;
-		self.allreduce_sum_u8 = self_allreduce;
-		self.broadcast = self_bcast;
+		sh_self_coll(&self);
 		coll_in = &self;
 	}
 	const Shard sh = {coll_in->rank, coll_in->world};
 	// device state: the single-GPU TreeBufs subset this loop uses
 	const size_t nb = (size_t) cdiv(n0, TB) + 1;
 	const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
-	size_t free_b = 0, total_b = 0;
-	CCG_CHECK(hipMemGetInfo(&free_b, &total_b));
-	// init column chunk: wide enough to keep the serial column sums parallel
-	size_t budget = coll_in->host_staged ? ((size_t) 64 << 20) : (free_b / 4 < ((size_t) 16 << 30) ? free_b / 4 : ((size_t) 16 << 30));
-	long long K = (long long) (budget / ((size_t) n0 * ET));
-	if(K < 256) K = 256;
-	if(K > n0) K = n0;
+	long long K = 0;
+	{
+		const int rk = sh_init_chunk(n0, ET, coll_in->host_staged != 0, &K);
+		if(rk) return rk;
+	}
 	const size_t xc_bytes = (size_t) K * (size_t) n0 * ET;
-	const size_t rp_bytes = (size_t) n0 * 12 + 16;
+	const size_t rp_bytes = sh_rp_bytes(n0);
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
 		size_t off = sz;
@@ -660,9 +472,7 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	long long *F = (long long *) (m + o_F);
 	ShRec *rec = (ShRec *) (m + o_rec);
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xc = (T *) (m + o_xc);
-	double *rp = (double *) (m + o_rp);
-	int *rcnt = (int *) (m + o_rp + (size_t) n0 * 8);
-	int *rmiss = rcnt + n0;
+	void *rp = m + o_rp;
 	long long *hF = (long long *) malloc((size_t) (nseg0 + 2) * 8);
 	TreeCtl init, hc;
 	long long launches = 0;
@@ -696,37 +506,10 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	SH_HIP(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	SH_HIP(hipEventRecord(ctx->ev0, st));
 	kt.init(st, a->profile != 0);
-	// initSummaD: owned row parts, gathered; then the column parts chunk by chunk
-	k_sh_init_rows<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, sh, rp, rcnt, rmiss);
-	SH_HIP(hipGetLastError());
-	kt.mark(CCG_K_INIT);
-	SH_TRY(cr.allreduce(rp, rp_bytes));
-	for(int c0 = 0; c0 < n0 - 1; c0 += (int) K) {
-		const int Kc = (int) (n0 - c0 < K ? n0 - c0 : K);
-		const long long cells = (long long) (n0 - c0 - 1) * Kc;
-		long long g = (cells + TB - 1) / TB;
-		if(g > 65536) g = 65536;
-		k_sh_pack_cols<ET><<<(unsigned) g, TB, 0, st>>>(D, n0, sh, c0, Kc, Xc);
-		kt.mark(CCG_K_INIT);
-		SH_TRY(cr.allreduce(Xc, (size_t) cells * ET));
-		k_sh_init_cols<ET><<<cdiv(Kc, TB), TB, 0, st>>>(Xc, n0, bs, c0, Kc, rp, rcnt, b.sD, b.N, b.ctl);
-		kt.mark(CCG_K_INIT);
-		launches += 2;
-	}
-	// the last column (n0 - 1) has no column part
 	{
-		const int c = n0 - 1;
-		SH_HIP(hipMemcpyAsync(b.sD + c, rp + c, 8, hipMemcpyDeviceToDevice, st));
-		SH_HIP(hipMemcpyAsync(b.N + c, rcnt + c, 4, hipMemcpyDeviceToDevice, st));
-	}
-	SH_HIP(hipGetLastError());
-	launches += 1;
-	{
-		int hm = 0;
-		SH_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
-		SH_HIP(hipMemcpyAsync(&hm, rmiss, 4, hipMemcpyDeviceToHost, st));
-		SH_HIP(hipStreamSynchronize(st));
-		if(hc.has_missing || hm) {
+		int missing = 0;
+		SH_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, rp, Xc, K, b, &launches, &missing));
+		if(missing) {
 			rc = CCG_EUNSUP;   // the missing-entry quirks of updateD run on one GPU only
 			goto out;
 		}
@@ -810,6 +593,10 @@ out:
 	return rc;
 }
 
+// tree_shard_dnj.hip
+int ccg_tree_shard_dnj_impl(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
+                            int *njoins, int *final_n, double *final_d, int64_t *stats);
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -886,7 +673,6 @@ static int shard_check(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll)
 	if(coll && (coll->world < 1 || coll->rank < 0 || coll->rank >= coll->world || !coll->allreduce_sum_u8 ||
 	            !coll->broadcast))
 		return CCG_EINVAL;
-	if(a->method != CCG_TREE_NJ) return CCG_EUNSUP;
 	return CCG_OK;
 }
 
@@ -897,6 +683,14 @@ int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll,
 	if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
 	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
+	if(a->method == CCG_TREE_DNJ) {
+		ccg_coll self;
+		if(!coll) {
+			sh_self_coll(&self);
+			coll = &self;
+		}
+		return ccg_tree_shard_dnj_impl(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+	}
 	switch(a->etype) {
 		case 8: return tree_shard_run_t<8>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
 		case 4: return tree_shard_run_t<4>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);

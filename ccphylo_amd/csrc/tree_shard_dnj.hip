@@ -1,0 +1,604 @@
+// tree_shard_dnj.hip -- DNJ (dnj.c:985 loop, the reference's default tree
+// method) over an LT matrix whose rows are split across ranks, one process
+// per GPU.  Same layout as the sharded NJ (ccg_shard.h):
+// bands of CCG_SHARD_BAND rows dealt round-robin, a rank's rows back to back;
+// sD, N, Q, P and the join list are replicated and every rank updates them
+// with the same arithmetic.
+//
+// Per join at matrix size n:
+//   0. broadcast of row n-1 from its owner (the pop moves it to slot i,
+//      dnj.c:817 / matrix.c:518);
+//   1. minQpair's search (dnj.c:43) with the single-GPU kernels of
+//      ccg_dnj_search.h under the Shard row policy.  The candidate row, m0
+//      and the top-B rows S depend on the replicated Q only, so every rank
+//      computes the same ones.  Each rank rescans the rows of S it owns and
+//      bounds the serial running min below S with them alone:
+//      U_r = min(m0, min over its own k in S of max(fresh_k, Q_k)) is an upper
+//      bound of that running min for ANY subset of S (a rescanned k gives
+//      m <= fresh_k, a skipped one m <= Q_k).  It then rescans its own rows
+//      below S with Q < U_r; any other row is provably skipped by dnj.c:88;
+//   2. the fresh (q, j) of the rescanned rows go into a record array indexed
+//      by row -- a bitmap of the rescanned rows below S, f64 q, i32 j -- that
+//      each rank fills for its own rows and zeroes elsewhere, so one
+//      allreduce-sum gathers it exactly (the 8 rows of a bitmap byte are one
+//      band: one owner, no carries);
+//   3. every rank replays minQpair's accept/reject decisions over S and the
+//      rescanned rows below S in descending row order (replay_wave).  Rows
+//      of the union that the serial scan would skip have bound >= running
+//      min, so the replay rejects them: Q/P and the pair (i, j) are those of
+//      the single-GPU engine, on every rank;
+//   4. lines i and j gathered as in the sharded NJ; updateD (nj.c:836) on
+//      every rank for every k, own cells stored, the new line j kept whole;
+//   5. updateDNJ's Q/P pass (dnj.c:618-709) and DNJ_popArrange (dnj.c:817)
+//      over the replicated lines, own cells stored; the record array is
+//      zeroed for the next join.
+// Hence the joins are bit-identical to ccg_tree's DNJ for every world size.
+#define CCG_DNJ_NO_TRACE
+#include <stdio.h>
+#include <stdlib.h>
+#include "ccg_dnj_search.h"
+#include "ccg_shard.h"
+
+// ------------------------------------------------------------------ records
+// [bitmap of rows (u64 words)][f64 fresh q][i32 fresh j], laid out for size n
+static __host__ __device__ inline size_t rec_bits_bytes(int n) { return (size_t) ((n + 63) / 64) * 8; }
+static __host__ __device__ inline size_t rec_bytes(int n) { return rec_bits_bytes(n) + (size_t) n * 12; }
+
+struct RecView {
+	unsigned *bits;
+	double *f;
+	int *j;
+};
+static __host__ __device__ inline RecView rec_view(void *R, int n) {
+	RecView v;
+	v.bits = (unsigned *) R;
+	v.f = (double *) ((char *) R + rec_bits_bytes(n));
+	v.j = (int *) ((char *) R + rec_bits_bytes(n) + (size_t) n * 8);
+	return v;
+}
+
+// own rescans -> records: S rows from the folded S entries (k_dnj_find), the
+// rows below S by folding their units (k_dnj_scan) and setting their bit
+__global__ __launch_bounds__(TB) void k_shd_rec(TreeBufs b, int n, Shard sh, void *R) {
+	TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const RecView v = rec_view(R, n);
+	const int nS = ctl->nS, T = ctl->T, tot = nS + T;
+	for(int e = blockIdx.x * TB + threadIdx.x; e < tot; e += gridDim.x * TB) {
+		if(e < nS) {
+			const int r = b.S[e];
+			if(sh.owns(r)) {
+				const Entry en = b.Sent[e];
+				v.f[r] = en.f;
+				v.j[r] = en.j;
+			}
+		} else {
+			const int x = e - nS, r = b.crow[x];
+			double q = DBL_MAX;
+			int idx = 0;
+			fold_units(b.cq, b.cj, b.coff[x], b.coff[x + 1], q, idx);
+			v.f[r] = q;
+			v.j[r] = idx;
+			atomicOr(&v.bits[r >> 5], 1u << (r & 31));
+		}
+	}
+}
+
+// One block: the entries in scan order (S, then the rescanned rows below S,
+// descending), minQpair's replay (dnj.c:76-125) and the pair.  Thread t owns
+// a contiguous run of bitmap words, the highest runs first.
+#define RPL_T 1024
+__global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R) {
+	__shared__ int s_scan[RPL_T / 64];
+	TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const RecView v = rec_view(R, n);
+	const int nS = ctl->nS, smin = ctl->smin, tid = threadIdx.x;
+	const double m0 = ctl->m0;
+	for(int t = tid; t < nS; t += RPL_T) {
+		const int r = b.S[t];
+		b.erow[t] = r;
+		b.eb[t] = b.Sb[t];
+		b.ef[t] = v.f[r];
+		b.ej[t] = v.j[r];
+	}
+	// rows [1, smin) with their bit set (no rows below S unless |S| = DNJ_B;
+	// smin is 1 then)
+	const int nw = smin > 1 ? ((smin - 1) >> 5) + 1 : 0;
+	const int per = (nw + RPL_T - 1) / RPL_T;
+	auto word = [&](int w) -> unsigned {
+		unsigned x = v.bits[w];
+		if(w == 0) x &= ~1u;                                              // row 0 never qualifies
+		if(w == nw - 1 && (smin & 31)) x &= (1u << (smin & 31)) - 1u;     // rows >= smin
+		return x;
+	};
+	int cnt = 0;
+	for(int q = 0; q < per; ++q) {
+		const int w = nw - 1 - (tid * per + q);
+		if(w >= 0) cnt += __popc(word(w));
+	}
+	int total;
+	int pos = nS + block_excl_scan(cnt, s_scan, &total);
+	for(int q = 0; q < per; ++q) {
+		const int w = nw - 1 - (tid * per + q);
+		if(w < 0) break;
+		unsigned x = word(w);
+		while(x) {
+			const int bit = 31 - __clz((int) x);
+			x &= ~(1u << bit);
+			const int r = w * 32 + bit;
+			b.erow[pos] = r;
+			b.eb[pos] = b.Q[r];
+			b.ef[pos] = v.f[r];
+			b.ej[pos] = v.j[r];
+			++pos;
+		}
+	}
+	__syncthreads();
+	if(tid < 64) {
+		int pi = ctl->pos_i, pj = ctl->pos_j;
+		bool had_bad;
+		replay_wave(nS + total, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, true, b, pi, pj, &had_bad, n);
+		if(tid == 0) {
+			if(pi == 0 && pj == 0) {
+				ctl->done = 1;
+				ctl->final_n = n;
+			} else {
+				ctl->i = pi;
+				ctl->j = pj;
+			}
+			ctl->serial_replays += had_bad;
+		}
+	}
+}
+
+// the pieces of lines i and j this rank's rows hold: X[k] = D(i, k),
+// X[n + k] = D(j, k) (raw elements; zeros where another rank owns the cell)
+template <int ET>
+__global__ __launch_bounds__(TB) void k_shd_lines(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
+                                                  Shard sh, typename Elem<ET>::T *__restrict__ X) {
+	const int k = blockIdx.x * TB + threadIdx.x;
+	if(b.ctl->done || k >= n) return;
+	const int i = b.ctl->i, j = b.ctl->j;
+	typename Elem<ET>::T xi = 0, xj = 0;
+	if(k > i) {
+		if(sh.owns(k)) xi = D[sh.off(k) + i];
+	} else if(k < i && sh.owns(i)) {
+		xi = D[sh.off(i) + k];
+	}
+	if(k > j) {
+		if(sh.owns(k)) xj = D[sh.off(k) + j];
+	} else if(k < j && sh.owns(j)) {
+		xj = D[sh.off(j) + k];
+	}
+	X[k] = xi;
+	X[n + k] = xj;
+}
+
+// limbLength (nj.c:42/:81), the join record and updateD (nj.c:836) over the
+// gathered lines: every rank computes the whole new line j (kept in Xj and,
+// at k = n-1, patched into the broadcast row Xm) and stores its own cells
+template <int ET>
+__global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                                 Shard sh, const typename Elem<ET>::T *__restrict__ X,
+                                                 typename Elem<ET>::T *__restrict__ Xm,
+                                                 typename Elem<ET>::T *__restrict__ Xj) {
+	__shared__ int s_stop, s_nj, s_neg, s_exact, s_i, s_j;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x;
+	const int k = blockIdx.x * TB + tid;
+	double sDk = 0, Dik = 0, Dkj = 0;
+	int Nk = 0;
+	if(k < n) {
+		sDk = b.sD[k];
+		Nk = b.N[k];
+		Dik = Elem<ET>::get(X[k], bs);
+		Dkj = Elem<ET>::get(X[n + k], bs);
+	}
+	if(tid == 0) {
+		s_stop = ctl->done;
+		s_nj = ctl->njoins;
+		s_neg = ctl->neg;
+		s_exact = ctl->exact;
+		s_i = ctl->i;
+		s_j = ctl->j;
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j;
+	const double Dij = Elem<ET>::get(X[j], bs);
+	if(blockIdx.x == 0 && tid == 0) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, s_neg);
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[s_nj] = J;
+		ctl->njoins = s_nj + 1;
+	}
+	double d = 0;
+	int cnt = 0;
+	if(k < n && k != i && k != j) {
+		d = (Dik + Dkj - Dij) / 2;
+		d = d < 0 ? 0 : d;
+		const typename Elem<ET>::T v = Elem<ET>::put(d, 0.25, bs);
+		if(k > j) {
+			if(sh.owns(k)) D[sh.off(k) + j] = v;
+		} else if(sh.owns(j)) {
+			D[sh.off(j) + k] = v;
+		}
+		Xj[k] = v;
+		if(k == n - 1) Xm[j] = v;   // row n-1 moves to slot i in the pop
+		b.sD[k] = sDk - (Dik + Dkj - d);
+		b.N[k] = Nk - 1;
+		cnt = 1;
+	}
+	update_partials(b, n, s_exact, k, d, cnt, blockIdx.x);
+}
+
+// Row sum of j, updateDNJ's Q/P part (dnj.c:618-709) and DNJ_popArrange
+// (dnj.c:817-975) over the replicated lines Xj (new line j) and Xm (row n-1,
+// moved to i), in the partial format k_dnj_select folds (tree.hip's
+// k_dnj_requeue, without missing entries); then the records are zeroed in
+// the layout of size n-1.
+template <int ET>
+__global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                    int n, Shard sh, const typename Elem<ET>::T *__restrict__ Xm,
+                                                    const typename Elem<ET>::T *__restrict__ Xj, void *R) {
+	__shared__ double sq[4][TB / 64], sfq[TB / 64];
+	__shared__ int si[4][TB / 64], sfp[TB / 64];
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	TreeCtl *ctl = b.ctl;
+	const int nn = n - 1;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = blockIdx.x * TB + tid;
+	int Nk = 0, pkk0 = 0;
+	double sDk = 0, qk0 = 0;
+	typename Elem<ET>::T vm = 0, vj = 0;
+	if(k < n) {
+		Nk = b.N[k];
+		sDk = b.sD[k];
+		qk0 = b.Q[k];
+		pkk0 = b.P[k];
+		vj = Xj[k];
+	}
+	if(k < nn) vm = Xm[k];
+	const int Nm0 = b.N[nn];
+	const double sDm0 = b.sD[nn];
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need;
+			fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j, Nj = s_nj;
+	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = Nj;
+		if(s_serial) ctl->serial_sums++;
+	}
+	const bool move = i != nn;
+	const int Nm = move ? Nm0 : 0;
+	const double sDm = move ? sDm0 : 0;
+	if(k == j) {
+		Nk = Nj;
+		sDk = sdj;
+	}
+	double rq = DBL_MAX, pq = DBL_MAX, r2q = DBL_MAX, p2q = DBL_MAX, fq = DBL_MAX;
+	int rj = 0, pk = -1, r2j = 0, p2k = -1, fp = 0;
+	if(k < n) {
+		if(k < j) {
+			const double d = Elem<ET>::get(vj, bs);
+			if(0 <= d) {
+				rq = qcrit(Nj, Nk, d, sdj, sDk);
+				rj = k;
+			}
+		}
+		if(k > j && k != i) {
+			double qk = qk0;
+			int pkk = pkk0;
+			bool upd = false;
+			const double d = Elem<ET>::get(vj, bs);
+			if(0 <= d) {
+				const double q = qcrit(Nj, Nk, d, sdj, sDk);
+				if(q <= qk) {
+					qk = q;
+					pkk = j;
+					upd = true;
+					pq = q;
+					pk = k;
+				}
+			}
+			if(move && k > i && k < nn) {
+				if(sh.owns(k)) D[sh.off(k) + i] = vm;
+				const double dm = Elem<ET>::get(vm, bs);
+				if(0 <= dm) {
+					const double q = qcrit(Nm, Nk, dm, sDm, sDk);
+					if(q <= qk) {
+						qk = q;
+						pkk = i;
+						upd = true;
+						p2q = q;
+						p2k = k;
+					}
+				}
+			}
+			if(upd) {
+				b.Q[k] = qk;
+				b.P[k] = pkk;
+			}
+			fq = qk;    // the row's final (Q, P), carried with (pq, pk)
+			fp = pkk;
+		}
+		if(move && k < i) {
+			if(sh.owns(i)) D[sh.off(i) + k] = vm;
+			const double dm = Elem<ET>::get(vm, bs);
+			if(0 <= dm) {
+				r2q = qcrit(Nm, Nk, dm, sDm, sDk);
+				r2j = k;
+			}
+		}
+	}
+	// records of the next join (size n - 1): bitmap words, q and j
+	if(k < n) {
+		const RecView v = rec_view(R, nn);
+		if((k & 63) == 0) ((unsigned long long *) v.bits)[k >> 6] = 0;
+		if(k < nn) {
+			v.f[k] = 0;
+			v.j[k] = 0;
+		}
+	}
+	qarg_wave_reduce(rq, rj);
+	qarg_wave_reduce_carry(pq, pk, fq, fp);
+	qarg_wave_reduce(r2q, r2j);
+	qarg_wave_reduce(p2q, p2k);
+	if(lane == 0) {
+		sq[0][wid] = rq;
+		si[0][wid] = rj;
+		sq[1][wid] = pq;
+		si[1][wid] = pk;
+		sfq[wid] = fq;
+		sfp[wid] = fp;
+		sq[2][wid] = r2q;
+		si[2][wid] = r2j;
+		sq[3][wid] = p2q;
+		si[3][wid] = p2k;
+	}
+	__syncthreads();
+	if(tid < 4) {
+		double q = sq[tid][0], cq = sfq[0];
+		int ix = si[tid][0], cp = sfp[0];
+		for(int w = 1; w < TB / 64; ++w) {
+			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
+				q = sq[tid][w];
+				ix = si[tid][w];
+				cq = sfq[w];
+				cp = sfp[w];
+			}
+		}
+		b.qpart[4 * blockIdx.x + tid] = q;
+		b.ipart[4 * blockIdx.x + tid] = ix;
+		if(tid == 1) {
+			b.cfq[blockIdx.x] = cq;
+			b.cfp[blockIdx.x] = cp;
+		}
+	}
+}
+
+// initHNJ's (Q, P) of the owned rows into the zeroed records' q/j arrays
+template <int ET>
+static int shd_init_hnj(const typename Elem<ET>::T *D, int n0, double bs, const Shard &sh, CollRun &cr,
+                        hipStream_t st, TreeBufs &b, void *R) {
+	const RecView v = rec_view(R, n0);
+	CCG_CHECK(hipMemsetAsync(R, 0, rec_bytes(n0), st));
+	k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(sh, D, n0, bs, b.sD, b.N, v.f, v.j);
+	CCG_CHECK(hipGetLastError());
+	cr.kt->mark(CCG_K_INIT);
+	int rc = cr.allreduce(v.f, (size_t) n0 * 12);
+	if(rc) return rc;
+	CCG_CHECK(hipMemcpyAsync(b.Q, v.f, (size_t) n0 * 8, hipMemcpyDeviceToDevice, st));
+	CCG_CHECK(hipMemcpyAsync(b.P, v.j, (size_t) n0 * 4, hipMemcpyDeviceToDevice, st));
+	CCG_CHECK(hipMemsetAsync(R, 0, rec_bytes(n0), st));
+	k_dnj_prep<><<<1, TB, 0, st>>>(b, n0);
+	CCG_CHECK(hipGetLastError());
+	cr.kt->mark(CCG_K_INIT);
+	return CCG_OK;
+}
+
+// ------------------------------------------------------------------ host driver
+template <int ET>
+static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, void *Dd,
+                                ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	typedef typename Elem<ET>::T T;
+	T *D = (T *) Dd;
+	const int n0 = a->n;
+	const double bs = a->byteScale;
+	hipStream_t st = ctx->stream;
+	const Shard sh = {coll->rank, coll->world};
+	long long K = 0;
+	int rc = sh_init_chunk(n0, ET, coll->host_staged != 0, &K);
+	if(rc) return rc;
+	TreeWork w;
+	if((rc = ccg_tree_alloc(&w, n0, st))) return rc;
+	TreeBufs b = w.b;
+	// shard buffers: records, lines i/j, row n-1, new line j, init gathers
+	const size_t xc_bytes = (size_t) K * (size_t) n0 * ET, rp_bytes = sh_rp_bytes(n0);
+	size_t sz = 0;
+	auto take = [&](size_t bytes) {
+		size_t off = sz;
+		sz += (bytes + 255) & ~(size_t) 255;
+		return off;
+	};
+	const size_t o_R = take(rec_bytes(n0)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	const size_t o_Xj = take((size_t) n0 * ET + 8), o_rp = take(rp_bytes), o_xc = take(xc_bytes);
+	char *m = NULL;
+	unsigned char *h = NULL;
+	if(hipMalloc((void **) &m, sz) != hipSuccess) {
+		hipFree(w.mem);
+		return CCG_ENOMEM;
+	}
+	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
+	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
+	if(rec_bytes(n0) > hcap) hcap = rec_bytes(n0);
+	if(coll->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
+		hipFree(m);
+		hipFree(w.mem);
+		return CCG_ENOMEM;
+	}
+	static KTimer kt;
+	CollRun cr = {coll, st, h, &kt};
+	void *R = m + o_R;
+	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj), *Xc = (T *) (m + o_xc);
+	TreeCtl init, hc;
+	long long launches = 0;
+	int n = n0;
+	float ms = 0;
+	memset(&init, 0, sizeof(init));
+	init.neg = (a->flags & 2) != 0;
+	init.exact = a->exact != 0;
+	init.method = a->method;
+#define SD_TRY(x)                          \
+	do {                                   \
+		if((rc = (x)) != CCG_OK) goto out; \
+	} while(0)
+#define SD_HIP(x)                                                    \
+	do {                                                             \
+		hipError_t e_ = (x);                                         \
+		if(e_ != hipSuccess) {                                       \
+			ccg_set_last_error(e_, #x, __FILE__, __LINE__);         \
+			rc = e_ == hipErrorOutOfMemory ? CCG_ENOMEM : CCG_EHIP; \
+			goto out;                                                \
+		}                                                            \
+	} while(0)
+	SD_HIP(hipMemsetAsync(m, 0, sz - xc_bytes, st));
+	SD_HIP(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
+	SD_HIP(hipEventRecord(ctx->ev0, st));
+	kt.init(st, a->profile != 0);
+	{
+		int missing = 0;
+		SD_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, m + o_rp, Xc, K, b, &launches, &missing));
+		if(missing) {
+			rc = CCG_EUNSUP;   // the missing-entry quirks of updateD run on one GPU only
+			goto out;
+		}
+	}
+	SD_TRY(shd_init_hnj<ET>(D, n0, bs, sh, cr, st, b, R));
+	launches += 2;
+	{
+		int since_check = 0;
+		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
+		while(n > stop_n) {
+			const int root = ccg_shard_owner(n - 1, sh.world);
+			SD_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
+			                root));
+			const unsigned gn = cdiv(n, TB);
+			unsigned gs = DNJ_B * cdiv(n - 1, SEG);
+			if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
+			unsigned gc = cdiv(n, 4);
+			if(gc > 2048) gc = 2048;
+			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh);
+			kt.mark(CCG_K_TOP);
+			k_dnj_find<<<1, TBF, 0, st>>>(b, n, sh);
+			kt.mark(CCG_K_FIND);
+			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh);
+			kt.mark(CCG_K_REST);
+			k_shd_rec<<<64, TB, 0, st>>>(b, n, sh, R);
+			kt.mark(CCG_K_REST);
+			SD_TRY(cr.allreduce(R, rec_bytes(n)));
+			k_shd_replay<<<1, RPL_T, 0, st>>>(b, n, R);
+			k_shd_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, X);
+			kt.mark(CCG_K_UPDATE);
+			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
+			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xm, Xj);
+			kt.mark(CCG_K_UPDATE);
+			k_shd_requeue<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
+			kt.mark(CCG_K_REQUEUE);
+			SD_HIP(hipGetLastError());
+			launches += 8;
+			--n;
+			if(++since_check == 1024) {
+				since_check = 0;
+				SD_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
+				SD_HIP(hipStreamSynchronize(st));
+				if(hc.done) break;
+			}
+		}
+	}
+	SD_HIP(hipEventRecord(ctx->ev1, st));
+	kt.finish();
+	SD_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
+	SD_HIP(hipStreamSynchronize(st));
+	SD_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+	*njoins = hc.njoins;
+	*final_n = hc.done ? hc.final_n : n;
+	if(hc.njoins) {
+		SD_HIP(hipMemcpyAsync(joins, b.joins, (size_t) hc.njoins * sizeof(ccg_join), hipMemcpyDeviceToHost, st));
+	}
+	*final_d = -1.0;
+	if(*final_n == 2) {
+		// D(1, 0): row 1 is in band 0, owned by rank 0
+		SD_TRY(cr.bcast(sh.rank == 0 ? (const void *) (D + sh.off(1)) : NULL, Xm, ET, 0));
+		T v;
+		SD_HIP(hipMemcpyAsync(&v, Xm, sizeof(T), hipMemcpyDeviceToHost, st));
+		SD_HIP(hipStreamSynchronize(st));
+		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
+	}
+	if(stats) {
+		stats[0] = hc.rows;
+		stats[1] = hc.cells;
+		stats[2] = launches;
+		stats[3] = (int64_t) (ms * 1000.0);
+		if(a->profile) {
+			for(int c = 0; c < CCG_NKSTAT; ++c) {
+				stats[4 + 2 * c] = kt.cnt[c];
+				stats[5 + 2 * c] = kt.ns[c];
+			}
+			stats[4 + 2 * CCG_NKSTAT] = hc.cells_top;
+			stats[5 + 2 * CCG_NKSTAT] = hc.cells_rest;
+		}
+	}
+out:
+#undef SD_TRY
+#undef SD_HIP
+	if(rc != CCG_OK) kt.on = false;
+	hipStreamSynchronize(st);
+	if(h) hipHostFree(h);
+	hipFree(m);
+	hipFree(w.mem);
+	return rc;
+}
+
+// called by ccg_tree_shard_dev (tree_shard.hip) for method CCG_TREE_DNJ;
+// arguments already checked there, coll non-null
+int ccg_tree_shard_dnj_impl(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
+                            int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	switch(a->etype) {
+		case 8: return tree_shard_dnj_run_t<8>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		case 4: return tree_shard_dnj_run_t<4>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		case 2: return tree_shard_dnj_run_t<2>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+		default: return tree_shard_dnj_run_t<1>(c, a, coll, Dloc, joins, njoins, final_n, final_d, stats);
+	}
+}

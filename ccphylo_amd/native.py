@@ -323,8 +323,9 @@ class Device:
 
     def tree_shard(self, D, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
                    profile=False, max_joins=0):
-        """Sharded NJ from the full host LT (ccg_tree_shard): this rank uploads
-        its own row bands only.  `coll`: a HostColl / RcclColl (None = world 1)."""
+        """Sharded NJ / DNJ from the full host LT (ccg_tree_shard): this rank
+        uploads its own row bands only.  `coll`: a HostColl / RcclColl (None =
+        world 1)."""
         D = np.ascontiguousarray(D, dtype=ETYPES[etype])
         assert D.size == n * (n - 1) // 2
         return self._tree_shard(self.lib.ccg_tree_shard, D.ctypes.data, n, coll, etype, byte_scale, method, flags,
@@ -332,7 +333,7 @@ class Device:
 
     def tree_shard_dev(self, dptr, n, coll=None, etype=8, byte_scale=1.0, method=CCG_TREE_NJ, flags=0, exact=True,
                        profile=False, max_joins=0):
-        """Sharded NJ on this rank's device row bands (ccg_tree_shard_dev; consumed)."""
+        """Sharded NJ / DNJ on this rank's device row bands (ccg_tree_shard_dev; consumed)."""
         return self._tree_shard(self.lib.ccg_tree_shard_dev, dptr, n, coll, etype, byte_scale, method, flags,
                                 exact, profile, max_joins)
 

@@ -230,11 +230,12 @@ int ccg_rccl_unique_id(void *id);
 int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *out);
 int ccg_rccl_close(ccg_coll *coll);
 
-/* NJ (a->method = CCG_TREE_NJ) on the rank's rows.  Every rank returns the
- * full join list, identical on all ranks and bit-identical to ccg_tree with
- * the same `exact` flag for any world size.  Dloc_dev holds the rank's
- * ccg_shard_elems(n, rank, world) elements and is consumed.  CCG_EUNSUP for
- * DNJ and for matrices with missing (negative) entries. */
+/* NJ (a->method = CCG_TREE_NJ, nj_thread nj.c:1612) or DNJ (CCG_TREE_DNJ,
+ * dnj_thread dnj.c:1054) on the rank's rows.  Every rank returns the full
+ * join list, identical on all ranks and bit-identical to ccg_tree with the
+ * same method and `exact` flag for any world size.  Dloc_dev holds the
+ * rank's ccg_shard_elems(n, rank, world) elements and is consumed.
+ * CCG_EUNSUP for matrices with missing (negative) entries. */
 int ccg_tree_shard_dev(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc_dev,
                        ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
 /* Same from the full host LT (every rank passes the whole matrix; only the

@@ -176,3 +176,23 @@ def test_dist_row_range(dev):
         assert (Dg[lo:hi] == Do[lo:hi]).all()
         acc[lo:hi] = Dg[lo:hi]
     assert (acc == Do).all()
+
+
+@pytest.mark.parametrize("et", [8, 4, 2, 1])
+@pytest.mark.parametrize("n", [70, 300])
+@pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
+def test_tree_all_ties(dev, et, n, method):
+    """A matrix of one repeated value: every Q and every D ties, so only the
+    reference's tie rules (initHNJ hclust.c:110-115, initQ `<=`, minQpair) pick
+    the joins.  Guards the tie branch ROCm 7.2 miscompiled in k_init_hnj for
+    u8 elements (P stayed at column 63)."""
+    from oracle import pyoracle
+    dt = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}[et]
+    D = np.full(n * (n - 1) // 2, 200, dtype=dt)
+    got, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=1.0, method=method, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=method, etype=et, byte_scale=1.0)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got["i"] == ref["i"]).all() and (got["j"] == ref["j"]).all()
+    assert (got["Li"] == ref["Li"]).all() and (got["Lj"] == ref["Lj"]).all()
+    sh, sfn, sfd, _ = dev.tree_shard(D, n, None, etype=et, byte_scale=1.0, method=method, exact=True)
+    assert (sfn, sfd) == (rfn, rfd) and (sh == got).all()

@@ -1,4 +1,4 @@
-"""GPU parity of the row-sharded NJ engine (ccg_tree_shard).
+"""GPU parity of the row-sharded NJ and DNJ engines (ccg_tree_shard).
 
 Its joins must be bit-identical to the single-GPU engine's (and so, in exact
 mode, to the reference's) for every world size:
@@ -58,18 +58,38 @@ def _same(a, b):
     assert (ja == jb).all()
 
 
+def _clade(n, seed, L=4000, clades=24):
+    """clade-structured SNP distances (config-3-like): DNJ's minQpair
+    qualifies many rows per join, past the LDS replay table"""
+    rng = np.random.default_rng(seed)
+    roots = rng.integers(0, 4, (clades, L))
+    X = roots[rng.integers(0, clades, n)]
+    flip = rng.random((n, L)) < 0.01
+    X = np.where(flip, rng.integers(0, 4, (n, L)), X)
+    same = sum((X == c).astype(np.float64) @ (X == c).astype(np.float64).T for c in range(4))
+    i, j = np.tril_indices(n, -1)
+    return L - same[i, j]
+
+
+def _data(kind, n):
+    return {"euc": _euclid, "snp": _snp, "clade": _clade}[kind](n, n)
+
+
+@pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
 @pytest.mark.parametrize("n,kind,et,exact", [(600, "euc", 8, True), (600, "euc", 8, False), (1100, "snp", 8, True),
                                              (700, "snp", 4, True), (700, "snp", 2, False), (500, "snp", 1, True),
-                                             (2100, "euc", 8, False)])
-def test_shard_world1_matches_single(dev, n, kind, et, exact):
-    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
-    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=0, exact=exact)[:3]
-    got = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=0, exact=exact)[:3]
+                                             (2100, "euc", 8, False), (3000, "clade", 8, True)])
+def test_shard_world1_matches_single(dev, n, kind, et, exact, method):
+    D, bs = _typed(_data(kind, n), et)
+    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=method, exact=exact)[:3]
+    got = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=method, exact=exact)[:3]
     _same(got, ref)
 
 
-@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if "nj" in c["args"] and not c["name"].startswith("miss")], ids=lambda c: c["name"])
-def test_shard_golden_nj(dev, case):
+# miss80 and multi.phy's second matrix hold missing entries (CCG_EUNSUP below)
+@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if not c["name"].startswith(("miss", "multi"))],
+                         ids=lambda c: c["name"])
+def test_shard_golden(dev, case):
     import ccphylo_amd as cg
     path, method, et, bs, flags, prec = parse_tree_args(case["args"])
 
@@ -80,15 +100,15 @@ def test_shard_golden_nj(dev, case):
     assert ("\n".join(trees) + "\n").encode() == golden_bytes(case)
 
 
-def test_shard_refuses_dnj_and_missing(dev):
+def test_shard_refuses_missing(dev):
+    """missing (negative) entries: updateD's quirks run on one GPU only"""
     import ccphylo_amd as cg
     n = 50
     D = _euclid(n, 1)
-    with pytest.raises(cg.CcgError, match="not supported"):
-        dev.tree_shard(D, n, None, method=1)
     D[17] = -1.0
-    with pytest.raises(cg.CcgError, match="not supported"):
-        dev.tree_shard(D, n, None, method=0)
+    for method in (0, 1):
+        with pytest.raises(cg.CcgError, match="not supported"):
+            dev.tree_shard(D, n, None, method=method)
 
 
 def _free_port():
@@ -99,7 +119,7 @@ def _free_port():
     return port
 
 
-def _rank_main(rank, world, port, n, kind, et, exact, transport, out_dir):
+def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
@@ -108,16 +128,16 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
+    D, bs = _typed(_data(kind, n), et)
     dev = cg.Device(0)
     coll = nt.HostColl(dist) if transport == "gloo" else nt.RcclColl(dev, dist)
     if transport == "gloo":
-        joins, fn, fd, st = dev.tree_shard(D, n, coll, etype=et, byte_scale=bs, method=0, exact=exact)
+        joins, fn, fd, st = dev.tree_shard(D, n, coll, etype=et, byte_scale=bs, method=method, exact=exact)
     else:
         loc = nt.shard_extract(D, n, rank, world)
         p = dev.malloc(max(loc.nbytes, 1))
         dev.h2d(p, loc)
-        joins, fn, fd, st = dev.tree_shard_dev(p, n, coll, etype=et, byte_scale=bs, method=0, exact=exact)
+        joins, fn, fd, st = dev.tree_shard_dev(p, n, coll, etype=et, byte_scale=bs, method=method, exact=exact)
         dev.free(p)
         coll.close()
     np.save(os.path.join(out_dir, f"j{rank}.npy"), joins)
@@ -127,14 +147,19 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,kind,et,exact,transport", [(2, 700, "euc", 8, True, "gloo"),
-                                                             (3, 450, "snp", 8, True, "gloo"),
-                                                             (2, 400, "snp", 2, False, "gloo"),
-                                                             (1, 900, "euc", 8, True, "rccl")])
-def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport):
-    D, bs = _typed(_euclid(n, n) if kind == "euc" else _snp(n, n), et)
-    ref_j, ref_fn, ref_fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=0, exact=exact)
-    mp.start_processes(_rank_main, args=(world, _free_port(), n, kind, et, exact, transport, str(tmp_path)),
+@pytest.mark.parametrize("world,n,kind,et,exact,transport,method", [(2, 700, "euc", 8, True, "gloo", 0),
+                                                                    (3, 450, "snp", 8, True, "gloo", 0),
+                                                                    (2, 400, "snp", 2, False, "gloo", 0),
+                                                                    (1, 900, "euc", 8, True, "rccl", 0),
+                                                                    (2, 700, "euc", 8, True, "gloo", 1),
+                                                                    (3, 500, "snp", 8, True, "gloo", 1),
+                                                                    (2, 400, "snp", 2, False, "gloo", 1),
+                                                                    (3, 1200, "clade", 4, True, "gloo", 1),
+                                                                    (1, 900, "euc", 8, True, "rccl", 1)])
+def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport, method):
+    D, bs = _typed(_data(kind, n), et)
+    ref_j, ref_fn, ref_fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=method, exact=exact)
+    mp.start_processes(_rank_main, args=(world, _free_port(), n, kind, et, exact, transport, method, str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")
     for r in range(world):
         j = np.load(tmp_path / f"j{r}.npy")
@@ -149,8 +174,12 @@ def test_max_joins_prefix(dev):
     D = _euclid(n, 5)
     full = dev.tree(D, n, method=0)[0]
     for fn in (lambda: dev.tree(D, n, method=0, max_joins=k), lambda: dev.tree(D, n, method=1, max_joins=k),
-               lambda: dev.tree_shard(D, n, None, method=0, max_joins=k)):
+               lambda: dev.tree_shard(D, n, None, method=0, max_joins=k),
+               lambda: dev.tree_shard(D, n, None, method=1, max_joins=k)):
         j, fin, fd, _ = fn()
         assert len(j) == k and fin == n - k and fd == -1.0
     j = dev.tree_shard(D, n, None, method=0, max_joins=k)[0]
     assert (j == full[:k]).all()
+    fullq = dev.tree(D, n, method=1)[0]
+    j = dev.tree_shard(D, n, None, method=1, max_joins=k)[0]
+    assert (j == fullq[:k]).all()
