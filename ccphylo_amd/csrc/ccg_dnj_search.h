@@ -7,6 +7,7 @@
 // owns bands of rows dealt round-robin.  Rows a rank does not own contribute
 // no rescan units, so a sharded rank rescans only its own candidates.
 #pragma once
+#include <stdlib.h>
 #include "ccg_tree_common.h"
 
 struct DenseRows {
@@ -23,6 +24,41 @@ struct DenseRows {
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
 #define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
+#define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
+
+// Grids of the search kernels: k_dnj_select min(DNJ_B * ceil((n-1)/SEG),
+// sel_max), k_dnj_scan min(ceil(n / scan_div), scan_max).  CCG_SEL_MAX,
+// CCG_SCAN_DIV and CCG_SCAN_MAX override them (tests shrink the grids so
+// that the unit pruning of later grid waves runs at small n).
+struct DnjGrid {
+	int sel_max = SEL_BLOCKS, scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
+	void load() {
+		if(const char *e = getenv("CCG_SEL_MAX")) sel_max = atoi(e) > 0 ? atoi(e) : SEL_BLOCKS;
+		if(const char *e = getenv("CCG_SCAN_DIV")) scan_div = atoi(e) > 0 ? atoi(e) : 4;
+		if(const char *e = getenv("CCG_SCAN_MAX")) scan_max = atoi(e) > 0 ? atoi(e) : 2048;
+		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
+	}
+	// cells per rescan unit: SEG up to 8 units per row, then growing with n
+	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
+	int seg(int n) const {
+		int m = seg_mul ? seg_mul : n / (8 * SEG);
+		m = m < 1 ? 1 : m > 8 ? 8 : m;
+		return m * SEG;
+	}
+	// rows with many units: fold each row's unit partials once (k_dnj_fold)
+	// instead of in every block of k_dnj_join
+	bool prefold(int n) const { return n > prefold_n; }
+	unsigned sel(int n) const {
+		const int s = seg(n);
+		const long long g = (long long) DNJ_B * ((n - 1 + s - 1) / s);
+		return (unsigned) (g < sel_max ? g : sel_max);
+	}
+	unsigned scan(int n) const {
+		const long long g = (n + scan_div - 1) / scan_div;
+		return (unsigned) (g < scan_max ? g : scan_max);
+	}
+};
 
 // ---- diagnostic build only (make trace): s_memrealtime stamps (100 MHz) of
 // block 0's entry and phases and of the last block exit, for the joins at
@@ -219,7 +255,7 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 // (rows n-1, n-2, ... with Q[r] < m0).  Then the whole block rescans units.
 template <int ET, bool GEN, class Rows>
 __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                    int n, int first, Rows rows) {
+                                                    int n, int first, Rows rows, int seg) {
 	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
 	__shared__ double sQS[DNJ_B];
 	__shared__ double sq[TB / 64];
@@ -333,12 +369,12 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 			}
 			const int nS = cnt < DNJ_B ? cnt : DNJ_B;
 			wave_sync();
-			// ---- units of SEG cells per row of S (lane: rows 2*lane, 2*lane+1)
+			// ---- units of seg cells per row of S (lane: rows 2*lane, 2*lane+1)
 			const int t0 = 2 * lane, t1 = 2 * lane + 1;
 			const int r0 = t0 < nS ? sS[t0] : 0, r1 = t1 < nS ? sS[t1] : 0;
 			// rows this rank does not hold get no units (their fresh min stays
 			// DBL_MAX here and comes from their owner)
-			const int u0 = rows.owns(r0) ? dcdiv(r0, SEG) : 0, u1 = rows.owns(r1) ? dcdiv(r1, SEG) : 0;
+			const int u0 = rows.owns(r0) ? dcdiv(r0, seg) : 0, u1 = rows.owns(r1) ? dcdiv(r1, seg) : 0;
 			int utot;
 			const int upre = wave_excl_scan(u0 + u1, &utot);
 			if(t0 < nS) so[t0] = upre;
@@ -396,7 +432,7 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 	const int nS = s_nS, isub = s_isub, Nm = s_Nm;
 	const double sDm = s_sDm;
 	const int nunits = so[nS];
-	// ---- rescans, one unit of SEG cells per block iteration
+	// ---- rescans, one unit of seg cells per block iteration
 	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
 		int lo = 0, hi = nS - 1;   // last t with so[t] <= u
 		while(lo < hi) {
@@ -404,12 +440,13 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 			if(so[mid] <= u) lo = mid; else hi = mid - 1;
 		}
 		const int r = sS[lo];
-		const int c0 = (u - so[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int c0 = (u - so[lo]) * seg, c1 = c0 + seg < r ? c0 + seg : r;
 		const int Nr = GEN ? (r == isub ? Nm : b.N[r]) : n;
 		const double sDr = r == isub ? sDm : b.sD[r];
 		double qq = DBL_MAX;
 		int idx = 0;
-		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, sDr, isub, GEN ? Nm : n, sDm, qq, idx);
+		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, sDr, isub, GEN ? Nm : n, sDm, qq,
+		                                       idx);
 		qarg_block_reduce1(qq, idx, sq, si);
 		TS(0, 4);
 		if(tid == 0) {
@@ -428,7 +465,7 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 // descending order (any other row is provably skipped by minQpair, see the
 // file comment) with their SEG-cell unit offsets, for k_dnj_scan/k_dnj_join.
 template <class Rows>
-__global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows) {
+__global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, int seg) {
 	constexpr int NW = TBF / 64, FR = FIND_RPT;
 	__shared__ double sq[NW];
 	__shared__ double s_U;
@@ -568,7 +605,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows) 
 		const int e = tid * K + k;
 		if(e < T) {
 			const int r = e < REPLAY_CAP ? lrow[e] : b.crow[e];   // past the LDS copy: HBM
-			mysum += dcdiv(r, SEG);
+			mysum += dcdiv(r, seg);
 			cells += r;
 		}
 	}
@@ -578,7 +615,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows) 
 		const int e = tid * K + k;
 		if(e < T) {
 			b.coff[e] = pre;
-			pre += dcdiv(e < REPLAY_CAP ? lrow[e] : b.crow[e], SEG);
+			pre += dcdiv(e < REPLAY_CAP ? lrow[e] : b.crow[e], seg);
 		}
 	}
 	cells = wave_sum_int(cells);
@@ -599,7 +636,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows) 
 // whole grid.
 template <int ET, bool GEN, class Rows>
 __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                 int n, Rows rows) {
+                                                 int n, Rows rows, int seg) {
 	__shared__ int erow[REPLAY_CAP];
 	__shared__ int eoff[REPLAY_CAP + 1];
 	__shared__ double sq[TB / 64];
@@ -636,7 +673,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 			if(off[mid] <= u) lo = mid; else hi = mid - 1;
 		}
 		const int r = lds ? erow[lo] : b.crow[lo];
-		const int c0 = (u - off[lo]) * SEG, c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int c0 = (u - off[lo]) * seg, c1 = c0 + seg < r ? c0 + seg : r;
 		const int Nr = GEN ? b.N[r] : n;
 		double qq = DBL_MAX;
 		int idx = 0;
@@ -650,6 +687,36 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	}
 	TS(2, 2);
 	TS_EXIT(2);
+}
+
+// ------------------------------------------------------------------ DNJ fold
+// Rows with many units (large n): each rest entry's unit partials folded once,
+// one wave per entry, into (rf, rj); k_dnj_join then reads one pair per entry
+// instead of folding every entry's units in each of its blocks.
+template <int UNUSED = 0>
+__global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n) {
+	const TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const int T = ctl->T, lane = threadIdx.x & 63;
+	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
+	for(int e = w0; e < T; e += nw) {
+		const int ua = b.coff[e], ub = b.coff[e + 1];
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int u = ua + lane; u < ub; u += 64) {
+			const double oq = b.cq[u];
+			const int oi = b.cj[u];
+			if(qarg_better(oq, oi, q, idx)) {
+				q = oq;
+				idx = oi;
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		if(lane == 0) {
+			b.rf[e] = q;
+			b.rj[e] = idx;
+		}
+	}
 }
 
 // ------------------------------------------------------------------ minQpair replay

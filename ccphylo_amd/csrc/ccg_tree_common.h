@@ -58,6 +58,8 @@ struct TreeBufs {
 	double *cfq;         // requeue: final (Q, P) of the row of each block's
 	int *cfp;            // column-j (q, idx) partial, carried to the fold
 	long long *fpart;
+	double *rf;          // per rest entry: fresh (q, j) folded once by k_dnj_fold
+	int *rj;             // (rows with many units)
 	ccg_join *joins;
 	TreeCtl *ctl;
 	int maxu;

@@ -45,7 +45,7 @@
 
 #include "ccg_dnj_search.h"
 
-static int g_scan_div = 4, g_scan_max = 2048;   // grid of k_dnj_scan: min(n / div, max)
+static DnjGrid g_grid;   // loaded per tree run
 
 // ------------------------------------------------------------------ init
 // nj.c:111 initSummaD: per row, the row part (m < k) then the column part
@@ -133,7 +133,7 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 // replay; then limbLength, the join record and updateD with the whole grid.
 template <int ET, bool GEN>
 __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
-                                                 int general) {
+                                                 int general, int prefold) {
 	__shared__ int e_row[DNJ_B + REPLAY_CAP], e_j[DNJ_B + REPLAY_CAP];
 	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
 	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
@@ -146,11 +146,20 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	const bool writer = blockIdx.x == 0;
 	TS_ENTRY(3);
 	TS(3, 0);
-	// every thread prefetches rest-unit partials (their count is not known yet)
+	// every thread prefetches rest-unit partials (their count is not known yet);
+	// with k_dnj_fold (prefold) the entries' folded pairs instead
+	if(prefold) {
 #pragma unroll
-	for(int m = 0; m < JOIN_UPRE / TB; ++m) {
-		lq[tid + m * TB] = b.cq[tid + m * TB];
-		lj[tid + m * TB] = b.cj[tid + m * TB];
+		for(int m = 0; m < JOIN_UPRE / TB; ++m) {
+			lq[tid + m * TB] = b.rf[tid + m * TB];
+			lj[tid + m * TB] = b.rj[tid + m * TB];
+		}
+	} else {
+#pragma unroll
+		for(int m = 0; m < JOIN_UPRE / TB; ++m) {
+			lq[tid + m * TB] = b.cq[tid + m * TB];
+			lj[tid + m * TB] = b.cj[tid + m * TB];
+		}
 	}
 	__syncthreads();
 	if(wid == 0) {
@@ -205,7 +214,10 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				const int ua = c0[m], ub = c1[m];
 				double q = DBL_MAX;
 				int idx = 0;
-				if(ub <= JOIN_UPRE) {
+				if(prefold) {
+					q = lq[e];   // e < 256 <= JOIN_UPRE
+					idx = lj[e];
+				} else if(ub <= JOIN_UPRE) {
 					for(int u = ua; u < ub; ++u) {
 						if(qarg_better(lq[u], lj[u], q, idx)) {
 							q = lq[u];
@@ -240,11 +252,15 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
 			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
 			for(int e = 256 + tid; e < T; e += TB) {
-				const int r = b.crow[e], ua = b.coff[e], ub = b.coff[e + 1];
+				const int r = b.crow[e];
 				const double bnd = b.cbnd[e];
 				double q = DBL_MAX;
 				int idx = 0;
-				if(ub <= JOIN_UPRE) {
+				if(prefold) {
+					q = e < JOIN_UPRE ? lq[e] : b.rf[e];
+					idx = e < JOIN_UPRE ? lj[e] : b.rj[e];
+				} else if(b.coff[e + 1] <= JOIN_UPRE) {
+					const int ua = b.coff[e], ub = b.coff[e + 1];
 					for(int u = ua; u < ub; ++u) {
 						if(qarg_better(lq[u], lj[u], q, idx)) {
 							q = lq[u];
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 						}
 					}
 				} else {
-					fold_units(b.cq, b.cj, ua, ub, q, idx);
+					fold_units(b.cq, b.cj, b.coff[e], b.coff[e + 1], q, idx);
 				}
 				x_row[nS + e] = r;
 				x_j[nS + e] = idx;
@@ -880,6 +896,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_qp = take((nb > nq ? nb : nq) * 4 * 8), o_ip = take((nb > nq ? nb : nq) * 4 * 4);
 	size_t o_fp = take(nq * 8), o_cfq = take(nb * 8), o_cfp = take(nb * 4);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
+	const size_t nrf = ncand > JOIN_UPRE ? ncand : JOIN_UPRE;   // k_dnj_join prefetches JOIN_UPRE
+	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
 	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
@@ -916,6 +934,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.cfq = (double *) (m + o_cfq);
 	b.cfp = (int *) (m + o_cfp);
 	b.joins = (ccg_join *) (m + o_j);
+	b.rf = (double *) (m + o_rf);
+	b.rj = (int *) (m + o_rj);
 	b.ctl = (TreeCtl *) (m + o_ctl);
 	b.maxu = (int) maxu;
 	return CCG_OK;
@@ -928,22 +948,21 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	const unsigned gn = cdiv(n, TB);
 	const int general = GEN;
 	if(method == CCG_TREE_DNJ) {
-		unsigned gs = DNJ_B * cdiv(n - 1, SEG);
-		if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
-		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows());
+		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
+		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
+		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows(), seg);
 		kt.mark(CCG_K_TOP);
-		unsigned gc = cdiv(n, g_scan_div);
-		if(gc > (unsigned) g_scan_max) gc = g_scan_max;
-		k_dnj_find<<<1, TBF, 0, st>>>(b, n, DenseRows());
+		k_dnj_find<<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
 		kt.mark(CCG_K_FIND);
-		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows());
+		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n);
 		kt.mark(CCG_K_REST);
-		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_UPDATE);
 		k_dnj_requeue<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
-		return GEN ? 6 : 5;
+		return (GEN ? 6 : 5) + prefold;
 	}
 	const unsigned g = (unsigned) nj_blocks(n);
 	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
@@ -965,8 +984,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	const double bs = a->byteScale;
 	hipStream_t st = ctx->stream;
 	TreeWork w;
-	if(const char *e = getenv("CCG_SCAN_DIV")) g_scan_div = atoi(e) > 0 ? atoi(e) : 4;
-	if(const char *e = getenv("CCG_SCAN_MAX")) g_scan_max = atoi(e) > 0 ? atoi(e) : 2048;
+	g_grid = DnjGrid();
+	g_grid.load();
 	int rc = ccg_tree_alloc(&w, n0, st);
 	if(rc) return rc;
 	TreeBufs b = w.b;

@@ -63,20 +63,31 @@ __global__ __launch_bounds__(TB) void k_shd_rec(TreeBufs b, int n, Shard sh, voi
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
 	const RecView v = rec_view(R, n);
-	const int nS = ctl->nS, T = ctl->T, tot = nS + T;
-	for(int e = blockIdx.x * TB + threadIdx.x; e < tot; e += gridDim.x * TB) {
-		if(e < nS) {
-			const int r = b.S[e];
-			if(sh.owns(r)) {
-				const Entry en = b.Sent[e];
-				v.f[r] = en.f;
-				v.j[r] = en.j;
+	const int nS = ctl->nS, T = ctl->T, lane = threadIdx.x & 63;
+	for(int e = blockIdx.x * TB + threadIdx.x; e < nS; e += gridDim.x * TB) {
+		const int r = b.S[e];
+		if(sh.owns(r)) {
+			const Entry en = b.Sent[e];
+			v.f[r] = en.f;
+			v.j[r] = en.j;
+		}
+	}
+	// rows below S: one wave per entry folds its units
+	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
+	for(int x = w0; x < T; x += nw) {
+		const int r = b.crow[x], ua = b.coff[x], ub = b.coff[x + 1];
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int u = ua + lane; u < ub; u += 64) {
+			const double oq = b.cq[u];
+			const int oi = b.cj[u];
+			if(qarg_better(oq, oi, q, idx)) {
+				q = oq;
+				idx = oi;
 			}
-		} else {
-			const int x = e - nS, r = b.crow[x];
-			double q = DBL_MAX;
-			int idx = 0;
-			fold_units(b.cq, b.cj, b.coff[x], b.coff[x + 1], q, idx);
+		}
+		qarg_wave_reduce(q, idx);
+		if(lane == 0) {
 			v.f[r] = q;
 			v.j[r] = idx;
 			atomicOr(&v.bits[r >> 5], 1u << (r & 31));
@@ -470,6 +481,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	static KTimer kt;
 	CollRun cr = {coll, st, h, &kt};
+	DnjGrid grid;
+	grid.load();
 	void *R = m + o_R;
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj), *Xc = (T *) (m + o_xc);
 	TreeCtl init, hc;
@@ -515,17 +528,15 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			SD_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
 			                root));
 			const unsigned gn = cdiv(n, TB);
-			unsigned gs = DNJ_B * cdiv(n - 1, SEG);
-			if(gs > SEL_BLOCKS) gs = SEL_BLOCKS;
-			unsigned gc = cdiv(n, 4);
-			if(gc > 2048) gc = 2048;
-			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh);
+			const unsigned gs = grid.sel(n), gc = grid.scan(n);
+			const int seg = grid.seg(n);
+			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg);
 			kt.mark(CCG_K_TOP);
-			k_dnj_find<<<1, TBF, 0, st>>>(b, n, sh);
+			k_dnj_find<<<1, TBF, 0, st>>>(b, n, sh, seg);
 			kt.mark(CCG_K_FIND);
-			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh);
+			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg);
 			kt.mark(CCG_K_REST);
-			k_shd_rec<<<64, TB, 0, st>>>(b, n, sh, R);
+			k_shd_rec<<<FOLD_BLOCKS, TB, 0, st>>>(b, n, sh, R);
 			kt.mark(CCG_K_REST);
 			SD_TRY(cr.allreduce(R, rec_bytes(n)));
 			k_shd_replay<<<1, RPL_T, 0, st>>>(b, n, R);

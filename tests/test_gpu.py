@@ -196,3 +196,42 @@ def test_tree_all_ties(dev, et, n, method):
     assert (got["Li"] == ref["Li"]).all() and (got["Lj"] == ref["Lj"]).all()
     sh, sfn, sfd, _ = dev.tree_shard(D, n, None, etype=et, byte_scale=1.0, method=method, exact=True)
     assert (sfn, sfd) == (rfn, rfd) and (sh == got).all()
+
+
+def _clade_ltd(n, seed, L=3000, clades=16):
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, 4, (clades, L))[rng.integers(0, clades, n)]
+    X = np.where(rng.random((n, L)) < 0.01, rng.integers(0, 4, (n, L)), X)
+    same = sum((X == c).astype(np.float64) @ (X == c).astype(np.float64).T for c in range(4))
+    i, j = np.tril_indices(n, -1)
+    return L - same[i, j]
+
+
+@pytest.mark.parametrize("kind,n,env", [("euc", 1500, "8,8,3,0"), ("euc", 2500, "64,16,2,0"),
+                                        ("clade", 1500, "8,8,4,0"), ("clade", 2500, "32,4,1,0"),
+                                        ("clade", 3000, "1024,2048,8,0")])
+def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
+    """The large-n settings of the DNJ search at small n: rescan units of
+    several SEG (CCG_SEG_MUL), each rest row's units folded once by k_dnj_fold
+    (CCG_PREFOLD_N=0) and grids far smaller than the units (CCG_SEL_MAX,
+    CCG_SCAN_MAX: many grid waves).  Joins bit-identical to the serial
+    reference (exact row sums), single GPU and sharded."""
+    from oracle import pyoracle
+    if kind == "euc":
+        rng = np.random.default_rng(n)
+        pts = rng.random((n, 8))
+        i, j = np.tril_indices(n, -1)
+        D = np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
+    else:
+        D = _clade_ltd(n, n)
+    sel, scan, segm, pf = env.split(",")
+    monkeypatch.setenv("CCG_SEL_MAX", sel)
+    monkeypatch.setenv("CCG_SCAN_MAX", scan)
+    monkeypatch.setenv("CCG_SEG_MUL", segm)
+    monkeypatch.setenv("CCG_PREFOLD_N", pf)
+    got, fn, fd, st = dev.tree(D, n, method=1, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=1)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
+    sh = dev.tree_shard(D, n, None, method=1, exact=True)[0]
+    assert (sh == got).all()

@@ -1,0 +1,113 @@
+/* sim_stages.c -- development aid: rescanned cells of the GPU engine's DNJ
+ * candidate selection strategies against the serial reference (minQpair
+ * dnj.c:43), on the serial DNJ of oracle/ccoracle.c (Euclidean U[0,1)^8):
+ *   CUR   S = top-B rows with Q < m0, U from S, every row below S with Q < U
+ *   MS(K) the same S, then stages of up to K rows below the previous stage
+ *         with Q < U_k, U_{k+1} tightened by each stage, until no row is left
+ * Build: gcc -O2 -std=gnu99 -ffp-contract=off -Ioracle tools/sim_stages.c -lm -o /tmp/sim_stages
+ *        /tmp/sim_stages N [every] */
+#include "../oracle/ccoracle.c"
+#include <stdio.h>
+
+#define NK 6
+/* stage-size sequences: stage k takes up to seq[k] rows (the last repeats) */
+static const int Seqs[NK][6] = {{128, 1 << 30}, {128, 256}, {8, 32, 128, 1 << 30}, {4, 16, 64, 256, 1 << 30},
+                                {16, 64, 256, 1 << 30}, {32, 1 << 30}};
+static double cref, ccur[NK], stages[NK], maxst[NK], its;
+
+static double fresh_of(const Ltd *D, int r, const double *sD, const int32_t *N, double *memo, char *have) {
+	if(!have[r]) {
+		int mj;
+		memo[r] = row_min(D, r, sD, N, &mj, 0);
+		have[r] = 1;
+	}
+	return memo[r];
+}
+
+static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, const double *Q, int cand) {
+	double m0 = DBL_MAX;
+	if(cand && m0 != Q[cand]) m0 = Q[cand];
+	double *memo = malloc(n * sizeof(double));
+	char *have = calloc(n, 1);
+	/* reference */
+	double m = m0;
+	for(int r = n - 1; r >= 1; --r) {
+		if(Q[r] < m) {
+			double f = fresh_of(D, r, sD, N, memo, have);
+			cref += r;
+			if(f < m) m = f;
+		}
+	}
+	for(int k = 0; k < NK; ++k) {
+		double U = m0, cells = 0;
+		int r = n - 1, st = 0, si = 0;
+		while(r >= 1) {
+			const int lim = Seqs[k][si];
+			if(si < 5 && Seqs[k][si + 1]) ++si;
+			double U2 = U;
+			int taken = 0;
+			for(; r >= 1 && taken < lim; --r) {
+				if(Q[r] < U) {
+					double f = fresh_of(D, r, sD, N, memo, have);
+					double v = f > Q[r] ? f : Q[r];
+					U2 = v < U2 ? v : U2;
+					cells += r;
+					++taken;
+				}
+			}
+			++st;
+			U = U2;
+			if(taken < lim) break;   /* every row below was under test */
+		}
+		ccur[k] += cells;
+		stages[k] += st;
+		if(st > maxst[k]) maxst[k] = st;
+	}
+	its += 1;
+	free(memo);
+	free(have);
+}
+
+int main(int argc, char **argv) {
+	int n = argc > 1 ? atoi(argv[1]) : 2000;
+	int every = argc > 2 ? atoi(argv[2]) : 1;
+	double *Dm = malloc((size_t) n * (n - 1) / 2 * sizeof(double));
+	srand(1);
+	double *pts = malloc((size_t) n * 8 * sizeof(double));
+	for(int k = 0; k < n * 8; ++k) pts[k] = rand() / (RAND_MAX + 1.0);
+	for(int i = 1; i < n; ++i)
+		for(int j = 0; j < i; ++j) {
+			double s = 0;
+			for(int d = 0; d < 8; ++d) s += (pts[i * 8 + d] - pts[j * 8 + d]) * (pts[i * 8 + d] - pts[j * 8 + d]);
+			Dm[tri(i) + j] = round(sqrt(s) * 1e9) / 1e9;
+		}
+	Ltd D = {8, 1.0, Dm};
+	double *sD = malloc(n * sizeof(double)), *Q = malloc(n * sizeof(double));
+	int32_t *N = malloc(n * sizeof(int32_t)), *P = malloc(n * sizeof(int32_t));
+	init_sums(&D, n, sD, N);
+	init_hnj(&D, n, sD, N, Q, P);
+	int j = min_q_row(Q, n);
+	uint64_t pos;
+	int joins = 0;
+	const int n0 = n;
+	while(n != 2) {
+		if(joins % every == 0) sim_iter(&D, n, sD, N, Q, j);
+		if(!(pos = min_q_pair(&D, n, sD, N, Q, P, j, 0))) break;
+		j = (int) (pos & 0xFFFFFFFFu);
+		int i = (int) (pos >> 32);
+		double Li, Lj;
+		limb_length(&Li, &Lj, i, j, sD, N, ld(&D, tri(i) + j), 0);
+		update_d(&D, n, sD, N, i, j, Li, Lj);
+		int mi = update_dnj_q(&D, n, sD, N, Q, P, i, j);
+		int mj = dnj_pop_arrange(&D, &n, sD, N, Q, P, i);
+		j = mj == n ? mi : mi == n ? mj : min_pos(Q, mi, mj);
+		++joins;
+		if(joins % (n0 / 8) == 0) {
+			printf("  after %d joins: ref cells/join %.0f", joins, cref / its);
+			for(int k = 0; k < NK; ++k) printf(" | %d,%d,%d x%.2f st %.2f (max %.0f)", Seqs[k][0], Seqs[k][1], Seqs[k][2], ccur[k] / cref, stages[k] / its, maxst[k]);
+			printf("\n");
+			fflush(stdout);
+		}
+	}
+	return 0;
+}

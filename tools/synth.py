@@ -14,17 +14,18 @@ def euclid(n, seed=1, dim=8):
     return np.round(D * 1e9) / 1e9
 
 
-def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=512):
+def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=512, dtype=None):
     """This rank's row bands (ccg_tree_shard_dev layout: bands of `band` rows
     dealt round-robin, owned rows back to back, row r = D(r, 0..r-1)) of the
     Euclidean distances between n points of U[0,1)^dim, computed on the GPU.
-    Every rank draws the same points (CPU generator, fixed seed)."""
+    Every rank draws the same points (CPU generator, fixed seed); computed in
+    double, stored as `dtype` (default float64; float32 = `-p`)."""
     g = torch.Generator().manual_seed(seed)
     pts = torch.rand((n, dim), generator=g, dtype=torch.float64).cuda()
     nb = (n + band - 1) // band
     mine = list(range(rank, nb, world))
     sizes = [sum(range(b * band, min(b * band + band, n))) for b in mine]
-    out = torch.empty(max(sum(sizes), 1), dtype=torch.float64, device="cuda")
+    out = torch.empty(max(sum(sizes), 1), dtype=dtype or torch.float64, device="cuda")
     per = max(1, chunk_rows // band)
     pos = 0
     for c in range(0, len(mine), per):
