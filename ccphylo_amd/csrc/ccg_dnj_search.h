@@ -15,13 +15,16 @@ struct DenseRows {
 	__host__ __device__ __forceinline__ long long row(long long r) const { return tri(r); }
 };
 
-#define DNJ_B 128        // |S|: top candidate rows rescanned speculatively
+#define DNJ_B 128        // capacity of S, the candidate rows rescanned speculatively
+#define DNJ_BANDS 64     // S: the top rows with Q < m0, then the min-Q row of each
+                         // of at most this many bands below them (DnjGrid::top/bands)
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
 #define SEL_BLOCKS 1024  // max grid of k_dnj_select
 #define SCAN_BLOCKS 1024 // max grid of k_dnj_scan (default; CCG_SCAN_MAX overrides)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
 #define TBF 1024         // threads of k_dnj_find (one block)
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
+#define FIND_CHUNKS 16384 // 64-row chunks of k_dnj_find's S-rank table (n <= 2^20)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
 #define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
@@ -32,7 +35,11 @@ struct DenseRows {
 // that the unit pruning of later grid waves runs at small n).
 struct DnjGrid {
 	int sel_max = SEL_BLOCKS, scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
+	int s_top = 0, s_bands = -1, s_split_n = 16384;
 	void load() {
+		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
+		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
 		if(const char *e = getenv("CCG_SEL_MAX")) sel_max = atoi(e) > 0 ? atoi(e) : SEL_BLOCKS;
 		if(const char *e = getenv("CCG_SCAN_DIV")) scan_div = atoi(e) > 0 ? atoi(e) : 4;
 		if(const char *e = getenv("CCG_SCAN_MAX")) scan_max = atoi(e) > 0 ? atoi(e) : 2048;
@@ -49,6 +56,18 @@ struct DnjGrid {
 	// rows with many units: fold each row's unit partials once (k_dnj_fold)
 	// instead of in every block of k_dnj_join
 	bool prefold(int n) const { return n > prefold_n; }
+	// S: `top` rows from the top, then up to `bands` band-minimum rows.  Small
+	// matrices are latency-bound: 128 top rows, no bands; beyond s_split_n the
+	// bands cut the rescanned cells several-fold (tools/sim_stages.c)
+	int top(int n) const {
+		const int t = s_top ? s_top : n > s_split_n ? 16 : DNJ_B;
+		return t < 1 ? 1 : t > DNJ_B ? DNJ_B : t;
+	}
+	int bands(int n) const {
+		int b = s_bands >= 0 ? s_bands : n > s_split_n ? DNJ_BANDS : 0;
+		b = b > DNJ_BANDS ? DNJ_BANDS : b;
+		return top(n) + b > DNJ_B ? DNJ_B - top(n) : b;
+	}
 	unsigned sel(int n) const {
 		const int s = seg(n);
 		const long long g = (long long) DNJ_B * ((n - 1 + s - 1) / s);
@@ -255,7 +274,7 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 // (rows n-1, n-2, ... with Q[r] < m0).  Then the whole block rescans units.
 template <int ET, bool GEN, class Rows>
 __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                    int n, int first, Rows rows, int seg) {
+                                                    int n, int first, Rows rows, int seg, int ktop, int kbands) {
 	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
 	__shared__ double sQS[DNJ_B];
 	__shared__ double sq[TB / 64];
@@ -292,6 +311,14 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 					}
 				}
 			}
+		}
+		// band candidates: lane l holds the min-Q row of the requeue blocks
+		// [l G / 64, (l + 1) G / 64) (rows ascending with the lane)
+		double bcq = DBL_MAX;
+		int bcr = 0;
+		if(!first && lane < kbands) {
+			const int G = (int) cdiv(n + 1, TB);
+			fold_units(b.bmq, b.bmr, lane * G / kbands, (lane + 1) * G / kbands, bcq, bcr);
 		}
 		double topQ[SEL_RPL];
 #pragma unroll
@@ -347,10 +374,11 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 #undef QSUB
 #undef PSUB
 			TS(0, 1);
-			// ---- S: 64*SEL_RPL rows per step; row base - (m*64 + lane), so the
-			// descending order is (m, lane) and ballots give the positions
+			// ---- S, top part: ktop rows, 64*SEL_RPL rows per step; row
+			// base - (m*64 + lane), so the descending order is (m, lane) and
+			// ballots give the positions
 			int cnt = 0;
-			for(int base = n - 1, step = 0; base >= 1 && cnt < DNJ_B; base -= 64 * SEL_RPL, ++step) {
+			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop; base -= 64 * SEL_RPL, ++step) {
 #pragma unroll
 				for(int m = 0; m < SEL_RPL; ++m) {
 					const int r = base - (m * 64 + lane);
@@ -360,14 +388,31 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 					const unsigned long long bm = __ballot(f);
 					const int pos = cnt + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm >> 32),
 					                                                     __builtin_amdgcn_mbcnt_lo((unsigned) bm, 0));
-					if(f && pos < DNJ_B) {
+					if(f && pos < ktop) {
 						sS[pos] = r;
 						sQS[pos] = v;
 					}
 					cnt += __popcll(bm);
 				}
 			}
-			const int nS = cnt < DNJ_B ? cnt : DNJ_B;
+			const int ntop = cnt < ktop ? cnt : ktop;
+			int nS = ntop;
+			const int smin = ntop == ktop ? sS[ktop - 1] : 1;
+			// ---- S, band part: below the top part, each band's min-Q row with
+			// Q < m0.  Any choice of S is exact (the bounds only use rows above,
+			// the replay runs in row order); spread over all depths these rows
+			// bound the rows below them far better than more top rows do
+			// (tools/sim_stages.c).  Descending rows = higher lanes first.
+			if(smin > 1 && kbands) {
+				const bool f = bcr >= 1 && bcr < smin && bcq < m0;
+				const unsigned long long bm = __ballot(f);
+				const int pos = ntop + __popcll(lane == 63 ? 0ull : bm >> (lane + 1));
+				if(f) {
+					sS[pos] = bcr;
+					sQS[pos] = bcq;
+				}
+				nS = ntop + __popcll(bm);
+			}
 			wave_sync();
 			// ---- units of seg cells per row of S (lane: rows 2*lane, 2*lane+1)
 			const int t0 = 2 * lane, t1 = 2 * lane + 1;
@@ -411,7 +456,8 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 					ctl->pos_i = pos_i;
 					ctl->pos_j = pos_j;
 					ctl->nS = nS;
-					ctl->smin = nS == DNJ_B ? sS[DNJ_B - 1] : 1;
+					ctl->ntop = ntop;
+					ctl->smin = smin;
 					ctl->rows += nS;
 					ctl->cells += cells;
 					ctl->cells_top += cells;
@@ -468,15 +514,17 @@ template <class Rows>
 __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, int seg) {
 	constexpr int NW = TBF / 64, FR = FIND_RPT;
 	__shared__ double sq[NW];
-	__shared__ double s_U;
 	__shared__ int s_mw[FR * NW], s_cnt, s_scan[NW];
 	__shared__ int lrow[REPLAY_CAP];
+	__shared__ double spm[DNJ_B];
+	__shared__ int ssr[DNJ_B];
+	__shared__ int sch[FIND_CHUNKS];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 	TS_ENTRY(1);
 	TS(1, 0);
 	// ---- loads that do not depend on U (rows n-2 down; rows >= smin masked)
-	const int done = ctl->done, nS = ctl->nS, smin = ctl->smin;
+	const int done = ctl->done, nS = ctl->nS, smin = ctl->smin, ntop = ctl->ntop;
 	const double m0 = ctl->m0;
 	int sr = 0, su = 0;
 	double sb = DBL_MAX;
@@ -524,23 +572,57 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		b.Sent[tid] = e;
 	}
 	{
-		double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
-		v = readlane_d(wave_incl_min(v), 63);
-		if(lane == 0) sq[wid] = v;
+		// bound of the rows below S row t: min(m0, max(fresh, Q) over S rows
+		// 0..t), a prefix min in scan order (S spans at most 2 waves)
+		const double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
+		const double x = wave_incl_min(v);
+		if(lane == 63) sq[wid] = x;
 		__syncthreads();
-		if(tid == 0) {
-			double U = m0;
-			for(int w = 0; w < NW; ++w) U = sq[w] < U ? sq[w] : U;
-			s_U = U;
+		double c = m0;
+		for(int w = 0; w < wid && w < 2; ++w) c = sq[w] < c ? sq[w] : c;
+		if(tid < nS) {
+			spm[tid] = x < c ? x : c;
+			ssr[tid] = sr;
 		}
 		__syncthreads();
 	}
-	const double U = s_U;
+	// every row below the top part is under the bound after it
+	const double U = smin > 1 ? spm[ntop - 1] : m0;
+	// S rows above row r: a table over 64-row chunks (the S rows above the
+	// chunk), then the at most two band rows inside the chunk (band rows come
+	// from distinct 256-row requeue blocks).  No dependent LDS chains per row.
+	const int nch0 = smin > 1 && nS > ntop ? ((smin - 1) >> 6) + 1 : 0;
+	const bool table = nch0 <= FIND_CHUNKS;   // else (n > 2^20) a binary search per row
+	const int nch = table ? nch0 : 0;
+	for(int c = tid; c < nch; c += TBF) {
+		int lo = ntop, hi = nS;   // S rows at or above row 64 (c + 1)
+		while(lo < hi) {
+			const int mid = (lo + hi) >> 1;
+			if(ssr[mid] >= 64 * (c + 1)) lo = mid + 1; else hi = mid;
+		}
+		sch[c] = lo;
+	}
+	if(nch) __syncthreads();   // uniform
+	auto s_above = [&](int r) {
+		int k;
+		if(table) {
+			k = sch[r >> 6];
+			while(k < nS && ssr[k] > r) ++k;
+		} else {
+			int lo = ntop, hi = nS;
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(ssr[mid] > r) lo = mid + 1; else hi = mid;
+			}
+			k = lo;
+		}
+		return k;
+	};
 	TS(1, 1);
 	// ---- rows [1, smin) with Q[r] < U, descending: per (m, wave) ballot
 	// counts, one prefix over them, then mbcnt within the wave
 	int T = 0;
-	if(nS == DNJ_B) {
+	if(smin > 1) {
 		for(int base = top; base >= 1; base -= TBF * FR) {
 			if(base != top) {
 #pragma unroll
@@ -550,10 +632,19 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 				}
 			}
 			unsigned long long bm[FR];
+			int above[FR];
 #pragma unroll
 			for(int m = 0; m < FR; ++m) {
 				const int r = base - (m * TBF + tid);
-				bm[m] = __ballot(r >= 1 && r < smin && qv[m] < U && rows.owns(r));
+				bool f = r >= 1 && r < smin && qv[m] < U && rows.owns(r);
+				above[m] = ntop;
+				if(f && nS > ntop) {
+					// its own bound (the S rows above it), and not an S row itself
+					const int t = s_above(r);
+					f = qv[m] < spm[t - 1] && !(t < nS && ssr[t] == r);
+					above[m] = t;
+				}
+				bm[m] = __ballot(f);
 				if(lane == 0) s_mw[m * NW + wid] = __popcll(bm[m]);
 			}
 			__syncthreads();
@@ -588,6 +679,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 					if(pos < REPLAY_CAP) lrow[pos] = r;
 					b.crow[pos] = r;
 					b.cbnd[pos] = qv[m];
+					b.cslot[pos] = pos + above[m];
 				}
 			}
 			T += s_cnt;
@@ -596,7 +688,29 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		}
 	}
 	if(tid == 0) ctl->T = T;
-	if(T == 0) return;
+	// slots of the S rows in scan order: the rest rows above each come first
+	// (stored last: a store before a barrier would make the barrier wait for it)
+	int spos = tid;
+	if(tid < nS) {
+		int lo = 0, hi = tid < ntop ? 0 : T;   // first rest entry below S row tid (none above the top part)
+		const int r = ssr[tid];
+		if(T <= REPLAY_CAP) {   // the list in LDS (kept apart: no flat loads)
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(lrow[mid] > r) lo = mid + 1; else hi = mid;
+			}
+		} else {
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(b.crow[mid] > r) lo = mid + 1; else hi = mid;
+			}
+		}
+		spos = tid + lo;
+	}
+	if(T == 0) {
+		if(tid < nS) b.Spos[tid] = spos;
+		return;
+	}
 	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
 	const int K = dcdiv(T, TBF);
 	int mysum = 0;
@@ -627,6 +741,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		b.coff[T] = utot;
 		ctl->rows += T;
 	}
+	if(tid < nS) b.Spos[tid] = spos;
 	TS(1, 2);
 	TS_EXIT(1);
 }

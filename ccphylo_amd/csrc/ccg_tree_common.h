@@ -26,7 +26,8 @@ struct TreeCtl {
 	double cand_q;       // Q/P of the first candidate (k_dnj_prep)
 	int cand_p;
 	int pos_i, pos_j;    // minQpair's initial pos
-	int nS, smin;        // |S| and its lowest row (1 when |S| < DNJ_B)
+	int nS, smin;        // |S| and the lowest row of its top part (1: no rows below S)
+	int ntop;            // S = ntop top rows (descending), then band-minimum rows below them
 	int T;               // rows found below S
 	double m0;           // minQpair's initial min
 	unsigned tick;       // k_dnj_select's last-block ticket
@@ -58,6 +59,10 @@ struct TreeBufs {
 	double *cfq;         // requeue: final (Q, P) of the row of each block's
 	int *cfp;            // column-j (q, idx) partial, carried to the fold
 	long long *fpart;
+	double *bmq;         // requeue: each block's min-Q row (candidates of the next S)
+	int *bmr;
+	int *Spos;           // entry slot of each S row in the descending scan order
+	int *cslot;          // and of each rest entry (k_dnj_find)
 	double *rf;          // per rest entry: fresh (q, j) folded once by k_dnj_fold
 	int *rj;             // (rows with many units)
 	ccg_join *joins;

@@ -170,10 +170,12 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		Entry se0, se1;
 		se0 = b.Sent[lane];
 		se1 = b.Sent[lane + 64];
-		int rr[4], c0[4], c1[4];
+		const int sp0 = b.Spos[lane], sp1 = b.Spos[lane + 64];
+		int rr[4], c0[4], c1[4], cs[4];
 		double bb[4];
 #pragma unroll
 		for(int m = 0; m < 4; ++m) {
+			cs[m] = b.cslot[lane + 64 * m];
 			rr[m] = b.crow[lane + 64 * m];
 			bb[m] = b.cbnd[lane + 64 * m];
 			c0[m] = b.coff[lane + 64 * m];
@@ -193,17 +195,19 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			const bool lds = T <= REPLAY_CAP;
 			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
 			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
+			// entries in scan order: S rows and rest rows interleave below the
+			// top part of S (slots from k_dnj_find)
 			if(lane < nS) {
-				x_row[lane] = se0.row;
-				x_j[lane] = se0.j;
-				x_b[lane] = se0.bnd;
-				x_f[lane] = se0.f;
+				x_row[sp0] = se0.row;
+				x_j[sp0] = se0.j;
+				x_b[sp0] = se0.bnd;
+				x_f[sp0] = se0.f;
 			}
 			if(lane + 64 < nS) {
-				x_row[lane + 64] = se1.row;
-				x_j[lane + 64] = se1.j;
-				x_b[lane + 64] = se1.bnd;
-				x_f[lane + 64] = se1.f;
+				x_row[sp1] = se1.row;
+				x_j[sp1] = se1.j;
+				x_b[sp1] = se1.bnd;
+				x_f[sp1] = se1.f;
 			}
 			// fresh (q, j) of the first 256 rest entries: fold of their units
 			// (entries past 256 are folded by the whole block below)
@@ -227,10 +231,10 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				} else {
 					fold_units(b.cq, b.cj, ua, ub, q, idx);
 				}
-				x_row[nS + e] = rr[m];
-				x_j[nS + e] = idx;
-				x_b[nS + e] = bb[m];
-				x_f[nS + e] = q;
+				x_row[cs[m]] = rr[m];
+				x_j[cs[m]] = idx;
+				x_b[cs[m]] = bb[m];
+				x_f[cs[m]] = q;
 			}
 			wave_sync();
 			if(lane == 0) {
@@ -247,7 +251,6 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	if(T > 256) {
 		__syncthreads();
 		if(!s_stop) {
-			const int nS = s_nS;
 			const bool lds = T <= REPLAY_CAP;
 			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
 			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
@@ -270,10 +273,11 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				} else {
 					fold_units(b.cq, b.cj, b.coff[e], b.coff[e + 1], q, idx);
 				}
-				x_row[nS + e] = r;
-				x_j[nS + e] = idx;
-				x_b[nS + e] = bnd;
-				x_f[nS + e] = q;
+				const int s = b.cslot[e];
+				x_row[s] = r;
+				x_j[s] = idx;
+				x_b[s] = bnd;
+				x_f[s] = q;
 			}
 		}
 	}
@@ -474,11 +478,11 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 // Row sum of j, then updateDNJ's Q/P part (dnj.c:618-709) and DNJ_popArrange
 // (dnj.c:817-975); the four (q, idx) reductions go to per-block partials that
 // the next k_dnj_select folds.
-template <int ET>
+template <int ET, bool BANDS>
 __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, int general) {
-	__shared__ double sq[4][TB / 64], sfq[TB / 64];
-	__shared__ int si[4][TB / 64], sfp[TB / 64];
+	__shared__ double sq[5][TB / 64], sfq[TB / 64];
+	__shared__ int si[5][TB / 64], sfp[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
 	TreeCtl *ctl = b.ctl;
@@ -591,6 +595,18 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			}
 		}
 	}
+	// the row's bound for the next join: each block's min-Q row becomes a
+	// candidate of the next S (rows j and i take theirs from k_dnj_select's
+	// fold); only when the next S has a band part
+	double bq = DBL_MAX;
+	int bk = 0;
+	if(BANDS) {
+		if(k >= 1 && k < nn && k != i && k != j) {
+			bq = k > j ? fq : qk0;
+			bk = k;
+		}
+		qarg_wave_reduce(bq, bk);
+	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
 	qarg_wave_reduce(r2q, r2j);
@@ -606,9 +622,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		si[2][wid] = r2j;
 		sq[3][wid] = p2q;
 		si[3][wid] = p2k;
+		if(BANDS) {
+			sq[4][wid] = bq;
+			si[4][wid] = bk;
+		}
 	}
 	__syncthreads();
-	if(tid < 4) {
+	if(tid < (BANDS ? 5 : 4)) {
 		double q = sq[tid][0], cq = sfq[0];
 		int ix = si[tid][0], cp = sfp[0];
 		for(int w = 1; w < TB / 64; ++w) {
@@ -619,8 +639,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				cp = sfp[w];
 			}
 		}
-		b.qpart[4 * blockIdx.x + tid] = q;
-		b.ipart[4 * blockIdx.x + tid] = ix;
+		if(tid == 4) {
+			b.bmq[blockIdx.x] = q;
+			b.bmr[blockIdx.x] = ix;
+		} else {
+			b.qpart[4 * blockIdx.x + tid] = q;
+			b.ipart[4 * blockIdx.x + tid] = ix;
+		}
 		if(tid == 1) {
 			b.cfq[blockIdx.x] = cq;
 			b.cfp[blockIdx.x] = cp;
@@ -897,6 +922,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_fp = take(nq * 8), o_cfq = take(nb * 8), o_cfp = take(nb * 4);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	const size_t nrf = ncand > JOIN_UPRE ? ncand : JOIN_UPRE;   // k_dnj_join prefetches JOIN_UPRE
+	size_t o_bq = take(nb * 8), o_br = take(nb * 4), o_sp = take((DNJ_B + 1) * 4), o_cs = take(ncand * 4);
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
@@ -934,6 +960,10 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.cfq = (double *) (m + o_cfq);
 	b.cfp = (int *) (m + o_cfp);
 	b.joins = (ccg_join *) (m + o_j);
+	b.bmq = (double *) (m + o_bq);
+	b.bmr = (int *) (m + o_br);
+	b.Spos = (int *) (m + o_sp);
+	b.cslot = (int *) (m + o_cs);
 	b.rf = (double *) (m + o_rf);
 	b.rj = (int *) (m + o_rj);
 	b.ctl = (TreeCtl *) (m + o_ctl);
@@ -950,7 +980,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	if(method == CCG_TREE_DNJ) {
 		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
-		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows(), seg);
+		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n));
 		kt.mark(CCG_K_TOP);
 		k_dnj_find<<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
 		kt.mark(CCG_K_FIND);
@@ -960,7 +990,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_UPDATE);
-		k_dnj_requeue<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
 		return (GEN ? 6 : 5) + prefold;
 	}

@@ -101,18 +101,14 @@ __global__ __launch_bounds__(TB) void k_shd_rec(TreeBufs b, int n, Shard sh, voi
 #define RPL_T 1024
 __global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R) {
 	__shared__ int s_scan[RPL_T / 64];
+	__shared__ int ssr[DNJ_B];
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
 	const RecView v = rec_view(R, n);
-	const int nS = ctl->nS, smin = ctl->smin, tid = threadIdx.x;
+	const int nS = ctl->nS, ntop = ctl->ntop, smin = ctl->smin, tid = threadIdx.x;
 	const double m0 = ctl->m0;
-	for(int t = tid; t < nS; t += RPL_T) {
-		const int r = b.S[t];
-		b.erow[t] = r;
-		b.eb[t] = b.Sb[t];
-		b.ef[t] = v.f[r];
-		b.ej[t] = v.j[r];
-	}
+	if(tid < nS) ssr[tid] = b.S[tid];
+	__syncthreads();
 	// rows [1, smin) with their bit set (no rows below S unless |S| = DNJ_B;
 	// smin is 1 then)
 	const int nw = smin > 1 ? ((smin - 1) >> 5) + 1 : 0;
@@ -129,7 +125,7 @@ __global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R
 		if(w >= 0) cnt += __popc(word(w));
 	}
 	int total;
-	int pos = nS + block_excl_scan(cnt, s_scan, &total);
+	int pos = block_excl_scan(cnt, s_scan, &total);   // among the rest rows
 	for(int q = 0; q < per; ++q) {
 		const int w = nw - 1 - (tid * per + q);
 		if(w < 0) break;
@@ -138,12 +134,34 @@ __global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R
 			const int bit = 31 - __clz((int) x);
 			x &= ~(1u << bit);
 			const int r = w * 32 + bit;
-			b.erow[pos] = r;
-			b.eb[pos] = b.Q[r];
-			b.ef[pos] = v.f[r];
-			b.ej[pos] = v.j[r];
+			int lo = ntop, hi = nS;   // S rows above r come first in scan order
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(ssr[mid] > r) lo = mid + 1; else hi = mid;
+			}
+			const int s = pos + lo;
+			b.crow[pos] = r;      // the rest rows, descending (this rank's own list is spent)
+			b.erow[s] = r;
+			b.eb[s] = b.Q[r];
+			b.ef[s] = v.f[r];
+			b.ej[s] = v.j[r];
 			++pos;
 		}
+	}
+	__syncthreads();
+	// S rows: the rest rows above each come first (none above the top part)
+	if(tid < nS) {
+		const int r = ssr[tid];
+		int lo = 0, hi = tid < ntop ? 0 : total;
+		while(lo < hi) {
+			const int mid = (lo + hi) >> 1;
+			if(b.crow[mid] > r) lo = mid + 1; else hi = mid;
+		}
+		const int s = tid + lo;
+		b.erow[s] = r;
+		b.eb[s] = b.Sb[tid];
+		b.ef[s] = v.f[r];
+		b.ej[s] = v.j[r];
 	}
 	__syncthreads();
 	if(tid < 64) {
@@ -257,12 +275,12 @@ __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restric
 // moved to i), in the partial format k_dnj_select folds (tree.hip's
 // k_dnj_requeue, without missing entries); then the records are zeroed in
 // the layout of size n-1.
-template <int ET>
+template <int ET, bool BANDS>
 __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, Shard sh, const typename Elem<ET>::T *__restrict__ Xm,
                                                     const typename Elem<ET>::T *__restrict__ Xj, void *R) {
-	__shared__ double sq[4][TB / 64], sfq[TB / 64];
-	__shared__ int si[4][TB / 64], sfp[TB / 64];
+	__shared__ double sq[5][TB / 64], sfq[TB / 64];
+	__shared__ int si[5][TB / 64], sfp[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
 	TreeCtl *ctl = b.ctl;
@@ -382,6 +400,18 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 			v.j[k] = 0;
 		}
 	}
+	// the row's bound for the next join: each block's min-Q row becomes a
+	// candidate of the next S (rows j and i take theirs from k_dnj_select's
+	// fold); only when the next S has a band part
+	double bq = DBL_MAX;
+	int bk = 0;
+	if(BANDS) {
+		if(k >= 1 && k < nn && k != i && k != j) {
+			bq = k > j ? fq : qk0;
+			bk = k;
+		}
+		qarg_wave_reduce(bq, bk);
+	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
 	qarg_wave_reduce(r2q, r2j);
@@ -397,9 +427,13 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 		si[2][wid] = r2j;
 		sq[3][wid] = p2q;
 		si[3][wid] = p2k;
+		if(BANDS) {
+			sq[4][wid] = bq;
+			si[4][wid] = bk;
+		}
 	}
 	__syncthreads();
-	if(tid < 4) {
+	if(tid < (BANDS ? 5 : 4)) {
 		double q = sq[tid][0], cq = sfq[0];
 		int ix = si[tid][0], cp = sfp[0];
 		for(int w = 1; w < TB / 64; ++w) {
@@ -410,8 +444,13 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 				cp = sfp[w];
 			}
 		}
-		b.qpart[4 * blockIdx.x + tid] = q;
-		b.ipart[4 * blockIdx.x + tid] = ix;
+		if(tid == 4) {
+			b.bmq[blockIdx.x] = q;
+			b.bmr[blockIdx.x] = ix;
+		} else {
+			b.qpart[4 * blockIdx.x + tid] = q;
+			b.ipart[4 * blockIdx.x + tid] = ix;
+		}
 		if(tid == 1) {
 			b.cfq[blockIdx.x] = cq;
 			b.cfp[blockIdx.x] = cp;
@@ -530,7 +569,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			const unsigned gn = cdiv(n, TB);
 			const unsigned gs = grid.sel(n), gc = grid.scan(n);
 			const int seg = grid.seg(n);
-			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg);
+			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n));
 			kt.mark(CCG_K_TOP);
 			k_dnj_find<<<1, TBF, 0, st>>>(b, n, sh, seg);
 			kt.mark(CCG_K_FIND);
@@ -545,7 +584,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xm, Xj);
 			kt.mark(CCG_K_UPDATE);
-			k_shd_requeue<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
+			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
+			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
 			launches += 8;

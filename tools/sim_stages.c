@@ -14,6 +14,15 @@
 static const int Seqs[NK][6] = {{128, 1 << 30}, {128, 256}, {8, 32, 128, 1 << 30}, {4, 16, 64, 256, 1 << 30},
                                 {16, 64, 256, 1 << 30}, {32, 1 << 30}};
 static double cref, ccur[NK], stages[NK], maxst[NK], its;
+#define NH 4
+static const int HA[NH] = {32, 16, 16, 8}, HB[NH] = {-64, -64, -112, -120};   /* -k: minima of k equal row blocks */
+static double chyb[NH];
+static int cmpq_desc_rows;   /* unused */
+static const double *g_Q;
+static int by_q(const void *a, const void *b) {
+	double x = g_Q[*(const int *) a], y = g_Q[*(const int *) b];
+	return x < y ? -1 : x > y ? 1 : (*(const int *) b - *(const int *) a);
+}
 
 static double fresh_of(const Ltd *D, int r, const double *sD, const int32_t *N, double *memo, char *have) {
 	if(!have[r]) {
@@ -63,6 +72,56 @@ static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, co
 		stages[k] += st;
 		if(st > maxst[k]) maxst[k] = st;
 	}
+	/* hybrid: S = top-A rows with Q < m0 plus the B smallest-Q rows below them
+	 * (Q < m0); every other row r with Q < m0 is rescanned iff Q[r] < bound(r)
+	 * = min(m0, min over S rows above r of max(fresh, Q)) */
+	{
+		int *cand = malloc(n * sizeof(int)), nc = 0;
+		for(int r = n - 1; r >= 1; --r) if(Q[r] < m0) cand[nc++] = r;
+		char *inS = calloc(n, 1);
+		for(int h = 0; h < NH; ++h) {
+			memset(inS, 0, n);
+			double cells = 0;
+			int A = HA[h] < nc ? HA[h] : nc;
+			for(int k = 0; k < A; ++k) inS[cand[k]] = 1;
+			int rem = nc - A;
+			if(rem > 0 && HB[h] < 0) {
+				const int lowest = A ? cand[A - 1] : n;
+				const int g = (lowest + (-HB[h]) - 1) / (-HB[h]);
+				for(int b0 = 0; b0 < lowest; b0 += g) {
+					int best = -1;
+					for(int r = b0; r < b0 + g && r < lowest; ++r)
+						if(r >= 1 && Q[r] < m0 && (best < 0 || Q[r] < Q[best])) best = r;
+					if(best >= 0) inS[best] = 1;
+				}
+			}
+			if(rem > 0 && HB[h] > 0) {
+				int *tmp = malloc(rem * sizeof(int));
+				memcpy(tmp, cand + A, rem * sizeof(int));
+				g_Q = Q;
+				qsort(tmp, rem, sizeof(int), by_q);
+				for(int k = 0; k < HB[h] && k < rem; ++k) inS[tmp[k]] = 1;
+				free(tmp);
+			}
+			double bound = m0;
+			for(int k = 0; k < nc; ++k) {   /* descending rows */
+				int r = cand[k];
+				if(inS[r]) {
+					double f = fresh_of(D, r, sD, N, memo, have);
+					double v = f > Q[r] ? f : Q[r];
+					cells += r;
+					if(v < bound) bound = v;
+				} else if(Q[r] < bound) {
+					double f = fresh_of(D, r, sD, N, memo, have);
+					(void) f;
+					cells += r;
+				}
+			}
+			chyb[h] += cells;
+		}
+		free(inS);
+		free(cand);
+	}
 	its += 1;
 	free(memo);
 	free(have);
@@ -105,6 +164,7 @@ int main(int argc, char **argv) {
 		if(joins % (n0 / 8) == 0) {
 			printf("  after %d joins: ref cells/join %.0f", joins, cref / its);
 			for(int k = 0; k < NK; ++k) printf(" | %d,%d,%d x%.2f st %.2f (max %.0f)", Seqs[k][0], Seqs[k][1], Seqs[k][2], ccur[k] / cref, stages[k] / its, maxst[k]);
+			for(int h = 0; h < NH; ++h) printf(" | H%d+%d x%.2f", HA[h], HB[h], chyb[h] / cref);
 			printf("\n");
 			fflush(stdout);
 		}
