@@ -24,7 +24,7 @@ struct DenseRows {
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
 #define TBF 1024         // threads of k_dnj_find (one block)
 #define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
-#define FIND_CHUNKS 16384 // 64-row chunks of k_dnj_find's S-rank table (n <= 2^20)
+#define FIND_CHUNKS 2048  // 64-row chunks of k_dnj_find's S-rank table (n <= 131072; else binary searches)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
 #define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
@@ -510,10 +510,11 @@ __global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *_
 // U = min(m0, min_k max(fresh_k, Q_k)) and the rows below S with Q[r] < U in
 // descending order (any other row is provably skipped by minQpair, see the
 // file comment) with their SEG-cell unit offsets, for k_dnj_scan/k_dnj_join.
-template <class Rows>
+template <class Rows, bool BANDS>
 __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, int seg) {
 	constexpr int NW = TBF / 64, FR = FIND_RPT;
 	__shared__ double sq[NW];
+	__shared__ double s_U;
 	__shared__ int s_mw[FR * NW], s_cnt, s_scan[NW];
 	__shared__ int lrow[REPLAY_CAP];
 	__shared__ double spm[DNJ_B];
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		e.j = fj;
 		b.Sent[tid] = e;
 	}
-	{
+	if(BANDS) {
 		// bound of the rows below S row t: min(m0, max(fresh, Q) over S rows
 		// 0..t), a prefix min in scan order (S spans at most 2 waves)
 		const double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
@@ -585,13 +586,28 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 			ssr[tid] = sr;
 		}
 		__syncthreads();
+		// every row below the top part is under the bound after it
+		if(tid == 0) s_U = smin > 1 ? spm[ntop - 1] : m0;
+		__syncthreads();
+	} else {
+		// S all on top: one bound for every row below it
+		double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
+		v = readlane_d(wave_incl_min(v), 63);
+		if(lane == 0) sq[wid] = v;
+		__syncthreads();
+		if(tid == 0) {
+			double U = m0;
+			for(int w = 0; w < NW; ++w) U = sq[w] < U ? sq[w] : U;
+			s_U = U;
+		}
+		__syncthreads();
 	}
-	// every row below the top part is under the bound after it
-	const double U = smin > 1 ? spm[ntop - 1] : m0;
+	const double U = s_U;
 	// S rows above row r: a table over 64-row chunks (the S rows above the
 	// chunk), then the at most two band rows inside the chunk (band rows come
 	// from distinct 256-row requeue blocks).  No dependent LDS chains per row.
-	const int nch0 = smin > 1 && nS > ntop ? ((smin - 1) >> 6) + 1 : 0;
+	const bool bands = BANDS && nS > ntop;   // else S is all above the listed rows (k_dnj_join's plain slots)
+	const int nch0 = smin > 1 && bands ? ((smin - 1) >> 6) + 1 : 0;
 	const bool table = nch0 <= FIND_CHUNKS;   // else (n > 2^20) a binary search per row
 	const int nch = table ? nch0 : 0;
 	for(int c = tid; c < nch; c += TBF) {
@@ -638,7 +654,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 				const int r = base - (m * TBF + tid);
 				bool f = r >= 1 && r < smin && qv[m] < U && rows.owns(r);
 				above[m] = ntop;
-				if(f && nS > ntop) {
+				if(bands && f) {
 					// its own bound (the S rows above it), and not an S row itself
 					const int t = s_above(r);
 					f = qv[m] < spm[t - 1] && !(t < nS && ssr[t] == r);
@@ -679,7 +695,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 					if(pos < REPLAY_CAP) lrow[pos] = r;
 					b.crow[pos] = r;
 					b.cbnd[pos] = qv[m];
-					b.cslot[pos] = pos + above[m];
+					if(bands) b.cslot[pos] = pos + above[m];
 				}
 			}
 			T += s_cnt;
@@ -691,7 +707,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 	// slots of the S rows in scan order: the rest rows above each come first
 	// (stored last: a store before a barrier would make the barrier wait for it)
 	int spos = tid;
-	if(tid < nS) {
+	if(bands && tid < nS) {
 		int lo = 0, hi = tid < ntop ? 0 : T;   // first rest entry below S row tid (none above the top part)
 		const int r = ssr[tid];
 		if(T <= REPLAY_CAP) {   // the list in LDS (kept apart: no flat loads)
@@ -708,7 +724,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		spos = tid + lo;
 	}
 	if(T == 0) {
-		if(tid < nS) b.Spos[tid] = spos;
+		if(bands && tid < nS) b.Spos[tid] = spos;
 		return;
 	}
 	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
@@ -741,7 +757,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 		b.coff[T] = utot;
 		ctl->rows += T;
 	}
-	if(tid < nS) b.Spos[tid] = spos;
+	if(bands && tid < nS) b.Spos[tid] = spos;
 	TS(1, 2);
 	TS_EXIT(1);
 }

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	__shared__ int e_row[DNJ_B + REPLAY_CAP], e_j[DNJ_B + REPLAY_CAP];
 	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
 	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
-	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact, s_nS;
+	__shared__ int s_pi, s_pj, s_stop, s_nj, s_neg, s_exact, s_nS, s_merged;
 	__shared__ double s_m0;
 	__shared__ double lq[JOIN_UPRE];
 	__shared__ int lj[JOIN_UPRE];
@@ -165,17 +165,18 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	if(wid == 0) {
 		// ---- loads independent of the outcome
 		const int done = ctl->done, nS = ctl->nS, T = ctl->T;
+		const bool merged = ctl->ntop != nS;   // band rows of S interleave with the rest
 		const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
 		const double m0 = ctl->m0;   // read early (independent of the outcome)
 		Entry se0, se1;
 		se0 = b.Sent[lane];
 		se1 = b.Sent[lane + 64];
-		const int sp0 = b.Spos[lane], sp1 = b.Spos[lane + 64];
+		const int sp0 = merged ? b.Spos[lane] : lane, sp1 = merged ? b.Spos[lane + 64] : lane + 64;
 		int rr[4], c0[4], c1[4], cs[4];
 		double bb[4];
 #pragma unroll
 		for(int m = 0; m < 4; ++m) {
-			cs[m] = b.cslot[lane + 64 * m];
+			cs[m] = merged ? b.cslot[lane + 64 * m] : nS + lane + 64 * m;
 			rr[m] = b.crow[lane + 64 * m];
 			bb[m] = b.cbnd[lane + 64 * m];
 			c0[m] = b.coff[lane + 64 * m];
@@ -239,6 +240,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			wave_sync();
 			if(lane == 0) {
 				s_stop = 0;
+				s_merged = merged;
 				s_pi = pi;
 				s_pj = pj;
 				s_nS = nS;
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				} else {
 					fold_units(b.cq, b.cj, b.coff[e], b.coff[e + 1], q, idx);
 				}
-				const int s = b.cslot[e];
+				const int s = s_merged ? b.cslot[e] : s_nS + e;
 				x_row[s] = r;
 				x_j[s] = idx;
 				x_b[s] = bnd;
@@ -982,7 +984,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
 		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n));
 		kt.mark(CCG_K_TOP);
-		k_dnj_find<<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
+		if(g_grid.bands(n)) k_dnj_find<DenseRows, true><<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
+		else k_dnj_find<DenseRows, false><<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
 		kt.mark(CCG_K_FIND);
 		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n);

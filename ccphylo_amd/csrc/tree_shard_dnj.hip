@@ -571,7 +571,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			const int seg = grid.seg(n);
 			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n));
 			kt.mark(CCG_K_TOP);
-			k_dnj_find<<<1, TBF, 0, st>>>(b, n, sh, seg);
+			if(grid.bands(n)) k_dnj_find<Shard, true><<<1, TBF, 0, st>>>(b, n, sh, seg);
+			else k_dnj_find<Shard, false><<<1, TBF, 0, st>>>(b, n, sh, seg);
 			kt.mark(CCG_K_FIND);
 			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg);
 			kt.mark(CCG_K_REST);
