@@ -14,7 +14,8 @@ divided by the max over ranks of the timed span.  One N=10k tree does not
 gain from more GPUs (a join is ~35 us of dependent steps); the sharded path is
 measured where it pays, in extras.nj_sharded: ONE N=100k matrix (40 GB) with
 its LT row bands dealt over all ranks, NJ joins with RCCL exchanges
-(ccg_tree_shard_dev), strong scaling.
+(ccg_tree_shard_dev), strong scaling; and extras.dnj_sharded,
+configs[3]: ONE N=200k matrix (float, 80 GB) sharded the same way, DNJ joins.
 
 Also reported: the dominant kernel's roofline (HIP-event timing of every
 kernel in one profiled extra step on the engine stream; algorithmic bytes as
@@ -48,7 +49,7 @@ VALU_INT_LANE_OPS = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
-SHARD_LEG_TIMEOUT_S = 300
+SHARD_LEG_TIMEOUT_S = 480
 
 
 from tools.synth import euclid as euclid_ltd  # noqa: E402
@@ -276,6 +277,7 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, 
     cnt, ns = pst[4 + 2 * 3], pst[5 + 2 * 3]
     kern_gb = (8.0 * cells / world + 8.0 * n * joins) / (ns / 1e9) / 1e9 if ns else None
     del loc, work
+    torch.cuda.empty_cache()
     return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 3), "joins": joins,
             "n": n, "world": world, "seconds": round(dt, 4),
             "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, {8 * n * (n - 1) / 2 / 1e9:.1f} GB) with "
@@ -284,6 +286,51 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, 
             "hbm_GBps_aggregate": round(gb, 1), "hbm_frac_aggregate": round(gb / (HBM_PEAK_GBS * world), 4),
             "argmin_kernel_GBps_per_gpu": round(kern_gb, 1) if kern_gb else None,
             "coll_us_per_join": round(pst[5 + 2 * 8] / 1e3 / (joins + 1), 2) if pst[4 + 2 * 8] else 0.0}
+
+
+def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=200_000, joins=4000, transport="rccl"):
+    """configs[3]: DNJ with the LT rows sharded over the ranks (ccg_tree_shard_dev
+    with CCG_TREE_DNJ): ONE n-taxon Euclidean matrix (n = 200k,
+    float = `-p`: 80 GB in all), rank g holding the row bands g, g + world, ...;
+    collectives over RCCL (world > 1).  Timed: the first `joins` joins, as
+    time(joins + 1) - time(1), so the exact initSummaD, initHNJ and the setup
+    are excluded.  Every rank takes part."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    from tools.synth import euclid_shard_dev
+    coll = None
+    if world > 1:
+        coll = nt.RcclColl(dev, dist) if transport == "rccl" else nt.HostColl(dist)
+    loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
+    work = torch.empty_like(loc)
+
+    def run(k):
+        work.copy_(loc)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        j, fn, fd, st = dev.tree_shard_dev(work.data_ptr(), n, coll, etype=4, method=cg.CCG_TREE_DNJ, exact=False,
+                                           max_joins=k)
+        dt = time.perf_counter() - t0
+        assert len(j) == k, (len(j), k)
+        return shard_max(dt, dist), st
+
+    try:
+        t1, _ = run(1)
+        tk, st = run(joins + 1)
+    finally:
+        if coll is not None and transport == "rccl":
+            coll.close()
+    dt = tk - t1
+    del loc, work
+    torch.cuda.empty_cache()
+    return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 4), "joins": joins,
+            "n": n, "world": world, "seconds": round(dt, 4),
+            "rows_rescanned_rank0": int(st[0]), "cells_rescanned_rank0": int(st[1]),
+            "config": f"configs[3]: DNJ (-m dnj) on one N={n} Euclidean matrix (float, "
+                      f"{4 * n * (n - 1) / 2 / 1e9:.0f} GB) with its LT row bands dealt over {world} GPU(s) "
+                      f"({transport if world > 1 else 'no'} transport); first {joins} joins; fast row sums"}
 
 
 def shard_max(x, dist):
@@ -305,6 +352,8 @@ def main():
     ap.add_argument("--no-config3", action="store_true", help="skip the 50k x 5M dist+tree leg (~40 s)")
     ap.add_argument("--shard-n", type=int, default=100_000)
     ap.add_argument("--shard-joins", type=int, default=64)
+    ap.add_argument("--dnj-shard-n", type=int, default=200_000)
+    ap.add_argument("--dnj-shard-joins", type=int, default=4000)
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
     args = ap.parse_args()
@@ -437,7 +486,8 @@ def main():
 
         def _timeout():
             if rank == 0:
-                result["extras"]["nj_sharded"] = {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"}
+                for leg in ("nj_sharded", "dnj_sharded"):
+                    result["extras"].setdefault(leg, {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"})
                 print(json.dumps(result), flush=True)
             os._exit(0)
         wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
@@ -448,8 +498,15 @@ def main():
                                joins=args.shard_joins, transport=args.shard_transport)
         except Exception as e:  # noqa: BLE001
             d = {"error": str(e)}
-        wd.cancel()
         result["extras"]["nj_sharded"] = d
+        torch.cuda.empty_cache()
+        try:
+            d = dnj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None,
+                                n=args.dnj_shard_n, joins=args.dnj_shard_joins, transport=args.shard_transport)
+        except Exception as e:  # noqa: BLE001
+            d = {"error": str(e)}
+        wd.cancel()
+        result["extras"]["dnj_sharded"] = d
     dev.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
