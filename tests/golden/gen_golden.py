@@ -164,6 +164,16 @@ def main():
     case(f"{b}_b", ["dist", "-i", "msa64.fsa", "-b"], f"{b}_b.out", "dist")
     case(f"{b}_P", ["dist", "-i", "msa64.fsa", "-P", "10"], f"{b}_P.out", "dist")
     case(f"{b}_P2", ["dist", "-i", "msa_odd.fsa", "-P", "2"], f"msa_odd_P2.out", "dist")
+    # pair mode with proximity masking (maskProxi, fsacmp.c:355)
+    case("msa64_f3P10", ["dist", "-i", "msa64.fsa", "-f", "3", "-P", "10"], "msa64_f3P10.out", "dist")
+    case("msa_odd_f3P2", ["dist", "-i", "msa_odd.fsa", "-f", "3", "-P", "2"], "msa_odd_f3P2.out", "dist")
+    case("msa_word_f3P40W", ["dist", "-i", "msa_word.fsa", "-f", "3", "-P", "40", "-W", "1000"],
+         "msa_word_f3P40W.out", "dist")
+    case("msa64_f3P5pn", ["dist", "-i", "msa64.fsa", "-f", "3", "-P", "5", "-p", "-n", "/dev/null"],
+         "msa64_f3P5pn.out", "dist")
+    case("msa_crlf_f3P100s", ["dist", "-i", "msa_crlf.fsa", "-f", "3", "-P", "100", "-s", "10"],
+         "msa_crlf_f3P100s.out", "dist")
+    case("msa64_f11P7", ["dist", "-i", "msa64.fsa", "-f", "11", "-P", "7"], "msa64_f11P7.out", "dist")
     case(f"{b}_L", ["dist", "-i", "msa64.fsa", "-f", "3", "-L", "2978", "-C", "0"], f"{b}_L.out", "dist")
     case(f"{b}_n", ["dist", "-i", "msa64.fsa", "-f", "3", "-n", "/dev/null"], f"{b}_n.out", "dist")
     case(f"{b}_x3", ["dist", "-i", "msa64.fsa", "-W", "7", "-x", "3"], f"{b}_x3.out", "dist")

@@ -52,10 +52,13 @@ def main():
         add(NJ_NAMES, per_kernel(f"{src}/pmc_fetch_nj/run_counter_collection.csv"),
             per_kernel(f"{src}/pmc_write_nj/run_counter_collection.csv"))
     cal = {}
-    for r in csv.DictReader(open(f"{src}/pmc_cal/run_counter_collection.csv")):
+    cal_csv = f"{src}/pmc_cal/run_counter_collection.csv"
+    for r in (csv.DictReader(open(cal_csv)) if os.path.exists(cal_csv) else []):
         if "k_rescan<256, 8, false>" in r["Kernel_Name"] and r["Grid_Size"] == "327680":
             cal.setdefault("fetch_kib", []).append(float(r["Counter_Value"]))
     calib = None
+    if not cal and os.path.exists(out):
+        calib = json.load(open(out)).get("calibration")  # keep the last measured calibration
     if cal:
         kib = statistics.mean(cal["fetch_kib"])
         calib = {"kernel": "tools/micro/rescan.hip k_rescan<256,8,false>, 256 rows x 9000 f64",
