@@ -317,6 +317,148 @@ __global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restric
 	}
 }
 
+// ------------------------------------------------- pair mode with -P > 0
+// maskProxi (fsacmp.c:355-485) followed by fsacmpair (fsacmp.c:587).  The
+// reference walks the pair's SNPs (inc_i & inc_j set, codes differ) from the
+// last position down; its counter i stands for position p + 1 (the "label"),
+// and with lastSNP starting at len + proxi it clears include bits
+// [label, lastSNP] whenever lastSNP - label <= proxi, then lastSNP = label.
+// The cleared set is therefore the union of the closed intervals between
+// consecutive labels (plus the sentinel len + proxi) that are at most proxi
+// apart, and the pair's (dist, n) are the unmasked counts minus the counts
+// over that union.  Consecutive intervals share one end point, which is
+// added back once when both sides qualify.
+//
+// One wave per pair, 64 words per step (one per lane, coalesced): a max-scan
+// of the lanes' highest labels gives every lane the label below its first
+// SNP; a second scan over (label, qualified) carries whether that label's
+// own lower gap qualified.  Interval counts re-read the (cached) words they
+// cover.  The sequential dependency of maskProxi is only between consecutive
+// SNPs, so the result is exact and independent of the lane split.
+__device__ __forceinline__ int wave_scan_max_incl(int v, int lane) {
+#pragma unroll
+	for(int o = 1; o < 64; o <<= 1) {
+		int t = __shfl_up(v, o, 64);
+		if(lane >= o) v = v > t ? v : t;
+	}
+	return v;
+}
+
+// positions [s, e] (clipped to the W32 counted words) of pair rows A, B
+__device__ __forceinline__ void range_counts(const uint4 *__restrict__ A, const uint4 *__restrict__ B, int W32, int s,
+                                             int e, uint32_t &cm, uint32_t &cd) {
+	cm = cd = 0;
+	if(e > 32 * W32 - 1) e = 32 * W32 - 1;
+	for(int w = s >> 5; w <= (e >> 5) && s <= e; ++w) {
+		const int ks = w == (s >> 5) ? (s & 31) : 0, ke = w == (e >> 5) ? (e & 31) : 31;
+		const uint32_t msk = (0xFFFFFFFFu >> ks) & (0xFFFFFFFFu << (31 - ke));
+		const uint4 a = A[w], b = B[w];
+		const uint32_t m = a.z & b.z & msk;
+		cm += __popc(m);
+		cd += __popc(xor_or(a.x, b.x, a.y ^ b.y) & m);
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(256) void k_snp_pair_proxi(const uint4 *__restrict__ P, int Wp, int W32, int len, int proxi,
+                                                        long long f0, long long f1, unsigned norm, unsigned minLength,
+                                                        double bs, typename Elem<ET>::T *__restrict__ D,
+                                                        typename Elem<ET>::T *__restrict__ Nm) {
+	const int lane = threadIdx.x & 63;
+	const long long stride = (long long) gridDim.x * 4;
+	for(long long f = f0 + (long long) blockIdx.x * 4 + (threadIdx.x >> 6); f < f1; f += stride) {
+		long long i = (long long) ((1.0 + sqrt(1.0 + 8.0 * (double) f)) * 0.5);
+		while(tri(i) > f) --i;
+		while(tri(i + 1) <= f) ++i;
+		const long long j = f - tri(i);
+		const uint4 *A = P + (size_t) i * Wp, *B = P + (size_t) j * Wp;
+		int dist = 0, cnt = 0;
+		int cL = -1, cQ = 0;                 // highest label so far, and whether its lower gap qualified
+		for(int w0 = 0; w0 < W32; w0 += 64) {
+			const int w = w0 + lane;
+			uint32_t m = 0, d = 0;
+			if(w < W32) {
+				const uint4 a = A[w], b = B[w];
+				m = a.z & b.z;
+				d = xor_or(a.x, b.x, a.y ^ b.y) & m;
+			}
+			cnt += __popc(m);
+			dist += __popc(d);
+			// bit 31 - k <-> position 32w + k; label = position + 1
+			const int hiL = d ? 32 * w + 32 - (__ffs(d)) + 1 : -1;
+			int incl = wave_scan_max_incl(hiL, lane);
+			int prevL = __shfl_up(incl, 1, 64);
+			if(lane == 0) prevL = -1;
+			if(cL > prevL) prevL = cL;
+			// q of each own label: gap to the label below <= proxi
+			int qhi = 0;
+			{
+				int prev = prevL;
+				for(uint32_t x = d; x;) {
+					const int k = __clz(x);
+					x &= ~(0x80000000u >> k);
+					const int cur = 32 * w + k + 1;
+					qhi = prev >= 0 && cur - prev <= proxi;
+					prev = cur;
+				}
+			}
+			const int packed = hiL >= 0 ? 2 * hiL + qhi : -1;
+			const int incl2 = wave_scan_max_incl(packed, lane);
+			int prevP = __shfl_up(incl2, 1, 64);
+			if(lane == 0) prevP = -1;
+			const int cP = cL >= 0 ? 2 * cL + cQ : -1;
+			if(cP > prevP) prevP = cP;
+			// subtract the qualifying intervals ending at this lane's labels
+			{
+				int prev = prevL, qprev = prevP >= 0 ? (prevP & 1) : 0;
+				for(uint32_t x = d; x;) {
+					const int k = __clz(x);
+					x &= ~(0x80000000u >> k);
+					const int cur = 32 * w + k + 1;
+					const int qc = prev >= 0 && cur - prev <= proxi;
+					if(qc) {
+						uint32_t rm, rd;
+						range_counts(A, B, W32, prev, cur, rm, rd);
+						cnt -= rm;
+						dist -= rd;
+						if(qprev) {
+							range_counts(A, B, W32, prev, prev, rm, rd);
+							cnt += rm;
+							dist += rd;
+						}
+					}
+					prev = cur;
+					qprev = qc;
+				}
+			}
+			const int top = __shfl(incl2, 63, 64);
+			if(top >= 0 && (top >> 1) > cL) {
+				cL = top >> 1;
+				cQ = top & 1;
+			}
+		}
+		// the highest SNP against the sentinel lastSNP = len + proxi (fsacmp.c:367)
+		if(lane == 0 && cL >= 0 && (long long) len + proxi - cL <= proxi) {
+			uint32_t rm, rd;
+			const long long e = (long long) len + proxi;
+			range_counts(A, B, W32, cL, e < 32LL * W32 ? (int) e : 32 * W32 - 1, rm, rd);
+			cnt -= rm;
+			dist -= rd;
+			if(cQ) {
+				range_counts(A, B, W32, cL, cL, rm, rd);
+				cnt += rm;
+				dist += rd;
+			}
+		}
+#pragma unroll
+		for(int o = 32; o > 0; o >>= 1) {
+			dist += __shfl_xor(dist, o, 64);
+			cnt += __shfl_xor(cnt, o, 64);
+		}
+		if(lane == 0) pair_store<ET>(D, Nm, f, (uint32_t) dist, (uint32_t) cnt, norm, minLength, bs);
+	}
+}
+
 // ------------------------------------------------------------------ host
 static inline long long cdivll(long long a, long long b) { return (a + b - 1) / b; }
 
@@ -327,6 +469,17 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 	long long Ilo = rb / TILE, Ihi = (re - 1) / TILE;   // tile rows touching [rb, re)
 	long long t_begin = Ilo * (Ilo + 1) / 2, t_end = (Ihi + 1) * (Ihi + 2) / 2;
 	const long long batch = 1 << 14;
+	if(a->pair && a->proxi) {
+		const long long f0 = tri(rb), f1 = tri(re), g = cdivll(f1 - f0, 4);
+		const int W32 = (a->len + 31) / 32;
+		if(f1 > f0) {
+			k_snp_pair_proxi<ET><<<(unsigned) (g < 16384 ? g : 16384), 256, 0, ctx->stream>>>(
+			    (const uint4 *) planes, Wp, W32, a->len, (int) a->proxi, f0, f1, a->norm, a->minLength, a->byteScale,
+			    (T *) D, (T *) N);
+			CCG_CHECK(hipGetLastError());
+		}
+		return CCG_OK;
+	}
 	if(a->pair) {
 		for(long long t = t_begin; t < t_end; t += batch) {
 			long long cnt = t_end - t < batch ? t_end - t : batch;
@@ -385,7 +538,6 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
 	if(!a || a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
-	if(a->proxi && a->pair) return CCG_EUNSUP;
 	if(a->n < 2) {
 		if(inc_out && !a->pair) {
 			int *d_inc;

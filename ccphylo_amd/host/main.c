@@ -705,19 +705,11 @@ static int main_dist(int argc, char **argv) {
 		                flag, precision, et, bs, threads, device);
 	}
 	if(tmpl && nfiles > 1) {
-		if((flag & 2) && proxi) {
-			fprintf(stderr, "ccphylo_amd: pairwise proximity masking (-f 2 with -P) is not implemented by the GPU engine.\n");
-			return 1;
-		}
 		return dist_fsa_files(files, nfiles, tmpl, outname, noutname, flag, norm, minLength, minCov, proxi,
 		                      precision, et, bs, device);
 	}
 	if(nfiles > 1) {
 		fprintf(stderr, "ccphylo_amd: multi-file dist input is not implemented by the GPU engine (use one MSA).\n");
-		return 1;
-	}
-	if((flag & 2) && proxi) {
-		fprintf(stderr, "ccphylo_amd: pairwise proximity masking (-f 2 with -P) is not implemented by the GPU engine.\n");
 		return 1;
 	}
 	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");

@@ -63,7 +63,7 @@ typedef struct {
 	int pair;              /* 0: cmpFsaThrd semantics, 1: cmpairFsaThrd semantics */
 	unsigned norm;         /* -W */
 	unsigned minLength;    /* already max(minLength, minCov*len) (cdist.c:289) */
-	unsigned proxi;        /* -P; the GPU engine supports 0 only (CCG_EUNSUP otherwise) */
+	unsigned proxi;        /* -P; pair mode: maskProxi (fsacmp.c:355) per pair */
 	int etype;             /* 8 double, 4 float, 2 u16, 1 u8 (matrix.c:59-71) */
 	double byteScale;      /* ByteScale for etype 2/1 (bytescale.c:45) */
 	int64_t row_begin;     /* LT rows [row_begin, row_end) to compute; 0,0 = all */

@@ -263,6 +263,7 @@ def main():
     case("ff_b_W", ["dist", "-i"] + ffiles + ["-r", "gene_b", "-W", "1000", "-f", "5"], "ff_b_W.out", "fsafiles")
     case("ff_b_f3", ["dist", "-i"] + ffiles + ["-r", "gene_b", "-f", "3", "-n", "-"], "ff_b_f3.out", "fsafiles")
     case("ff_a_f3s", ["dist", "-i"] + ffiles + ["-r", "gene_a", "-f", "3", "-s", "10"], "ff_a_f3s.out", "fsafiles")
+    case("ff_b_f3P", ["dist", "-i"] + ffiles + ["-r", "gene_b", "-f", "3", "-P", "6"], "ff_b_f3P.out", "fsafiles")
 
     with open("golden.json", "w") as f:
         json.dump({"reference": "ccphylo 0.8.5 (oracle/_ref/ccphylo, built by oracle/Makefile)",

@@ -13,7 +13,7 @@ from conftest import GOLDEN, golden_bytes, golden_cases, print_phylip
 
 
 def parse_args(args):
-    o = dict(files=[], tmpl=None, flag=1, norm=0, minLength=1, minCov=0.5, et=8, bs=1.0, prec=9, nout=False)
+    o = dict(files=[], tmpl=None, flag=1, norm=0, minLength=1, minCov=0.5, et=8, bs=1.0, prec=9, nout=False, proxi=0)
     k = 1
     while k < len(args):
         a, nxt = args[k], (args[k + 1] if k + 1 < len(args) else None)
@@ -25,6 +25,7 @@ def parse_args(args):
         elif a == "-f": o["flag"] = int(nxt); k += 1
         elif a == "-W": o["norm"] = int(nxt); k += 1
         elif a == "-n": o["nout"] = True; k += 1
+        elif a == "-P": o["proxi"] = int(nxt); k += 1
         elif a == "-s":
             o["et"] = 2
             if nxt and not nxt.startswith("-"):
@@ -120,7 +121,7 @@ def test_fsa_files_oracle_matches_reference(case):
         S = np.stack([seqs[k] for k in idx])
         I = np.stack([incs[k] for k in idx])
         D, N, _ = pyoracle.snp_ltd(S, I, Dn, length, pair=True, norm=o["norm"], min_length=minL, etype=o["et"],
-                                   byte_scale=o["bs"], want_n=o["nout"])
+                                   byte_scale=o["bs"], proxi=o["proxi"], want_n=o["nout"])
     else:
         L = pyoracle.lib()
         inc = L.orc_npos(gmask.ctypes.data, length)

@@ -42,8 +42,6 @@ def test_tree_golden_engine(dev, case):
 def test_cli_golden(case):
     import ccphylo_amd as cg
     args = list(case["args"])
-    if case["kind"] == "dist" and any(a == "-P" for a in args) and "3" in args:
-        pytest.skip("pairwise proximity masking is not on the GPU engine")
     p = subprocess.run([cg.CLI_PATH] + args, cwd=GOLDEN, capture_output=True, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert p.stdout == golden_bytes(case)
@@ -59,7 +57,7 @@ def test_dist_golden_engine(dev, case):
     out = b""
     if n > 1:
         D, N, inc = dev.snp_ltd(seqs, incs, n, L, pair=pair, norm=o["norm"], min_length=minLength, etype=o["et"],
-                                byte_scale=o["bs"], want_n=o["nout"])
+                                byte_scale=o["bs"], proxi=o["proxi"] if pair else 0, want_n=o["nout"])
         out = print_phylip(D, n, heads, o["flag"], o["prec"], o["et"], o["bs"])
         if N is not None:
             out += print_phylip(N, n, heads, o["flag"], o["prec"], o["et"], o["bs"])
@@ -156,6 +154,57 @@ def test_dist_random_vs_oracle(dev, n, L, pair, et, norm):
     assert (Dg == Do).all()
     if pair:
         assert (Ng == No).all()
+
+
+def _related_msa(rng, n, L, rate, nrate=0.02):
+    """Packed taxa that differ from one random reference at `rate` (2-bit codes
+    MSB-first, qseqs.c:60) and per-taxon include masks with ~nrate holes."""
+    W = L // 32 + 1
+    base = rng.integers(0, 4, L)
+    codes = np.tile(base, (n, 1))
+    mut = rng.random((n, L)) < rate
+    codes[mut] = rng.integers(0, 4, int(mut.sum()))
+    codes[:, L - 1] = np.arange(n) % 4          # a SNP at the last position (the sentinel case, fsacmp.c:367)
+    pad = np.zeros((n, W * 32), np.uint64)
+    pad[:, :L] = codes
+    sh = np.uint64(62) - np.uint64(2) * (np.arange(32, dtype=np.uint64))
+    seqs = (pad.reshape(n, W, 32) << sh).sum(2, dtype=np.uint64)
+    inc = np.zeros((n, W * 32), np.uint64)
+    inc[:, :L] = rng.random((n, L)) >= nrate
+    incs = (inc.reshape(n, W, 32) << (np.uint64(31) - np.arange(32, dtype=np.uint64))).sum(2, dtype=np.uint64)
+    return seqs, incs.astype(np.uint32)
+
+
+@pytest.mark.parametrize("n,L,proxi,rate,et,norm", [(70, 3000, 10, 0.05, 8, 0), (65, 4097, 2, 0.3, 8, 1000),
+                                                    (40, 20000, 40, 0.01, 4, 0), (33, 2048, 100, 0.02, 2, 100),
+                                                    (50, 9000, 1, 0.7, 1, 100), (20, 70000, 33, 0.002, 8, 0),
+                                                    (30, 1000, 5000, 0.01, 8, 0)])
+def test_dist_pair_proxi_vs_oracle(dev, n, L, proxi, rate, et, norm):
+    """Pair mode with -P (maskProxi, fsacmp.c:355): bit-exact (dist, n) and the
+    A7 epilogue vs the oracle, from dense to sparse SNPs, proxi spanning words."""
+    from oracle import pyoracle
+    rng = np.random.default_rng(n * L + proxi)
+    seqs, incs = _related_msa(rng, n, L, rate)
+    ml = int(0.5 * L)
+    Dg, Ng, _ = dev.snp_ltd(seqs, incs, n, L, pair=True, norm=norm, min_length=ml, etype=et, byte_scale=2.0,
+                            proxi=proxi, want_n=True)
+    Do, No, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=True, norm=norm, min_length=ml, proxi=proxi, etype=et,
+                                 byte_scale=2.0, want_n=True)
+    assert (Dg == Do).all() and (Ng == No).all()
+    D0, _, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=True, norm=norm, min_length=ml, etype=et, byte_scale=2.0)
+    assert not (D0 == Do).all()     # the masking did something
+
+
+def test_dist_pair_proxi_row_range(dev):
+    from oracle import pyoracle
+    rng = np.random.default_rng(11)
+    n, L = 90, 5000
+    seqs, incs = _related_msa(rng, n, L, 0.03)
+    Do, _, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=True, proxi=8)
+    for rb, re_ in [(0, 31), (31, 64), (64, 90)]:
+        Dg, _, _ = dev.snp_ltd(seqs, incs, n, L, pair=True, proxi=8, row_range=(rb, re_))
+        lo, hi = rb * (rb - 1) // 2, re_ * (re_ - 1) // 2
+        assert (Dg[lo:hi] == Do[lo:hi]).all()
 
 
 def test_dist_row_range(dev):
