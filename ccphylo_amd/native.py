@@ -110,7 +110,7 @@ HOST_SYMBOLS = [
     "ccq_new", "ccq_free", "ccq_open", "ccq_close", "ccq_peek",
     "ccq_ltd_new", "ccq_ltd_free", "ccq_ltd_reserve", "ccq_ltd_get", "ccq_ltd_set",
     "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
-    "ccq_replay_newick", "ccq_newick_pair",
+    "ccq_replay_newick", "ccq_replay_newick_strings", "ccq_newick_pair",
     "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
     "ccq_load_msa", "ccq_msa_free", "ccq_load_fsa_files", "ccq_load_kma", "ccq_kma_free",
 ]

@@ -85,6 +85,11 @@ typedef struct {
  * flags: tree -f (1 = bifurcating root).  Result in T->names[0]. */
 void ccq_replay_newick(ccq_names *T, int n0, const ccq_join *joins, int njoins,
                        int final_n, double final_d, int flags, int precision);
+/* The same bytes by editing the strings join by join as nwck.c does (O(N^2)
+ * bytes for caterpillar trees); ccq_replay_newick replays only capacities and
+ * lengths, then writes the string once.  Kept for tests and comparison. */
+void ccq_replay_newick_strings(ccq_names *T, int n0, const ccq_join *joins, int njoins,
+                               int final_n, double final_d, int flags, int precision);
 /* tree.c:95-97: a two-taxon matrix */
 void ccq_newick_pair(ccq_names *T, double d, int precision);
 
