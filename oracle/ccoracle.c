@@ -728,6 +728,93 @@ static int min_q_row(const double *Q, int n) {
 	return mi;
 }
 
+/* hclust.c:413-450 updatePrevQ: Q[k] from the row's remembered partner P[k]
+ * for k = 0 .. n-2 (the last row is not revisited).  Row 0 reads element
+ * P[0] = 0 of the flat buffer, i.e. D(1, 0) (mat[0] is the buffer base). */
+static void update_prev_q(const Ltd *D, int n, const double *sD, const int32_t *N, double *Q, const int32_t *P) {
+	for(int64_t k = 0; k < n - 1; ++k) {
+		double d = ld(D, tri(k) + P[k]);
+		if(0 <= d) {
+			Q[k] = ((N[k] + N[P[k]] - 4) >> 1) * d - sD[k] - sD[P[k]];
+		}
+	}
+}
+
+/* hclust.c:452-561 updateHNJ after updateD: updatePrevQ, row j, then column
+ * j over k > j, k != i (the min/p it tracks is never used by hclust) */
+static void update_hnj_q(const Ltd *D, int n, const double *sD, const int32_t *N, double *Q, int32_t *P, int i, int j) {
+	update_prev_q(D, n, sD, N, Q, P);
+	double qj = DBL_MAX;
+	int pj = 0;
+	int64_t base = tri(j);
+	for(int64_t k = 0; k < j; ++k) {
+		double d = ld(D, base + k);
+		if(0 <= d) {
+			double q = ((N[j] + N[k] - 4) >> 1) * d - sD[j] - sD[k];
+			if(q <= qj) {
+				qj = q;
+				pj = (int) k;
+			}
+		}
+	}
+	Q[j] = qj;
+	P[j] = pj;
+	for(int64_t k = j + 1; k < n; ++k) {
+		if(k == i) {
+			continue;
+		}
+		double d = ld(D, tri(k) + j);
+		if(0 <= d) {
+			double q = ((N[j] + N[k] - 4) >> 1) * d - sD[j] - sD[k];
+			if(P[k] == i || P[k] == j) {
+				Q[k] = q;
+				P[k] = j;
+			} else if(q <= Q[k]) {
+				Q[k] = q;
+				if(P[k] < j) {
+					P[k] = j;
+				}
+			}
+		}
+	}
+}
+
+/* hclust.c:1308-1432 HNJ_popArrange; *n is decremented */
+static void hnj_pop_arrange(Ltd *D, int *n, double *sD, int32_t *N, double *Q, int32_t *P, int pos) {
+	int nn = --*n;
+	if(pos == nn) {
+		return;
+	}
+	sD[pos] = sD[nn];
+	N[pos] = N[nn];
+	pop_arrange(D, nn, pos);
+	double qp = DBL_MAX;
+	int pp = 0;
+	int64_t base = tri(pos);
+	for(int64_t k = 0; k < pos; ++k) {
+		double d = ld(D, base + k);
+		if(0 <= d) {
+			double q = d * ((N[pos] + N[k] - 4) >> 1) - sD[pos] - sD[k];
+			if(q <= qp) {
+				qp = q;
+				pp = (int) k;
+			}
+		}
+	}
+	Q[pos] = qp;
+	P[pos] = pp;
+	for(int64_t k = pos + 1; k < nn; ++k) {
+		double d = ld(D, tri(k) + pos);
+		if(0 <= d) {
+			double q = d * ((N[pos] + N[k] - 4) >> 1) - sD[pos] - sD[k];
+			if(q <= Q[k] && (P[k] < pos || q < Q[k])) {
+				Q[k] = q;
+				P[k] = pos;
+			}
+		}
+	}
+}
+
 int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int flags,
              orc_join *joins, int *final_n, double *final_d, int64_t *stats) {
 	Ltd D = {etype, byteScale, Dbase};
@@ -754,6 +841,22 @@ int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int fl
 			pop_arrange(&D, n, i);
 			sD[i] = sD[n];
 			N[i] = N[n];
+		}
+	} else if(method == 2) {
+		/* hclust.c:1671-1718 hclust with initHNJ / minQ / updateHNJ / HNJ_popArrange */
+		init_hnj(&D, n, sD, N, Q, P);
+		while(n != 2) {
+			int i = min_q_row(Q, n);
+			int j = P[i];
+			if(i == 0 && j == 0) {
+				break;
+			}
+			double Li, Lj;
+			limb_length(&Li, &Lj, i, j, sD, N, ld(&D, tri(i) + j), neg);
+			joins[nj].i = i; joins[nj].j = j; joins[nj].Li = Li; joins[nj].Lj = Lj; ++nj;
+			update_d(&D, n, sD, N, i, j, Li, Lj);
+			update_hnj_q(&D, n, sD, N, Q, P, i, j);
+			hnj_pop_arrange(&D, &n, sD, N, Q, P, i);
 		}
 	} else {
 		/* dnj.c:985-1052 */

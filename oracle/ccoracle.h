@@ -48,7 +48,7 @@ int orc_snp_ltd(int n, int len, const uint64_t *seqs, const uint32_t *incs, int 
                 int etype, double byteScale, void *D, void *N);
 
 /* C/D: tree construction.  D is the packed LT matrix (destroyed).
- * method: 0 = nj (nj.c:1560), 1 = dnj (dnj.c:985).  flags: tree -f
+ * method: 0 = nj (nj.c:1560), 1 = dnj (dnj.c:985), 2 = hnj (hclust.c:1671).  flags: tree -f
  * (2 = limbLengthNeg).  Writes up to n-2 joins, returns the number of joins;
  * *final_n receives D->n at exit and *final_d the last pair's distance
  * (valid when *final_n == 2).  stats (may be NULL): [0] rows rescanned,

@@ -52,7 +52,7 @@ def lib():
 
 
 def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False):
-    """Serial NJ (method 0) / DNJ (method 1) exactly as the reference.
+    """Serial NJ (method 0) / DNJ (method 1) / HNJ (method 2) exactly as the reference.
     Returns (joins, final_n, final_d[, stats])."""
     D = np.array(D, dtype=ETYPES[etype], copy=True)
     joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)

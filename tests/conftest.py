@@ -53,7 +53,7 @@ def parse_tree_args(args):
         if a == "-i":
             inp = args[k + 1]; k += 1
         elif a == "-m":
-            method = 0 if args[k + 1] == "nj" else 1; k += 1
+            method = {"nj": 0, "dnj": 1, "hnj": 2}[args[k + 1]]; k += 1
         elif a == "-p":
             et = 4
         elif a in ("-s", "-b"):

@@ -190,12 +190,23 @@ def main():
         case(f"euc400_{m}", ["tree", "-i", "euc400.phy.gz", "-m", m], f"euc400_{m}.out", "tree")
     case("euc400_p", ["tree", "-i", "euc400.phy.gz", "-p"], "euc400_p.out", "tree")
 
+    # HNJ (-m hnj, hclust.c:1671): the heuristic NJ on the same inputs
+    case("test_hnj", ["tree", "-i", "test.phy.gz", "-m", "hnj"], "test_hnj.out", "tree")
+    case("test_hnj_p", ["tree", "-i", "test.phy.gz", "-m", "hnj", "-p"], "test_hnj_p.out", "tree")
+    case("test_hnj_f1", ["tree", "-i", "test.phy.gz", "-m", "hnj", "-f", "1"], "test_hnj_f1.out", "tree")
+    case("test_hnj_f2", ["tree", "-i", "test.phy.gz", "-m", "hnj", "-f", "2"], "test_hnj_f2.out", "tree")
+    case("snp300_hnj", ["tree", "-i", "snp300.phy", "-m", "hnj"], "snp300_hnj.out", "tree")
+    case("snp300_hnj_b", ["tree", "-i", "snp300.phy", "-m", "hnj", "-b"], "snp300_hnj_b.out", "tree")
+    case("snp300_hnj_s", ["tree", "-i", "snp300.phy", "-m", "hnj", "-s"], "snp300_hnj_s.out", "tree")
+    case("euc400_hnj", ["tree", "-i", "euc400.phy.gz", "-m", "hnj"], "euc400_hnj.out", "tree")
+
     # (iv) missing data: pairwise distances with -1 where the overlap is short
     msa("msa_miss.fsa", 80, 1500, seed=7, nrate=0.12, exclude=0, gaps=False, iupac=False, lower=False)
     run(["dist", "-i", "msa_miss.fsa", "-f", "3", "-L", "1150", "-C", "0"], "miss80.phy")
     for m in ("dnj", "nj"):
         case(f"miss80_{m}", ["tree", "-i", "miss80.phy", "-m", m], f"miss80_{m}.out", "tree")
     case("miss80_p", ["tree", "-i", "miss80.phy", "-p"], "miss80_p.out", "tree")
+    case("miss80_hnj", ["tree", "-i", "miss80.phy", "-m", "hnj"], "miss80_hnj.out", "tree")
 
     # multi-matrix Phylip with a comment header (tree.c:101-104, phy.c:275)
     with open("multi.phy", "w") as f:
@@ -203,6 +214,7 @@ def main():
             f.write(f"#matrix{k}\n")
             f.write(open(fn).read())
     case("multi_dnj", ["tree", "-i", "multi.phy"], "multi_dnj.out", "tree")
+    case("multi_hnj", ["tree", "-i", "multi.phy", "-m", "hnj"], "multi_hnj.out", "tree")
 
     # (v) KMA count matrices (B1/B2): 9 samples x 2 templates -- insertion rows
     # (s2, s5: stripMat's 7-short stride), a low-depth sample (s3), a missing
