@@ -439,7 +439,7 @@ def main():
         extras = {}
         pb = dev.malloc(nbytes)
         for label, method, ex in (("dnj_exact_sums" if not exact else "dnj_fast_sums", cg.CCG_TREE_DNJ, not exact),
-                                  ("nj", cg.CCG_TREE_NJ, exact)):
+                                  ("nj", cg.CCG_TREE_NJ, exact), ("hnj", cg.CCG_TREE_HNJ, exact)):
             dev.h2d(pb, D)
             torch.cuda.synchronize()
             t1 = time.perf_counter()

@@ -7,7 +7,7 @@ Native pieces (built in-tree by ``__graft_entry__.build()`` / ``make -C ccphylo_
 
 Python here is only a thin ctypes layer for tests and the benchmark.
 """
-from .native import (CCG_TREE_DNJ, CCG_TREE_NJ, CLI_PATH, CcgError, Device, ETYPES, JOIN_DTYPE,  # noqa: F401
+from .native import (CCG_TREE_DNJ, CCG_TREE_HNJ, CCG_TREE_NJ, CLI_PATH, CcgError, Device, ETYPES, JOIN_DTYPE,  # noqa: F401
                      engine_lib, host_lib, load_msa, load_phylip, newick_from_phylip)
 
 __version__ = "0.1.0"

@@ -137,7 +137,8 @@ done:
 int ccg_tree_dev(ccg_ctx *c, const ccg_tree_args *a, void *D, ccg_join *joins, int *njoins, int *final_n,
                  double *final_d, int64_t *stats) {
 	if(!c || !a || !D || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
-	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ)) return CCG_EINVAL;
+	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ && a->method != CCG_TREE_HNJ))
+		return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));

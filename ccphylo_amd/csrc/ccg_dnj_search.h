@@ -780,6 +780,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	const int r0 = b.crow[tid], o0 = b.coff[tid];
 	const int done = ctl->done, T = ctl->T;
 	if(done || T == 0) return;
+	// blocks beyond the unit count leave before staging the table
+	if((int) blockIdx.x >= b.coff[T]) return;
 	// the entry table in LDS when it fits, else searched in HBM (L2-resident)
 	const bool lds = T <= REPLAY_CAP;
 	if(lds) {

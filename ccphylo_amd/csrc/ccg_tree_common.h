@@ -34,6 +34,7 @@ struct TreeCtl {
 	int neg, exact, method, has_missing;
 	int serial_sums, serial_replays;
 	long long rows, cells, cells_top, cells_rest;
+	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
 };
 
 struct TreeBufs {

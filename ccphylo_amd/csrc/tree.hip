@@ -753,7 +753,7 @@ __global__ __launch_bounds__(TB) void k_nj_argmin(const typename Elem<ET>::T *__
 // fold of the argmin partials (wave 0), limbLength, the join record and updateD
 template <int ET>
 __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
-                                                int G, int general) {
+                                                int G, int general, double q0) {
 	__shared__ long long s_bf, s_wf[TB / 64];
 	__shared__ double s_wq[TB / 64];
 	__shared__ int s_stop, s_nj, s_neg, s_exact;
@@ -767,7 +767,7 @@ __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict
 		Nk = b.N[k];
 	}
 	// fold of the argmin partials by the whole block (G grows as n^2)
-	double fq = 1.0;
+	double fq = q0;
 	long long ff = -1;
 	for(int g = tid; g < G; g += TB) {
 		double oq = b.qpart[g];
@@ -894,6 +894,266 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 	}
 }
 
+
+// ------------------------------------------------------------------ HNJ
+// hclust.c:1671 hclust with initHNJ / minQ / updateHNJ / HNJ_popArrange
+// (-m hnj).  Every step is O(n) per join; per join:
+//   k_hnj_argmin  folds the last join's two row minima (row j from
+//                 k_hnj_update, row i from k_hnj_pop) into Q/P, then per-block
+//                 minQ partials (q, tri(r) + P[r]) over rows 1..n-1: P[r] < r,
+//                 so the larger flat index is the later row, minQ's `<=` rule
+//                 (hclust.c:353);
+//   k_nj_join     (shared with NJ, fold start DBL_MAX) limbLength, the join
+//                 record and updateD;
+//   k_hnj_update  per row k: updatePrevQ (hclust.c:413, rows 0..n-2, row 0
+//                 reading flat element P[0]) then updateHNJ's column-j rule
+//                 (hclust.c:516-558); the row-j minimum as per-block partials;
+//   k_hnj_pop     HNJ_popArrange (hclust.c:1308): row n-1 into row i (its
+//                 minimum as partials) and column i with `P < pos || q < Q`.
+
+// (q, k) `<=` rule over ascending k: smaller q, then the later k
+__device__ __forceinline__ void qk_take(double &bq, int &bk, double q, int k) {
+	if(q < bq || (q == bq && k > bk)) {
+		bq = q;
+		bk = k;
+	}
+}
+
+template <int NT>
+__device__ __forceinline__ void qk_block_reduce(double &bq, int &bk, double *sq, int *sk) {
+	for(int o = 32; o > 0; o >>= 1) {
+		const double oq = __shfl_xor(bq, o, 64);
+		const int ok = __shfl_xor(bk, o, 64);
+		qk_take(bq, bk, oq, ok);
+	}
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	if(lane == 0) {
+		sq[wid] = bq;
+		sk[wid] = bk;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int w = 1; w < NT / 64; ++w) qk_take(bq, bk, sq[w], sk[w]);
+	}
+}
+
+// one wave: fold of G row-minimum partials (blocks in ascending k order)
+__device__ __forceinline__ void qk_fold_wave(const double *pq, const int *pk, int G, double &bq, int &bk) {
+	const int lane = threadIdx.x & 63;
+	bq = DBL_MAX;
+	bk = -1;
+	for(int g = lane; g < G; g += 64) qk_take(bq, bk, pq[g], pk[g]);
+	for(int o = 32; o > 0; o >>= 1) {
+		const double oq = __shfl_xor(bq, o, 64);
+		const int ok = __shfl_xor(bk, o, 64);
+		qk_take(bq, bk, oq, ok);
+	}
+}
+
+template <int UNUSED = 0>
+__global__ __launch_bounds__(TB) void k_hnj_argmin(TreeBufs b, int n) {
+	__shared__ double sq[TB / 64], fq[2];
+	__shared__ long long sf[TB / 64];
+	__shared__ int fk[2];
+	const TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+	const int r = (int) blockIdx.x * TB + tid;
+	const int hj = ctl->hj, hi = ctl->hi;
+	const bool own_j = hj >= 0 && hj / TB == (int) blockIdx.x, own_i = hi >= 0 && hi / TB == (int) blockIdx.x;
+	if(own_j || own_i) {
+		if(wid < 2 && ((wid == 0 && own_j) || (wid == 1 && own_i))) {
+			double q;
+			int k;
+			if(wid == 0) qk_fold_wave(b.bmq, b.bmr, ctl->hjb, q, k);
+			else qk_fold_wave(b.cfq, b.cfp, ctl->hib, q, k);
+			if(lane == 0) {
+				fq[wid] = q;
+				fk[wid] = k;
+			}
+		}
+		__syncthreads();
+	}
+	double q = DBL_MAX;
+	long long f = -1;
+	if(r < n) {
+		double qr = b.Q[r];
+		int pr = b.P[r];
+		const int w = own_j && r == hj ? 0 : own_i && r == hi ? 1 : -1;
+		if(w >= 0) {
+			qr = fq[w];
+			pr = fk[w] < 0 ? 0 : fk[w];
+			b.Q[r] = qr;
+			b.P[r] = pr;
+		}
+		if(r >= 1 && qr <= DBL_MAX) {
+			q = qr;
+			f = tri(r) + pr;
+		}
+	}
+	qf_wave_reduce(q, f);
+	if(lane == 0) {
+		sq[wid] = q;
+		sf[wid] = f;
+	}
+	__syncthreads();
+	if(tid == 0) {
+		for(int k = 1; k < TB / 64; ++k) {
+			if(sq[k] < q || (sq[k] == q && sf[k] > f)) {
+				q = sq[k];
+				f = sf[k];
+			}
+		}
+		b.qpart[blockIdx.x] = q;
+		b.fpart[blockIdx.x] = f;
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(TB) void k_hnj_update(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                   int n, int general) {
+	__shared__ double s_sd, sq[TB / 64];
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, sk[TB / 64];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = (int) blockIdx.x * TB + tid;
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need;
+			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j;
+	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	const int nj = s_nj;
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = nj;
+		ctl->hj = j;
+		ctl->hjb = (int) cdiv(j, TB);
+		if(s_serial) ctl->serial_sums++;
+	}
+	double rq = DBL_MAX;
+	int rk = -1;
+	if(k < n) {
+		const int Nk = k == j ? nj : b.N[k];
+		const double sDk = k == j ? sdj : b.sD[k];
+		double Qk = b.Q[k];
+		int Pk = b.P[k];
+		if(k <= n - 2) {   // updatePrevQ (hclust.c:441-449)
+			const int pk = Pk;
+			const double d = Elem<ET>::get(D[tri(k) + pk], bs);
+			if(0 <= d) {
+				const int Np = pk == j ? nj : b.N[pk];
+				const double sDp = pk == j ? sdj : b.sD[pk];
+				Qk = ((Nk + Np - 4) >> 1) * d - sDk - sDp;
+			}
+		}
+		if(k > j && k != i) {   // column j (hclust.c:530-556)
+			const double d = Elem<ET>::get(D[tri(k) + j], bs);
+			if(0 <= d) {
+				const double q = ((nj + Nk - 4) >> 1) * d - sdj - sDk;
+				if(Pk == i || Pk == j) {
+					Qk = q;
+					Pk = j;
+				} else if(q <= Qk) {
+					Qk = q;
+					if(Pk < j) Pk = j;
+				}
+			}
+		}
+		if(k != j) {
+			b.Q[k] = Qk;
+			b.P[k] = Pk;
+		}
+		if(k < j) {   // row j (hclust.c:497-511)
+			const double d = Elem<ET>::get(D[tri(j) + k], bs);
+			if(0 <= d) {
+				rq = ((nj + Nk - 4) >> 1) * d - sdj - sDk;
+				rk = k;
+			}
+		}
+	}
+	if((int) blockIdx.x * TB < j) {
+		qk_block_reduce<TB>(rq, rk, sq, sk);
+		if(tid == 0) {
+			b.bmq[blockIdx.x] = rq;
+			b.bmr[blockIdx.x] = rk;
+		}
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(TB) void k_hnj_pop(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n) {
+	__shared__ double sq[TB / 64];
+	__shared__ int sk[TB / 64];
+	TreeCtl *ctl = b.ctl;
+	if(ctl->done) return;
+	const int nn = n - 1, i = ctl->i;
+	const int tid = threadIdx.x;
+	if(i == nn) {
+		if(blockIdx.x == 0 && tid == 0) ctl->hi = -1;
+		return;
+	}
+	const int k = (int) blockIdx.x * TB + tid;
+	const double sDi = b.sD[nn];
+	const int Ni = b.N[nn];
+	double rq = DBL_MAX;
+	int rk = -1;
+	if(k < nn && k != i) {
+		const typename Elem<ET>::T vm = D[tri(nn) + k];
+		const double d = Elem<ET>::get(vm, bs);
+		double q = 0;
+		if(0 <= d) q = d * ((Ni + b.N[k] - 4) >> 1) - sDi - b.sD[k];
+		if(k < i) {
+			D[tri(i) + k] = vm;
+			if(0 <= d) {
+				rq = q;
+				rk = k;
+			}
+		} else {
+			D[tri(k) + i] = vm;
+			if(0 <= d) {
+				const double Qk = b.Q[k];
+				const int Pk = b.P[k];
+				if(q <= Qk && (Pk < i || q < Qk)) {
+					b.Q[k] = q;
+					b.P[k] = i;
+				}
+			}
+		}
+	}
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[i] = sDi;
+		b.N[i] = Ni;
+		ctl->hi = i;
+		ctl->hib = (int) cdiv(i, TB);
+	}
+	if((int) blockIdx.x * TB < i) {
+		qk_block_reduce<TB>(rq, rk, sq, sk);
+		if(tid == 0) {
+			b.cfq[blockIdx.x] = rq;
+			b.cfp[blockIdx.x] = rk;
+		}
+	}
+}
+
 // ------------------------------------------------------------------ host
 int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
@@ -998,10 +1258,21 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_REQUEUE);
 		return (GEN ? 6 : 5) + prefold;
 	}
+	if(method == CCG_TREE_HNJ) {
+		k_hnj_argmin<><<<gn, TB, 0, st>>>(b, n);
+		kt.mark(CCG_K_ARGMIN);
+		k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) gn, general, DBL_MAX);
+		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		kt.mark(CCG_K_UPDATE);
+		k_hnj_pop<ET><<<gn, TB, 0, st>>>(D, bs, b, n);
+		kt.mark(CCG_K_POP);
+		return GEN ? 5 : 4;
+	}
 	const unsigned g = (unsigned) nj_blocks(n);
 	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
 	kt.mark(CCG_K_ARGMIN);
-	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general);
+	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general, 1.0);
 	if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
 	kt.mark(CCG_K_UPDATE);
 	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general);
@@ -1028,6 +1299,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	init.neg = (a->flags & 2) != 0;
 	init.exact = a->exact != 0;
 	init.method = a->method;
+	init.hj = init.hi = -1;
 	CCG_CHECK(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	long long launches = 0;
 	static KTimer kt;
@@ -1040,6 +1312,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(DenseRows(), D, n0, bs, b.sD, b.N, b.Q, b.P);
 		k_dnj_prep<><<<1, TB, 0, st>>>(b, n0);
 		launches += 2;
+	} else if(a->method == CCG_TREE_HNJ) {
+		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(DenseRows(), D, n0, bs, b.sD, b.N, b.Q, b.P);   // hclust.c:56
+		launches += 1;
 	}
 	kt.mark(CCG_K_INIT);
 	CCG_CHECK(hipGetLastError());

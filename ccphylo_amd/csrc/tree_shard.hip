@@ -667,6 +667,7 @@ int ccg_rccl_close(ccg_coll *c) {
 
 static int shard_check(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll) {
 	if(!c || !a) return CCG_EINVAL;
+	if(a->method == CCG_TREE_HNJ) return CCG_EUNSUP;   // HNJ runs on one GPU
 	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ)) return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;

@@ -188,15 +188,18 @@ static int main_tree(int argc, char **argv) {
 		m = CCG_TREE_DNJ;
 	} else if(!strcmp(method, "nj")) {
 		m = CCG_TREE_NJ;
+	} else if(!strcmp(method, "hnj")) {
+		m = CCG_TREE_HNJ;
 	} else if(!strcmp(method, "mh")) {
 		fprintf(stdout, "# Tree construction methods:\n#\n");
 		fprintf(stdout, "# %-8s\t%s\n", "nj", "Neighbor-Joining");
+		fprintf(stdout, "# %-8s\t%s\n", "hnj", "Heuristic Neighbor-Joining");
 		fprintf(stdout, "# %-8s\t%s\n", "dnj", "Dynamic Neighbor-Joining");
 		fprintf(stdout, "#\n");
 		return 0;
 	} else if(!strcmp(method, "upgma") || !strcmp(method, "cf") || !strcmp(method, "ff") || !strcmp(method, "mn") ||
-	          !strcmp(method, "hnj") || !strcmp(method, "frank")) {
-		fprintf(stderr, "ccphylo_amd: tree method \"%s\" is not implemented by the GPU engine (nj, dnj are).\n", method);
+	          !strcmp(method, "frank")) {
+		fprintf(stderr, "ccphylo_amd: tree method \"%s\" is not implemented by the GPU engine (nj, dnj, hnj are).\n", method);
 		return 1;
 	} else {
 		die_opt("Invalid", "\"-m\"");

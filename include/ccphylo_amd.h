@@ -141,12 +141,13 @@ typedef struct {
 
 #define CCG_TREE_NJ   0    /* -m nj  (nj.c:1560, the -t 1 semantics) */
 #define CCG_TREE_DNJ  1    /* -m dnj (dnj.c:985, default) */
+#define CCG_TREE_HNJ  2    /* -m hnj (hclust.c:1671: initHNJ, minQ, updateHNJ, HNJ_popArrange) */
 
 typedef struct {
 	int n;                 /* taxa (> 2) */
 	int etype;             /* 8, 4, 2, 1 */
 	double byteScale;
-	int method;            /* CCG_TREE_NJ / CCG_TREE_DNJ */
+	int method;            /* CCG_TREE_NJ / CCG_TREE_DNJ / CCG_TREE_HNJ */
 	int flags;             /* tree -f: bit 2 = limbLengthNeg (nj.c:81) */
 	int exact;             /* 1: row sums of a join accumulated serially in the
 	                          reference order (bit-identical to the reference);

@@ -284,3 +284,64 @@ def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
     assert len(got) == len(ref) and (got == ref).all()
     sh = dev.tree_shard(D, n, None, method=1, exact=True)[0]
     assert (sh == got).all()
+
+
+def _missing_ltd(n, seed, frac=0.05):
+    """Euclidean distances with a fraction of cells set to -1 (missing,
+    nj.c:111 initSummaD skips them; updateD's quirky branches run)."""
+    D = _euclid(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    D[rng.random(D.size) < frac] = -1.0
+    return D
+
+
+@pytest.mark.parametrize("n,kind", [(600, "euc"), (1500, "snp"), (2500, "euc"), (3000, "clade"), (400, "miss"),
+                                    (1100, "miss")])
+def test_hnj_vs_oracle(dev, n, kind):
+    """-m hnj (hclust.c:1671): joins bit-identical to the serial reference
+    restatement in exact mode, including updatePrevQ's row-0 / last-row
+    quirks, the column-j `P == i || P == j` rule and HNJ_popArrange's
+    `P < pos || q < Q` rule; matrices with missing entries take the general
+    updateD."""
+    from oracle import pyoracle
+    D = {"euc": lambda: _euclid(n, n), "snp": lambda: _snp(n, n), "clade": lambda: _clade_ltd(n, n),
+         "miss": lambda: _missing_ltd(n, n)}[kind]()
+    got, fn, fd, _ = dev.tree(D, n, method=2, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=2)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
+
+
+@pytest.mark.parametrize("et", [4, 2, 1])
+def test_hnj_types_vs_oracle(dev, et):
+    from oracle import pyoracle
+    n = 700
+    D = _snp(n, 17)
+    bs = {4: 1.0, 2: 4.0, 1: 1.0}[et]
+    Dt = D.astype(np.float32) if et == 4 else np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(
+        np.uint8 if et == 1 else np.uint16)
+    got, fn, fd, _ = dev.tree(Dt, n, etype=et, byte_scale=bs, method=2, exact=True)
+    ref, rfn, rfd = pyoracle.tree(Dt, n, etype=et, byte_scale=bs, method=2)
+    assert (fn, fd) == (rfn, rfd) and (got == ref).all()
+
+
+@pytest.mark.parametrize("et", [8, 1])
+def test_hnj_all_ties(dev, et):
+    from oracle import pyoracle
+    n = 300
+    D = np.full(n * (n - 1) // 2, 200, dtype=np.float64 if et == 8 else np.uint8)
+    got, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=1.0, method=2, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=2, etype=et, byte_scale=1.0)
+    assert (fn, fd) == (rfn, rfd) and (got == ref).all()
+
+
+def test_hnj_fast_sums(dev):
+    """--fast_sums: same joins, lengths within 1e-9 relative (stated tolerance)."""
+    from oracle import pyoracle
+    n = 2000
+    D = _euclid(n, 5)
+    got, fn, fd, _ = dev.tree(D, n, method=2, exact=False)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=2)
+    assert fn == rfn and (got["i"] == ref["i"]).all() and (got["j"] == ref["j"]).all()
+    for f in ("Li", "Lj"):
+        np.testing.assert_allclose(got[f], ref[f], rtol=1e-9, atol=1e-12)

@@ -87,7 +87,8 @@ def test_shard_world1_matches_single(dev, n, kind, et, exact, method):
 
 
 # miss80 and multi.phy's second matrix hold missing entries (CCG_EUNSUP below)
-@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if not c["name"].startswith(("miss", "multi"))],
+@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if not c["name"].startswith(("miss", "multi"))
+                                  and "hnj" not in c["args"]],
                          ids=lambda c: c["name"])
 def test_shard_golden(dev, case):
     import ccphylo_amd as cg
@@ -183,3 +184,11 @@ def test_max_joins_prefix(dev):
     fullq = dev.tree(D, n, method=1)[0]
     j = dev.tree_shard(D, n, None, method=1, max_joins=k)[0]
     assert (j == fullq[:k]).all()
+
+
+def test_shard_hnj_unsupported(dev):
+    """HNJ runs on one GPU: the sharded entry point says so (CCG_EUNSUP)."""
+    import ccphylo_amd as cg
+    D = np.arange(10 * 9 // 2, dtype=np.float64)
+    with pytest.raises(cg.CcgError, match="not supported"):
+        dev.tree_shard(D, 10, None, method=cg.CCG_TREE_HNJ)
