@@ -47,6 +47,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # 2.4 GHz = 3.93e13 is exceeded, i.e. the engine clock runs above 2.4 GHz).
 VALU_INT_LANE_OPS = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
+OPS_PER_WORD_PAIR_PAIRMODE = 6.0   # v_and (masks), v_xor, v_bitop3, v_and, 2x v_bcnt (dist and n)
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
 SHARD_LEG_TIMEOUT_S = 480
@@ -158,7 +159,7 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
             "sample": f"full N={n} DNJ tree with the oracle's serial C restatement (reference binary absent)"}
 
 
-def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=None):
+def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=None, pair=False):
     """SNP distances (non-pair, double) with device-resident packed input.
     With world > 1 the LT rows are sharded over the ranks (SURVEY 8(e):
     pairs are independent, so no data-path collective): rank g computes rows
@@ -168,34 +169,40 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     W = L // 32 + 1
     g = torch.Generator(device="cuda").manual_seed(3)
     seqs = torch.randint(-2**62, 2**62, (n, W), dtype=torch.int64, device="cuda", generator=g)
-    incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
-    incs[(L + 31) // 32:] = 0
+    incs = torch.full((n, W) if pair else (W,), -1, dtype=torch.int32, device="cuda")
+    incs[..., (L + 31) // 32:] = 0
     if L % 32:
-        incs[(L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+        incs[..., (L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    if pair:   # per-taxon masks with ~1/16 of the positions excluded
+        incs &= torch.randint(-2**31, 2**31, incs.shape, dtype=torch.int32, device="cuda", generator=g) | 0x7FFF7FFF
     m = n * (n - 1) // 2
     r0, r1 = shard.lt_row_ranges(n, world)[rank]
     Dd = torch.empty(m, dtype=torch.float64, device="cuda")
+    Nd = torch.empty(m, dtype=torch.float64, device="cuda") if pair else None
+    kw = dict(row_range=(r0, r1), pair=pair, N_ptr=Nd.data_ptr() if pair else None)
     torch.cuda.synchronize()
-    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), row_range=(r0, r1))
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), **kw)
     times = []
     for _ in range(reps):
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
-        dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), row_range=(r0, r1))
+        dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr(), **kw)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         times.append(shard.reduce_max(dt, dist) if dist is not None else dt)
     dt = min(times)
     words = (L + 31) // 32
-    ops = m * words * OPS_PER_WORD_PAIR / world   # per GPU
-    del seqs, incs, Dd
+    opw = OPS_PER_WORD_PAIR_PAIRMODE if pair else OPS_PER_WORD_PAIR
+    ops = m * words * opw / world   # per GPU
+    del seqs, incs, Dd, Nd
+    mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
-            "config": f"N={n} x L={L} random MSA (non-pair, double), input in HBM, LT rows sharded over {world} GPU(s)",
+            "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
             "roofline": {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": VALU_INT_LANE_OPS / 1e12,
                          "unit": "T int lane-ops/s", "frac": round(ops / dt / VALU_INT_LANE_OPS, 4),
-                         "ops_per_word_pair": OPS_PER_WORD_PAIR}}
+                         "ops_per_word_pair": opw}}
 
 
 def kma_extra(dev, torch, n=1024, L=50_000, reps=3, metric="cos"):
@@ -459,6 +466,10 @@ def main():
             d = {"error": str(e)}
         result.setdefault("extras", {})["dist"] = d
         if world == 1:
+            try:
+                result["extras"]["dist_pair"] = dist_extra(dev, torch, pair=True)
+            except Exception as e:  # noqa: BLE001
+                result["extras"]["dist_pair"] = {"error": str(e)}
             try:
                 result["extras"]["kma_cos"] = kma_extra(dev, torch)
             except Exception as e:  # noqa: BLE001

@@ -253,19 +253,29 @@ __device__ __forceinline__ void pair_store(typename Elem<ET>::T *D, typename Ele
 	}
 }
 
-template <int ET>
-__global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
-                                                          unsigned norm, unsigned minLength, double bs,
+// Pair tiles: as k_snp_tile, with each taxon's mask beside its planes
+// (uint4 {hi, lo, m, 0} per word): double-buffered KCP-word chunks of both
+// 128-row panels, XCD-contiguous tile order, and split-K over word slices when
+// the tiles do not fill the chip (exact u32 atomics of dist and n, then
+// k_snp_pair_finish applies the A7 epilogue).
+template <int ET, bool SPLIT>
+__global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
+                                                          long long items, int S, int Wk, unsigned norm,
+                                                          unsigned minLength, double bs,
                                                           typename Elem<ET>::T *__restrict__ D,
-                                                          typename Elem<ET>::T *__restrict__ Nm,
-                                                          long long rowBegin, long long rowEnd) {
-	__shared__ __attribute__((aligned(16))) uint4 As[KCP * RSP];
-	__shared__ __attribute__((aligned(16))) uint4 Bs[KCP * RSP];
+                                                          typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
+                                                          long long rowEnd, unsigned *__restrict__ cd,
+                                                          unsigned *__restrict__ cn, long long cbase) {
+	__shared__ __attribute__((aligned(16))) uint4 As[2][KCP * RSP];
+	__shared__ __attribute__((aligned(16))) uint4 Bs[2][KCP * RSP];
 	int I, J;
-	tile_ij(t0 + blockIdx.x, I, J);
+	const long long item = t0 + xcd_tile(blockIdx.x, items);
+	tile_ij(item / S, I, J);
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	const int Wl = we - wb;   // a multiple of KCP
 	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-	const uint4 *Ap = P + (size_t) I * TILE * Wp;
-	const uint4 *Bp = P + (size_t) J * TILE * Wp;
+	const uint4 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint4 *Bp = P + (size_t) J * TILE * Wp + wb;
 	uint32_t ad[8][8], an[8][8];
 #pragma unroll
 	for(int a = 0; a < 8; ++a)
@@ -274,32 +284,59 @@ __global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restric
 			ad[a][c] = 0;
 			an[a][c] = 0;
 		}
-	for(int w0 = 0; w0 < Wp; w0 += KCP) {
+	uint4 va[4], vb[4];
 #pragma unroll
-		for(int q = 0; q < 4; ++q) {
-			int e = q * 256 + threadIdx.x;
-			int row = e >> 3, wp = e & 7;
-			As[wp * RSP + row] = Ap[(size_t) row * Wp + w0 + wp];
-			Bs[wp * RSP + row] = Bp[(size_t) row * Wp + w0 + wp];
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		va[q] = Ap[(size_t) row * Wp + wp];
+		vb[q] = Bp[(size_t) row * Wp + wp];
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][wp * RSP + row] = va[q];
+		Bs[0][wp * RSP + row] = vb[q];
+	}
+	__syncthreads();
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KCP, buf ^= 1) {
+		const bool more = w0 + KCP < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = Ap[(size_t) row * Wp + w0 + KCP + wp];
+				vb[q] = Bp[(size_t) row * Wp + w0 + KCP + wp];
+			}
 		}
-		__syncthreads();
+		const uint4 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 1
 		for(int w = 0; w < KCP; ++w) {
 			uint4 a[8], b[8];
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
-				a[2 * q] = As[w * RSP + 2 * ty + 32 * q];
-				a[2 * q + 1] = As[w * RSP + 2 * ty + 32 * q + 1];
-				b[2 * q] = Bs[w * RSP + 2 * tx + 32 * q];
-				b[2 * q + 1] = Bs[w * RSP + 2 * tx + 32 * q + 1];
+				a[2 * q] = Ac[w * RSP + 2 * ty + 32 * q];
+				a[2 * q + 1] = Ac[w * RSP + 2 * ty + 32 * q + 1];
+				b[2 * q] = Bc[w * RSP + 2 * tx + 32 * q];
+				b[2 * q + 1] = Bc[w * RSP + 2 * tx + 32 * q + 1];
 			}
 #pragma unroll
 			for(int x = 0; x < 8; ++x) {
 #pragma unroll
 				for(int y = 0; y < 8; ++y) {
-					uint32_t m = a[x].z & b[y].z;
+					const uint32_t m = a[x].z & b[y].z;
 					ad[x][y] += __popc(xor_or(a[x].x, b[y].x, a[x].y ^ b[y].y) & m);
 					an[x][y] += __popc(m);
 				}
+			}
+		}
+		if(more) {
+			uint4 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[wp * RSP + row] = va[q];
+				Bn[wp * RSP + row] = vb[q];
 			}
 		}
 		__syncthreads();
@@ -312,8 +349,26 @@ __global__ __launch_bounds__(256, 1) void k_snp_tile_pair(const uint4 *__restric
 #pragma unroll
 		for(int c = 0; c < 8; ++c) {
 			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
-			if(j < i) pair_store<ET>(D, Nm, base + j, ad[a][c], an[a][c], norm, minLength, bs);
+			if(j < i) {
+				if(SPLIT) {
+					atomicAdd(&cd[base + j - cbase], ad[a][c]);
+					atomicAdd(&cn[base + j - cbase], an[a][c]);
+				} else {
+					pair_store<ET>(D, Nm, base + j, ad[a][c], an[a][c], norm, minLength, bs);
+				}
+			}
 		}
+	}
+}
+
+// split-K epilogue of pair mode: the A7 store of the summed (dist, n)
+template <int ET>
+__global__ void k_snp_pair_finish(const unsigned *__restrict__ cd, const unsigned *__restrict__ cn, long long f0,
+                                  long long f1, unsigned norm, unsigned minLength, double bs,
+                                  typename Elem<ET>::T *__restrict__ D, typename Elem<ET>::T *__restrict__ Nm) {
+	for(long long f = f0 + (long long) blockIdx.x * blockDim.x + threadIdx.x; f < f1;
+	    f += (long long) gridDim.x * blockDim.x) {
+		pair_store<ET>(D, Nm, f, cd[f - f0], cn[f - f0], norm, minLength, bs);
 	}
 }
 
@@ -480,37 +535,59 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 		}
 		return CCG_OK;
 	}
-	if(a->pair) {
-		for(long long t = t_begin; t < t_end; t += batch) {
-			long long cnt = t_end - t < batch ? t_end - t : batch;
-			k_snp_tile_pair<ET><<<(unsigned) cnt, 256, 0, ctx->stream>>>(
-			    (const uint4 *) planes, Wp, a->n, t, a->norm, a->minLength, a->byteScale, (T *) D, (T *) N, rb, re);
-			CCG_CHECK(hipGetLastError());
-		}
-		return CCG_OK;
-	}
 	// split-K: enough (tile, slice) items that the tail round of resident
 	// blocks (2 per CU) is small; each slice keeps >= 4 chunks
 	hipDeviceProp_t prop;
 	CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
 	const long long slots = 2LL * prop.multiProcessorCount;
 	const long long tiles = t_end - t_begin;
-	const int chunks = Wp / KC;
+	const int kc = a->pair ? KCP : KC;
+	const int chunks = Wp / kc;
 	int S = 1;
 	if(tiles < 16 * slots) {
 		S = (int) cdivll(16 * slots, tiles);
 		if(S > chunks / 4) S = chunks / 4;
 		if(S < 1) S = 1;
 	}
-	const int Wk = (int) cdivll(chunks, S) * KC;
+	const int Wk = (int) cdivll(chunks, S) * kc;
 	S = (int) cdivll(Wp, Wk);
-	unsigned *cnt = NULL;
 	const long long f0 = tri(rb), f1 = tri(re);
+	const long long i_begin = t_begin * S, i_end = t_end * S;
+	if(a->pair) {
+		unsigned *cd = NULL, *cn = NULL;
+		if(S > 1) {
+			CCG_CHECK(hipMalloc(&cd, (size_t) (f1 - f0) * 2 * sizeof(unsigned)));
+			cn = cd + (f1 - f0);
+			CCG_CHECK(hipMemsetAsync(cd, 0, (size_t) (f1 - f0) * 2 * sizeof(unsigned), ctx->stream));
+		}
+		for(long long t = i_begin; t < i_end; t += batch) {
+			long long items = i_end - t < batch ? i_end - t : batch;
+			if(S > 1) {
+				k_snp_tile_pair<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, a->n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) N, rb, re, cd, cn, f0);
+			} else {
+				k_snp_tile_pair<ET, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, a->n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) N, rb, re, cd, cn, f0);
+			}
+			CCG_CHECK(hipGetLastError());
+		}
+		if(S > 1) {
+			long long g = cdivll(f1 - f0, 256);
+			k_snp_pair_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(
+			    cd, cn, f0, f1, a->norm, a->minLength, a->byteScale, (T *) D, (T *) N);
+			CCG_CHECK(hipGetLastError());
+			CCG_CHECK(hipStreamSynchronize(ctx->stream));
+			CCG_CHECK(hipFree(cd));
+		}
+		return CCG_OK;
+	}
+	unsigned *cnt = NULL;
 	if(S > 1) {
 		CCG_CHECK(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)));
 		CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
 	}
-	const long long i_begin = t_begin * S, i_end = t_end * S;
 	for(long long t = i_begin; t < i_end; t += batch) {
 		long long items = i_end - t < batch ? i_end - t : batch;
 		if(S > 1) {

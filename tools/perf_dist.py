@@ -1,5 +1,5 @@
 """dist throughput on device-resident random MSAs (development aid):
-    python tools/perf_dist.py [N] [L]"""
+    python tools/perf_dist.py [N] [L] [pair]"""
 import os
 import sys
 
@@ -12,4 +12,4 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 L = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 torch.cuda.set_device(0)
 dev = cg.Device(0)
-print(dist_extra(dev, torch, n=n, L=L), flush=True)
+print(dist_extra(dev, torch, n=n, L=L, pair=len(sys.argv) > 3 and sys.argv[3] == "pair"), flush=True)
