@@ -93,6 +93,26 @@ def pmc_traffic(kernel):
         return None, None
 
 
+KERNEL_STATS = os.path.join(ROOT, "profiles", "r01_kernel_stats.csv")
+KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_find", "update": "k_dnj_join",
+        "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop"}
+
+
+def rocprof_mean_us(kernel):
+    """Mean kernel duration of `kernel` in the committed rocprofv3
+    --kernel-trace --stats summary (begin to end of the dispatch)."""
+    import csv
+    sym = KSYM.get(kernel)
+    try:
+        with open(KERNEL_STATS) as f:
+            for r in csv.DictReader(f):
+                if sym and r["Name"].replace("void ", "").startswith(sym + "<"):
+                    return round(float(r["AverageNs"]) / 1e3, 3)
+    except (OSError, KeyError, ValueError):
+        pass
+    return None
+
+
 def roofline(stats, n, s):
     """Dominant kernel (largest total device time) of a profiled run."""
     per = {}
@@ -113,6 +133,17 @@ def roofline(stats, n, s):
            "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares}
     if src:
         out["traffic_source"] = src
+    rp = rocprof_mean_us(name)
+    if rp:
+        # HIP events on the engine stream are stamped when the previous event
+        # and the kernel complete, so avg_launch_us also holds the dependent
+        # dispatch gap before the kernel (2-4 us here); rocprofv3 times the
+        # dispatch from begin to end.  frac uses the event time (conservative).
+        out["rocprof_mean_us"] = rp
+        out["frac_rocprof_duration"] = round(tot / cnt / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
+        out["timing_note"] = ("avg_launch_us: HIP events around each launch on the engine stream (includes the "
+                              "dispatch gap after the previous kernel); rocprof_mean_us: rocprofv3 --kernel-trace "
+                              "--stats mean of the same kernel (profiles/r01_kernel_stats.csv)")
     return out
 
 
