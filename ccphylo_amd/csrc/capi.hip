@@ -5,6 +5,7 @@
 #include "ccg_internal.h"
 
 int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out);
+int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out);
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
                   double *final_d, int64_t *stats);
 
@@ -84,6 +85,13 @@ int ccg_snp_ltd_dev(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *in
 	CCG_CHECK(hipSetDevice(c->device));
 	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
 	return ccg_snp_dev_impl(c, a, D, N, inc_out);
+}
+
+int ccg_snp_ltd_shard_dev(ccg_ctx *c, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
+	if(!c || !a || !Dloc) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());
+	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out);
 }
 
 int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {

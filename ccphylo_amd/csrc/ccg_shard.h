@@ -7,22 +7,8 @@
 #include <string.h>
 #include "ccg_tree_common.h"
 
-#define SB CCG_SHARD_BAND
+#include "ccg_shard_layout.h"
 static_assert(SB == NJ_RB, "a shard band is one NJ argmin row band");
-
-struct Shard {
-	int rank, world;
-	__host__ __device__ __forceinline__ bool owns(long long r) const { return (int) ((r / SB) % world) == rank; }
-	__host__ __device__ __forceinline__ long long row(long long r) const { return off(r); }
-	// elements before owned row r in the rank's buffer: full owned bands below
-	// r's band (band g holds SB*SB*g + SB*(SB-1)/2 elements), then r's
-	// predecessors in its band
-	__host__ __device__ __forceinline__ long long off(long long r) const {
-		const long long gb = r / SB, t = r - gb * SB, lb = gb / world;
-		return (long long) SB * SB * world * (lb * (lb - 1) / 2) + (long long) SB * SB * rank * lb +
-		       lb * (SB * (SB - 1) / 2) + SB * gb * t + t * (t - 1) / 2;
-	}
-};
 
 struct ShRec {   // one rank's argmin record (q, flat index); zeros in other ranks' slots
 	double q;

@@ -17,7 +17,9 @@
 // This is VALU-integer-bound (no dense contraction, MFMA not used): 128x128
 // pair tiles, 8x8 pairs per thread in registers, KC-word chunks of both row
 // panels staged through LDS.
+#include <vector>
 #include "ccg_internal.h"
+#include "ccg_shard_layout.h"
 
 #define TILE 128
 #define KC 16          // words per LDS chunk (non-pair)
@@ -199,6 +201,115 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P
 					D[base + j] = Elem<ET>::put(v, 0.5, bs);
 				}
 			}
+		}
+	}
+}
+
+// The same tiles for one rank of the row-sharded layout (ccg_shard.h): the A
+// panel gathers the rank's owned rows, so a rank computes only its own rows
+// and writes them where ccg_tree_shard_dev reads them.
+template <int ET>
+__global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restrict__ P, int Wp, int n,
+                                                          const long long *__restrict__ pfx, int npanels, long long t0,
+                                                          long long items, double nFactor, double bs,
+                                                          typename Elem<ET>::T *__restrict__ Dloc, int rank, int world) {
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
+	// tile t of the rank's list: panel I = last with pfx[I] <= t, J = t - pfx[I]
+	const long long t = t0 + xcd_tile(blockIdx.x, items);
+	int lo = 0, hi = npanels - 1;
+	while(lo < hi) {
+		const int mid = (lo + hi + 1) >> 1;
+		if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
+	}
+	const int I = lo, J = (int) (t - pfx[lo]);
+	const Shard sh{rank, world};
+	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+	// A panel: the rank's owned rows I*TILE .. I*TILE+127 in its own order
+	// (band g = rows [SB g, SB g + SB) of rank g % world); rows past n read row 0
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE + l, lb = L / SB, g = lb * world + rank, r = g * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const uint2 *Bp = P + (size_t) J * TILE * Wp;
+	const int Wl = Wp;
+	uint32_t acc[8][8];
+#pragma unroll
+	for(int a = 0; a < 8; ++a)
+#pragma unroll
+		for(int c = 0; c < 8; ++c) acc[a][c] = 0;
+	// this thread's staging slots: rows e>>3, word pairs 2*(e&7), e = q*256 + tid
+	uint4 va[4], vb[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		va[q] = *(const uint4 *) (P + (size_t) arow(row) * Wp + 2 * wp);
+		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+		As[0][(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+		Bs[0][(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+		Bs[0][(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+	}
+	__syncthreads();
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KC, buf ^= 1) {
+		const bool more = w0 + KC < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = *(const uint4 *) (P + (size_t) arow(row) * Wp + w0 + KC + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
+			}
+		}
+		const uint2 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 1
+		for(int w = 0; w < KC; ++w) {
+			uint4 a[4], b[4];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				a[q] = *(const uint4 *) &Ac[w * RS + 2 * ty + 32 * q];
+				b[q] = *(const uint4 *) &Bc[w * RS + 2 * tx + 32 * q];
+			}
+#pragma unroll
+			for(int qa = 0; qa < 4; ++qa) {
+#pragma unroll
+				for(int qb = 0; qb < 4; ++qb) {
+					acc[2 * qa][2 * qb] += __popc(xor_or(a[qa].x, b[qb].x, a[qa].y ^ b[qb].y));
+					acc[2 * qa][2 * qb + 1] += __popc(xor_or(a[qa].x, b[qb].z, a[qa].y ^ b[qb].w));
+					acc[2 * qa + 1][2 * qb] += __popc(xor_or(a[qa].z, b[qb].x, a[qa].w ^ b[qb].y));
+					acc[2 * qa + 1][2 * qb + 1] += __popc(xor_or(a[qa].z, b[qb].z, a[qa].w ^ b[qb].w));
+				}
+			}
+		}
+		if(more) {
+			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+				Bn[(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+			}
+		}
+		__syncthreads();
+	}
+	// epilogue: the rank's row i at Shard::off(i) (fsacmpthrd.c:247-255 values)
+#pragma unroll
+	for(int a = 0; a < 8; ++a) {
+		const int l = 2 * ty + 32 * (a >> 1) + (a & 1);
+		const long long L = (long long) I * TILE + l, lb = L / SB, i = (lb * world + rank) * SB + (L - lb * SB);
+		if(i >= n) continue;
+		const long long base = sh.off(i);
+#pragma unroll
+		for(int c = 0; c < 8; ++c) {
+			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
+			if(j < i) Dloc[base + j] = Elem<ET>::put(nFactor * (double) acc[a][c], 0.5, bs);
 		}
 	}
 }
@@ -612,7 +723,63 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 	return CCG_OK;
 }
 
+// the rank's owned rows of the band layout, in its own order: panels of TILE
+// owned rows, each against the column tiles below its last row
+template <int ET>
+static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D,
+                           int rank, int world) {
+	typedef typename Elem<ET>::T T;
+	const long long n = a->n;
+	auto row_of = [&](long long L) {
+		const long long lb = L / SB;
+		return (lb * world + rank) * SB + (L - lb * SB);
+	};
+	long long nloc = 0;   // owned rows below n
+	const long long nb = (n + SB - 1) / SB;
+	if(rank < nb) {
+		const long long owned = (nb - 1 - rank) / world + 1, last = (owned - 1) * world + rank;
+		nloc = (owned - 1) * SB + (n - last * SB < SB ? n - last * SB : SB);
+	}
+	// tiles per panel (column tiles with a cell j < i), prefix-summed so that a
+	// launch spans many panels and fills the chip
+	const int npanels = (int) cdivll(nloc, TILE);
+	if(npanels == 0) return CCG_OK;
+	std::vector<long long> pfx(npanels + 1, 0);
+	for(long long I = 0; I < npanels; ++I) {
+		const long long Lmax = (I + 1) * TILE - 1 < nloc - 1 ? (I + 1) * TILE - 1 : nloc - 1;
+		pfx[I + 1] = pfx[I] + cdivll(row_of(Lmax), TILE);
+	}
+	long long *d_pfx = NULL;
+	CCG_CHECK(hipMalloc(&d_pfx, (size_t) (npanels + 1) * sizeof(long long)));
+	CCG_CHECK(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
+	                         ctx->stream));
+	const long long total = pfx[npanels], batch = 1 << 16;
+	for(long long t = 0; t < total; t += batch) {
+		const long long items = total - t < batch ? total - t : batch;
+		k_snp_tile_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
+		                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
+		                                                             rank, world);
+		CCG_CHECK(hipGetLastError());
+	}
+	CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	CCG_CHECK(hipFree(d_pfx));
+	return CCG_OK;
+}
+
+static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world);
+
 int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
+	return snp_run(ctx, a, D, N, inc_out, 0, 0);
+}
+
+int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
+	if(!a || world < 1 || rank < 0 || rank >= world) return CCG_EINVAL;
+	if(a->pair) return CCG_EUNSUP;
+	if(a->row_begin || a->row_end) return CCG_EINVAL;
+	return snp_run(ctx, a, Dloc, NULL, inc_out, rank, world);
+}
+
+static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world) {
 	if(!a || a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if(a->n < 2) {
@@ -660,7 +827,14 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 		return CCG_EINVAL;
 	}
 	int rc = CCG_OK;
-	if(re > rb) {
+	if(world > 0) {
+		switch(a->etype) {
+			case 8: rc = snp_launch_band<8>(ctx, a, planes, Wp, nFactor, D, rank, world); break;
+			case 4: rc = snp_launch_band<4>(ctx, a, planes, Wp, nFactor, D, rank, world); break;
+			case 2: rc = snp_launch_band<2>(ctx, a, planes, Wp, nFactor, D, rank, world); break;
+			default: rc = snp_launch_band<1>(ctx, a, planes, Wp, nFactor, D, rank, world); break;
+		}
+	} else if(re > rb) {
 		switch(a->etype) {
 			case 8: rc = snp_launch<8>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
 			case 4: rc = snp_launch<4>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;

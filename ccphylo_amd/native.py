@@ -104,7 +104,7 @@ ENGINE_SYMBOLS = [
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
-    "ccg_kma_ltd", "ccg_kma_ltd_dev",
+    "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -409,6 +409,17 @@ class Device:
         inc = C.c_int(0)
         self._check(self.lib.ccg_snp_ltd_dev(self.h, C.byref(a), C.c_void_p(D_ptr),
                                              C.c_void_p(N_ptr) if N_ptr else None, C.byref(inc)), "ccg_snp_ltd_dev")
+        return inc.value
+
+
+    def snp_ltd_shard_dev(self, seqs_ptr, incs_ptr, n, length, stride, Dloc_ptr, rank, world, norm=0, etype=8,
+                          byte_scale=1.0):
+        """ccg_snp_ltd_shard_dev: the rank's rows of the band layout, straight
+        into its shard buffer (device pointers).  Returns getNpos(mask)."""
+        a = SnpArgs(n, length, stride, seqs_ptr, incs_ptr, 0, norm, 1, 0, etype, byte_scale, 0, 0)
+        inc = C.c_int(0)
+        self._check(self.lib.ccg_snp_ltd_shard_dev(self.h, C.byref(a), rank, world, C.c_void_p(Dloc_ptr),
+                                                   C.byref(inc)), "ccg_snp_ltd_shard_dev")
         return inc.value
 
 

@@ -192,3 +192,69 @@ def test_shard_hnj_unsupported(dev):
     D = np.arange(10 * 9 // 2, dtype=np.float64)
     with pytest.raises(cg.CcgError, match="not supported"):
         dev.tree_shard(D, 10, None, method=cg.CCG_TREE_HNJ)
+
+
+def _rand_msa(n, L, seed):
+    rng = np.random.default_rng(seed)
+    W = L // 32 + 1
+    base = rng.integers(0, 2 ** 63, size=W, dtype=np.uint64)
+    seqs = np.tile(base, (n, 1))
+    flip = rng.random((n, W)) < 0.3          # related taxa: distances spread, with ties
+    seqs[flip] = rng.integers(0, 2 ** 63, size=int(flip.sum()), dtype=np.uint64)
+    nw = (L + 31) // 32
+    inc = np.zeros(W, np.uint32)
+    inc[:nw] = 0xFFFFFFFF
+    inc[3] = 0xF0F0F0F0
+    if L % 32:
+        inc[nw - 1] = (0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF
+    return seqs, inc, W
+
+
+@pytest.mark.parametrize("n,L,et,norm", [(300, 4000, 8, 0), (1000, 3000, 4, 0), (517, 2049, 2, 100), (129, 1000, 1, 0),
+                                         (2300, 1500, 8, 1000)])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_dist_shard_layout(dev, n, L, et, norm, world):
+    """ccg_snp_ltd_shard_dev writes each rank's rows exactly where
+    ccg_tree_shard_dev reads them: equal to the band extract of the full LT
+    (itself bit-exact vs the oracle elsewhere)."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    seqs, inc, W = _rand_msa(n, L, n + world)
+    dt = cg.ETYPES[et]
+    full, _, _ = dev.snp_ltd(seqs, inc, n, L, norm=norm, etype=et, byte_scale=2.0)
+    ps, pi = dev.malloc(seqs.nbytes), dev.malloc(inc.nbytes)
+    dev.h2d(ps, seqs)
+    dev.h2d(pi, inc)
+    try:
+        for rank in range(world):
+            m = nt.shard_elems(n, rank, world)
+            pd = dev.malloc(max(m, 1) * et)
+            dev.snp_ltd_shard_dev(ps, pi, n, L, W, pd, rank, world, norm=norm, etype=et, byte_scale=2.0)
+            got = np.empty(m, dtype=dt)
+            if m:
+                dev.d2h(got, pd)
+            dev.free(pd)
+            assert (got == nt.shard_extract(full, n, rank, world)).all()
+    finally:
+        dev.free(ps)
+        dev.free(pi)
+
+
+def test_dist_shard_to_tree_in_place(dev):
+    """configs[4] in miniature on one GPU: dist writes the shard, the sharded
+    DNJ consumes it in place; joins equal the single-GPU tree's."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    n, L = 1500, 6000
+    seqs, inc, W = _rand_msa(n, L, 3)
+    full, _, _ = dev.snp_ltd(seqs, inc, n, L)
+    ref = dev.tree(full, n, method=cg.CCG_TREE_DNJ, exact=True)[:3]
+    ps, pi = dev.malloc(seqs.nbytes), dev.malloc(inc.nbytes)
+    dev.h2d(ps, seqs)
+    dev.h2d(pi, inc)
+    pd = dev.malloc(nt.shard_elems(n, 0, 1) * 8)
+    dev.snp_ltd_shard_dev(ps, pi, n, L, W, pd, 0, 1)
+    got = dev.tree_shard_dev(pd, n, None, method=cg.CCG_TREE_DNJ, exact=True)[:3]
+    for p in (ps, pi, pd):
+        dev.free(p)
+    _same(got, ref)
