@@ -345,3 +345,29 @@ def test_hnj_fast_sums(dev):
     assert fn == rfn and (got["i"] == ref["i"]).all() and (got["j"] == ref["j"]).all()
     for f in ("Li", "Lj"):
         np.testing.assert_allclose(got[f], ref[f], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("method", [0, 1, 2], ids=["nj", "dnj", "hnj"])
+@pytest.mark.parametrize("n", [3, 4, 5, 17, 65, 257])
+def test_tree_small_n(dev, method, n):
+    """Smallest matrices (the loop runs n - 2 joins down to the final pair) and
+    sizes around the wave / block edges, every method, vs the oracle."""
+    from oracle import pyoracle
+    for seed in range(3):
+        D = _euclid(n, 100 * n + seed)
+        got, fn, fd, _ = dev.tree(D, n, method=method, exact=True)
+        ref, rfn, rfd = pyoracle.tree(D, n, method=method)
+        assert (fn, fd) == (rfn, rfd) and len(got) == len(ref) and (got == ref).all()
+
+
+@pytest.mark.parametrize("L,proxi", [(1, 1), (31, 3), (32, 40), (33, 1), (64, 63), (65, 2)])
+def test_dist_pair_proxi_short(dev, L, proxi):
+    """Pair mode with -P on alignments shorter than or just past one word (the
+    sentinel lastSNP = len + proxi reaches past the counted words)."""
+    from oracle import pyoracle
+    rng = np.random.default_rng(L * 7 + proxi)
+    n = 9
+    seqs, incs = _related_msa(rng, n, L, 0.3, nrate=0.1)
+    Dg, Ng, _ = dev.snp_ltd(seqs, incs, n, L, pair=True, proxi=proxi, want_n=True)
+    Do, No, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=True, proxi=proxi, want_n=True)
+    assert (Dg == Do).all() and (Ng == No).all()
