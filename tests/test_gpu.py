@@ -371,3 +371,35 @@ def test_dist_pair_proxi_short(dev, L, proxi):
     Dg, Ng, _ = dev.snp_ltd(seqs, incs, n, L, pair=True, proxi=proxi, want_n=True)
     Do, No, _ = pyoracle.snp_ltd(seqs, incs, n, L, pair=True, proxi=proxi, want_n=True)
     assert (Dg == Do).all() and (Ng == No).all()
+
+
+@pytest.mark.parametrize("n,kind", [(2000, "euc"), (1200, "snp")])
+def test_nj_fast_sums(dev, n, kind):
+    """-m nj with fast (fixed-order) row sums: same joins as the reference;
+    lengths within 1e-9 relative (the stated tolerance; on SNP data the
+    averaged distances grow dyadic denominators until sums round, so fast
+    and serial sums differ in the last bits there too).  On clade-structured
+    data with exact Q ties those last bits can reorder tied joins, which is
+    why the CLI default is the exact (serial) sum and --fast_sums is opt-in."""
+    from oracle import pyoracle
+    D = {"euc": lambda: _euclid(n, 7), "snp": lambda: _snp(n, 9), "clade": lambda: _clade_ltd(n, 3)}[kind]()
+    got, fn, fd, _ = dev.tree(D, n, method=0, exact=False)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=0)
+    assert fn == rfn and len(got) == len(ref)
+    assert (got["i"] == ref["i"]).all() and (got["j"] == ref["j"]).all()
+    for f in ("Li", "Lj"):
+        np.testing.assert_allclose(got[f], ref[f], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("et", [4, 2, 1])
+def test_nj_fast_sums_types(dev, et):
+    n = 600
+    D = _snp(n, 21)
+    bs = {4: 1.0, 2: 4.0, 1: 1.0}[et]
+    Dt = D.astype(np.float32) if et == 4 else np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(
+        np.uint8 if et == 1 else np.uint16)
+    fast = dev.tree(Dt, n, etype=et, byte_scale=bs, method=0, exact=False)
+    exact = dev.tree(Dt, n, etype=et, byte_scale=bs, method=0, exact=True)
+    assert fast[1] == exact[1] and (fast[0]["i"] == exact[0]["i"]).all() and (fast[0]["j"] == exact[0]["j"]).all()
+    for f in ("Li", "Lj"):
+        np.testing.assert_allclose(fast[0][f], exact[0][f], rtol=1e-9, atol=1e-12)
