@@ -899,7 +899,7 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 // hclust.c:1671 hclust with initHNJ / minQ / updateHNJ / HNJ_popArrange
 // (-m hnj).  Every step is O(n) per join; per join:
 //   k_hnj_argmin  folds the last join's two row minima (row j from
-//                 k_hnj_update, row i from k_hnj_pop) into Q/P, then per-block
+//                 k_hnj_update, row i from its pop) into Q/P, then per-block
 //                 minQ partials (q, tri(r) + P[r]) over rows 1..n-1: P[r] < r,
 //                 so the larger flat index is the later row, minQ's `<=` rule
 //                 (hclust.c:353);
@@ -907,9 +907,10 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 //                 record and updateD;
 //   k_hnj_update  per row k: updatePrevQ (hclust.c:413, rows 0..n-2, row 0
 //                 reading flat element P[0]) then updateHNJ's column-j rule
-//                 (hclust.c:516-558); the row-j minimum as per-block partials;
-//   k_hnj_pop     HNJ_popArrange (hclust.c:1308): row n-1 into row i (its
-//                 minimum as partials) and column i with `P < pos || q < Q`.
+//                 (hclust.c:516-558), the row-j minimum as per-block partials,
+//                 and HNJ_popArrange (hclust.c:1308) in the same pass: row
+//                 n-1 into row i (its minimum as partials) and column i with
+//                 `P < pos || q < Q`.
 
 // (q, k) `<=` rule over ascending k: smaller q, then the later k
 __device__ __forceinline__ void qk_take(double &bq, int &bk, double q, int k) {
@@ -961,6 +962,10 @@ __global__ __launch_bounds__(TB) void k_hnj_argmin(TreeBufs b, int n) {
 	const int r = (int) blockIdx.x * TB + tid;
 	const int hj = ctl->hj, hi = ctl->hi;
 	const bool own_j = hj >= 0 && hj / TB == (int) blockIdx.x, own_i = hi >= 0 && hi / TB == (int) blockIdx.x;
+	if(blockIdx.x == 0 && tid == 0 && hi >= 0) {   // the pop's sD/N of row i (row n before the join)
+		b.sD[hi] = b.sD[n];
+		b.N[hi] = b.N[n];
+	}
 	if(own_j || own_i) {
 		if(wid < 2 && ((wid == 0 && own_j) || (wid == 1 && own_i))) {
 			double q;
@@ -1010,10 +1015,10 @@ __global__ __launch_bounds__(TB) void k_hnj_argmin(TreeBufs b, int n) {
 }
 
 template <int ET>
-__global__ __launch_bounds__(TB) void k_hnj_update(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+__global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int general) {
-	__shared__ double s_sd, sq[TB / 64];
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, sk[TB / 64];
+	__shared__ double s_sd, sq[TB / 64], sq2[TB / 64];
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, sk[TB / 64], sk2[TB / 64];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 	const int k = (int) blockIdx.x * TB + tid;
@@ -1042,15 +1047,22 @@ __global__ __launch_bounds__(TB) void k_hnj_update(const typename Elem<ET>::T *_
 	const int i = s_i, j = s_j;
 	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
 	const int nj = s_nj;
+	const int nn = n - 1;
+	const bool move = i != nn;
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = nj;
 		ctl->hj = j;
 		ctl->hjb = (int) cdiv(j, TB);
+		// row i of the pop: its minimum is in this kernel's partials; its sD/N
+		// (row nn's) are persisted by the next k_hnj_argmin (sD[i] is still
+		// read here as a partner's sum)
+		ctl->hi = move ? i : -1;
+		ctl->hib = (int) cdiv(i, TB);
 		if(s_serial) ctl->serial_sums++;
 	}
-	double rq = DBL_MAX;
-	int rk = -1;
+	double rq = DBL_MAX, pq = DBL_MAX;
+	int rk = -1, pk2 = -1;
 	if(k < n) {
 		const int Nk = k == j ? nj : b.N[k];
 		const double sDk = k == j ? sdj : b.sD[k];
@@ -1078,16 +1090,40 @@ __global__ __launch_bounds__(TB) void k_hnj_update(const typename Elem<ET>::T *_
 				}
 			}
 		}
-		if(k != j) {
-			b.Q[k] = Qk;
-			b.P[k] = Pk;
-		}
 		if(k < j) {   // row j (hclust.c:497-511)
 			const double d = Elem<ET>::get(D[tri(j) + k], bs);
 			if(0 <= d) {
 				rq = ((nj + Nk - 4) >> 1) * d - sdj - sDk;
 				rk = k;
 			}
+		}
+		// HNJ_popArrange (hclust.c:1308) in the same pass: row nn moves to row
+		// i (cells k < i; its minimum as partials) and column i (rows i < k < nn,
+		// `q <= Q && (P < pos || q < Q)`).  Thread k read its own cells of row /
+		// column i above; row nn is not written by this kernel.
+		if(move && k < nn && k != i) {
+			const typename Elem<ET>::T vm = D[tri(nn) + k];
+			const double d = Elem<ET>::get(vm, bs);
+			const double sDi = b.sD[nn];
+			const int Ni = b.N[nn];
+			const double q = 0 <= d ? d * ((Ni + Nk - 4) >> 1) - sDi - sDk : 0.0;
+			if(k < i) {
+				D[tri(i) + k] = vm;
+				if(0 <= d) {
+					pq = q;
+					pk2 = k;
+				}
+			} else {
+				D[tri(k) + i] = vm;
+				if(0 <= d && q <= Qk && (Pk < i || q < Qk)) {
+					Qk = q;
+					Pk = i;
+				}
+			}
+		}
+		if(k != j) {
+			b.Q[k] = Qk;
+			b.P[k] = Pk;
 		}
 	}
 	if((int) blockIdx.x * TB < j) {
@@ -1097,59 +1133,11 @@ __global__ __launch_bounds__(TB) void k_hnj_update(const typename Elem<ET>::T *_
 			b.bmr[blockIdx.x] = rk;
 		}
 	}
-}
-
-template <int ET>
-__global__ __launch_bounds__(TB) void k_hnj_pop(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n) {
-	__shared__ double sq[TB / 64];
-	__shared__ int sk[TB / 64];
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	const int nn = n - 1, i = ctl->i;
-	const int tid = threadIdx.x;
-	if(i == nn) {
-		if(blockIdx.x == 0 && tid == 0) ctl->hi = -1;
-		return;
-	}
-	const int k = (int) blockIdx.x * TB + tid;
-	const double sDi = b.sD[nn];
-	const int Ni = b.N[nn];
-	double rq = DBL_MAX;
-	int rk = -1;
-	if(k < nn && k != i) {
-		const typename Elem<ET>::T vm = D[tri(nn) + k];
-		const double d = Elem<ET>::get(vm, bs);
-		double q = 0;
-		if(0 <= d) q = d * ((Ni + b.N[k] - 4) >> 1) - sDi - b.sD[k];
-		if(k < i) {
-			D[tri(i) + k] = vm;
-			if(0 <= d) {
-				rq = q;
-				rk = k;
-			}
-		} else {
-			D[tri(k) + i] = vm;
-			if(0 <= d) {
-				const double Qk = b.Q[k];
-				const int Pk = b.P[k];
-				if(q <= Qk && (Pk < i || q < Qk)) {
-					b.Q[k] = q;
-					b.P[k] = i;
-				}
-			}
-		}
-	}
-	if(blockIdx.x == 0 && tid == 0) {
-		b.sD[i] = sDi;
-		b.N[i] = Ni;
-		ctl->hi = i;
-		ctl->hib = (int) cdiv(i, TB);
-	}
-	if((int) blockIdx.x * TB < i) {
-		qk_block_reduce<TB>(rq, rk, sq, sk);
+	if(move && (int) blockIdx.x * TB < i) {
+		qk_block_reduce<TB>(pq, pk2, sq2, sk2);
 		if(tid == 0) {
-			b.cfq[blockIdx.x] = rq;
-			b.cfp[blockIdx.x] = rk;
+			b.cfq[blockIdx.x] = pq;
+			b.cfp[blockIdx.x] = pk2;
 		}
 	}
 }
@@ -1263,11 +1251,10 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_ARGMIN);
 		k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) gn, general, DBL_MAX);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
-		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_UPDATE);
-		k_hnj_pop<ET><<<gn, TB, 0, st>>>(D, bs, b, n);
+		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);   // updateHNJ's Q/P pass + HNJ_popArrange
 		kt.mark(CCG_K_POP);
-		return GEN ? 5 : 4;
+		return GEN ? 4 : 3;
 	}
 	const unsigned g = (unsigned) nj_blocks(n);
 	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
