@@ -190,6 +190,38 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
             "sample": f"full N={n} DNJ tree with the oracle's serial C restatement (reference binary absent)"}
 
 
+def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=16):
+    """The reference's `ccphylo dist` (oracle/_ref, -t 16) on random MSAs of
+    `sizes` taxa x L bp (FASTA text, seeded; the data of the GPU dist leg).  The process wall time is
+    parse + compare; with two sizes, t = a n + b n^2 separates the quadratic
+    (compare) term, whose rate is reported as nt-comparisons/s."""
+    import numpy as np
+    ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
+    if not os.path.exists(ref):
+        return None
+    rng = np.random.default_rng(11)
+    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
+    walls = {}
+    for n in sizes:
+        path = os.path.join(tmpdir, f"cpu_dist_{n}.fsa")
+        with open(path, "wb") as f:   # random MSA, as the GPU dist leg (every word pair differs)
+            for k in range(n):
+                f.write(b">t%d\n" % k + lut[rng.integers(0, 4, L)].tobytes() + b"\n")
+        t0 = time.perf_counter()
+        subprocess.run([ref, "dist", "-i", path, "-t", str(threads), "-o", os.path.join(tmpdir, "d.phy")],
+                       capture_output=True, timeout=900, check=True)
+        walls[n] = time.perf_counter() - t0
+        os.unlink(path)
+    (n1, t1), (n2, t2) = sorted(walls.items())
+    b = (t2 / n2 - t1 / n1) / (n2 - n1)          # t/n = a + b n
+    pairs_s = 0.5 / b if b > 0 else None         # pairs ~ n^2 / 2
+    return {"value": round(pairs_s * L, 1) if pairs_s else None, "unit": "nt-comparisons/s",
+            "taxa_pairs_per_s": round(pairs_s, 1) if pairs_s else None, "cores": threads, "kind": "reference",
+            "sample": f"reference ccphylo 0.8.5 `dist -t {threads}` on random MSAs of {list(sizes)} taxa x {L} "
+                      f"bp (FASTA); walls " + ", ".join(f"n={n}: {w:.2f} s" for n, w in sorted(walls.items())) +
+                      "; the rate is the quadratic (compare) term of t = a n + b n^2"}
+
+
 def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=None, pair=False):
     """SNP distances (non-pair, double) with device-resident packed input.
     With world > 1 the LT rows are sharded over the ranks (SURVEY 8(e):
@@ -521,6 +553,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)
+            if not args.no_extras and isinstance(result.get("extras", {}).get("dist"), dict):
+                try:
+                    result["extras"]["dist"]["cpu_baseline"] = cpu_baseline_dist(td)
+                except Exception as e:  # noqa: BLE001
+                    result["extras"]["dist"]["cpu_baseline"] = {"error": str(e)}
     if not args.no_extras:
         # last, under a watchdog: a collective that never completes (e.g. an
         # RCCL bootstrap failure on one rank) must not cost the whole line
