@@ -245,7 +245,7 @@ static __device__ void fold_update_wave(const TreeBufs &b, int G, bool exact, bo
 // the reference's serial sum of the contributions in increasing k (nj.c:911 /
 // :1002); thread 0 runs the chain while the block stages the next chunk
 static __device__ double serial_sum_block(const TreeBufs &b, int n) {
-	__shared__ double buf[8 * TB];
+	__shared__ __attribute__((aligned(16))) double buf[8 * TB];
 	__shared__ double s_sd;
 	double sd = 0;
 	double nxt[4];
@@ -263,8 +263,21 @@ static __device__ double serial_sum_block(const TreeBufs &b, int n) {
 		}
 		if(threadIdx.x == 0) {
 			const double *cur = buf + p * 4 * TB;
-			int lim = n - c0 < 4 * TB ? n - c0 : 4 * TB;
-			for(int u = 0; u < lim; ++u) sd += cur[u];
+			const int lim = n - c0 < 4 * TB ? n - c0 : 4 * TB;
+			// one dependent add per element; the 16-byte LDS loads of the next
+			// 16 elements are issued ahead of the chain
+			int u = 0;
+			for(; u + 16 <= lim; u += 16) {
+				double2 v[8];
+#pragma unroll
+				for(int q = 0; q < 8; ++q) v[q] = *(const double2 *) (cur + u + 2 * q);
+#pragma unroll
+				for(int q = 0; q < 8; ++q) {
+					sd += v[q].x;
+					sd += v[q].y;
+				}
+			}
+			for(; u < lim; ++u) sd += cur[u];
 		}
 #pragma unroll
 		for(int m = 0; m < 4; ++m) buf[(p ^ 1) * 4 * TB + m * TB + threadIdx.x] = nxt[m];
