@@ -8,6 +8,7 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out);
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
                   double *final_d, int64_t *stats);
+int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel);
 
 static char g_last_error[512];
 
@@ -204,6 +205,12 @@ int ccg_synchronize(ccg_ctx *c) {
 	if(!c) return CCG_EINVAL;
 	CCG_CHECK(hipStreamSynchronize(c->stream));
 	return CCG_OK;
+}
+
+int ccg_selftest_row_sum(ccg_ctx *c, const double *v, int n, double *out, int *parallel) {
+	if(!c || !v || n < 1 || !out || !parallel) return CCG_EINVAL;
+	hipSetDevice(c->device);
+	return ccg_selftest_row_sum_impl(c, v, n, out, parallel);
 }
 
 }   // extern "C"

@@ -128,6 +128,48 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 }
 
 
+// ------------------------------------------------------------------ exact row sum of j
+// Exact mode (the default): the reference's serial sum of the new row of j
+// (nj.c:911 / :1002), once per join by one 1024-thread block between updateD
+// and its consumers (k_dnj_requeue, k_nj_pop, k_hnj_update read ctl->xsum):
+// the fixed-order fold when that is provably the serial sum (integer-like
+// data), else the parallel binade-segmented form, else the chain.
+#define XS_NT 512
+#define XS_ET_BIG 16   // LDS tiles of 8192 elements
+template <int UNUSED = 0>
+__global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_need, s_stop;
+	TreeCtl *ctl = b.ctl;
+	if(threadIdx.x < 64) {
+		const int done = ctl->done;
+		double sd = 0;
+		int nj = 0;
+		bool need = false;
+		if(!done) fold_update_wave(b, G, true, false, &sd, &nj, &need);
+		if(threadIdx.x == 0) {
+			s_stop = done;
+			s_sd = sd;
+			s_nj = nj;
+			s_need = need;
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	double r = s_sd;
+	bool chain = false;
+	if(s_need && !exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &r)) {
+		r = serial_sum_t<XS_NT>(b.contrib, n);
+		chain = true;
+	}
+	if(threadIdx.x == 0) {
+		ctl->xsum = r;
+		ctl->xnj = s_nj;
+		ctl->serial_sums += s_need;
+		ctl->chain_sums += chain;
+	}
+}
+
 // ------------------------------------------------------------------ DNJ join
 // Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
 // replay; then limbLength, the join record and updateD with the whole grid.
@@ -517,7 +559,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			double sd;
 			int nj;
 			bool need;
-			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(exact && !general) {   // k_exact_sum ran
+				sd = ctl->xsum;
+				nj = ctl->xnj;
+				need = false;
+			} else {
+				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			}
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
@@ -528,7 +576,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j, Nj = s_nj;
-	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
 	TS(4, 1);
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
@@ -864,7 +912,13 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 			double sd;
 			int nj;
 			bool need;
-			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(exact && !general) {   // k_exact_sum ran
+				sd = ctl->xsum;
+				nj = ctl->xnj;
+				need = false;
+			} else {
+				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			}
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
@@ -875,7 +929,7 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = s_nj;
@@ -1034,7 +1088,13 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 			double sd;
 			int nj;
 			bool need;
-			fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			if(exact && !general) {   // k_exact_sum ran
+				sd = ctl->xsum;
+				nj = ctl->xnj;
+				need = false;
+			} else {
+				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
+			}
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
@@ -1045,7 +1105,7 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
 	const int nj = s_nj;
 	const int nn = n - 1;
 	const bool move = i != nn;
@@ -1224,9 +1284,10 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 // One join's kernels for a matrix of n taxa; returns the launch count.
 template <int ET, bool GEN>
 static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first,
-                             int method, KTimer &kt) {
+                             int method, int exact, KTimer &kt) {
 	const unsigned gn = cdiv(n, TB);
 	const int general = GEN;
+	const int xs = exact && !GEN;   // the exact row sum as its own 1024-thread block
 	if(method == CCG_TREE_DNJ) {
 		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
@@ -1240,31 +1301,34 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_REST);
 		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+		if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 		kt.mark(CCG_K_UPDATE);
 		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
-		return (GEN ? 6 : 5) + prefold;
+		return (GEN ? 6 : 5) + prefold + xs;
 	}
 	if(method == CCG_TREE_HNJ) {
 		k_hnj_argmin<><<<gn, TB, 0, st>>>(b, n);
 		kt.mark(CCG_K_ARGMIN);
 		k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) gn, general, DBL_MAX);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+		if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 		kt.mark(CCG_K_UPDATE);
 		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);   // updateHNJ's Q/P pass + HNJ_popArrange
 		kt.mark(CCG_K_POP);
-		return GEN ? 4 : 3;
+		return (GEN ? 4 : 3) + xs;
 	}
 	const unsigned g = (unsigned) nj_blocks(n);
 	k_nj_argmin<ET, GEN><<<g, TB, 0, st>>>(D, bs, b, n);
 	kt.mark(CCG_K_ARGMIN);
 	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general, 1.0);
 	if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
+	if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 	kt.mark(CCG_K_UPDATE);
 	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general);
 	kt.mark(CCG_K_POP);
-	return GEN ? 4 : 3;
+	return (GEN ? 4 : 3) + xs;
 }
 
 template <int ET>
@@ -1321,8 +1385,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	bool stopped = false;
 	const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 	while(n > stop_n) {
-		launches += general ? enqueue_iteration<ET, true>(st, D, bs, b, n, n == n0, a->method, kt)
-		                    : enqueue_iteration<ET, false>(st, D, bs, b, n, n == n0, a->method, kt);
+		launches += general ? enqueue_iteration<ET, true>(st, D, bs, b, n, n == n0, a->method, a->exact, kt)
+		                    : enqueue_iteration<ET, false>(st, D, bs, b, n, n == n0, a->method, a->exact, kt);
 		CCG_CHECK(hipGetLastError());
 		--n;
 		if(++since_check == 1024) {
@@ -1402,10 +1466,73 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			}
 			stats[4 + 2 * CCG_NKSTAT] = h.cells_top;
 			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest;
+			stats[6 + 2 * CCG_NKSTAT] = h.serial_sums;
+			stats[7 + 2 * CCG_NKSTAT] = h.chain_sums;
 		}
 	}
 	CCG_CHECK(hipStreamSynchronize(st));
 	CCG_CHECK(hipFree(w.mem));
+	return CCG_OK;
+}
+
+// ------------------------------------------------------------------ self-test of the exact row sum
+template <int NT>
+__global__ __launch_bounds__(NT) void k_selftest_row_sum(TreeBufs b, int n, double *out, int *par,
+                                                        unsigned long long *stamps) {
+	double s;
+	if(stamps && threadIdx.x == 0) stamps[15] = __builtin_amdgcn_s_memrealtime();
+	const bool ok = NT == TB ? exact_sum_t<TB, 16>(b.contrib, n, &s, stamps)
+	                         : exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &s, stamps);
+	if(!ok) s = serial_sum_t<NT>(b.contrib, n);
+	if(threadIdx.x == 0) {
+		out[0] = s;
+		par[0] = ok;
+	}
+}
+
+int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel) {
+	hipStream_t st = ctx->stream;
+	char *m;
+	CCG_CHECK(hipMalloc((void **) &m, (size_t) (n + 1) * 8 + 64 + 64 * 8));
+	TreeBufs b;
+	memset(&b, 0, sizeof(b));
+	b.contrib = (double *) m;
+	double *dout = (double *) (m + (size_t) (n + 1) * 8);
+	int *dpar = (int *) (dout + 1);
+	unsigned long long *dst = (unsigned long long *) (m + (size_t) (n + 1) * 8 + 64);
+	CCG_CHECK(hipMemcpyAsync(b.contrib, c, (size_t) n * 8, hipMemcpyHostToDevice, st));
+	const bool small = getenv("CCG_SELFTEST_TB256") != nullptr;   // the per-block form of the sharded engines
+	auto launch = [&](unsigned long long *stp) {
+		if(small) k_selftest_row_sum<TB><<<1, TB, 0, st>>>(b, n, dout, dpar, stp);
+		else k_selftest_row_sum<XS_NT><<<1, XS_NT, 0, st>>>(b, n, dout, dpar, stp);
+	};
+	launch(nullptr);
+	CCG_CHECK(hipGetLastError());
+	if(const char *e = getenv("CCG_SELFTEST_REPS")) {   // development timing
+		const int reps = atoi(e);
+		CCG_CHECK(hipEventRecord(ctx->ev0, st));
+		for(int r = 0; r < reps; ++r) launch(nullptr);
+		CCG_CHECK(hipEventRecord(ctx->ev1, st));
+		CCG_CHECK(hipEventSynchronize(ctx->ev1));
+		float ms = 0;
+		CCG_CHECK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+		fprintf(stderr, "selftest_row_sum n=%d: %.2f us per launch\n", n, 1000.0 * ms / (reps > 0 ? reps : 1));
+		unsigned long long hs[64] = {0};
+		CCG_CHECK(hipMemsetAsync(dst, 0, 64 * 8, st));
+		launch(dst);
+		CCG_CHECK(hipMemcpyAsync(hs, dst, 64 * 8, hipMemcpyDeviceToHost, st));
+		CCG_CHECK(hipStreamSynchronize(st));
+		for(int w = 0; w < 4; ++w) {
+			fprintf(stderr, "  wave %d phases (us from entry):", w);
+			for(int i = 0; i < 15; ++i)
+				fprintf(stderr, " %d:%.2f", i, hs[16 * w + i] ? (double) (hs[16 * w + i] - hs[15]) / 100.0 : -1.0);
+			fprintf(stderr, "\n");
+		}
+	}
+	CCG_CHECK(hipMemcpyAsync(out, dout, 8, hipMemcpyDeviceToHost, st));
+	CCG_CHECK(hipMemcpyAsync(parallel, dpar, 4, hipMemcpyDeviceToHost, st));
+	CCG_CHECK(hipStreamSynchronize(st));
+	CCG_CHECK(hipFree(m));
 	return CCG_OK;
 }
 

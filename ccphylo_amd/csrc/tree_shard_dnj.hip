@@ -323,7 +323,7 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j, Nj = s_nj;
-	const double sdj = s_serial ? serial_sum_block(b, n) : s_sd;
+	const double sdj = s_serial ? exact_row_sum(b, n) : s_sd;
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = Nj;

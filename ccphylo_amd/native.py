@@ -104,7 +104,7 @@ ENGINE_SYMBOLS = [
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
-    "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev",
+    "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_selftest_row_sum",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -174,6 +174,8 @@ def engine_lib():
         lib.ccg_tree_shard_dev.argtypes = lib.ccg_tree_shard.argtypes
         lib.ccg_kma_ltd.argtypes = [C.c_void_p, C.POINTER(KmaArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
         lib.ccg_kma_ltd_dev.argtypes = lib.ccg_kma_ltd.argtypes
+        lib.ccg_selftest_row_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_double),
+                                             C.POINTER(C.c_int)]
         _engine = lib
     return _engine
 
@@ -316,7 +318,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (6 + 2 * NKSTAT))()
+        st = (C.c_int64 * (8 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         rc = fn_(self.h, C.byref(a), C.c_void_p(dptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd), st)
         self._check(rc, "ccg_tree")
@@ -343,7 +345,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (6 + 2 * NKSTAT))()
+        st = (C.c_int64 * (8 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         cp = C.byref(coll.c) if coll is not None else None
         rc = fn_(self.h, C.byref(a), cp, C.c_void_p(ptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd),
@@ -381,6 +383,16 @@ class Device:
                                              C.c_void_p(N_ptr) if N_ptr else None, C.byref(fatal)),
                     "ccg_kma_ltd_dev")
         return fatal.value
+
+    def selftest_row_sum(self, c):
+        """The engine's exact-mode row sum of c (ccg_selftest_row_sum): returns
+        (serial sum, True when the parallel binade-segmented form produced it)."""
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        out = C.c_double(0)
+        par = C.c_int(0)
+        self._check(self.lib.ccg_selftest_row_sum(self.h, c.ctypes.data, len(c), C.byref(out), C.byref(par)),
+                    "ccg_selftest_row_sum")
+        return out.value, bool(par.value)
 
     # ---- device memory (ccg_malloc & co.) for HBM-resident inputs
     def malloc(self, nbytes):

@@ -159,11 +159,13 @@ typedef struct {
 	                          prefix of a large tree); 0: run to n = 2 */
 } ccg_tree_args;
 
-/* stats layout (ccg_tree / ccg_tree_dev, 6 + 2*CCG_NKSTAT entries when
+/* stats layout (ccg_tree / ccg_tree_dev, 8 + 2*CCG_NKSTAT entries when
  * profile = 1, else 4): [0] rows rescanned, [1] cells rescanned, [2] kernel
  * launches, [3] device time (us); then for kernel class c: [4+2c] launches,
  * [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT] cells rescanned by
- * CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST.  Classes: */
+ * CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST; [6+2*CCG_NKSTAT] exact row
+ * sums that needed the serial order, [7+2*CCG_NKSTAT] of those computed by
+ * the serial chain (the parallel form declined).  Classes: */
 #define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
 #define CCG_K_TOP      1   /* DNJ k_dnj_select: requeue fold, top rows S, their rescans */
 #define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the rows below S with Q < U */
@@ -260,6 +262,15 @@ int ccg_free(ccg_ctx *ctx, void *ptr);
 int ccg_memcpy_h2d(ccg_ctx *ctx, void *dst, const void *src, size_t bytes);
 int ccg_memcpy_d2h(ccg_ctx *ctx, void *dst, const void *src, size_t bytes);
 int ccg_synchronize(ccg_ctx *ctx);
+
+/* ------------------------------------------------------------------ */
+/* self-test hook (tests/test_gpu_exact_sum.py)                        */
+/* ------------------------------------------------------------------ */
+/* The serial sum s = ((0 + c[0]) + c[1]) + ... of n doubles c[k] >= 0 as the
+ * tree engine's exact mode computes the new row sum of j (nj.c:911 / :1002):
+ * the parallel binade-segmented form, or the chain where it declines.
+ * *parallel = 1 when the parallel form produced it. */
+int ccg_selftest_row_sum(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel);
 
 #ifdef __cplusplus
 }

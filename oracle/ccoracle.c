@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include "ccoracle.h"
 
 /* ------------------------------------------------------------------ */
@@ -383,6 +384,77 @@ static void init_sums(const Ltd *D, int n, double *sD, int32_t *N) {
 	}
 }
 
+/* the same sums with `threads` pthreads: thread t owns a range of k and
+ * keeps each sD[k]'s order (its row part d(k, 0..k-1), then its column part
+ * d(k+1, k), d(k+2, k), ...), so the result equals init_sums bit for bit.
+ * Test infrastructure for large n (tests/test_gpu_large.py). */
+typedef struct {
+	const Ltd *D;
+	int n, k0, k1;
+	double *sD, *Q;
+	int32_t *N, *P;
+	int stride;   /* init_hnj_par: rows k0, k0 + stride, ... */
+} ParArg;
+
+static void *init_sums_worker(void *p) {
+	ParArg *a = p;
+	const Ltd *D = a->D;
+	for(int64_t k = a->k0; k < a->k1; ++k) {
+		double s = 0;
+		int32_t c = 1;
+		int64_t base = tri(k);
+		for(int64_t m = 0; m < k; ++m) {
+			double d = ld(D, base + m);
+			if(0 <= d) {
+				s += d;
+				++c;
+			}
+		}
+		a->sD[k] = s;
+		a->N[k] = c;
+	}
+	for(int64_t i = a->k0 + 1; i < a->n; ++i) {
+		int64_t base = tri(i), lim = i < a->k1 ? i : a->k1;
+		for(int64_t k = a->k0; k < lim; ++k) {
+			double d = ld(D, base + k);
+			if(0 <= d) {
+				a->sD[k] += d;
+				++a->N[k];
+			}
+		}
+	}
+	return NULL;
+}
+
+static void *init_hnj_worker(void *p);
+
+static void run_par(void *(*fn)(void *), ParArg *proto, int threads, int by_rows) {
+	pthread_t th[256];
+	ParArg args[256];
+	if(threads > 256) threads = 256;
+	for(int t = 0; t < threads; ++t) {
+		args[t] = *proto;
+		if(by_rows) {
+			args[t].k0 = t;
+			args[t].stride = threads;
+		} else {
+			args[t].k0 = (int) ((int64_t) proto->n * t / threads);
+			args[t].k1 = (int) ((int64_t) proto->n * (t + 1) / threads);
+		}
+		pthread_create(&th[t], NULL, fn, &args[t]);
+	}
+	for(int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+}
+
+static void init_sums_par(const Ltd *D, int n, double *sD, int32_t *N, int threads) {
+	if(threads <= 1 || n < 1024) {
+		init_sums(D, n, sD, N);
+		return;
+	}
+	ParArg a = {D, n, 0, 0, sD, NULL, N, NULL, 1};
+	run_par(init_sums_worker, &a, threads, 0);
+}
+
 void orc_init_sums(int n, int etype, double byteScale, const void *D, double *sD, int32_t *N) {
 	Ltd L = {etype, byteScale, (void *) D};
 	init_sums(&L, n, sD, N);
@@ -605,6 +677,41 @@ static void init_hnj(const Ltd *D, int n, const double *sD, const int32_t *N, do
 	}
 }
 
+/* init_hnj over interleaved rows with `threads` pthreads (rows are independent) */
+static void init_hnj_rows(const Ltd *D, int64_t i, const double *sD, const int32_t *N, double *Q, int32_t *P) {
+	double min = DBL_MAX, minD = DBL_MAX;
+	int pos = 0;
+	int64_t base = tri(i);
+	for(int64_t j = 0; j < i; ++j) {
+		double d = ld(D, base + j);
+		if(0 <= d) {
+			double q = qval(N[i], N[j], d, sD[i], sD[j]);
+			if(q <= min && (q < min || d <= minD)) {
+				min = q;
+				minD = d;
+				pos = j;
+			}
+		}
+	}
+	Q[i] = min;
+	P[i] = pos;
+}
+
+static void *init_hnj_worker(void *p) {
+	ParArg *a = p;
+	for(int64_t i = a->k0; i < a->n; i += a->stride) init_hnj_rows(a->D, i, a->sD, a->N, a->Q, a->P);
+	return NULL;
+}
+
+static void init_hnj_par(const Ltd *D, int n, const double *sD, const int32_t *N, double *Q, int32_t *P, int threads) {
+	if(threads <= 1 || n < 1024) {
+		init_hnj(D, n, sD, N, Q, P);
+		return;
+	}
+	ParArg a = {D, n, 0, n, (double *) sD, Q, (int32_t *) N, P, 1};
+	run_par(init_hnj_worker, &a, threads, 1);
+}
+
 /* fresh min over LT row i with `<=` (dnj.c:99-112) */
 static double row_min(const Ltd *D, int i, const double *sD, const int32_t *N, int *pj, int64_t *cells) {
 	double best = DBL_MAX;
@@ -817,6 +924,13 @@ static void hnj_pop_arrange(Ltd *D, int *n, double *sD, int32_t *N, double *Q, i
 
 int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int flags,
              orc_join *joins, int *final_n, double *final_d, int64_t *stats) {
+	return orc_tree_ex(n, etype, byteScale, Dbase, method, flags, joins, final_n, final_d, stats, 0, 1);
+}
+
+int orc_tree_ex(int n, int etype, double byteScale, void *Dbase, int method, int flags,
+                orc_join *joins, int *final_n, double *final_d, int64_t *stats, int max_joins, int threads) {
+	/* max_joins > 0: stop after that many joins (a prefix of the same run) */
+	const int lim = max_joins > 0 ? max_joins : INT_MAX;
 	Ltd D = {etype, byteScale, Dbase};
 	int neg = (flags & 2) != 0;
 	int nj = 0;
@@ -827,11 +941,11 @@ int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int fl
 	if(stats) {
 		stats[0] = stats[1] = 0;
 	}
-	init_sums(&D, n, sD, N);
+	init_sums_par(&D, n, sD, N, threads);
 	if(method == 0) {
 		/* nj.c:1560-1610 */
 		uint64_t pair;
-		while(n != 2 && (pair = init_q(&D, n, sD, N))) {
+		while(n != 2 && nj < lim && (pair = init_q(&D, n, sD, N))) {
 			int j = (int) (pair & 0xFFFFFFFFu), i = (int) (pair >> 32);
 			double Li, Lj;
 			limb_length(&Li, &Lj, i, j, sD, N, ld(&D, tri(i) + j), neg);
@@ -844,8 +958,8 @@ int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int fl
 		}
 	} else if(method == 2) {
 		/* hclust.c:1671-1718 hclust with initHNJ / minQ / updateHNJ / HNJ_popArrange */
-		init_hnj(&D, n, sD, N, Q, P);
-		while(n != 2) {
+		init_hnj_par(&D, n, sD, N, Q, P, threads);
+		while(n != 2 && nj < lim) {
 			int i = min_q_row(Q, n);
 			int j = P[i];
 			if(i == 0 && j == 0) {
@@ -860,10 +974,10 @@ int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int fl
 		}
 	} else {
 		/* dnj.c:985-1052 */
-		init_hnj(&D, n, sD, N, Q, P);
+		init_hnj_par(&D, n, sD, N, Q, P, threads);
 		int j = min_q_row(Q, n);
 		uint64_t pos;
-		while(n != 2 && (pos = min_q_pair(&D, n, sD, N, Q, P, j, stats))) {
+		while(n != 2 && nj < lim && (pos = min_q_pair(&D, n, sD, N, Q, P, j, stats))) {
 			j = (int) (pos & 0xFFFFFFFFu);
 			int i = (int) (pos >> 32);
 			double Li, Lj;

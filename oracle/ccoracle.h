@@ -56,6 +56,12 @@ int orc_snp_ltd(int n, int len, const uint64_t *seqs, const uint32_t *incs, int 
 int orc_tree(int n, int etype, double byteScale, void *D, int method, int flags,
              orc_join *joins, int *final_n, double *final_d, int64_t *stats);
 
+/* orc_tree with a join limit (max_joins > 0: the first max_joins joins of the
+ * same run) and `threads` pthreads for the O(n^2) initSummaD / initHNJ passes
+ * (same per-row operation order, so bit-identical to threads = 1). */
+int orc_tree_ex(int n, int etype, double byteScale, void *D, int method, int flags,
+                orc_join *joins, int *final_n, double *final_d, int64_t *stats, int max_joins, int threads);
+
 /* B1/B2: distances between KMA count matrices (*.mat[.gz]) of template
  * `tmpl` (ltdmatrixthrd.c:376 ltdMatrixThrd, matcmp.c:448 cmpMats, metrics
  * matcmp.c:63-446; kma_oracle.c).  D/N receive the packed LT of the *n_out

@@ -32,6 +32,8 @@ def lib():
         L = C.CDLL(LIB)
         L.orc_tree.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_void_p]
+        L.orc_tree_ex.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                  C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_void_p, C.c_int, C.c_int]
         L.orc_snp_ltd.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_uint, C.c_double,
                                   C.c_uint, C.c_int, C.c_double, C.c_void_p, C.c_void_p]
         L.orc_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
@@ -51,16 +53,24 @@ def lib():
     return _lib
 
 
-def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False):
+def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False, max_joins=0, threads=1, copy=True):
     """Serial NJ (method 0) / DNJ (method 1) / HNJ (method 2) exactly as the reference.
+    max_joins > 0 stops after that many joins (a prefix of the same run);
+    threads > 1 runs the O(n^2) initSummaD / initHNJ passes on pthreads (same
+    per-row order, bit-identical).  copy=False destroys D in place (it must
+    then be a writable contiguous array of the element type: large n).
     Returns (joins, final_n, final_d[, stats])."""
-    D = np.array(D, dtype=ETYPES[etype], copy=True)
-    joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
+    if copy:
+        D = np.array(D, dtype=ETYPES[etype], copy=True)
+    else:
+        assert D.dtype == ETYPES[etype] and D.flags.c_contiguous and D.flags.writeable
+    cap = min(n, max_joins) if max_joins > 0 else n
+    joins = np.zeros(max(cap, 1), dtype=JOIN_DTYPE)
     fn = C.c_int(0)
     fd = C.c_double(0)
     st = np.zeros(2, dtype=np.int64)
-    nj = lib().orc_tree(n, etype, byte_scale, D.ctypes.data, method, flags, joins.ctypes.data, C.byref(fn),
-                        C.byref(fd), st.ctypes.data)
+    nj = lib().orc_tree_ex(n, etype, byte_scale, D.ctypes.data, method, flags, joins.ctypes.data, C.byref(fn),
+                           C.byref(fd), st.ctypes.data, max_joins, threads)
     res = (joins[:nj], fn.value, fd.value)
     return res + (st,) if stats else res
 

@@ -1,0 +1,181 @@
+"""GPU parity at the BASELINE.json sizes (configs[1]-[3]), against the oracle's
+serial restatement (oracle/ccoracle.c, pinned by the reference's golden
+vectors; test infrastructure only).
+
+- configs[1], N = 10,000 (the bench matrix: Euclidean U[0,1)^8, seed 1,
+  %.9f-quantized): exact DNJ and HNJ, whole trees, joins and branch lengths
+  bit-identical; NJ (O(n^3) in the oracle) as a join prefix.  Also an
+  integer SNP matrix of 10k taxa (tie-heavy, from the GPU dist on a
+  clade-structured alignment): exact DNJ prefix.
+- configs[2], 50k taxa x 5 Mbp tree-like alignment: the GPU dist (sampled
+  LT cells against orc_fsacmp, fsacmp.c:552) then exact DNJ on that matrix,
+  a join prefix against the oracle's prefix on a host copy.
+- configs[3], N = 200k float (80 GB) through the row-sharded engine
+  (ccg_tree_shard_dev) at world 1: exact DNJ, the first 500 joins.
+
+The sharded / multi-rank paths at smaller n are in test_gpu_shard.py.
+Reference rules stressed here: minQpair dnj.c:43-128 (rescans and ties),
+the serial row sums nj.c:911 / :1002 (exact mode), initSummaD nj.c:111.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 4)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import ccphylo_amd as cg
+    d = cg.Device(0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
+def d10k():
+    from tools.synth import euclid
+    return euclid(10_000, seed=1)
+
+
+def _same_joins(got, ref, what):
+    (gj, gfn, gfd), (rj, rfn, rfd) = got, ref
+    assert len(gj) == len(rj), (what, len(gj), len(rj))
+    bad = np.nonzero((gj["i"] != rj["i"]) | (gj["j"] != rj["j"]))[0]
+    assert bad.size == 0, (what, "first differing join", int(bad[0]) if bad.size else None)
+    # branch lengths bit-identical (exact row sums are the reference's serial sums)
+    assert (gj["Li"] == rj["Li"]).all() and (gj["Lj"] == rj["Lj"]).all(), what
+    assert (gfn, gfd) == (rfn, rfd), (what, gfn, gfd, rfn, rfd)
+
+
+def test_config1_dnj_exact_full(dev, d10k):
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    n = 10_000
+    ref = pyoracle.tree(d10k, n, method=cg.CCG_TREE_DNJ, threads=THREADS)
+    got = dev.tree(d10k, n, method=cg.CCG_TREE_DNJ, exact=True)[:3]
+    assert len(ref[0]) == n - 2
+    _same_joins(got, ref, "dnj 10k exact")
+
+
+def test_config1_hnj_exact_full(dev, d10k):
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    n = 10_000
+    ref = pyoracle.tree(d10k, n, method=cg.CCG_TREE_HNJ, threads=THREADS)
+    got = dev.tree(d10k, n, method=cg.CCG_TREE_HNJ, exact=True)[:3]
+    _same_joins(got, ref, "hnj 10k exact")
+
+
+def test_config1_nj_exact_prefix(dev, d10k):
+    """NJ: every join is a full initQ scan (nj.c:182), 5e7 cells at 10k, so
+    the oracle runs a prefix; the GPU runs the same prefix (max_joins)."""
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    n, k = 10_000, 120
+    ref = pyoracle.tree(d10k, n, method=cg.CCG_TREE_NJ, max_joins=k, threads=THREADS)
+    got = dev.tree(d10k, n, method=cg.CCG_TREE_NJ, exact=True, max_joins=k)
+    assert len(ref[0]) == k and len(got[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "nj 10k exact prefix")
+
+
+def test_config1_fast_sums_topology(dev, d10k):
+    """Fast row sums (--fast_sums, not the default): a fixed-order tree sum of
+    the new row instead of the serial one.  On this matrix the tree must be
+    the same (same splits); the join order may differ at near-ties."""
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    from tools.parity_large import splits
+    n = 10_000
+    ref, rfn, _ = pyoracle.tree(d10k, n, method=cg.CCG_TREE_DNJ, threads=THREADS)
+    got, fn, _, _ = dev.tree(d10k, n, method=cg.CCG_TREE_DNJ, exact=False)
+    assert splits(got, n, fn) == splits(ref, n, rfn)
+
+
+def _clade_snp_ltd(dev, torch, n, L, clades, etype=8, seed=3):
+    """LT (device tensor) of the SNP distances of a clade-structured packed
+    alignment (tools/config3.make_packed), computed by the GPU dist."""
+    from tools.config3 import make_packed
+    W = L // 32 + 1
+    seqs = make_packed(torch, n, W, clades=clades, seed=seed)
+    incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
+    incs[::10] = 0
+    incs[(L + 31) // 32:] = 0
+    if L % 32:
+        incs[(L + 31) // 32 - 1] &= ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    dt = {8: torch.float64, 4: torch.float32}[etype]
+    D = torch.empty(n * (n - 1) // 2, dtype=dt, device="cuda")
+    torch.cuda.synchronize()
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr(), etype=etype)
+    torch.cuda.synchronize()
+    return seqs, incs, D
+
+
+def test_config1_snp_dnj_exact_prefix(dev):
+    """Integer SNP counts at N = 10k (configs[1] (b)): many exactly tied Q
+    values, the case minQpair's strict `<` rescans and the tie rules decide."""
+    import torch
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    n, k = 10_000, 1500
+    seqs, incs, D = _clade_snp_ltd(dev, torch, n, 100_000, clades=256)
+    del seqs, incs
+    host = D.cpu().numpy()
+    got = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
+    del D
+    torch.cuda.empty_cache()
+    ref = pyoracle.tree(host, n, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
+    assert len(ref[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "dnj 10k SNP exact prefix")
+
+
+def test_config2_dist_and_dnj_prefix(dev):
+    """configs[2]: 50k taxa x 5 Mbp (packed 2-bit, 62.5 GB in HBM), the
+    non-pair dist into a double LT (10 GB), sampled cells against the
+    oracle's fsacmp, then exact DNJ on that matrix (a join prefix)."""
+    import torch
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    n, L, k = 50_000, 5_000_000, 60
+    seqs, incs, D = _clade_snp_ltd(dev, torch, n, L, clades=512)
+    lib = pyoracle.lib()
+    hinc = incs.cpu().numpy().view(np.uint32).copy()
+    rng = np.random.default_rng(2)
+    pairs = [(1, 0), (n - 1, 0), (n - 1, n - 2), (n // 2, n // 3)] + \
+            [tuple(sorted(rng.choice(n, 2, replace=False).tolist(), reverse=True)) for _ in range(12)]
+    for i, j in pairs:
+        a = seqs[i].cpu().numpy().view(np.uint64).copy()
+        b = seqs[j].cpu().numpy().view(np.uint64).copy()
+        want = lib.orc_fsacmp(a.ctypes.data, b.ctypes.data, hinc.ctypes.data, L)
+        assert float(D[i * (i - 1) // 2 + j].item()) == float(want), (i, j)
+    del seqs, incs
+    torch.cuda.empty_cache()
+    host = D.cpu().numpy()
+    got = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
+    del D
+    torch.cuda.empty_cache()
+    ref = pyoracle.tree(host, n, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
+    assert len(ref[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "dnj configs[2] exact prefix")
+
+
+def test_config3_sharded_dnj_prefix(dev):
+    """configs[3]: N = 200k Euclidean (seed 4), float (`-p`, 80 GB), through
+    the row-sharded engine at world 1 (band layout = the packed LT), exact
+    DNJ, the first 500 joins against the oracle's prefix."""
+    import torch
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    from tools.synth import euclid_shard_dev
+    n, k = 200_000, 500
+    loc = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)
+    host = loc.cpu().numpy()
+    got = dev.tree_shard_dev(loc.data_ptr(), n, None, etype=4, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
+    del loc
+    torch.cuda.empty_cache()
+    ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
+    assert len(ref[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "sharded dnj 200k float exact prefix")

@@ -55,3 +55,28 @@ def test_kma_oracle_matches_reference(case):
                                      min_depth=o["minDepth"], min_length=o["minLength"], min_cov=o["minCov"],
                                      etype=o["et"], byte_scale=o["bs"], want_n=o["nout"])
     assert kma_phylip(o, D, N, inc, n) == golden_bytes(case)
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("et", [8, 4, 2])
+def test_oracle_threaded_init_and_prefix(method, et):
+    """orc_tree_ex (the large-n checker of tests/test_gpu_large.py): the
+    threaded initSummaD / initHNJ give the serial run bit for bit, and a
+    max_joins run is a prefix of the full run (missing entries included)."""
+    import numpy as np
+    from oracle import pyoracle
+    from tools.synth import euclid
+    n = 1500
+    D = euclid(n, 5)
+    D[::97] = -1.0
+    bs = 1.0
+    if et == 4:
+        D = D.astype(np.float32)
+    elif et == 2:
+        bs = 100.0
+        D = np.where(D < 0, 65535, np.round(D * bs)).astype(np.uint16)
+    full = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=method)
+    par = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=method, threads=5)
+    pre = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=method, threads=3, max_joins=40)
+    assert (full[0] == par[0]).all() and full[1:] == par[1:]
+    assert len(pre[0]) == 40 and (pre[0] == full[0][:40]).all()
