@@ -6,7 +6,18 @@ Metric (BASELINE.json): "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa".
 reference's default method, which yields the exact NJ join sequence) on
 configs[1]: an N=10,000-taxon distance matrix, one full tree per step, the
 packed LT already resident in HBM when the timed region starts (one fresh
-device copy per step; the engine consumes its input).
+device copy per step; the engine consumes its input).  Row sums are exact
+(the CLI default): the join list and the Newick bytes equal the reference's,
+checked in the cpu_baseline leg against the reference binary's own output.
+extras.dnj_fast_sums is the non-default --fast_sums mode with its parity
+status at this config (join list identical or not, splits differing).
+
+extras.config3: configs[2], the largest single-GPU configuration: a 50k taxa
+x 5 Mbp synthetic tree-like alignment, packed in HBM -> dist -> exact DNJ in
+place, steps-timed, with its own roofline (dist: VALU issue; tree: HBM) and
+cpu_baseline (the reference's `dist -t <threads>` on row subsamples of the
+same alignment written as FASTA, whose distances are also compared with the
+GPU's cells).
 
 Multi-GPU (torchrun, one process per GPU): every rank builds its own N=10k
 tree on its own GPU ("replicas") -> scaling "weak", value = all ranks' joins
@@ -40,15 +51,17 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # dist roofline: 32-bit integer VALU issue.  A 32-position word pair costs 3
-# instructions (v_xor, v_bitop3, v_bcnt with accumulate).  Peak = the
-# register-only issue rate of that mix measured by tools/micro/popc_rate.hip
-# on MI355X: 5.31e13 "4-op" lane-ops/s over 208 real instructions per 256
-# counted = 4.31e13 instruction-lanes/s (the nominal 256 CU x 64 lanes x
-# 2.4 GHz = 3.93e13 is exceeded, i.e. the engine clock runs above 2.4 GHz).
-VALU_INT_LANE_OPS = 4.31e13
+# instructions (v_xor, v_bitop3, v_bcnt with accumulate).  Nominal peak
+# (MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz =
+# 7.86e13 instruction-lanes/s.  The measured issue rate of exactly this mix
+# in registers (tools/micro/popc_rate.hip) is 4.31e13 = 55% of nominal; both
+# fractions are reported (DESIGN.md 5 discusses the gap).
+VALU_NOMINAL_LANE_OPS = 256 * 4 * 32 * 2.4e9
+VALU_MIX_CEILING = 4.31e13
 OPS_PER_WORD_PAIR = 3.0
 OPS_PER_WORD_PAIR_PAIRMODE = 6.0   # v_and (masks), v_xor, v_bitop3, v_and, 2x v_bcnt (dist and n)
-KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
+KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll",
+          "exact_sum"]
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
 SHARD_LEG_TIMEOUT_S = 480
 
@@ -78,6 +91,8 @@ def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan):
         return 2.0 * s * sn
     if kernel == "init":            # two passes over the LT
         return 2.0 * s * n * (n - 1) / 2
+    if kernel == "exact_sum":       # the new row's contributions, read once (+ the update partials)
+        return 8.0 * sn + 32.0 * sum((k + 255) // 256 for k in sizes)
     return 0.0
 
 
@@ -95,7 +110,7 @@ def pmc_traffic(kernel):
 
 KERNEL_STATS = os.path.join(ROOT, "profiles", "r01_kernel_stats.csv")
 KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_find", "update": "k_dnj_join",
-        "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop"}
+        "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop", "exact_sum": "k_exact_sum"}
 
 
 def rocprof_mean_us(kernel):
@@ -263,9 +278,156 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "roofline": {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": VALU_INT_LANE_OPS / 1e12,
-                         "unit": "T int lane-ops/s", "frac": round(ops / dt / VALU_INT_LANE_OPS, 4),
-                         "ops_per_word_pair": opw}}
+            "roofline": valu_roofline(ops, dt, opw)}
+
+
+def valu_roofline(ops, dt, opw):
+    """dist: integer VALU issue (instruction-lanes/s) against the nominal
+    peak, and against the measured ceiling of the kernel's instruction mix."""
+    return {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": round(VALU_NOMINAL_LANE_OPS / 1e12, 2),
+            "unit": "T int instruction-lanes/s", "frac": round(ops / dt / VALU_NOMINAL_LANE_OPS, 4),
+            "mix_ceiling": VALU_MIX_CEILING / 1e12, "frac_of_mix_ceiling": round(ops / dt / VALU_MIX_CEILING, 4),
+            "ops_per_word_pair": opw}
+
+
+def packed_rows_to_fasta(path, words, L, masked_words):
+    """FASTA text of packed 2-bit rows (qseq2nibble layout, MSB-first, codes
+    0..3 = A C G T, qseqs.c:60), the positions of `masked_words` written as N
+    in the first taxon only (the non-pair dist ANDs every taxon's include
+    mask, cdist.c:273, so those positions drop out for all pairs)."""
+    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
+    shifts = (62 - 2 * np.arange(32, dtype=np.uint64)).astype(np.uint64)
+    with open(path, "wb") as f:
+        for t in range(words.shape[0]):
+            codes = ((words[t][:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.uint8).reshape(-1)[:L]
+            txt = lut[codes]
+            if t == 0:
+                txt = txt.reshape(-1)
+                for w in masked_words:
+                    txt[32 * w:32 * w + 32] = ord("N")
+            f.write(b">t%d\n" % t + txt.tobytes() + b"\n")
+
+
+def read_phylip_values(path):
+    """The LT cells of a (relaxed) Phylip file as floats, row by row."""
+    vals = []
+    with open(path) as f:
+        n = int(f.readline())
+        for i in range(n):
+            parts = f.readline().split()
+            vals.extend(float(x) for x in parts[1:1 + i])
+    return n, np.array(vals)
+
+
+def config3_cpu_baseline(seqs_host, L, masked_words, tmpdir, gpu_cells, sizes=(96, 192), threads=16):
+    """The reference's `ccphylo dist -t <threads>` (oracle/_ref, built from
+    the reference's sources) on the first 96 and 192 taxa of the configs[2]
+    alignment written as FASTA.  Wall = parse + compare; t = a n + b n^2
+    separates the compare term.  The reference's distances for those taxa are
+    compared with the GPU's LT cells (same rows)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
+    if not os.path.exists(ref):
+        return {"error": "reference binary absent (oracle/_ref not built)"}
+    walls, mism = {}, 0
+    for m in sizes:
+        path = os.path.join(tmpdir, f"c3_{m}.fsa")
+        packed_rows_to_fasta(path, seqs_host[:m], L, masked_words)
+        out = os.path.join(tmpdir, f"c3_{m}.phy")
+        t0 = time.perf_counter()
+        subprocess.run([ref, "dist", "-i", path, "-t", str(threads), "-o", out], capture_output=True, timeout=900,
+                       check=True)
+        walls[m] = time.perf_counter() - t0
+        os.unlink(path)
+        nn, vals = read_phylip_values(out)
+        os.unlink(out)
+        k = m * (m - 1) // 2
+        mism += int(nn != m) + int((vals != gpu_cells[:k]).sum())
+    (n1, t1), (n2, t2) = sorted(walls.items())
+    b = (t2 / n2 - t1 / n1) / (n2 - n1)          # t / n = a + b n
+    pairs_s = 0.5 / b if b > 0 else None
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count()
+    return {"value": round(pairs_s, 2) if pairs_s else None, "unit": "taxa-pairs/s", "cores": threads,
+            "host_cpus_available": ncpu, "kind": "reference",
+            "nt_comparisons_per_s": round(pairs_s * L, 1) if pairs_s else None,
+            "parity_mismatched_cells": mism,
+            "sample": f"reference ccphylo 0.8.5 `dist -t {threads}` on the first {list(sizes)} taxa of the same "
+                      f"{L / 1e6:g} Mbp alignment (FASTA); walls " +
+                      ", ".join(f"{m} taxa: {w:.2f} s" for m, w in sorted(walls.items())) +
+                      "; the rate is the quadratic (compare) term of t = a n + b n^2; its distances equal the GPU's "
+                      "LT cells of the same taxa when parity_mismatched_cells is 0"}
+
+
+def config3_leg(dev, torch, tmpdir, n=50_000, L=5_000_000, steps=1, cpu=True):
+    """configs[2]: N=50k taxa x L=5 Mbp synthetic tree-like alignment on one
+    GPU, end to end in HBM: packed sequences (62.5 GB) -> ccg_snp_ltd_dev
+    (double LT, 10 GB) -> ccg_tree_dev DNJ with exact row sums, in place.  A
+    step = dist + tree (steps-timed); the alignment is generated once."""
+    import ccphylo_amd as cg
+    from tools.config3 import make_packed
+    W = L // 32 + 1
+    seqs = make_packed(torch, n, W)
+    incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
+    masked_words = list(range(0, (L + 31) // 32, 10))
+    incs[::10] = 0
+    incs[(L + 31) // 32:] = 0
+    m = n * (n - 1) // 2
+    D = torch.empty(m, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t_dist, t_tree, joins, cells, rows = [], [], 0, 0, 0
+    first_cells = None
+    for k in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if first_cells is None:   # the LT block of the first 192 taxa, for the reference check
+            first_cells = D[:192 * 191 // 2].cpu().numpy()
+            torch.cuda.synchronize()
+            t1b = time.perf_counter()
+        else:
+            t1b = t1
+        j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_dist.append(t1 - t0)
+        t_tree.append(t2 - t1b)
+        joins, rows, cells = len(j), int(st[0]), int(st[1])
+    dist_s, tree_s = sum(t_dist) / steps, sum(t_tree) / steps
+    words = (L + 31) // 32
+    ops = m * words * OPS_PER_WORD_PAIR
+    # tree HBM bytes: initSummaD + initHNJ (two LT passes), the rescanned cells,
+    # and per join the O(n) update / requeue / row-sum traffic (DESIGN.md 4)
+    sizes_sum = n * (n + 1) / 2.0
+    tree_bytes = 2.0 * 8 * m + 8.0 * cells + (7 * 8 + 48) * sizes_sum
+    res = {"n": n, "L": L, "steps": steps, "ms_per_step": round(1000 * (dist_s + tree_s), 1),
+           "dist_s": round(dist_s, 3), "tree_s": round(tree_s, 3),
+           "taxa_pairs_per_s": round(m / dist_s, 1), "nt_comparisons_per_s": m * L / dist_s,
+           "joins_per_s": round(joins / tree_s, 1), "joins": joins, "rows_rescanned": rows,
+           "cells_rescanned": cells, "included_positions": inc, "row_sums": "exact",
+           "roofline": {"dist": valu_roofline(ops, dist_s, OPS_PER_WORD_PAIR),
+                        "tree": {"bound": "hbm", "achieved": round(tree_bytes / tree_s / 1e9, 1),
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(tree_bytes / tree_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 "algorithmic_bytes": tree_bytes,
+                                 "note": "2 LT passes (init) + 8 B per rescanned cell + ~104 B per active taxon per "
+                                         "join; latency-bound joins, see DESIGN.md 4"}},
+           "tree_parity": "exact row sums; tests/test_gpu_large.py::test_config2_dist_and_dnj_prefix pins this "
+                          "configuration's dist cells (fsacmp) and DNJ join prefix against the oracle"}
+    del D, incs
+    torch.cuda.empty_cache()
+    if cpu:
+        try:
+            host = seqs[:192].cpu().numpy().view(np.uint64)
+            res["cpu_baseline"] = config3_cpu_baseline(host, L, masked_words, tmpdir, first_cells)
+        except Exception as e:  # noqa: BLE001
+            res["cpu_baseline"] = {"error": str(e)}
+    del seqs
+    torch.cuda.empty_cache()
+    return res
 
 
 def kma_extra(dev, torch, n=1024, L=50_000, reps=3, metric="cos"):
@@ -410,16 +572,43 @@ def shard_max(x, dist):
     return shard.reduce_max(x, dist)
 
 
+def reference_tree_parity(D, n, exact_joins, fast_joins, td):
+    """Checks in the cpu_baseline leg: the reference binary's Newick for the
+    bench matrix against the GPU's exact-mode tree (byte identity), and the
+    fast-sum tree against the exact one (join identity, splits differing)."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native
+    from tools.parity_large import splits
+    out = {}
+    ref_nwk = os.path.join(td, "ref.nwk")
+    path = os.path.join(td, "bench_ref.phy")
+    if os.path.exists(ref_nwk):
+        native.write_phylip(path, D, n, [f"t{k}" for k in range(n)])
+        ej, efn, efd = exact_joins
+        trees = cg.newick_from_phylip(path, lambda _D, _n: (ej, efn, efd))
+        os.unlink(path)
+        with open(ref_nwk, "rb") as f:
+            out["exact_newick_identical_to_reference"] = ("\n".join(trees) + "\n").encode() == f.read()
+    if fast_joins is not None:
+        fj, ffn, _ = fast_joins
+        ej, efn, _ = exact_joins
+        same = len(fj) == len(ej) and bool((fj["i"] == ej["i"]).all() and (fj["j"] == ej["j"]).all())
+        out["fast_joins_identical"] = same
+        out["fast_splits_differing"] = len(splits(fj, n, ffn) ^ splits(ej, n, efn)) // 2
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=10000)
-    ap.add_argument("--sums", choices=["fast", "exact"], default="fast")
+    ap.add_argument("--sums", choices=["fast", "exact"], default="exact")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--no-config3", action="store_true", help="skip the 50k x 5M dist+tree leg (~40 s)")
+    ap.add_argument("--no-config3", action="store_true", help="skip the 50k x 5M dist+tree leg (~1 min)")
+    ap.add_argument("--c3-steps", type=int, default=1)
     ap.add_argument("--shard-n", type=int, default=100_000)
     ap.add_argument("--shard-joins", type=int, default=64)
     ap.add_argument("--dnj-shard-n", type=int, default=200_000)
@@ -467,6 +656,7 @@ def main():
         joins += len(j)
     barrier()
     dt = time.perf_counter() - t0
+    main_joins = (j, fn, fd)
     if world > 1:
         t = torch.tensor([dt])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -485,6 +675,8 @@ def main():
     _, _, _, pst = dev.tree_dev(pb, n, method=cg.CCG_TREE_DNJ, exact=exact, profile=True)
     dev.free(pb)
     roof = roofline(pst, n, s)
+    roof["row_sums_serial_order"] = int(pst[6 + 2 * len(KNAMES)])
+    roof["row_sums_by_serial_chain"] = int(pst[7 + 2 * len(KNAMES)])
 
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
@@ -505,17 +697,22 @@ def main():
                    "row_sums": args.sums, "parallelism": f"replicas x{world}"},
         "roofline": roof,
     }
+    fast_joins = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = {}
         pb = dev.malloc(nbytes)
-        for label, method, ex in (("dnj_exact_sums" if not exact else "dnj_fast_sums", cg.CCG_TREE_DNJ, not exact),
+        other = "dnj_exact_sums" if not exact else "dnj_fast_sums"
+        for label, method, ex in ((other, cg.CCG_TREE_DNJ, not exact),
                                   ("nj", cg.CCG_TREE_NJ, exact), ("hnj", cg.CCG_TREE_HNJ, exact)):
             dev.h2d(pb, D)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            j, _, _, st = dev.tree_dev(pb, n, method=method, exact=ex)
+            j2, fn2, fd2, st = dev.tree_dev(pb, n, method=method, exact=ex)
             t2 = time.perf_counter() - t1
-            extras[label] = {"joins_per_s": round(len(j) / t2, 2), "seconds": round(t2, 4)}
+            extras[label] = {"joins_per_s": round(len(j2) / t2, 2), "seconds": round(t2, 4),
+                             "row_sums": "exact" if ex else "fast"}
+            if label == "dnj_fast_sums":
+                fast_joins = (j2, fn2, fd2)
         dev.h2d(pb, D)
         _, _, _, nst = dev.tree_dev(pb, n, method=cg.CCG_TREE_NJ, exact=exact, profile=True)
         extras["nj"]["roofline"] = roofline(nst, n, s)
@@ -538,21 +735,30 @@ def main():
             except Exception as e:  # noqa: BLE001
                 result["extras"]["kma_cos"] = {"error": str(e)}
             if not args.no_config3:
-                # configs[2]: N=50k x L=5M tree-like alignment -> dist -> DNJ, all in HBM
+                # configs[2]: N=50k x L=5M tree-like alignment -> dist -> exact DNJ, all in HBM
                 try:
-                    from tools.config3 import run as config3_run
                     torch.cuda.empty_cache()
-                    c3 = config3_run(dev, torch)
+                    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+                        c3 = config3_leg(dev, torch, td, steps=args.c3_steps, cpu=not args.no_cpu)
                     c3["config"] = ("configs[2]: 50k taxa x 5 Mbp synthetic tree-like alignment (512 clades, ~0.8% "
                                     "codes flipped per taxon), packed in HBM -> ccg_snp_ltd_dev (double LT, 10 GB) "
-                                    "-> ccg_tree_dev DNJ with fast row sums")
-                    result["extras"]["config3_dist_tree"] = c3
+                                    "-> ccg_tree_dev DNJ with exact row sums")
+                    result["extras"]["config3"] = c3
                 except Exception as e:  # noqa: BLE001
-                    result["extras"]["config3_dist_tree"] = {"error": str(e)}
+                    result["extras"]["config3"] = {"error": str(e)}
                 torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu:
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             result["cpu_baseline"] = cpu_baseline(D, n, td)
+            if exact:
+                try:
+                    par = reference_tree_parity(D, n, main_joins, fast_joins, td)
+                    result["cpu_baseline"]["parity"] = par
+                    if "dnj_fast_sums" in result.get("extras", {}):
+                        result["extras"]["dnj_fast_sums"]["parity_vs_exact"] = {
+                            k: v for k, v in par.items() if k.startswith("fast")}
+                except Exception as e:  # noqa: BLE001
+                    result["cpu_baseline"]["parity"] = {"error": str(e)}
             if not args.no_extras and isinstance(result.get("extras", {}).get("dist"), dict):
                 try:
                     result["extras"]["dist"]["cpu_baseline"] = cpu_baseline_dist(td)

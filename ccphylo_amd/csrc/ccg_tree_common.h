@@ -213,7 +213,7 @@ __device__ __forceinline__ void update_partials(const TreeBufs &b, int n, bool e
 // a shfl_down tree), identical in every block.  In exact mode this is the
 // reference's serial sum whenever that is provable (all contributions
 // multiples of 2^e, sum |c| < 2^53 * 2^e, e.g. integer SNP distances);
-// otherwise *need_serial asks for serial_sum_block.  General (missing data):
+// otherwise *need_serial asks for the serial order (k_exact_sum).  General (missing data):
 // k_update_general left the serial sum in wsum[0].
 static __device__ void fold_update_wave(const TreeBufs &b, int G, bool exact, bool general, double *sd_out, int *nj_out,
                                  bool *need_serial) {
@@ -294,7 +294,6 @@ static __device__ double serial_sum_t(const double *__restrict__ c, int n) {
 	__syncthreads();
 	return s_sd;
 }
-static __device__ double serial_sum_block(const TreeBufs &b, int n) { return serial_sum_t<TB>(b.contrib, n); }
 
 // ------------------------------------------------------------------ exact row sum, in parallel
 // The reference's serial sum s_k = fl(s_{k-1} + c_k) (nj.c:911 / :1002) of
@@ -321,7 +320,7 @@ static __device__ double serial_sum_block(const TreeBufs &b, int n) { return ser
 // 3000 random, dyadic tie-heavy and wide-range inputs (tools/sim_exact_sum.py).
 #define XS_CAP 128                // crossings / ties listed per sum
 #define XS_HEAD 64                // elements summed serially first
-// a tile: NT chunks of ET consecutive elements (exact_sum_block<NT, ET>)
+// a tile: NT chunks of ET consecutive elements (exact_sum_t<NT, ET>)
 
 struct XsCross {
 	double v, run;   // c_k; provisional sum (units of its run's u) of the chunk's run before it
@@ -618,16 +617,50 @@ static __device__ bool exact_sum_t(const double *__restrict__ c, int n, double *
 }
 
 // the reference's serial row sum: the parallel form above, the chain when it declines
-static __device__ __forceinline__ bool exact_sum_block(const double *__restrict__ c, int n, double *out,
-                                                      unsigned long long *stamps = nullptr) {
-	return exact_sum_t<TB, 16>(c, n, out, stamps);
-}
 
-static __device__ double exact_row_sum(const TreeBufs &b, int n) {
-	double s;
-	if(exact_sum_block(b.contrib, n, &s)) return s;
-	if(blockIdx.x == 0 && threadIdx.x == 0) b.ctl->chain_sums++;
-	return serial_sum_block(b, n);
+
+// ------------------------------------------------------------------ exact row sum of j
+// Exact mode (the default): the reference's serial sum of the new row of j
+// (nj.c:911 / :1002), once per join by one 512-thread block between updateD
+// and its consumers (k_dnj_requeue, k_nj_pop, k_hnj_update and the sharded
+// engines' k_sh_pop / k_shd_requeue read ctl->xsum; every rank holds the whole
+// new line j, so every rank runs it identically):
+// the fixed-order fold when that is provably the serial sum (integer-like
+// data), else the parallel binade-segmented form, else the chain.
+#define XS_NT 512
+#define XS_ET_BIG 16   // LDS tiles of 8192 elements
+template <int UNUSED = 0>
+__global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
+	__shared__ double s_sd;
+	__shared__ int s_nj, s_need, s_stop;
+	TreeCtl *ctl = b.ctl;
+	if(threadIdx.x < 64) {
+		const int done = ctl->done;
+		double sd = 0;
+		int nj = 0;
+		bool need = false;
+		if(!done) fold_update_wave(b, G, true, false, &sd, &nj, &need);
+		if(threadIdx.x == 0) {
+			s_stop = done;
+			s_sd = sd;
+			s_nj = nj;
+			s_need = need;
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	double r = s_sd;
+	bool chain = false;
+	if(s_need && !exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &r)) {
+		r = serial_sum_t<XS_NT>(b.contrib, n);
+		chain = true;
+	}
+	if(threadIdx.x == 0) {
+		ctl->xsum = r;
+		ctl->xnj = s_nj;
+		ctl->serial_sums += s_need;
+		ctl->chain_sums += chain;
+	}
 }
 
 // (q, f) cells of initQ: smaller q wins, equal q -> larger flat index f

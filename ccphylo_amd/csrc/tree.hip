@@ -128,48 +128,6 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 }
 
 
-// ------------------------------------------------------------------ exact row sum of j
-// Exact mode (the default): the reference's serial sum of the new row of j
-// (nj.c:911 / :1002), once per join by one 1024-thread block between updateD
-// and its consumers (k_dnj_requeue, k_nj_pop, k_hnj_update read ctl->xsum):
-// the fixed-order fold when that is provably the serial sum (integer-like
-// data), else the parallel binade-segmented form, else the chain.
-#define XS_NT 512
-#define XS_ET_BIG 16   // LDS tiles of 8192 elements
-template <int UNUSED = 0>
-__global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
-	__shared__ double s_sd;
-	__shared__ int s_nj, s_need, s_stop;
-	TreeCtl *ctl = b.ctl;
-	if(threadIdx.x < 64) {
-		const int done = ctl->done;
-		double sd = 0;
-		int nj = 0;
-		bool need = false;
-		if(!done) fold_update_wave(b, G, true, false, &sd, &nj, &need);
-		if(threadIdx.x == 0) {
-			s_stop = done;
-			s_sd = sd;
-			s_nj = nj;
-			s_need = need;
-		}
-	}
-	__syncthreads();
-	if(s_stop) return;
-	double r = s_sd;
-	bool chain = false;
-	if(s_need && !exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &r)) {
-		r = serial_sum_t<XS_NT>(b.contrib, n);
-		chain = true;
-	}
-	if(threadIdx.x == 0) {
-		ctl->xsum = r;
-		ctl->xnj = s_nj;
-		ctl->serial_sums += s_need;
-		ctl->chain_sums += chain;
-	}
-}
-
 // ------------------------------------------------------------------ DNJ join
 // Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
 // replay; then limbLength, the join record and updateD with the whole grid.
@@ -1287,7 +1245,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
                              int method, int exact, KTimer &kt) {
 	const unsigned gn = cdiv(n, TB);
 	const int general = GEN;
-	const int xs = exact && !GEN;   // the exact row sum as its own 1024-thread block
+	const int xs = exact && !GEN;   // the exact row sum as its own block (k_exact_sum)
 	if(method == CCG_TREE_DNJ) {
 		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
@@ -1301,8 +1259,11 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_REST);
 		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
-		if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 		kt.mark(CCG_K_UPDATE);
+		if(xs) {
+			k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
+			kt.mark(CCG_K_XSUM);
+		}
 		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
@@ -1313,8 +1274,11 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		kt.mark(CCG_K_ARGMIN);
 		k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) gn, general, DBL_MAX);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
-		if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 		kt.mark(CCG_K_UPDATE);
+		if(xs) {
+			k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
+			kt.mark(CCG_K_XSUM);
+		}
 		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);   // updateHNJ's Q/P pass + HNJ_popArrange
 		kt.mark(CCG_K_POP);
 		return (GEN ? 4 : 3) + xs;
@@ -1324,8 +1288,11 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	kt.mark(CCG_K_ARGMIN);
 	k_nj_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, (int) g, general, 1.0);
 	if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
-	if(xs) k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 	kt.mark(CCG_K_UPDATE);
+	if(xs) {
+		k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
+		kt.mark(CCG_K_XSUM);
+	}
 	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general);
 	kt.mark(CCG_K_POP);
 	return (GEN ? 4 : 3) + xs;

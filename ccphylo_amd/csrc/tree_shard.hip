@@ -290,7 +290,13 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 			double sd;
 			int nj;
 			bool need;
-			fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			if(exact) {   // k_exact_sum ran
+				sd = ctl->xsum;
+				nj = ctl->xnj;
+				need = false;
+			} else {
+				fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			}
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_serial ? exact_row_sum(b, n) : s_sd;
+	const double sdj = s_sd;   // exact: k_exact_sum's
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = s_nj;
@@ -536,10 +542,14 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			SH_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xm);
 			kt.mark(CCG_K_UPDATE);
+			if(a->exact) {
+				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
+				kt.mark(CCG_K_XSUM);
+			}
 			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xm);
 			kt.mark(CCG_K_POP);
 			SH_HIP(hipGetLastError());
-			launches += (G > 0) + 5;
+			launches += (G > 0) + 5 + (a->exact != 0);
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;

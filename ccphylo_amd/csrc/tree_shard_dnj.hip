@@ -312,7 +312,13 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 			double sd;
 			int nj;
 			bool need;
-			fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			if(exact) {   // k_exact_sum ran
+				sd = ctl->xsum;
+				nj = ctl->xnj;
+				need = false;
+			} else {
+				fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
+			}
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j, Nj = s_nj;
-	const double sdj = s_serial ? exact_row_sum(b, n) : s_sd;
+	const double sdj = s_sd;   // exact: k_exact_sum's
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = Nj;
@@ -585,11 +591,15 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xm, Xj);
 			kt.mark(CCG_K_UPDATE);
+			if(a->exact) {
+				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
+				kt.mark(CCG_K_XSUM);
+			}
 			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
 			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
-			launches += 8;
+			launches += 8 + (a->exact != 0);
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;

@@ -28,8 +28,9 @@ ETYPES = {8: np.float64, 4: np.float32, 2: np.uint16, 1: np.uint8}
 CCG_TREE_NJ = 0
 CCG_TREE_DNJ = 1
 CCG_TREE_HNJ = 2
-NKSTAT = 9
-KSTAT_NAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll"]
+NKSTAT = 10
+KSTAT_NAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll",
+               "exact_sum"]
 SHARD_BAND = 8
 RCCL_ID_BYTES = 128
 

@@ -176,7 +176,8 @@ typedef struct {
 #define CCG_K_FIND     7   /* DNJ k_dnj_find: bound U and the rows below S under it */
 #define CCG_K_COLL     8   /* sharded engine: collectives (enqueue time, or the
                               host round trip of a host-staged transport) */
-#define CCG_NKSTAT     9
+#define CCG_K_XSUM     9   /* exact mode: k_exact_sum, the serial-order row sum of j */
+#define CCG_NKSTAT     10
 
 /* D: host LT (n(n-1)/2 elements), left unmodified.  joins: room for n-2.
  * On return *njoins joins were made; *final_n is the matrix size at exit
