@@ -320,7 +320,6 @@ static __device__ double serial_sum_t(const double *__restrict__ c, int n) {
 // 3000 random, dyadic tie-heavy and wide-range inputs (tools/sim_exact_sum.py).
 #define XS_CAP 128                // crossings / ties listed per sum
 #define XS_HEAD 64                // elements summed serially first
-// a tile: NT chunks of ET consecutive elements (exact_sum_t<NT, ET>)
 
 struct XsCross {
 	double v, run;   // c_k; provisional sum (units of its run's u) of the chunk's run before it
@@ -351,209 +350,221 @@ __device__ __forceinline__ int xs_par(double y) {
 		if(stamps && (threadIdx.x & 63) == 0 && threadIdx.x < 256) stamps[i + 16 * (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); \
 	} while(0)
 
-// whole block (blockDim = TB); true and *out = the serial sum, or false.
-// Tiles of XS_TILE elements are staged through LDS with coalesced loads (the
-// next tile's loads in flight during the current one); thread t then owns
-// the chunk [t XS_ET, (t + 1) XS_ET) of the tile, chunks in element order.
-// Increments are taken provisionally as RN_u(c) with ties rounded up,
-// floor(c/u + 1/2); the walk takes back the ties that go down.
-template <int NT, int XS_ET>
-static __device__ bool exact_sum_t(const double *__restrict__ c, int n, double *out,
+// whole block of NT threads; true and *out = the serial sum, or false.  Wave w owns
+// a contiguous range of rows of 256 elements (lane l: elements 4l .. 4l+3),
+// walks them in order with wave-level scans only, and keeps its crossing and
+// tie records, in element order, in its own lists; one block barrier then
+// joins the waves.  The binade of the running sum is predicted per element
+// from one approximate prefix chain (each lane continues the lane before it,
+// each row the row before it); a crossing is an element whose predicted
+// binade differs from its predecessor's, so every run uses one unit.
+#define XW_CAP 32                 // crossing / tie records per wave
+#define XW_EL 4                   // elements per lane per row
+
+template <int NT, int RB>
+static __device__ bool exact_sum_w(const double *__restrict__ c, int n, double *out,
                                    unsigned long long *stamps = nullptr) {
-	constexpr int XS_TILE = NT * XS_ET;
-	__shared__ double s_tile[XS_TILE + NT];   // chunk t at t (XS_ET + 1): padded against bank conflicts
-	__shared__ XsCross xe[XS_CAP];
-	__shared__ XsTie te[XS_CAP];
-	__shared__ double s_seg[XS_CAP + 1], s_wd[NT / 64], s_out;
-	__shared__ long long s_wl[NT / 64];
-	__shared__ int s_bad, s_eh;
-	__shared__ double s_head;
-	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	constexpr int NW = NT / 64, RE = 64 * XW_EL;
+	__shared__ XsCross xw[NW][XW_CAP];
+	__shared__ XsTie tw[NW][XW_CAP];
+	__shared__ double s_wt[NW], s_tail[NW], s_seg[XS_CAP + 1], s_out, s_head;
+	__shared__ int s_nc[NW], s_nt[NW], s_tp[NW], s_ex0[NW], s_bad, s_eh;
+	__shared__ __attribute__((aligned(16))) double s_hb[XS_HEAD];
+	const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 	if(tid == 0) s_bad = 0;
-	for(int s = tid; s <= XS_CAP; s += NT) s_seg[s] = 0.0;
+	for(int q = tid; q <= XS_CAP; q += NT) s_seg[q] = 0.0;
 	XS_STAMP(0);
-	const int ntiles = (n + XS_TILE - 1) / XS_TILE;
-	double r[XS_ET];
+	const int rows = (n + RE - 1) / RE, rpw = (rows + NW - 1) / NW;
+	const int r0 = w * rpw, r1 = r0 + rpw < rows ? r0 + rpw : rows;
+	const bool inreg = rpw <= RB;   // uniform
+	double x[RB][XW_EL];
+	auto load = [&](int rb) {   // rows rb .. rb + RB - 1 of this wave (clamped)
 #pragma unroll
-	for(int i = 0; i < XS_ET; ++i) {
-		const int k = tid + NT * i;
-		r[i] = c[k < n ? k : n - 1];
+		for(int q = 0; q < RB; ++q)
+#pragma unroll
+			for(int e = 0; e < XW_EL; ++e) {
+				const int k = (rb + q) * RE + XW_EL * lane + e;
+				const double v = c[k < n && rb + q < r1 ? k : n - 1];
+				x[q][e] = k < n && k >= XS_HEAD && rb + q < r1 ? v : 0.0;
+			}
+	};
+	// ---- pass 1: the wave's total (approximate prefixes of the waves)
+	double wt = 0;
+	bool bad = false;
+	for(int rb = r0; rb < r1; rb += RB) {
+		load(rb);
+#pragma unroll
+		for(int q = 0; q < RB; ++q)
+#pragma unroll
+			for(int e = 0; e < XW_EL; ++e) {
+				bad |= !(x[q][e] >= 0.0 && x[q][e] <= DBL_MAX);
+				wt += x[q][e];
+			}
 	}
 	// the head: the first XS_HEAD elements summed serially (wave 0, one
-	// dependent add each; most binade changes of s happen here, while s is
-	// small), so the parallel part starts from an exact s_H with few crossings
-	if(wid == 0) {
-		const double hx = lane < n ? c[lane] : 0.0;
-		double S = 0;
-		for(int l = 0; l < XS_HEAD; ++l) S += readlane_d(hx, l);
-		if(lane == 0) {
+	// dependent add each; most binade changes of s happen while s is small)
+	if(w == 0) {
+		s_hb[lane] = lane < n ? c[lane] : 0.0;
+		wave_sync();
+		if(lane == 0) {   // 16-byte LDS loads ahead of one dependent add each
+			double S = 0;
+#pragma unroll
+			for(int l = 0; l < XS_HEAD; l += 2) {
+				const double2 v = *(const double2 *) (s_hb + l);
+				S += v.x;
+				S += v.y;
+			}
 			s_head = S;
 			s_eh = xs_bexp(S);
 		}
 	}
+	wt = wave_sum_fixed(wt);
+	if(lane == 0) s_wt[w] = wt;
 	__syncthreads();
+	XS_STAMP(9);
 	const double SH = s_head;
 	const int eH = s_eh;
-	double tileP = SH;          // approximate prefix before the tile (uniform)
-	int X = 0, NTIE = 0, RP = 0;  // crossings, ties, last-run parities before the tile (uniform)
-	bool bad = false;
-	for(int tile = 0; tile < ntiles; ++tile) {
-		const int base = tile * XS_TILE;
-		__syncthreads();   // the previous tile's LDS reads are done
+	double P = SH;
+	for(int q = 0; q < w; ++q) P += s_wt[q];
+	int ep_c = xs_bexp(P);   // predicted binade before the wave's first element
+	if(lane == 0) s_ex0[w] = ep_c;
+	bad |= P != 0.0 && ep_c == 0;
+	// ---- pass 2: rows in order
+	int nc = 0, nt = 0;      // the wave's records so far (uniform)
+	double acc = 0;          // provisional sum of the current run in this wave (units of its u)
+	for(int rb = r0; rb < r1; rb += RB) {
+		if(!inreg) load(rb);
 #pragma unroll
-		for(int i = 0; i < XS_ET; ++i) {
-			const int e = tid + NT * i;   // element of the tile; chunk e / XS_ET
-			s_tile[e + e / XS_ET] = base + e < n && base + e >= XS_HEAD ? r[i] : 0.0;
-		}
-		__syncthreads();
-		if(tile == 0) XS_STAMP(9);
-		if(tile + 1 < ntiles) {
-#pragma unroll
-			for(int i = 0; i < XS_ET; ++i) {
-				const int k = base + XS_TILE + tid + NT * i;
-				r[i] = c[k < n ? k : n - 1];
-			}
-		}
-		double v[XS_ET];
-		double cs = 0;
-#pragma unroll
-		for(int m = 0; m < XS_ET; ++m) {
-			v[m] = s_tile[tid * (XS_ET + 1) + m];   // elements past n are 0: no effect
-			bad |= !(v[m] >= 0.0 && v[m] <= DBL_MAX);
-			cs += v[m];
-		}
-		// approximate exclusive prefix of the chunk sums
-		double x = cs;
-#define S_(C, R_) x += dpp_d<C, R_>(0.0, x);
-		CCG_DPP_STEPS(S_)
+		for(int q = 0; q < RB; ++q) {
+			if(rb + q >= r1) break;   // uniform
+			// lane prefix within the row (approximate), continuing the chain
+			const double cs = x[q][0] + x[q][1] + x[q][2] + x[q][3];
+			double xs = cs;
+#define S_(C, R_) xs += dpp_d<C, R_>(0.0, xs);
+			CCG_DPP_STEPS(S_)
 #undef S_
-		if(lane == 63) s_wd[wid] = x;
-		__syncthreads();
-		double P = tileP + (x - cs);
-		double tot = 0;
+			double Pl = P + (xs - cs);
+			double Pn[XW_EL];
+			int en[XW_EL];
 #pragma unroll
-		for(int w = 0; w < NT / 64; ++w) {
-			if(w < wid) P += s_wd[w];
-			tot += s_wd[w];
-		}
-		tileP += tot;
-		if(tile == 0) XS_STAMP(10);
-		// ---- branch-free pass: crossing and tie masks, provisional increments
-		const double P0 = P;
-		const int ep0 = xs_bexp(P);
-		bad |= P0 != 0.0 && ep0 == 0;   // subnormal running sum
-		int ep = ep0;
-		unsigned cm = 0, tm = 0;
-		double inc[XS_ET];
-		double run = 0;
+			for(int e = 0; e < XW_EL; ++e) {
+				Pl += x[q][e];
+				Pn[e] = Pl;
+				en[e] = xs_bexp(Pl);
+			}
+			// binade before the lane's first element: the previous lane's last
+			int epl = dpp_i<DPP_WAVE_SHR1, 0xF>(ep_c, en[XW_EL - 1]);
+			unsigned cm = 0, tm = 0;
+			double fl[XW_EL], run = 0;
 #pragma unroll
-		for(int m = 0; m < XS_ET; ++m) {
-			const double Pn = P + v[m];
-			const int en = xs_bexp(Pn);
-			cm |= (unsigned) (ep != en) << m;          // (x = 0 keeps P, so a change means x > 0)
-			const double t = ldexp(v[m], 1075 - ep) + 0.5;   // c / u + 1/2 (< 2^52 off crossings)
-			const double fl = floor(t);
-			tm |= (unsigned) (t == fl) << m;          // remainder exactly u / 2
-			inc[m] = fl;
-			run += fl;
-			P = Pn;
-			ep = en;
-		}
-		bad |= ep == 0x7FF;
-		tm &= ~cm;
-		const int nc = __popc(cm), ntl = __popc(tm);
-		if(cm) {   // the last run starts after the last crossing
-			const int lc = 31 - __clz(cm);
-			run = 0;
+			for(int e = 0; e < XW_EL; ++e) {
+				const int ep = e ? en[e - 1] : epl;
+				const double t = ldexp(x[q][e], 1075 - ep) + 0.5;
+				fl[e] = floor(t);
+				cm |= (unsigned) (ep != en[e]) << e;
+				tm |= (unsigned) (t == fl[e]) << e;
+				run += fl[e];
+			}
+			tm &= ~cm;
+			ep_c = __builtin_amdgcn_readlane(en[XW_EL - 1], 63);
+			P = readlane_d(Pn[XW_EL - 1], 63);
+			const unsigned long long fm = __ballot((cm | tm) != 0u);
+			if(fm == 0ull) {
+				acc += wave_sum_fixed(run);   // integers below 2^53: exact in any order
+				continue;
+			}
+			// a row with crossings or ties (few): flagged lanes in order, the
+			// complete chunks between them as masked sums
+			int from = 0;
+			for(unsigned long long f = fm; f; f &= f - 1) {
+				const int L = __ffsll((long long) f) - 1;
+				acc += wave_sum_fixed(lane >= from && lane < L ? run : 0.0);
+				const unsigned cmL = __builtin_amdgcn_readlane(cm, L), tmL = __builtin_amdgcn_readlane(tm, L);
 #pragma unroll
-			for(int m = 0; m < XS_ET; ++m) run += m > lc ? inc[m] : 0.0;
-		}
-		if(tile == 0) XS_STAMP(11);
-		// ---- positions: crossings, ties and last-run parities before the chunk
-		const long long pk = ((long long) nc << 40) | ((long long) ntl << 20) | (long long) xs_par(run);
-		const long long incl = wave_incl_sum_l(pk);
-		if(lane == 63) s_wl[wid] = incl;
-		__syncthreads();
-		long long pre = incl - pk, ttot = 0;
-#pragma unroll
-		for(int w = 0; w < NT / 64; ++w) {
-			if(w < wid) pre += s_wl[w];
-			ttot += s_wl[w];
-		}
-		const int cb = X + (int) (pre >> 40), tb = NTIE + (int) ((pre >> 20) & 0xFFFFF),
-		          Rc = RP + (int) (pre & 0xFFFFF);
-		const int tx = (int) (ttot >> 40), tt = (int) ((ttot >> 20) & 0xFFFFF);
-		if(X + tx > XS_CAP - 1 || NTIE + tt > XS_CAP) {
-			bad = true;   // uniform
-			break;
-		}
-		if(tile == 0) XS_STAMP(12);
-		// ---- chunks with crossings or ties (few): list them, in element order
-		if(cm | tm) {
-			double Pw = P0;
-			int ci = 0, ti = 0;
-			double rw = 0;
-#pragma unroll
-			for(int m = 0; m < XS_ET; ++m) {
-				Pw += v[m];
-				if((cm >> m) & 1u) {
-					XsCross q;
-					q.v = v[m];
-					q.run = rw;
-					q.k = base + tid * XS_ET + m;
-					q.x = xs_bexp(Pw);
-					q.R = Rc;
-					q.tb = tb + ti;
-					xe[cb + ci] = q;
-					++ci;
-					rw = 0;
-				} else {
-					if((tm >> m) & 1u) {
-						XsTie q;
-						q.k = base + tid * XS_ET + m;
-						q.pi = (xs_par(rw) + xs_par(inc[m]) + 1) & 1;   // floor = inc - 1
-						q.R = Rc;
-						q.first = ci == 0;
-						te[tb + ti] = q;
-						++ti;
+				for(int e = 0; e < XW_EL; ++e) {
+					const double fe = readlane_d(fl[e], L);
+					const int k = (rb + q) * RE + XW_EL * L + e;
+					if((cmL >> e) & 1u) {
+						if(nc < XW_CAP && lane == 0) {
+							XsCross r;
+							r.v = readlane_d(x[q][e], L);
+							r.run = acc;
+							r.k = k;
+							r.x = __builtin_amdgcn_readlane(en[e], L);
+							r.R = 0;
+							r.tb = nt;
+							xw[w][nc] = r;
+						}
+						++nc;
+						acc = 0;
+					} else {
+						if((tmL >> e) & 1u) {
+							if(nt < XW_CAP && lane == 0) {
+								XsTie r;
+								r.k = k;
+								r.pi = (xs_par(acc) + xs_par(fe) + 1) & 1;   // floor = fl - 1
+								r.R = nc;                                    // local run of the tie
+								r.first = nc == 0;
+								tw[w][nt] = r;
+							}
+							++nt;
+						}
+						acc += fe;
 					}
-					rw += inc[m];
 				}
+				from = L + 1;
 			}
+			acc += wave_sum_fixed(lane >= from ? run : 0.0);
 		}
-		if(tile == 0) XS_STAMP(13);
-		// the chunk's last run: segment cb + nc (atomics on integer-valued
-		// doubles below 2^53 are exact in any order; one per wave when the
-		// wave's last runs share a segment)
-		const int seg_last = cb + nc;
-		{
-			const int s0 = __builtin_amdgcn_readfirstlane(seg_last);
-			if(__ballot(seg_last != s0) == 0ull) {
-				const double ws = wave_sum_fixed(run);
-				if(lane == 0) atomicAdd(&s_seg[s0], ws);
-			} else {
-				atomicAdd(&s_seg[seg_last], run);
-			}
-		}
-		__syncthreads();
-		if(tile == 0) XS_STAMP(14);
-		// the binade the chunk's first run assumed must be its segment's
-		bad |= ep0 != (cb == 0 ? eH : xe[cb - 1].x);
-		X += tx;
-		NTIE += tt;
-		RP += (int) (ttot & 0xFFFFF);
 	}
-	XS_STAMP(3);
+	bad |= ep_c == 0x7FF || nc > XW_CAP || nt > XW_CAP;
+	if(lane == 0) {
+		s_tail[w] = acc;
+		s_nc[w] = nc;
+		s_nt[w] = nt;
+		s_tp[w] = xs_par(acc);
+	}
 	if(bad) s_bad = 1;
+	XS_STAMP(3);
 	__syncthreads();
 	XS_STAMP(5);
+	// ---- join the waves: global record indices, segment sums, checks
+	int co[NW + 1], to[NW + 1], Rw[NW + 1];
+	co[0] = to[0] = Rw[0] = 0;
+#pragma unroll
+	for(int q = 0; q < NW; ++q) {
+		co[q + 1] = co[q] + s_nc[q];
+		to[q + 1] = to[q] + s_nt[q];
+		Rw[q + 1] = Rw[q] + s_tp[q];
+	}
+	const int nx = co[NW], ntot = to[NW];
+	if(s_bad || nx > XS_CAP - 1 || ntot > XS_CAP) return false;
+	auto cross_at = [&](int g, int *wv) -> const XsCross & {   // global crossing g -> its record
+		int q = 0;
+#pragma unroll
+		for(int z = 1; z < NW; ++z) q += g >= co[z];
+		*wv = q;
+		return xw[q][g - co[q]];
+	};
+	auto tie_at = [&](int g, int *wv) -> const XsTie & {
+		int q = 0;
+#pragma unroll
+		for(int z = 1; z < NW; ++z) q += g >= to[z];
+		*wv = q;
+		return tw[q][g - to[q]];
+	};
+	// each wave's first run must have assumed its segment's binade; its last
+	// run's sum goes to its segment
+	if(tid < NW) {
+		int wc;
+		const int want = co[tid] == 0 ? eH : cross_at(co[tid] - 1, &wc).x;
+		if(s_ex0[tid] != want) s_bad = 1;
+		atomicAdd(&s_seg[co[tid] + s_nc[tid]], s_tail[tid]);   // integer-valued: exact in any order
+	}
+	__syncthreads();
 	if(s_bad) return false;
-	const int nx = X, nt = NTIE;
-	// ---- walk (wave 0).  Lane l prepares segments l and l + 64: start binade
-	// and provisional run sum less the ties that round down, for either parity
-	// of the start (A0 / A1), and the crossing that ends it; then the chain
-	// over the segments reads them with readlane (no memory on the dependent path).
-	if(wid == 0) {
+	// ---- walk (wave 0)
+	if(w == 0) {
 		double A0[2], A1[2], cvA[2];
 		int exA[2], cxA[2];
 #pragma unroll
@@ -562,21 +573,32 @@ static __device__ bool exact_sum_t(const double *__restrict__ c, int n, double *
 			A0[h] = A1[h] = cvA[h] = 0.0;
 			exA[h] = cxA[h] = 0;
 			if(s <= nx) {
-				const double seg = s_seg[s] + (s < nx ? xe[s].run : 0.0);
-				exA[h] = s ? xe[s - 1].x : eH;
-				const int R0 = s ? xe[s - 1].R : 0;
+				int wc = 0, wn = 0;
+				double seg = s_seg[s];
+				int ta = 0, tz = ntot;
+				if(s) {
+					const XsCross &p = cross_at(s - 1, &wc);
+					exA[h] = p.x;
+					ta = to[wc] + p.tb;
+				} else {
+					exA[h] = eH;
+				}
 				if(s < nx) {
-					cvA[h] = xe[s].v;
-					cxA[h] = xe[s].x;
+					const XsCross &q = cross_at(s, &wn);
+					cvA[h] = q.v;
+					cxA[h] = q.x;
+					seg += q.run;
+					tz = to[wn] + q.tb;
 				}
 				int dn0 = 0, dn1 = 0;
-				const int ta = s ? xe[s - 1].tb : 0, tz = s < nx ? xe[s].tb : nt;
-				for(int q = ta; q < tz; ++q) {
-					int pi = te[q].pi;
-					// a run that began in an earlier chunk: the parities of the
-					// runs of the chunks from the crossing's on come before it
-					if(te[q].first) pi ^= (te[q].R - R0) & 1;
-					dn0 += 1 - ((pi + dn0) & 1);        // round up iff start + prefix + floor is odd
+				for(int g = ta; g < tz; ++g) {
+					int wt2;
+					const XsTie &t = tie_at(g, &wt2);
+					int pi = t.pi;
+					// a run that began in an earlier wave: the parities of the last
+					// runs of the waves from the crossing's on come before it
+					if(t.first) pi ^= (Rw[wt2] - Rw[wc]) & 1;
+					dn0 += 1 - ((pi + dn0) & 1);
 					dn1 += 1 - ((1 + pi + dn1) & 1);
 				}
 				A0[h] = seg - (double) dn0;
@@ -616,9 +638,6 @@ static __device__ bool exact_sum_t(const double *__restrict__ c, int n, double *
 	return !s_bad;
 }
 
-// the reference's serial row sum: the parallel form above, the chain when it declines
-
-
 // ------------------------------------------------------------------ exact row sum of j
 // Exact mode (the default): the reference's serial sum of the new row of j
 // (nj.c:911 / :1002), once per join by one 512-thread block between updateD
@@ -628,7 +647,7 @@ static __device__ bool exact_sum_t(const double *__restrict__ c, int n, double *
 // the fixed-order fold when that is provably the serial sum (integer-like
 // data), else the parallel binade-segmented form, else the chain.
 #define XS_NT 512
-#define XS_ET_BIG 16   // LDS tiles of 8192 elements
+#define XS_RB 6        // rows (of 256) per wave held in registers: one load up to n = 12288 at 512 threads
 template <int UNUSED = 0>
 __global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
 	__shared__ double s_sd;
@@ -651,7 +670,7 @@ __global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
 	if(s_stop) return;
 	double r = s_sd;
 	bool chain = false;
-	if(s_need && !exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &r)) {
+	if(s_need && !exact_sum_w<XS_NT, XS_RB>(b.contrib, n, &r)) {
 		r = serial_sum_t<XS_NT>(b.contrib, n);
 		chain = true;
 	}

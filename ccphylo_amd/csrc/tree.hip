@@ -1448,8 +1448,8 @@ __global__ __launch_bounds__(NT) void k_selftest_row_sum(TreeBufs b, int n, doub
                                                         unsigned long long *stamps) {
 	double s;
 	if(stamps && threadIdx.x == 0) stamps[15] = __builtin_amdgcn_s_memrealtime();
-	const bool ok = NT == TB ? exact_sum_t<TB, 16>(b.contrib, n, &s, stamps)
-	                         : exact_sum_t<XS_NT, XS_ET_BIG>(b.contrib, n, &s, stamps);
+	// NT = TB: 4 waves, rows reloaded past n = 6144 (the second-pass path)
+	const bool ok = exact_sum_w<NT, XS_RB>(b.contrib, n, &s, stamps);
 	if(!ok) s = serial_sum_t<NT>(b.contrib, n);
 	if(threadIdx.x == 0) {
 		out[0] = s;
@@ -1468,7 +1468,7 @@ int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out,
 	int *dpar = (int *) (dout + 1);
 	unsigned long long *dst = (unsigned long long *) (m + (size_t) (n + 1) * 8 + 64);
 	CCG_CHECK(hipMemcpyAsync(b.contrib, c, (size_t) n * 8, hipMemcpyHostToDevice, st));
-	const bool small = getenv("CCG_SELFTEST_TB256") != nullptr;   // the per-block form of the sharded engines
+	const bool small = getenv("CCG_SELFTEST_TB256") != nullptr;   // 4 waves: exercises the reload path
 	auto launch = [&](unsigned long long *stp) {
 		if(small) k_selftest_row_sum<TB><<<1, TB, 0, st>>>(b, n, dout, dpar, stp);
 		else k_selftest_row_sum<XS_NT><<<1, XS_NT, 0, st>>>(b, n, dout, dpar, stp);

@@ -1,3 +1,15 @@
+"""CPU model of the exact-mode row sum (ccg_tree_common.h exact_sum_w), used
+to validate the algorithm before the HIP version: the reference's serial sum
+s_k = fl(s_{k-1} + c_k) (nj.c:911) of non-negative c_k, computed as exact
+integer sums of per-element increments RN_u(c_k) inside runs where s keeps
+one binade [2^e, 2^(e+1)) (u = 2^(e-52)), with the real add only at the
+elements where the binade changes, and half-ulp ties resolved from the
+parity of the running total.  Chunks play the role of the GPU's lanes /
+waves.  Compares against Python's serial float sum on random, %.9f-like,
+dyadic (tie-heavy) and wide-range inputs.
+
+    python tools/sim_exact_sum.py
+"""
 # Simulation of the binade-segmented exact serial sum (validation before the HIP version)
 import math, random, sys
 import numpy as np
