@@ -40,6 +40,10 @@ struct TreeCtl {
 	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
 };
 
+struct XsBlk;
+struct XsCross;
+struct XsTie;
+
 struct TreeBufs {
 	double *sD, *Q, *contrib;
 	int *N, *P;
@@ -71,6 +75,10 @@ struct TreeBufs {
 	int *rj;             // (rows with many units)
 	ccg_join *joins;
 	TreeCtl *ctl;
+	unsigned long long *xagg;   // exact row sum over the join blocks: tagged block sums (look-back)
+	XsBlk *xblk;                // and each block's summary, crossing and tie records
+	XsCross *xcr;
+	XsTie *xti;
 	int maxu;
 };
 
@@ -636,6 +644,337 @@ static __device__ bool exact_sum_w(const double *__restrict__ c, int n, double *
 	XS_STAMP(8);
 	*out = s_out;
 	return !s_bad;
+}
+
+// ------------------------------------------------------------------ exact row sum, over the join blocks
+// The single-GPU engine splits exact_sum_w over the kernels that already
+// exist, so no kernel of its own sits between updateD and its consumers:
+//   the join kernel (k_dnj_join / k_nj_join), block g holding the
+//   contributions of elements 256g .. 256g+255 after its updateD:
+//     1. publishes its (fixed-order) block sum as a tagged 8-byte granule;
+//     2. block 0 sums the head serially; block g > 0 takes the approximate
+//        prefix from the granules of blocks 0 .. g-1 (a decoupled look-back:
+//        a block only waits on lower-indexed blocks, which are dispatched
+//        before it and never wait on it; the spin is bounded);
+//     3. runs pass 2 of exact_sum_w over its row (wave 0, 4 elements per
+//        lane) and stores its crossing / tie records and tail in HBM;
+//   the consumer (k_dnj_requeue / k_nj_pop / k_hnj_update), wave 0 of every
+//   block: joins the rows' records (prefixes over the blocks, checks) and
+//   walks the crossings (xs_walk_blocks), exactly as exact_sum_w's wave 0 does.
+// Any failed check falls back to the serial chain, in the consumer.
+#define XB_CAP 8                  // crossing / tie records per join block
+#define XS_TAG_BITS 20
+
+struct XsBlk {
+	double tail, head;   // provisional sum of the block's last run (units of its u); block 0: the head's serial sum
+	int nc, nt, tp, ex0; // records, parity of tail, predicted binade before the block's first element
+	int eh, bad, pad0, pad1;
+};
+
+__device__ __forceinline__ unsigned long long xs_granule(double a, unsigned tag) {
+	return ((unsigned long long) __double_as_longlong(a) & ~((1ull << XS_TAG_BITS) - 1)) | tag;
+}
+// tag of the join at matrix size n (consecutive joins differ; never 0, the
+// value of the zeroed buffer)
+__device__ __forceinline__ unsigned xs_tag(int n) { return (unsigned) (n % ((1 << XS_TAG_BITS) - 1)) + 1u; }
+
+// all threads of a TB-thread join block; d = contribution of element
+// TB * blk + threadIdx.x (0 where none)
+__device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigned tag) {
+	__shared__ __attribute__((aligned(16))) double s_row[TB];
+	const int tid = threadIdx.x, lane = tid & 63;
+	s_row[tid] = d;
+	__syncthreads();
+	if(tid >= 64) return;
+	double x[XW_EL];
+#pragma unroll
+	for(int e = 0; e < XW_EL; ++e) x[e] = s_row[XW_EL * lane + e];
+	// 1. publish the block sum (approximate: only predicts binades)
+	const double A = wave_sum_fixed(x[0] + x[1] + x[2] + x[3]);
+	if(lane == 0) __hip_atomic_store(b.xagg + blk, xs_granule(A, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	const int k0 = TB * blk + XW_EL * lane;
+	bool bad = false;
+#pragma unroll
+	for(int e = 0; e < XW_EL; ++e) {
+		bad |= !(x[e] >= 0.0 && x[e] <= DBL_MAX);
+		if(k0 + e < XS_HEAD) x[e] = 0.0;   // the head is summed serially
+	}
+	// 2. prefix before the row
+	double P = 0, SH = 0;
+	int eH = 0;
+	if(blk == 0) {
+		if(lane == 0) {
+			double S = 0;
+#pragma unroll
+			for(int l = 0; l < XS_HEAD; l += 2) {
+				const double2 v = *(const double2 *) (s_row + l);
+				S += v.x;
+				S += v.y;
+			}
+			SH = S;
+		}
+		SH = readlane_d(SH, 0);
+		eH = xs_bexp(SH);
+		P = SH;
+	} else {
+		for(int g0 = 0; g0 < blk; g0 += 64) {
+			const int g = g0 + lane;
+			unsigned long long u = 0;
+			bool ok = g >= blk;
+			for(int spin = 0;; ++spin) {
+				if(!ok) {
+					u = __hip_atomic_load(b.xagg + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					ok = (unsigned) (u & ((1u << XS_TAG_BITS) - 1)) == tag;
+				}
+				if(__all(ok)) break;
+				if(spin > (1 << 22)) {   // bounded: a stuck predecessor costs the serial chain, never a hang
+					bad = true;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(2);
+			}
+			const double a = g < blk && ok ? __longlong_as_double((long long) (u & ~((1ull << XS_TAG_BITS) - 1))) : 0.0;
+			P += wave_sum_fixed(a);
+		}
+	}
+	int ep_c = xs_bexp(P);
+	const int ex0 = ep_c;
+	bad |= P != 0.0 && ep_c == 0;
+	// 3. pass 2 over the row (exact_sum_w's row body)
+	int nc = 0, nt = 0;
+	double acc = 0;
+	{
+		const double cs = x[0] + x[1] + x[2] + x[3];
+		double xs = cs;
+#define S_(C, R_) xs += dpp_d<C, R_>(0.0, xs);
+		CCG_DPP_STEPS(S_)
+#undef S_
+		double Pl = P + (xs - cs);
+		double Pn[XW_EL];
+		int en[XW_EL];
+#pragma unroll
+		for(int e = 0; e < XW_EL; ++e) {
+			Pl += x[e];
+			Pn[e] = Pl;
+			en[e] = xs_bexp(Pl);
+		}
+		const int epl = dpp_i<DPP_WAVE_SHR1, 0xF>(ep_c, en[XW_EL - 1]);
+		unsigned cm = 0, tm = 0;
+		double fl[XW_EL], run = 0;
+#pragma unroll
+		for(int e = 0; e < XW_EL; ++e) {
+			const int ep = e ? en[e - 1] : epl;
+			const double t = ldexp(x[e], 1075 - ep) + 0.5;
+			fl[e] = floor(t);
+			cm |= (unsigned) (ep != en[e]) << e;
+			tm |= (unsigned) (t == fl[e]) << e;
+			run += fl[e];
+		}
+		tm &= ~cm;
+		ep_c = __builtin_amdgcn_readlane(en[XW_EL - 1], 63);
+		const unsigned long long fm = __ballot((cm | tm) != 0u);
+		if(fm == 0ull) {
+			acc = wave_sum_fixed(run);   // integers below 2^53: exact in any order
+		} else {
+			XsCross *xc = b.xcr + (size_t) blk * XB_CAP;
+			XsTie *xt = b.xti + (size_t) blk * XB_CAP;
+			int from = 0;
+			for(unsigned long long f = fm; f; f &= f - 1) {
+				const int L = __ffsll((long long) f) - 1;
+				acc += wave_sum_fixed(lane >= from && lane < L ? run : 0.0);
+				const unsigned cmL = __builtin_amdgcn_readlane(cm, L), tmL = __builtin_amdgcn_readlane(tm, L);
+#pragma unroll
+				for(int e = 0; e < XW_EL; ++e) {
+					const double fe = readlane_d(fl[e], L);
+					const int k = TB * blk + XW_EL * L + e;
+					if((cmL >> e) & 1u) {
+						if(nc < XB_CAP && lane == 0) {
+							XsCross r;
+							r.v = readlane_d(x[e], L);
+							r.run = acc;
+							r.k = k;
+							r.x = __builtin_amdgcn_readlane(en[e], L);
+							r.R = 0;
+							r.tb = nt;
+							xc[nc] = r;
+						}
+						++nc;
+						acc = 0;
+					} else {
+						if((tmL >> e) & 1u) {
+							if(nt < XB_CAP && lane == 0) {
+								XsTie r;
+								r.k = k;
+								r.pi = (xs_par(acc) + xs_par(fe) + 1) & 1;
+								r.R = nc;
+								r.first = nc == 0;
+								xt[nt] = r;
+							}
+							++nt;
+						}
+						acc += fe;
+					}
+				}
+				from = L + 1;
+			}
+			acc += wave_sum_fixed(lane >= from ? run : 0.0);
+		}
+	}
+	bad |= ep_c == 0x7FF || nc > XB_CAP || nt > XB_CAP;
+	bad = __any(bad);
+	if(lane == 0) {
+		XsBlk s;
+		s.tail = acc;
+		s.head = SH;
+		s.nc = nc;
+		s.nt = nt;
+		s.tp = xs_par(acc);
+		s.ex0 = ex0;
+		s.eh = eH;
+		s.bad = bad;
+		s.pad0 = s.pad1 = 0;
+		b.xblk[blk] = s;
+	}
+	(void) n;
+}
+
+// wave 0 of a consumer block: the serial sum from the G join blocks'
+// records; false when a check fails (the caller then runs the chain)
+__device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
+	__shared__ XsCross lc[XS_CAP];
+	__shared__ int lcR[XS_CAP], lcT[XS_CAP];   // the crossing's block: Rw, global index of its first tie
+	__shared__ XsTie lt[XS_CAP];
+	__shared__ int ltR[XS_CAP];                // the tie's block: Rw
+	__shared__ double lseg[XS_CAP + 1];
+	const int lane = threadIdx.x & 63;
+	for(int q = lane; q <= XS_CAP; q += 64) lseg[q] = 0.0;
+	const double SH = b.xblk[0].head;
+	const int eH = b.xblk[0].eh;
+	int cob = 0, tob = 0, Rwb = 0;
+	bool bad = false;
+	wave_sync();
+	for(int g0 = 0; g0 < G; g0 += 64) {
+		const int g = g0 + lane;
+		XsBlk s;
+		if(g < G) {
+			s = b.xblk[g];
+		} else {
+			s.tail = 0;
+			s.nc = s.nt = s.tp = s.ex0 = s.bad = 0;
+		}
+		bad |= s.bad || s.nc > XB_CAP || s.nt > XB_CAP;
+		int tc, tt, tr;
+		const int co = cob + wave_excl_scan(s.nc, &tc);
+		const int to = tob + wave_excl_scan(s.nt, &tt);
+		const int Rw = Rwb + wave_excl_scan(s.tp, &tr);
+		for(int c = 0; c < s.nc && c < XB_CAP; ++c) {
+			if(co + c < XS_CAP) {
+				lc[co + c] = b.xcr[(size_t) g * XB_CAP + c];
+				lcR[co + c] = Rw;
+				lcT[co + c] = to;
+			}
+		}
+		for(int t = 0; t < s.nt && t < XB_CAP; ++t) {
+			if(to + t < XS_CAP) {
+				lt[to + t] = b.xti[(size_t) g * XB_CAP + t];
+				ltR[to + t] = Rw;
+			}
+		}
+		wave_sync();
+		if(g < G) {
+			// the block's first run must have assumed its segment's binade; its
+			// last run's sum goes to its segment (integer-valued: exact in any order)
+			const int want = co == 0 ? eH : co - 1 < XS_CAP ? lc[co - 1].x : -1;
+			bad |= s.ex0 != want;
+			if(co + s.nc <= XS_CAP) atomicAdd(&lseg[co + s.nc], s.tail);
+			else bad = true;
+		}
+		cob += tc;
+		tob += tt;
+		Rwb += tr;
+	}
+	const int nx = cob, ntot = tob;
+	bad = __any(bad) || nx > XS_CAP - 1 || ntot > XS_CAP;
+	if(bad) return false;
+	wave_sync();
+	// ---- per segment: its increment for an even / odd start (ties rounded to even)
+	double A0[2], A1[2], cvA[2];
+	int exA[2], cxA[2];
+#pragma unroll
+	for(int h = 0; h < 2; ++h) {
+		const int s = lane + 64 * h;
+		A0[h] = A1[h] = cvA[h] = 0.0;
+		exA[h] = cxA[h] = 0;
+		if(s <= nx) {
+			double seg = lseg[s];
+			int ta = 0, tz = ntot, Rc = 0;
+			if(s) {
+				const XsCross &p = lc[s - 1];
+				exA[h] = p.x;
+				ta = lcT[s - 1] + p.tb;
+				Rc = lcR[s - 1];
+			} else {
+				exA[h] = eH;
+			}
+			if(s < nx) {
+				const XsCross &q = lc[s];
+				cvA[h] = q.v;
+				cxA[h] = q.x;
+				seg += q.run;
+				tz = lcT[s] + q.tb;
+			}
+			int dn0 = 0, dn1 = 0;
+			for(int g = ta; g < tz; ++g) {
+				const XsTie &t = lt[g];
+				int pi = t.pi;
+				// a run that began in an earlier block: the parities of the last runs
+				// of the blocks from the crossing's on come before it
+				if(t.first) pi ^= (ltR[g] - Rc) & 1;
+				dn0 += 1 - ((pi + dn0) & 1);
+				dn1 += 1 - ((1 + pi + dn1) & 1);
+			}
+			A0[h] = seg - (double) dn0;
+			A1[h] = seg - (double) dn1;
+		}
+	}
+	// ---- the walk
+	double S = SH;
+	bool ok = (eH > 0 && eH < 0x7FF) || (SH == 0.0 && lseg[0] == 0.0);
+	for(int s = 0; s <= nx; ++s) {
+		const int h = s >> 6, l = s & 63;
+		if(s > 0 || eH > 0) {
+			const int exs = __builtin_amdgcn_readlane(h ? exA[1] : exA[0], l);
+			const double a0 = readlane_d(h ? A0[1] : A0[0], l), a1 = readlane_d(h ? A1[1] : A1[0], l);
+			const int ue = exs - 1075;
+			ok = ok && exs > 0 && exs < 0x7FF && xs_bexp(S) == exs;
+			const double T0 = ldexp(S, -ue);
+			const double T = T0 + (((unsigned) __double_as_longlong(T0) & 1u) ? a1 : a0);
+			ok = ok && T < 9007199254740992.0;
+			S = ldexp(T, ue);
+		}
+		if(s < nx) {
+			const double Sn = S + readlane_d(h ? cvA[1] : cvA[0], l);
+			ok = ok && xs_bexp(Sn) == __builtin_amdgcn_readlane(h ? cxA[1] : cxA[0], l);
+			S = Sn;
+		}
+	}
+	*out = S;
+	return ok;
+}
+
+// wave 0 of a consumer (k_dnj_requeue / k_nj_pop / k_hnj_update): the new
+// row sum of j and its count.  *chain: the whole block must run the serial
+// chain over b.contrib (rare: a failed check of the parallel form).
+__device__ void row_sum_j_wave(const TreeBufs &b, int n, bool exact, bool general, double *sd, int *nj, bool *need,
+                               bool *chain) {
+	const int G = (int) cdiv(n, TB);
+	fold_update_wave(b, G, exact, general, sd, nj, need);
+	*chain = false;
+	if(*need) {
+		double r;
+		if(xs_walk_blocks(b, G, &r)) *sd = r;
+		else *chain = true;
+	}
 }
 
 // ------------------------------------------------------------------ exact row sum of j

@@ -125,6 +125,9 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 		cnt = 1;
 	}
 	update_partials(b, n, exact, k, d, cnt, slot);
+	// exact mode: this block's row of the serial row sum (xs_join_row; the
+	// consumer walks the rows' records)
+	if(exact) xs_join_row(b, n, slot, d, xs_tag(n));   // tag: the matrix size, one per join and uniform over the grid
 }
 
 
@@ -486,7 +489,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
 	__shared__ int si[5][TB / 64], sfp[TB / 64];
 	__shared__ double s_sd;
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
 	const int nn = n - 1;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -516,25 +519,27 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		if(!done) {
 			double sd;
 			int nj;
-			bool need;
-			if(exact && !general) {   // k_exact_sum ran
-				sd = ctl->xsum;
-				nj = ctl->xnj;
-				need = false;
-			} else {
-				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
-			}
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, general, &sd, &nj, &need, &chain);
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
 				s_serial = need;
+				s_chain = chain;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j, Nj = s_nj;
-	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
+	// exact mode, a failed check of the parallel form: the serial chain (all threads)
+	if(s_chain) {
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
 	TS(4, 1);
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict
 template <int ET>
 __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, int general) {
 	__shared__ double s_sd;
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
 	const int nn = n - 1;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -869,25 +874,27 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 		if(!done) {
 			double sd;
 			int nj;
-			bool need;
-			if(exact && !general) {   // k_exact_sum ran
-				sd = ctl->xsum;
-				nj = ctl->xnj;
-				need = false;
-			} else {
-				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
-			}
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, general, &sd, &nj, &need, &chain);
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
 				s_serial = need;
+				s_chain = chain;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
+	// exact mode, a failed check of the parallel form: the serial chain (all threads)
+	if(s_chain) {
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = s_nj;
@@ -1030,7 +1037,7 @@ template <int ET>
 __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int general) {
 	__shared__ double s_sd, sq[TB / 64], sq2[TB / 64];
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, sk[TB / 64], sk2[TB / 64];
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain, sk[TB / 64], sk2[TB / 64];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 	const int k = (int) blockIdx.x * TB + tid;
@@ -1045,25 +1052,27 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 		if(!done) {
 			double sd;
 			int nj;
-			bool need;
-			if(exact && !general) {   // k_exact_sum ran
-				sd = ctl->xsum;
-				nj = ctl->xnj;
-				need = false;
-			} else {
-				fold_update_wave(b, (int) cdiv(n, TB), exact, general, &sd, &nj, &need);
-			}
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, general, &sd, &nj, &need, &chain);
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
 				s_serial = need;
+				s_chain = chain;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_sd;   // exact: k_exact_sum's (fold_update_wave never asks for the serial order here)
+	// exact mode, a failed check of the parallel form: the serial chain (all threads)
+	if(s_chain) {
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
 	const int nj = s_nj;
 	const int nn = n - 1;
 	const bool move = i != nn;
@@ -1192,6 +1201,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nrf = ncand > JOIN_UPRE ? ncand : JOIN_UPRE;   // k_dnj_join prefetches JOIN_UPRE
 	size_t o_bq = take(nb * 8), o_br = take(nb * 4), o_sp = take((DNJ_B + 1) * 4), o_cs = take(ncand * 4);
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
+	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
+	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
 	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
@@ -1235,6 +1246,10 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.rf = (double *) (m + o_rf);
 	b.rj = (int *) (m + o_rj);
 	b.ctl = (TreeCtl *) (m + o_ctl);
+	b.xagg = (unsigned long long *) (m + o_xa);
+	b.xblk = (XsBlk *) (m + o_xb);
+	b.xcr = (XsCross *) (m + o_xc);
+	b.xti = (XsTie *) (m + o_xt);
 	b.maxu = (int) maxu;
 	return CCG_OK;
 }
@@ -1245,7 +1260,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
                              int method, int exact, KTimer &kt) {
 	const unsigned gn = cdiv(n, TB);
 	const int general = GEN;
-	const int xs = exact && !GEN;   // the exact row sum as its own block (k_exact_sum)
+	const int xs = 0;   // exact row sums: split over the join kernel and its consumer (xs_join_row, xs_walk_blocks)
 	if(method == CCG_TREE_DNJ) {
 		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
