@@ -35,7 +35,7 @@ struct DenseRows {
 // that the unit pruning of later grid waves runs at small n).
 struct DnjGrid {
 	int sel_max = SEL_BLOCKS, scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
-	int s_top = 0, s_bands = -1, s_split_n = 16384;
+	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0;
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
@@ -45,6 +45,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_SCAN_MAX")) scan_max = atoi(e) > 0 ? atoi(e) : 2048;
 		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
+		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
@@ -759,6 +760,479 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 	}
 	if(bands && tid < nS) b.Spos[tid] = spos;
 	TS(1, 2);
+	TS_EXIT(1);
+}
+
+// ------------------------------------------------------------------ DNJ plan (one-phase search)
+// One block of TBF threads, before any rescan of the join; it replaces
+// k_dnj_select's prologue + k_dnj_find, so S and the rows below it are
+// rescanned in ONE phase (k_dnj_scan):
+//   wave 0: the previous join's updateDNJ / DNJ_popArrange fold, minPos and
+//   minQpair's start (dnj.c:1026-1032, :55-60), S (as k_dnj_select);
+//   the bound of the rows below S, from each S row k's Q criterion at its
+//   stored partner column P[k] evaluated now: fresh_k is the minimum over all
+//   of row k's columns, so q(k, P[k]) >= fresh_k and max(q(k, P[k]), Q_k)
+//   bounds minQpair's running min below row k as max(fresh_k, Q_k) does (a
+//   rescanned row leaves m <= fresh_k, a skipped one m <= Q_k; any subset of
+//   S gives a looser, still valid bound).  The partner is the fresh minimum
+//   in ~94% of S rows and the same rows qualify (tools/sim_bound.c, N=10k:
+//   120.0 rest rows per join either way);
+//   the entry list in scan order (descending rows: S, then the rows below
+//   with Q < their bound, band rows of S merged in) with SEG-cell unit
+//   offsets (crow / cbnd / coff, ctl->T), read by k_dnj_scan and k_dnj_join
+//   (which sees nS = 0: every entry is an "rest" entry).
+// Rows j and i of the previous join have their Q/P in the requeue partials
+// (substituted here, persisted by thread 0); the moved row i's sD/N (row n's)
+// are substituted as column and persisted for the kernels after.
+template <int ET, bool GEN, class Rows, bool BANDS>
+__global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                  int n, int first, Rows rows, int seg, int ktop, int kbands,
+                                                  int qdelay) {
+	// wave 0 folds and selects S; waves 1.. (LT threads) hold the rows of the
+	// listing and the speculative partner cells (their loads sit in the other
+	// branch of wave 0's prologue, so the two share registers)
+	constexpr int NW = TBF / 64, FR = FIND_RPT, NSP = TBF - 64, LT = TBF - 64, LW = NW - 1;
+	__shared__ int sS[DNJ_B];
+	__shared__ double sQS[DNJ_B], sQP[DNJ_B];   // S rows: Q, and the Q criterion at the partner cell (band rows)
+	__shared__ double spq[NSP];                 // the Q criterion at the partner cell of row top - t
+	__shared__ double spm[DNJ_B + 2];           // bound below S row t (prefix over S in scan order)
+	__shared__ int s_mw[FR * LW], s_mu[FR * LW], s_cnt, s_ucnt;
+	__shared__ int sch[FIND_CHUNKS];
+	__shared__ int s_done, s_isub, s_jsub, s_nS, s_ntop, s_smin, s_Nm, s_utop;
+	__shared__ double s_m0, s_Qj, s_Qi, s_sDm;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int top = n - 1;
+	TS_ENTRY(1);
+	TS(1, 0);
+	const int lt = tid - 64;   // listing thread (waves 1..)
+	double qv[FR];
+	const int rt = top - lt;
+	bool have_rt = false;
+	int pr = 0, nr = n, np = n;
+	double dpr = -1.0, sdr = 0.0, sdp = 0.0;
+	if(wid > 0) {
+		// ---- loads that do not depend on the fold: the partner cell of the
+		// top LT rows (speculative: S is not known yet), and Q of the listed
+		// rows in descending (m, lt) order, the bulk, held back by qdelay x 32 x
+		// 64 cycles so that wave 0's fold loads are not queued behind them
+		have_rt = rt >= 1 && rows.owns(rt);
+		if(have_rt) {
+			pr = b.P[rt];
+			pr = pr >= 0 && pr < rt ? pr : 0;
+			sdr = b.sD[rt];
+			dpr = Elem<ET>::get(D[rows.row(rt) + pr], bs);
+			sdp = b.sD[pr];
+			if(GEN) {
+				nr = b.N[rt];
+				np = b.N[pr];
+			}
+		}
+		for(int d = 0; d < qdelay; ++d) __builtin_amdgcn_s_sleep(32);
+#pragma unroll
+		for(int m = 0; m < FR; ++m) {
+			const int r = top - (m * LT + lt);
+			qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+		}
+	} else {
+		// ---- k_dnj_select's prologue: fold, minPos, m0, S
+		const int done = ctl->done;
+		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
+		const int cand0 = first ? ctl->cand : 0;
+		const double cand0_q = first ? ctl->cand_q : 0.0;
+		const int cand0_p = first ? ctl->cand_p : 0;
+		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, cq1 = DBL_MAX;
+		int ix[4] = {0, -1, 0, -1}, cp1 = 0;
+		__builtin_amdgcn_s_setprio(3);   // wave 0's loads first: the fold is the critical path
+		if(!first) {
+			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
+			for(int w = lane; w < G; w += 64) {
+				double oq[4], ocq;
+				int oi[4], ocp;
+#pragma unroll
+				for(int t = 0; t < 4; ++t) {   // every load issued before the first compare
+					oq[t] = b.qpart[4 * w + t];
+					oi[t] = b.ipart[4 * w + t];
+				}
+				ocq = b.cfq[w];
+				ocp = b.cfp[w];
+#pragma unroll
+				for(int t = 0; t < 4; ++t) {
+					if(qarg_better(oq[t], oi[t], q[t], ix[t])) {
+						q[t] = oq[t];
+						ix[t] = oi[t];
+						if(t == 1) {
+							cq1 = ocq;
+							cp1 = ocp;
+						}
+					}
+				}
+			}
+		}
+		// band candidates: lane l holds the min-Q row of the requeue blocks
+		// [l G / kbands, (l + 1) G / kbands) with its partner, and loads that
+		// partner's cell right away
+		double bcq = DBL_MAX, bd = -1.0, bsr = 0.0, bsp = 0.0;
+		int bcr = 0, bcp = 0, bnr = n, bnp = n;
+		if(BANDS && !first && lane < kbands) {
+			const int G = (int) cdiv(n + 1, TB);
+			const int ga = lane * G / kbands, gz = (lane + 1) * G / kbands;
+			for(int g0 = ga; g0 < gz; g0 += 4) {
+				double oq[4];
+				int orr[4], op[4];
+#pragma unroll
+				for(int m = 0; m < 4; ++m) {   // 4 loads in flight per array
+					const int g = g0 + m < gz ? g0 + m : gz - 1;
+					oq[m] = b.bmq[g];
+					orr[m] = b.bmr[g];
+					op[m] = b.bmp[g];
+				}
+#pragma unroll
+				for(int m = 0; m < 4; ++m) {
+					if(g0 + m < gz && qarg_better(oq[m], orr[m], bcq, bcr)) {
+						bcq = oq[m];
+						bcr = orr[m];
+						bcp = op[m];
+					}
+				}
+			}
+			if(bcr >= 1 && rows.owns(bcr)) {
+				bcp = bcp >= 0 && bcp < bcr ? bcp : 0;
+				bd = Elem<ET>::get(D[rows.row(bcr) + bcp], bs);
+				bsr = b.sD[bcr];
+				bsp = b.sD[bcp];
+				if(GEN) {
+					bnr = b.N[bcr];
+					bnp = b.N[bcp];
+				}
+			}
+		}
+		double topQ[SEL_RPL];
+#pragma unroll
+		for(int m = 0; m < SEL_RPL; ++m) {
+			const int r = n - 1 - (m * 64 + lane);
+			topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+		}
+		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
+		const int Nm = first ? 0 : b.N[n];
+		if(done) {
+			if(lane == 0) s_done = 1;
+		} else {
+			TS(1, 5);
+			qarg_wave_reduce(q[0], ix[0]);
+			qarg_wave_reduce_carry(q[1], ix[1], cq1, cp1);
+			qarg_wave_reduce(q[2], ix[2]);
+			qarg_wave_reduce(q[3], ix[3]);
+			const int nn = n;
+			const bool move = !first && i != nn;
+			const int isub = move ? i : -1, jsub = first ? -1 : j;
+			const double Qj = q[0], Qi = q[2];
+			const int Pj = ix[0], Pi = ix[2];
+#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : (r) == ix[1] ? cq1 : (r) == ix[3] ? q[3] : DBL_MAX)
+#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : (r) == ix[1] ? cp1 : (r) == ix[3] ? i : 0)
+			int cand;
+			if(first) {
+				cand = cand0;
+			} else {
+				int p = j;
+				if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
+				int p2 = 0;
+				if(move) {
+					p2 = i;
+					if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
+				}
+				if(p2 == nn) {
+					cand = p;
+				} else if(p == nn) {
+					cand = p2;
+				} else {
+					double Qp = QSUB(p), Qp2 = QSUB(p2);
+					cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
+				}
+			}
+			const double Qc = !cand ? DBL_MAX : first ? cand0_q : QSUB(cand);
+			double m0 = DBL_MAX;
+			if(cand && m0 != Qc) m0 = Qc;
+			const int pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
+			const int pos_j = (cand && m0 != DBL_MAX) ? (first ? cand0_p : PSUB(cand)) : 0;
+#undef QSUB
+#undef PSUB
+			TS(1, 6);
+			// ---- S, top part: ktop rows with Q < m0 from the top
+			int cnt = 0;
+			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop; base -= 64 * SEL_RPL, ++step) {
+#pragma unroll
+				for(int m = 0; m < SEL_RPL; ++m) {
+					if(cnt >= ktop) continue;   // uniform
+					const int r = base - (m * 64 + lane);
+					if(step) topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+					const double v = r == jsub ? Qj : r == isub ? Qi : topQ[m];
+					const bool f = r >= 1 && v < m0;
+					const unsigned long long bm = __ballot(f);
+					const int pos = cnt + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm >> 32),
+					                                                     __builtin_amdgcn_mbcnt_lo((unsigned) bm, 0));
+					if(f && pos < ktop) {
+						sS[pos] = r;
+						sQS[pos] = v;
+					}
+					cnt += __popcll(bm);
+				}
+			}
+			const int ntop = cnt < ktop ? cnt : ktop;
+			int nS = ntop;
+			const int smin = ntop == ktop ? sS[ktop - 1] : 1;
+			// ---- S, band part (large n): each band's min-Q row below the top
+			// part, with the Q criterion at its partner cell (rows j and i of the
+			// previous join are never band candidates)
+			if(BANDS && smin > 1 && kbands) {
+				const bool f = bcr >= 1 && bcr < smin && bcq < m0;
+				const unsigned long long bm = __ballot(f);
+				const int pos = ntop + __popcll(lane == 63 ? 0ull : bm >> (lane + 1));
+				if(f) {
+					const bool pm = bcp == isub;
+					sS[pos] = bcr;
+					sQS[pos] = bcq;
+					sQP[pos] = 0 <= bd ? qcrit(GEN ? bnr : n, GEN ? (pm ? Nm : bnp) : n, bd, bsr, pm ? sDm : bsp)
+					                   : DBL_MAX;
+				}
+				nS = ntop + __popcll(bm);
+			}
+			wave_sync();
+			TS(1, 7);
+			// ---- the top part is the head of the entry list: rows, bounds, units
+			const int t0 = 2 * lane, t1 = 2 * lane + 1;
+			const int r0 = t0 < ntop ? sS[t0] : 0, r1 = t1 < ntop ? sS[t1] : 0;
+			const int u0 = t0 < ntop && rows.owns(r0) ? dcdiv(r0, seg) : 0;
+			const int u1 = t1 < ntop && rows.owns(r1) ? dcdiv(r1, seg) : 0;
+			int utot;
+			const int upre = wave_excl_scan(u0 + u1, &utot);
+			if(t0 < ntop) {
+				b.crow[t0] = r0;
+				b.cbnd[t0] = sQS[t0];
+				b.coff[t0] = upre;
+			}
+			if(t1 < ntop) {
+				b.crow[t1] = r1;
+				b.cbnd[t1] = sQS[t1];
+				b.coff[t1] = upre + u0;
+			}
+			const long long ctop = wave_sum_int((long long) (u0 ? r0 : 0) + (u1 ? r1 : 0));
+			if(lane == 0) {
+				if(!first) {   // persist the fold for the kernels after
+					b.Q[j] = Qj;
+					b.P[j] = Pj;
+					if(move) {
+						b.Q[i] = Qi;
+						b.P[i] = Pi;
+						b.sD[i] = sDm;
+						b.N[i] = Nm;
+					}
+				}
+				ctl->cand = cand;
+				ctl->m0 = m0;
+				ctl->pos_i = pos_i;
+				ctl->pos_j = pos_j;
+				ctl->nS = 0;     // k_dnj_join: every entry is in the list
+				ctl->ntop = 0;
+				ctl->smin = smin;
+				if(ctop) {
+					atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) ctop);
+					atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) ctop);
+				}
+				s_done = 0;
+				s_nS = nS;
+				s_ntop = ntop;
+				s_smin = smin;
+				s_isub = isub;
+				s_jsub = jsub;
+				s_Qj = Qj;
+				s_Qi = Qi;
+				s_m0 = m0;
+				s_Nm = Nm;
+				s_sDm = sDm;
+				s_utop = utot;
+			}
+		}
+		__builtin_amdgcn_s_setprio(0);
+#pragma unroll
+		for(int m = 0; m < FR; ++m) qv[m] = DBL_MAX;   // wave 0 lists no rows
+	}
+	__syncthreads();
+	TS(1, 1);
+	if(s_done) return;
+	const int nS = s_nS, ntop = s_ntop, smin = s_smin, isub = s_isub, jsub = s_jsub;
+	const double m0 = s_m0;
+	// ---- the Q criterion at the partner cell of the top rows, with the fold's
+	// substitutions (rows j and i have a new partner in the partials: left
+	// out, which only loosens the bound)
+	if(wid > 0) {
+		double qp = DBL_MAX;
+		if(have_rt && rt != isub && rt != jsub && 0 <= dpr) {
+			const bool pm = pr == isub;
+			qp = qcrit(GEN ? nr : n, GEN ? (pm ? s_Nm : np) : n, dpr, sdr, pm ? s_sDm : sdp);
+		}
+		spq[lt] = qp;
+	}
+	__syncthreads();
+	// ---- the bound below each S row: prefix min over S in scan order of
+	// max(q at the partner, Q), starting at m0 (S spans at most 2 waves)
+	double U;
+	{
+		double v = DBL_MAX;
+		if(tid < nS) {
+			const int r = sS[tid];
+			const double qk = tid >= ntop ? sQP[tid] : top - r < NSP ? spq[top - r] : DBL_MAX;
+			const double Qk = sQS[tid];
+			v = qk > Qk ? qk : Qk;
+		}
+		const double x = wave_incl_min(v);
+		if(wid < 2 && lane == 63) spm[DNJ_B + wid] = x;
+		__syncthreads();
+		double c = m0;
+		if(wid == 1) c = spm[DNJ_B] < c ? spm[DNJ_B] : c;
+		if(tid < nS) spm[tid] = x < c ? x : c;
+		__syncthreads();
+		U = ntop ? spm[ntop - 1] : m0;   // every row below the top part is under it
+	}
+	TS(1, 2);
+	// ---- S rows above row r (band mode): chunk table, as k_dnj_find
+	const bool bands = BANDS && nS > ntop;
+	const int nch0 = smin > 1 && bands ? ((smin - 1) >> 6) + 1 : 0;
+	const bool table = nch0 <= FIND_CHUNKS;
+	const int nch = table ? nch0 : 0;
+	for(int c = tid; c < nch; c += TBF) {
+		int lo = ntop, hi = nS;
+		while(lo < hi) {
+			const int mid = (lo + hi) >> 1;
+			if(sS[mid] >= 64 * (c + 1)) lo = mid + 1; else hi = mid;
+		}
+		sch[c] = lo;
+	}
+	if(nch) __syncthreads();
+	auto s_above = [&](int r) {
+		int k;
+		if(table) {
+			k = sch[r >> 6];
+			while(k < nS && sS[k] > r) ++k;
+		} else {
+			int lo = ntop, hi = nS;
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(sS[mid] > r) lo = mid + 1; else hi = mid;
+			}
+			k = lo;
+		}
+		return k;
+	};
+	// ---- the rest of the entry list, after the top part: rows [1, smin) that
+	// are band rows of S or have Q < their bound, with positions and unit
+	// offsets from one prefix over (step, wave) counts
+	int T = ntop, UT = s_utop;
+	long long mycells = 0;
+	if(smin > 1) {
+		for(int base = top; base >= 1; base -= LT * FR) {
+			if(base != top && wid > 0) {
+#pragma unroll
+				for(int m = 0; m < FR; ++m) {
+					const int r = base - (m * LT + lt);
+					qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+				}
+			}
+			unsigned long long bm[FR];
+#pragma unroll
+			for(int m = 0; m < FR; ++m) bm[m] = 0ull;
+			const int mlim = (base - 1) / LT + 1 < FR ? (base - 1) / LT + 1 : FR;   // slots holding rows >= 1
+#pragma unroll
+			for(int m = 0; m < FR; ++m) {
+				if(m >= mlim) continue;   // uniform; no break: the loop stays unrolled (registers, not scratch)
+				const int r = wid > 0 ? base - (m * LT + lt) : 0;
+				qv[m] = r == jsub ? s_Qj : r == isub ? s_Qi : qv[m];
+				bool f = false;
+				if(r >= 1 && r < smin && rows.owns(r)) {
+					if(bands) {
+						const int t = s_above(r);
+						f = (t < nS && sS[t] == r) || qv[m] < (t ? spm[t - 1] : m0);
+					} else {
+						f = qv[m] < U;
+					}
+				}
+				mycells += f ? r : 0;
+				bm[m] = __ballot(f);
+				const int ut = bm[m] ? wave_sum_int(f ? dcdiv(r, seg) : 0) : 0;   // uniform branch
+				if(lane == 0 && wid > 0) {
+					s_mw[m * LW + wid - 1] = __popcll(bm[m]);
+					s_mu[m * LW + wid - 1] = ut;
+				}
+			}
+			if(lane == 0 && wid > 0) {
+#pragma unroll
+				for(int m = 0; m < FR; ++m)
+					if(m >= mlim) s_mw[m * LW + wid - 1] = s_mu[m * LW + wid - 1] = 0;
+			}
+			__syncthreads();
+			if(wid == 0) {
+				constexpr int NC = FR * LW, PER = (NC + 63) / 64;
+				int c[PER], cu[PER], sum = 0, usum = 0;
+#pragma unroll
+				for(int k = 0; k < PER; ++k) {
+					const int x = lane * PER + k;
+					c[k] = x < NC ? s_mw[x] : 0;
+					cu[k] = x < NC ? s_mu[x] : 0;
+					sum += c[k];
+					usum += cu[k];
+				}
+				int tot, utot;
+				int pre = wave_excl_scan(sum, &tot), upre = wave_excl_scan(usum, &utot);
+#pragma unroll
+				for(int k = 0; k < PER; ++k) {
+					const int x = lane * PER + k;
+					if(x < NC) {
+						s_mw[x] = pre;
+						s_mu[x] = upre;
+					}
+					pre += c[k];
+					upre += cu[k];
+				}
+				if(lane == 0) {
+					s_cnt = tot;
+					s_ucnt = utot;
+				}
+			}
+			__syncthreads();
+#pragma unroll
+			for(int m = 0; m < FR; ++m) {
+				if(bm[m] == 0ull) continue;   // uniform (always for wave 0)
+				const int r = base - (m * LT + lt);
+				const bool f = (bm[m] >> lane) & 1ull;
+				int ut;
+				const int uex = wave_excl_scan(f ? dcdiv(r, seg) : 0, &ut);   // recomputed: no registers held across the barriers
+				if(f) {
+					const int pos = T + s_mw[m * LW + wid - 1] +
+					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
+					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
+					b.crow[pos] = r;
+					b.cbnd[pos] = qv[m];
+					b.coff[pos] = UT + s_mu[m * LW + wid - 1] + uex;
+				}
+			}
+			T += s_cnt;
+			UT += s_ucnt;
+			if(base - LT * FR < 1) break;
+			__syncthreads();   // s_mw / s_mu are reused by the next step
+		}
+	}
+	TS(1, 3);
+	mycells = wave_sum_int(mycells);
+	if(lane == 0 && mycells) {
+		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) mycells);
+		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) mycells);
+	}
+	if(tid == 0) {
+		ctl->T = T;
+		b.coff[T] = UT;
+		ctl->rows += T;
+	}
+	TS(1, 4);
 	TS_EXIT(1);
 }
 

@@ -68,7 +68,7 @@ struct TreeBufs {
 	int *cfp;            // column-j (q, idx) partial, carried to the fold
 	long long *fpart;
 	double *bmq;         // requeue: each block's min-Q row (candidates of the next S)
-	int *bmr;
+	int *bmr, *bmp;      // and its partner P
 	int *Spos;           // entry slot of each S row in the descending scan order
 	int *cslot;          // and of each rest entry (k_dnj_find)
 	double *rf;          // per rest entry: fresh (q, j) folded once by k_dnj_fold

@@ -487,7 +487,7 @@ template <int ET, bool BANDS>
 __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, int general) {
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
-	__shared__ int si[5][TB / 64], sfp[TB / 64];
+	__shared__ int si[5][TB / 64], sfp[TB / 64], sbp[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
@@ -611,14 +611,15 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
 	// fold); only when the next S has a band part
-	double bq = DBL_MAX;
-	int bk = 0;
+	double bq = DBL_MAX, bdum = 0.0;
+	int bk = 0, bp = 0;
 	if(BANDS) {
 		if(k >= 1 && k < nn && k != i && k != j) {
 			bq = k > j ? fq : qk0;
 			bk = k;
+			bp = k > j ? fp : pkk0;   // its partner, for k_dnj_plan's partner-cell bound
 		}
-		qarg_wave_reduce(bq, bk);
+		qarg_wave_reduce_carry(bq, bk, bdum, bp);
 	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
@@ -638,23 +639,26 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		if(BANDS) {
 			sq[4][wid] = bq;
 			si[4][wid] = bk;
+			sbp[wid] = bp;
 		}
 	}
 	__syncthreads();
 	if(tid < (BANDS ? 5 : 4)) {
 		double q = sq[tid][0], cq = sfq[0];
-		int ix = si[tid][0], cp = sfp[0];
+		int ix = si[tid][0], cp = sfp[0], xp = BANDS ? sbp[0] : 0;
 		for(int w = 1; w < TB / 64; ++w) {
 			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
 				q = sq[tid][w];
 				ix = si[tid][w];
 				cq = sfq[w];
 				cp = sfp[w];
+				if(BANDS) xp = sbp[w];
 			}
 		}
 		if(tid == 4) {
 			b.bmq[blockIdx.x] = q;
 			b.bmr[blockIdx.x] = ix;
+			b.bmp[blockIdx.x] = xp;
 		} else {
 			b.qpart[4 * blockIdx.x + tid] = q;
 			b.ipart[4 * blockIdx.x + tid] = ix;
@@ -1199,6 +1203,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_fp = take(nq * 8), o_cfq = take(nb * 8), o_cfp = take(nb * 4);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	const size_t nrf = ncand > JOIN_UPRE ? ncand : JOIN_UPRE;   // k_dnj_join prefetches JOIN_UPRE
+	size_t o_bp = take(nb * 4);
 	size_t o_bq = take(nb * 8), o_br = take(nb * 4), o_sp = take((DNJ_B + 1) * 4), o_cs = take(ncand * 4);
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
@@ -1241,6 +1246,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.joins = (ccg_join *) (m + o_j);
 	b.bmq = (double *) (m + o_bq);
 	b.bmr = (int *) (m + o_br);
+	b.bmp = (int *) (m + o_bp);
 	b.Spos = (int *) (m + o_sp);
 	b.cslot = (int *) (m + o_cs);
 	b.rf = (double *) (m + o_rf);
@@ -1264,10 +1270,11 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	if(method == CCG_TREE_DNJ) {
 		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
-		k_dnj_select<ET, GEN><<<gs, TB, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n));
-		kt.mark(CCG_K_TOP);
-		if(g_grid.bands(n)) k_dnj_find<DenseRows, true><<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
-		else k_dnj_find<DenseRows, false><<<1, TBF, 0, st>>>(b, n, DenseRows(), seg);
+		// one-phase search: k_dnj_plan lists S and the rows below it under the
+		// partner-cell bound, k_dnj_scan rescans them all
+		(void) gs;
+		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
+		else k_dnj_plan<ET, GEN, DenseRows, false><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
 		kt.mark(CCG_K_FIND);
 		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n);
@@ -1282,7 +1289,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general);
 		kt.mark(CCG_K_REQUEUE);
-		return (GEN ? 6 : 5) + prefold + xs;
+		return (GEN ? 5 : 4) + prefold + xs;
 	}
 	if(method == CCG_TREE_HNJ) {
 		k_hnj_argmin<><<<gn, TB, 0, st>>>(b, n);
@@ -1397,27 +1404,35 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		// times in us relative to the kernel's first block entry, averaged over joins
 		double acc[NKT][16] = {{0}}, gap[NKT] = {0}, itv = 0;
 		int cnt = 0;
+		bool present[NKT] = {false};   // kernels launched in this pipeline (k_dnj_select is not)
+		for(int s = 0; s < 256; ++s)
+			for(int k = 0; k < nk; ++k) present[k] = present[k] || tr[(s * NKT + k) * 16 + 15];
 		for(int s = 0; s < 256; ++s) {
 			const unsigned long long *e = tr + s * NKT * 16;
 			bool ok = true;
-			for(int k = 0; k < nk; ++k) ok = ok && e[k * 16 + 15] && e[k * 16 + 14];
+			for(int k = 0; k < nk; ++k) ok = ok && (!present[k] || (e[k * 16 + 15] && e[k * 16 + 14]));
 			if(!ok) continue;
 			++cnt;
-			for(int k = 0; k < nk; ++k) {
+			int k0 = 0, prev = -1;
+			while(k0 < nk && !present[k0]) ++k0;
+			for(int k = k0; k < nk; ++k) {
+				if(!present[k]) continue;
 				unsigned long long t0 = ~e[k * 16 + 15];
 				for(int p = 0; p < 15; ++p)
 					if(e[k * 16 + p]) acc[k][p] += ((double) e[k * 16 + p] - (double) t0) / 100.0;
-				if(k) gap[k] += ((double) t0 - (double) e[(k - 1) * 16 + 14]) / 100.0;
+				if(prev >= 0) gap[k] += ((double) t0 - (double) e[prev * 16 + 14]) / 100.0;
+				prev = k;
 			}
-			if(s + 1 < 256 && tr[(s + 1) * NKT * 16 + 15]) {
-				gap[0] += ((double) ~tr[(s + 1) * NKT * 16 + 15] - (double) e[(nk - 1) * 16 + 14]) / 100.0;
-				itv += ((double) ~tr[(s + 1) * NKT * 16 + 15] - (double) ~e[15]) / 100.0;
+			if(s + 1 < 256 && tr[((s + 1) * NKT + k0) * 16 + 15]) {
+				gap[k0] += ((double) ~tr[((s + 1) * NKT + k0) * 16 + 15] - (double) e[(nk - 1) * 16 + 14]) / 100.0;
+				itv += ((double) ~tr[((s + 1) * NKT + k0) * 16 + 15] - (double) ~e[k0 * 16 + 15]) / 100.0;
 			}
 		}
-		const char *kn[NKT] = {"select", "find", "scan", "join", "requeue"};
+		const char *kn[NKT] = {"select", "plan/find", "scan", "join", "requeue"};
 		fprintf(stderr, "trace: %d joins at n <= %d; iteration %.2f us; serial replays %d, serial sums %d\n", cnt,
 		        trace_hi, cnt ? itv / (cnt - 1) : 0, h.serial_replays, h.serial_sums);
 		for(int k = 0; k < nk && cnt; ++k) {
+			if(!present[k]) continue;
 			fprintf(stderr, "  %-14s gap-before %6.2f  span %6.2f  block0:", kn[k], gap[k] / cnt, acc[k][14] / cnt);
 			for(int p = 0; p < 9; ++p) fprintf(stderr, " %6.2f", acc[k][p] / cnt);
 			fprintf(stderr, "\n");
