@@ -10,6 +10,7 @@ struct ccq_reader {
 	unsigned char *buf;
 	size_t cap, len, pos;
 	int eof;
+	char *path;      /* NULL for stdin; bulk readers re-open a plain file (fasta_par.c) */
 };
 
 void *ccq_xmalloc(size_t n);

@@ -48,12 +48,15 @@ void ccq_free(ccq_str *s) {
 /* ---------------- reader ---------------- */
 ccq_reader *ccq_open(const char *path) {
 	ccq_reader *r = ccq_xmalloc(sizeof(ccq_reader));
+	r->path = NULL;
 	if(path[0] == '-' && path[1] == 0) {
 		r->gz = gzdopen(0, "rb");
 	} else {
 		r->gz = gzopen(path, "rb");
+		r->path = strdup(path);
 	}
 	if(!r->gz) {
+		free(r->path);
 		free(r);
 		return NULL;
 	}
@@ -85,6 +88,7 @@ void ccq_close(ccq_reader *r) {
 	if(r) {
 		gzclose(r->gz);
 		free(r->buf);
+		free(r->path);
 		free(r);
 	}
 }

@@ -737,7 +737,9 @@ static int main_dist(int argc, char **argv) {
 		fprintf(stderr, "ccphylo_amd: count-matrix (.mat) / union input is not implemented by the GPU engine.\n");
 		return 1;
 	}
-	ccq_msa *M = ccq_load_msa(r, flag, minLength, minCov, proxi, stderr);
+	/* the per-sequence work on host threads (fasta_par.c; the same result as
+	 * the serial ccq_load_msa) */
+	ccq_msa *M = ccq_load_msa_par(r, flag, minLength, minCov, proxi, threads > 16 ? (int) threads : 16, stderr);
 	ccq_close(r);
 	int n = M->n;
 	if(n * (n - 1) / 2 < 1) {

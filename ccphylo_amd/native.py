@@ -114,7 +114,7 @@ HOST_SYMBOLS = [
     "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
     "ccq_replay_newick", "ccq_replay_newick_strings", "ccq_newick_pair",
     "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
-    "ccq_load_msa", "ccq_msa_free", "ccq_load_fsa_files", "ccq_load_kma", "ccq_kma_free",
+    "ccq_load_msa", "ccq_load_msa_par", "ccq_msa_free", "ccq_load_fsa_files", "ccq_load_kma", "ccq_kma_free",
 ]
 
 _engine = None
@@ -191,6 +191,8 @@ def host_lib():
         lib.ccq_new.argtypes = [C.c_uint32]
         lib.ccq_open.restype = C.c_void_p
         lib.ccq_open.argtypes = [C.c_char_p]
+        lib.ccq_peek.restype = C.c_int
+        lib.ccq_peek.argtypes = [C.c_void_p]
         lib.ccq_close.argtypes = [C.c_void_p]
         lib.ccq_ltd_new.restype = C.c_void_p
         lib.ccq_ltd_new.argtypes = [C.c_int, C.c_int, C.c_double]
@@ -208,6 +210,8 @@ def host_lib():
         lib.ccq_npos.argtypes = [C.c_void_p, C.c_int]
         lib.ccq_load_msa.restype = C.c_void_p
         lib.ccq_load_msa.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_double, C.c_uint, C.c_void_p]
+        lib.ccq_load_msa_par.restype = C.c_void_p
+        lib.ccq_load_msa_par.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_double, C.c_uint, C.c_int, C.c_void_p]
         lib.ccq_msa_free.argtypes = [C.c_void_p]
         lib.ccq_load_kma.restype = C.c_void_p
         lib.ccq_load_kma.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_uint, C.c_uint, C.c_double, C.c_int,
@@ -615,8 +619,10 @@ def newick_from_phylip(path, joins_fn, etype=8, byte_scale=1.0, flags=0, precisi
     return trees
 
 
-def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0):
-    """FASTA MSA -> (headers, seqs uint64[n, W], incs, minLength) per ltdMsaMatrix_get."""
+def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0, threads=0, log_path=None):
+    """FASTA MSA -> (headers, seqs uint64[n, W], incs, minLength) per ltdMsaMatrix_get.
+    threads > 0: the parallel loader (ccq_load_msa_par); log_path: where the
+    Included / Excluded lines go (default /dev/null)."""
     lib = host_lib()
     r = lib.ccq_open(path.encode())
     if not r:
@@ -625,9 +631,13 @@ def load_msa(path, flag=1, min_length=1, min_cov=0.5, proxi=0):
     libc.fopen.restype = C.c_void_p
     libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
     libc.fclose.argtypes = [C.c_void_p]
-    log = libc.fopen(b"/dev/null", b"w")
+    log = libc.fopen((log_path or "/dev/null").encode(), b"w")
     try:
-        Mp = lib.ccq_load_msa(r, flag, min_length, min_cov, proxi, log)
+        lib.ccq_peek(r)
+        if threads > 0:
+            Mp = lib.ccq_load_msa_par(r, flag, min_length, min_cov, proxi, threads, log)
+        else:
+            Mp = lib.ccq_load_msa(r, flag, min_length, min_cov, proxi, log)
     finally:
         lib.ccq_close(r)
         libc.fclose(log)

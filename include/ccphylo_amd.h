@@ -167,13 +167,14 @@ typedef struct {
  * sums that needed the serial order, [7+2*CCG_NKSTAT] of those computed by
  * the serial chain (the parallel form declined).  Classes: */
 #define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
-#define CCG_K_TOP      1   /* DNJ k_dnj_select: requeue fold, top rows S, their rescans */
-#define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the rows below S with Q < U */
+#define CCG_K_TOP      1   /* sharded DNJ k_dnj_select: requeue fold, top rows S, their rescans */
+#define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the listed rows (one GPU: S and the rows below it) */
 #define CCG_K_ARGMIN   3   /* NJ: full Q argmin (initQ) */
 #define CCG_K_UPDATE   4   /* updateD (DNJ: after minQpair's replay; NJ: after the argmin fold) */
 #define CCG_K_REQUEUE  5   /* DNJ: updateDNJ Q/P + DNJ_popArrange */
 #define CCG_K_POP      6   /* NJ: ltdMatrix_popArrange */
-#define CCG_K_FIND     7   /* DNJ k_dnj_find: bound U and the rows below S under it */
+#define CCG_K_FIND     7   /* DNJ k_dnj_plan (one GPU: requeue fold, S, partner-cell bound, entry
+                              list) / k_dnj_find (sharded: bound U and the rows below S) */
 #define CCG_K_COLL     8   /* sharded engine: collectives (enqueue time, or the
                               host round trip of a host-staged transport) */
 #define CCG_K_XSUM     9   /* exact mode: k_exact_sum, the serial-order row sum of j */

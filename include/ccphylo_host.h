@@ -117,6 +117,12 @@ typedef struct {
 ccq_msa *ccq_load_msa(ccq_reader *r, unsigned flag, unsigned minLength, double minCov,
                       unsigned proxi, FILE *log);
 void ccq_msa_free(ccq_msa *M);
+/* The same result as ccq_load_msa, the per-sequence work (codes, packing,
+ * include masks) on `threads` host threads over windows of the input
+ * (fasta_par.c); the Included/Excluded lines and the length-mismatch exit
+ * come in record order as the reference prints them. */
+ccq_msa *ccq_load_msa_par(ccq_reader *r, unsigned flag, unsigned minLength, double minCov, unsigned proxi, int threads,
+                          FILE *log);
 
 /* Multi-file FASTA with -r (cdist.c:36 ltdFsaMatrix_get): entry `tmpl` of
  * every file; n = nfiles (every file keeps its slot), include[nfiles] the
