@@ -31,7 +31,7 @@ configs[3]: ONE N=200k matrix (float, 80 GB) sharded the same way, DNJ joins.
 Also reported: the dominant kernel's roofline (HIP-event timing of every
 kernel in one profiled extra step on the engine stream; algorithmic bytes as
 defined in DESIGN.md; `traffic` from the committed rocprofv3 PMC summary of
-the same kernel, profiles/r01_pmc.json, when present), the reference CPU path
+the same kernel, profiles/r02_pmc.json, when present), the reference CPU path
 on the same matrix (rank 0, N=1), and extras (exact-row-sum mode, -m nj, and
 SNP `dist` throughput).
 """
@@ -53,16 +53,18 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # dist roofline: 32-bit integer VALU issue.  A 32-position word pair costs 3
 # instructions (v_xor, v_bitop3, v_bcnt with accumulate).  Nominal peak
 # (MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz =
-# 7.86e13 instruction-lanes/s.  The measured issue rate of exactly this mix
-# in registers (tools/micro/popc_rate.hip) is 4.31e13 = 55% of nominal; both
-# fractions are reported (DESIGN.md 5 discusses the gap).
+# 7.86e13 instruction-lanes/s (`peak`, `frac`).  Measured on gfx950
+# (profiles/r02_valu_mix.txt, profiles/r02_pmc_dist.json): these wave64
+# integer instructions issue once per ~4 cycles per SIMD (16 lanes/clk), each
+# alone as in the mix, so their ceiling is half the nominal: 256 x 4 x 16 x
+# 2.4e9 = 3.93e13 (`int32_wave64_ceiling`, `frac_of_int32_ceiling`).
 VALU_NOMINAL_LANE_OPS = 256 * 4 * 32 * 2.4e9
-VALU_MIX_CEILING = 4.31e13
+VALU_INT32_CEILING = 256 * 4 * 16 * 2.4e9
 OPS_PER_WORD_PAIR = 3.0
 OPS_PER_WORD_PAIR_PAIRMODE = 6.0   # v_and (masks), v_xor, v_bitop3, v_and, 2x v_bcnt (dist and n)
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll",
           "exact_sum"]
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc.json")
 SHARD_LEG_TIMEOUT_S = 480
 
 
@@ -75,12 +77,12 @@ def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan):
     s = bytes per D element; the n-vectors are f64 (sD, Q) and i32 (N, P)."""
     sizes = range(3, n + 1)
     sn = float(sum(sizes))
-    if kernel == "dnj_select":      # rescanned D cells of S + the sD vector once
+    if kernel == "dnj_select":      # (sharded engine) rescanned D cells of S + the sD vector once
         return s * cells_select + 8.0 * sn
-    if kernel == "dnj_scan":        # rescanned D cells below S + the sD vector once
-        return s * cells_scan + 8.0 * sn
-    if kernel == "dnj_find":        # Q below S
-        return 8.0 * sn
+    if kernel == "dnj_scan":        # one GPU: every rescanned D cell (S and the rows below it) + the sD vector once
+        return s * (cells_select + cells_scan) + 8.0 * sn
+    if kernel == "dnj_find":        # k_dnj_plan: Q of every row; P, the partner cell, sD of row and partner
+        return 8.0 * sn + (20.0 + s) * float(sum(min(k - 1, 960) for k in sizes))   # for the top rows
     if kernel == "nj_argmin":       # every LT cell + sD
         return sum(s * k * (k - 1) / 2 + 8.0 * k for k in sizes)
     if kernel == "update":          # D_ik, D_kj read, D_kj written; sD, N read+written
@@ -108,8 +110,8 @@ def pmc_traffic(kernel):
         return None, None
 
 
-KERNEL_STATS = os.path.join(ROOT, "profiles", "r01_kernel_stats.csv")
-KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_find", "update": "k_dnj_join",
+KERNEL_STATS = os.path.join(ROOT, "profiles", "r02_kernel_stats.csv")
+KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
         "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop", "exact_sum": "k_exact_sum"}
 
 
@@ -141,11 +143,23 @@ def roofline(stats, n, s):
     avg_s = ns / cnt / 1e9
     achieved = tot / cnt / avg_s / 1e9
     shares = {k: round(v[1] / sum(x[1] for x in per.values()), 4) for k, v in per.items()}
+    kernels = {}
+    for k, (c, t) in per.items():   # every kernel class: algorithmic bytes, HIP-event and rocprof rates, PMC bytes
+        if k == "init":
+            continue
+        ab = algorithmic_bytes_total(k, n, s, stats[4 + 2 * len(KNAMES)], stats[5 + 2 * len(KNAMES)]) / c
+        ev = t / c / 1e9
+        rp = rocprof_mean_us(k)
+        kernels[k] = {"algorithmic_bytes_per_launch": round(ab, 1), "avg_launch_us": round(ev * 1e6, 3),
+                      "frac": round(ab / ev / 1e9 / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(k)[0]}
+        if rp:
+            kernels[k]["rocprof_mean_us"] = rp
+            kernels[k]["frac_rocprof_duration"] = round(ab / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
     traffic, src = pmc_traffic(name)
     out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
            "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
-           "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares}
+           "algorithmic_bytes_per_launch": round(tot / cnt, 1), "time_shares": shares, "kernels": kernels}
     if src:
         out["traffic_source"] = src
     rp = rocprof_mean_us(name)
@@ -158,7 +172,7 @@ def roofline(stats, n, s):
         out["frac_rocprof_duration"] = round(tot / cnt / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
         out["timing_note"] = ("avg_launch_us: HIP events around each launch on the engine stream (includes the "
                               "dispatch gap after the previous kernel); rocprof_mean_us: rocprofv3 --kernel-trace "
-                              "--stats mean of the same kernel (profiles/r01_kernel_stats.csv)")
+                              "--stats mean of the same kernel (profiles/r02_kernel_stats.csv)")
     return out
 
 
@@ -286,8 +300,12 @@ def valu_roofline(ops, dt, opw):
     peak, and against the measured ceiling of the kernel's instruction mix."""
     return {"bound": "valu-int", "achieved": round(ops / dt / 1e12, 3), "peak": round(VALU_NOMINAL_LANE_OPS / 1e12, 2),
             "unit": "T int instruction-lanes/s", "frac": round(ops / dt / VALU_NOMINAL_LANE_OPS, 4),
-            "mix_ceiling": VALU_MIX_CEILING / 1e12, "frac_of_mix_ceiling": round(ops / dt / VALU_MIX_CEILING, 4),
-            "ops_per_word_pair": opw}
+            "int32_wave64_ceiling": round(VALU_INT32_CEILING / 1e12, 2),
+            "frac_of_int32_ceiling": round(ops / dt / VALU_INT32_CEILING, 4), "ops_per_word_pair": opw,
+            "ceiling_evidence": "profiles/r02_valu_mix.txt (v_xor / v_or / v_bitop3 / v_bcnt alone and mixed: ~4 cycles "
+                                "per wave64 instruction per SIMD) and profiles/r02_pmc_dist.json (k_snp_tile: "
+                                "SQ_INSTS_VALU = 1.035 x the algorithmic 3 per word pair, 3.66 cycles per "
+                                "instruction per SIMD at the 2.35 GHz GRBM_GUI_ACTIVE clock)"}
 
 
 def packed_rows_to_fasta(path, words, L, masked_words):

@@ -2,7 +2,7 @@
 corrected as MI355X_MICROARCH.md's HBM section prescribes, written to a JSON
 summary that bench.py reads for roofline.traffic.
 
-    python tools/pmc_summary.py gpurun_out/prof_r01 profiles/r01_pmc.json
+    python tools/pmc_summary.py gpurun_out/prof_r02 profiles/r02_pmc.json
 
 FETCH_SIZE/WRITE_SIZE are in KiB per dispatch.  FETCH_SIZE counts 64 B per
 128-B memory request on gfx950 (half the bytes of a coalesced streaming
@@ -18,7 +18,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-NAMES = {"k_dnj_select": "dnj_select", "k_dnj_find": "dnj_find", "k_dnj_scan": "dnj_scan",
+NAMES = {"k_dnj_select": "dnj_select", "k_dnj_plan": "dnj_find", "k_dnj_scan": "dnj_scan",
          "k_dnj_join": "update", "k_dnj_requeue": "dnj_requeue"}
 # the NJ passes (tools/perf_dnj.py 10000 nj), when present
 NJ_NAMES = {"k_nj_argmin": "nj_argmin", "k_nj_join": "nj_update", "k_nj_pop": "nj_pop"}
@@ -65,7 +65,7 @@ def main():
                  "known_read_kib": 256 * 9000 * 8 / 1024.0, "fetch_size_kib": round(kib, 1),
                  "ratio": round(kib / (256 * 9000 * 8 / 1024.0), 4)}
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     f"tools/perf_dnj.py 10000 dnj|nj (fast sums); FETCH_SIZE x2 per MI355X_MICROARCH.md",
+                     f"tools/perf_dnj.py 10000 dnj|nj exact (the CLI default); FETCH_SIZE x2 per MI355X_MICROARCH.md",
            "kernels": kernels, "calibration": calib}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
