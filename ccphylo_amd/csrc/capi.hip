@@ -37,6 +37,15 @@ const char *ccg_strerror(int code) {
 	}
 }
 
+int ccg_device_count(int *count) {
+	if(!count) return CCG_EINVAL;
+	*count = 0;
+	int c = 0;
+	if(hipGetDeviceCount(&c) != hipSuccess || c <= 0) return CCG_ENODEV;
+	*count = c;
+	return CCG_OK;
+}
+
 int ccg_init(int device, ccg_ctx **out) {
 	if(!out) return CCG_EINVAL;
 	*out = NULL;

@@ -1342,7 +1342,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	init.hj = init.hi = -1;
 	CCG_CHECK(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	long long launches = 0;
-	static KTimer kt;
+	static thread_local KTimer kt;   // one per host thread (the CLI runs one rank per thread)
 	CCG_CHECK(hipEventRecord(ctx->ev0, st));
 	kt.init(st, a->profile != 0);
 	k_init_rows<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);

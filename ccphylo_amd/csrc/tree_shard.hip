@@ -460,7 +460,7 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 		return CCG_ENOMEM;
 	}
 	int rc = CCG_OK;
-	static KTimer kt;
+	static thread_local KTimer kt;   // one per host thread (the CLI runs one rank per thread)
 	CollRun cr = {coll_in, st, h, &kt};
 	TreeBufs b;
 	memset(&b, 0, sizeof(b));

@@ -524,7 +524,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		hipFree(w.mem);
 		return CCG_ENOMEM;
 	}
-	static KTimer kt;
+	static thread_local KTimer kt;   // one per host thread (the CLI runs one rank per thread)
 	CollRun cr = {coll, st, h, &kt};
 	DnjGrid grid;
 	grid.load();

@@ -5,13 +5,16 @@
  * Mirrors ref main.c:99 (dispatch), dist.c:473 main_dist / :42 makeMatrix /
  * cdist.c:196 ltdMsaMatrix_get, and tree.c:146 main_tree / :37 formTree:
  * same options, same stdout bytes, same stderr progress lines.  Option forms
- * the GPU engine does not implement (-V, -y, -a, -P with pairwise masks,
- * count-matrix / multi-file / union inputs, non-NJ tree methods) are refused
- * with an error instead of being silently approximated.
+ * the GPU engine does not implement (-V, -y, -a, union inputs, the z / p /
+ * np count-matrix metrics, tree methods other than nj / dnj / hnj) are
+ * refused with an error instead of being silently approximated.
  *
  * Extra (not in the reference): `tree --fast_sums` uses a fixed-order
  * parallel row sum instead of the reference's serial one;
- * `--device N` selects the GPU.
+ * `--device N` selects the GPU; `tree --gpus G [--transport rccl|host]`
+ * shards the matrix over G ranks (host/mgpu.c); `dist --tree FILE` runs
+ * dist and the tree in HBM without the Phylip text (`-m`, `--gpus`,
+ * `--transport`, `--fast_sums` as for tree).
  */
 #include <ctype.h>
 #include <errno.h>
@@ -21,6 +24,7 @@
 #include <time.h>
 #include "ccphylo_amd.h"
 #include "ccphylo_host.h"
+#include "mgpu.h"
 
 static void die_opt(const char *kind, const char *opt) {
 	fprintf(stderr, "%s argument:\t\"%s\"\n", kind, opt);
@@ -98,12 +102,24 @@ static int tree_help(FILE *out) {
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'T', "tmp", "Set directory for temporary files", "");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "gpus", "Shard the matrix over G GPUs (nj, dnj)", "off");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "transport", "rccl / host collectives for --gpus", "rccl");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "fast_sums", "Parallel row sums (not the reference's)", "False");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "device", "First GPU", "0");
 	return out == stderr;
+}
+
+/* --transport value */
+static int transport_id(const char *v) {
+	if(!strcmp(v, "rccl")) return CCQ_TRANSPORT_RCCL;
+	if(!strcmp(v, "host")) return CCQ_TRANSPORT_HOST;
+	die_opt("Invalid", "\"--transport\"");
+	return -1;
 }
 
 static int main_tree(int argc, char **argv) {
 	const char *in = "-", *outname = "-", *method = "dnj";
-	int flag = 0, precision = 9, et = 8, fast = 0, device = 0, stats = 0;
+	int flag = 0, precision = 9, et = 8, fast = 0, device = 0, stats = 0, gpus = 0, transport = CCQ_TRANSPORT_RCCL;
 	char sep = '\t', quotes = 0;
 	double bs = 1.0;
 	Args A = {argc, 0, argv};
@@ -142,6 +158,8 @@ static int main_tree(int argc, char **argv) {
 			else if(!strcmp(name, "tmp")) (void) opt_value(&A, att, "tmp");
 			else if(!strcmp(name, "fast_sums")) fast = 1;
 			else if(!strcmp(name, "device")) device = (int) opt_num(&A, att, "device");
+			else if(!strcmp(name, "gpus")) gpus = (int) opt_num(&A, att, "gpus");
+			else if(!strcmp(name, "transport")) transport = transport_id(opt_value(&A, att, "transport"));
 			else if(!strcmp(name, "stats")) stats = 1;
 			else if(!strcmp(name, "help")) return tree_help(stdout);
 			else die_opt("Unknown", a);
@@ -206,6 +224,11 @@ static int main_tree(int argc, char **argv) {
 		return 1;
 	}
 	if((et == 2 || et == 1) && bs == 0) die_opt("Invalid", et == 2 ? "\"--short_precision\"" : "\"--byte_precision\"");
+	if(gpus < 0) die_opt("Invalid", "\"--gpus\"");
+	if(gpus && m == CCG_TREE_HNJ) {
+		fprintf(stderr, "ccphylo_amd: -m hnj runs on one GPU (--gpus shards nj and dnj).\n");
+		return 1;
+	}
 
 	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
 	if(!out) {
@@ -229,7 +252,6 @@ static int main_tree(int argc, char **argv) {
 		fprintf(stderr, "# Total time used loading matrix: %.2f s.\n", (double) (t1 - t0) / 1000000);
 		t0 = t1;
 		if(n > 2) {
-			if(!ctx) ctx = open_gpu(device);
 			if(jcap < (size_t) n) {
 				jcap = n;
 				joins = realloc(joins, jcap * sizeof(ccg_join));
@@ -238,12 +260,26 @@ static int main_tree(int argc, char **argv) {
 			int nj = 0, fn = 0;
 			double fd = 0;
 			int64_t st[6 + 2 * CCG_NKSTAT];
-			int rc = ccg_tree(ctx, &ta, D->mat, joins, &nj, &fn, &fd, st);
+			memset(st, 0, sizeof(st));
+			int rc;
+			if(gpus) {
+				/* one matrix over G ranks, one thread per rank (host/mgpu.c) */
+				ccq_mgpu mc = {gpus, device, transport};
+				char emsg[320] = "";
+				rc = ccq_mgpu_tree(&mc, D->mat, &ta, joins, &nj, &fn, &fd, emsg, sizeof(emsg));
+				if(rc) {
+					fprintf(stderr, "ccphylo_amd: sharded tree construction failed: %s\n", emsg);
+					return 1;
+				}
+			} else {
+				if(!ctx) ctx = open_gpu(device);
+				rc = ccg_tree(ctx, &ta, D->mat, joins, &nj, &fn, &fd, st);
+			}
 			if(rc) {
 				fprintf(stderr, "ccphylo_amd: tree construction failed: %s\n", ccg_strerror(rc));
 				return 1;
 			}
-			if(stats) {
+			if(stats && !gpus) {
 				fprintf(stderr, "# gpu: %d joins, %lld rows / %lld cells rescanned, %lld launches, %.3f ms\n", nj,
 				        (long long) st[0], (long long) st[1], (long long) st[2], st[3] / 1000.0);
 			}
@@ -289,6 +325,11 @@ static int dist_help(FILE *out) {
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'b', "byte_precision", "Byte precision on distance matrix", "double / 1e0");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree", "Also build the tree in HBM, Newick to FILE", "off");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_method", "nj / dnj for --tree", "dnj");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_flag", "tree -f flags for --tree", "0");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "gpus", "Shard --tree over G GPUs", "1");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "transport", "rccl / host collectives for --gpus", "rccl");
 	return out == stderr;
 }
 
@@ -545,10 +586,90 @@ static int dist_fsa_files(char **files, int nfiles, const char *tmpl, const char
 	return 0;
 }
 
+/* `dist --tree FILE`: the MSA's distances and the tree in HBM, without the
+ * Phylip text (configs[4]: a 1e6-taxon matrix has no text form).  The LT is
+ * written straight into the ranks' row bands (ccg_snp_ltd_shard_dev) and the
+ * sharded tree consumes it there; the Newick equals `ccphylo dist | ccphylo
+ * tree` for the same MSA (integer SNP counts print exactly; taxon names as
+ * that pipeline's reader holds them, ccq_names_set).  -W normalised
+ * distances are used unrounded (the pipeline rounds them to -x digits). */
+static int dist_tree(const char *in, const char *treename, const char *tmethod, int tflag, unsigned flag,
+                     unsigned norm, unsigned minLength, double minCov, unsigned proxi, int precision, int et,
+                     double bs, unsigned threads, int device, int gpus, int transport, int fast) {
+	int m;
+	if(!strcmp(tmethod, "dnj")) m = CCG_TREE_DNJ;
+	else if(!strcmp(tmethod, "nj")) m = CCG_TREE_NJ;
+	else {
+		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline shards nj and dnj.\n", tmethod);
+		return 1;
+	}
+	if(flag & 2) {
+		fprintf(stderr, "ccphylo_amd: --tree needs the non-pair distances (-f without 2).\n");
+		return 1;
+	}
+	FILE *tout = (treename[0] == '-' && treename[1] == 0) ? stdout : fopen(treename, "wb");
+	if(!tout) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	ccq_reader *r = ccq_open(in);
+	if(!r) {
+		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
+		return 1;
+	}
+	if(ccq_peek(r) != '>') {
+		fprintf(stderr, "ccphylo_amd: --tree needs an MSA (FASTA) input.\n");
+		return 1;
+	}
+	ccq_msa *M = ccq_load_msa_par(r, flag, minLength, minCov, proxi, threads > 16 ? (int) threads : 16, stderr);
+	ccq_close(r);
+	const int n = M->n;
+	if(n < 3) {
+		fprintf(stderr, "ccphylo_amd: --tree needs at least 3 included sequences (%d).\n", n);
+		return 1;
+	}
+	fprintf(stderr, "# %d / %d bases included in distance matrix.\n", ccq_npos(M->incs, M->len), M->len);
+	ccg_snp_args sa;
+	memset(&sa, 0, sizeof(sa));
+	sa.n = n;
+	sa.len = M->len;
+	sa.stride = M->W;
+	sa.seqs = M->seqs;
+	sa.incs = M->incs;
+	sa.pair = 0;
+	sa.norm = norm;
+	sa.minLength = M->minLength;
+	sa.etype = et;
+	sa.byteScale = bs;
+	ccg_tree_args ta = {n, et, bs, m, tflag, !fast, 0, 0};
+	ccg_join *joins = malloc((size_t) n * sizeof(ccg_join));
+	int nj = 0, fn = 0, inc = 0;
+	double fd = 0;
+	ccq_mgpu mc = {gpus > 0 ? gpus : 1, device, transport};
+	char emsg[320] = "";
+	clock_t t0 = clock();
+	int rc = ccq_mgpu_dist_tree(&mc, &sa, &ta, joins, &nj, &fn, &fd, &inc, emsg, sizeof(emsg));
+	if(rc) {
+		fprintf(stderr, "ccphylo_amd: dist --tree failed: %s\n", emsg);
+		return 1;
+	}
+	fprintf(stderr, "# Total time used computing distances and tree: %.2f s.\n", (double) (clock() - t0) / 1000000);
+	ccq_names *T = ccq_names_new(32, 4);   /* as tree.c:61-66 */
+	ccq_names_set(T, M->headers, n, flag, '\t');
+	ccq_replay_newick(T, n, (const ccq_join *) joins, nj, fn, fd, tflag, precision);
+	fprintf(tout, "%s;\n", (char *) T->names[0]->seq);
+	if(tout != stdout) fclose(tout);
+	else fflush(stdout);
+	ccq_names_free(T);
+	free(joins);
+	ccq_msa_free(M);
+	return 0;
+}
+
 static int main_dist(int argc, char **argv) {
-	const char *outname = "-", *noutname = NULL;
+	const char *outname = "-", *noutname = NULL, *treename = NULL, *tmethod = "dnj";
 	char **files = NULL;
-	int nfiles = 0, precision = 9, et = 8, device = 0;
+	int nfiles = 0, precision = 9, et = 8, device = 0, gpus = 0, transport = CCQ_TRANSPORT_RCCL, fast = 0, tflag = 0;
 	unsigned flag = 1, norm = 0, minLength = 1, proxi = 0, minDepth = 15, threads = 1;
 	double minCov = 0.5, bs = 1.0;
 	const char *unsup = NULL, *tmpl = NULL, *method = "cos";
@@ -598,6 +719,12 @@ static int main_dist(int argc, char **argv) {
 			else if(!strcmp(name, "mmap")) { }
 			else if(!strcmp(name, "tmp")) (void) opt_value(&A, att, "tmp");
 			else if(!strcmp(name, "device")) device = (int) opt_num(&A, att, "device");
+			else if(!strcmp(name, "tree")) treename = opt_value(&A, att, "tree");
+			else if(!strcmp(name, "tree_method")) tmethod = opt_value(&A, att, "tree_method");
+			else if(!strcmp(name, "tree_flag")) tflag = (int) opt_num(&A, att, "tree_flag");
+			else if(!strcmp(name, "gpus")) gpus = (int) opt_num(&A, att, "gpus");
+			else if(!strcmp(name, "transport")) transport = transport_id(opt_value(&A, att, "transport"));
+			else if(!strcmp(name, "fast_sums")) fast = 1;
 			else if(!strcmp(name, "distance")) method = opt_value(&A, att, name);
 			else if(!strcmp(name, "distance_help")) method = NULL;
 			else if(!strcmp(name, "min_depth")) minDepth = (unsigned) strtod(opt_value(&A, att, name), NULL);
@@ -714,6 +841,10 @@ static int main_dist(int argc, char **argv) {
 	if(nfiles > 1) {
 		fprintf(stderr, "ccphylo_amd: multi-file dist input is not implemented by the GPU engine (use one MSA).\n");
 		return 1;
+	}
+	if(treename) {
+		return dist_tree(nfiles ? files[0] : "-", treename, tmethod, tflag, flag, norm, minLength, minCov, proxi,
+		                 precision, et, bs, threads, device, gpus, transport, fast);
 	}
 	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
 	if(!out) {

@@ -1,0 +1,279 @@
+/*
+ * mgpu.c -- the multi-GPU drivers of the CLI: one LT matrix sharded over G
+ * ranks, one host thread per rank, each on its own device (rank g on device
+ * (dev0 + g) mod the device count), for `ccphylo tree --gpus G` and the fused
+ * `ccphylo dist --tree` (configs[3] / [4] of BASELINE.json).
+ *
+ * ref: tree.c:146 main_tree / tree.c:89-93 (the dnj_thread / nj_thread call
+ * sites the sharded engine replaces), dist.c:473 main_dist.
+ *
+ * Transports (ccg_coll, include/ccphylo_amd.h):
+ *   rccl:  RCCL over xGMI; the main thread makes the unique id and every
+ *          rank thread joins it with ccg_rccl_open (ncclCommInitRank), one
+ *          communicator per device;
+ *   host:  the ranks are threads of this process and the collectives go
+ *          through host memory (host_staged = 1): a barrier, then each rank
+ *          sums / copies its own slice of the byte range.  For G ranks on
+ *          fewer devices (tests on a one-GPU box) and as a reference for the
+ *          RCCL path.
+ * Every rank returns the whole join list; the drivers check that all ranks
+ * agree (the replicated state is computed identically by construction).
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+#include "ccphylo_amd.h"
+#include "ccphylo_host.h"
+#include "mgpu.h"
+
+/* ------------------------------------------------------------------ host transport */
+typedef struct {
+	int world;
+	pthread_barrier_t bar;
+	void **bufs;          /* each rank's buffer of the current call */
+	const void *root_buf;
+	unsigned char *acc;   /* the allreduce result */
+	size_t acap;
+} tgroup;
+
+typedef struct {
+	tgroup *g;
+	int rank;
+} tuser;
+
+static int tg_allreduce(void *user, void *buf, size_t bytes, void *stream) {
+	(void) stream;
+	tuser *u = user;
+	tgroup *g = u->g;
+	g->bufs[u->rank] = buf;
+	if(u->rank == 0 && g->acap < bytes) {
+		free(g->acc);
+		g->acc = malloc(bytes ? bytes : 1);
+		g->acap = g->acc ? bytes : 0;
+	}
+	pthread_barrier_wait(&g->bar);
+	if(!g->acc && bytes) return -1;
+	/* rank r sums slice r of every rank's buffer (one non-zero contributor
+	 * per byte: 64-bit adds never carry between bytes) */
+	const size_t words = bytes / 8, per = (words + g->world - 1) / g->world;
+	const size_t w0 = (size_t) u->rank * per, w1 = w0 + per < words ? w0 + per : words;
+	for(size_t w = w0; w < w1; ++w) {
+		uint64_t s = 0;
+		for(int q = 0; q < g->world; ++q) {
+			uint64_t x;
+			memcpy(&x, (const unsigned char *) g->bufs[q] + 8 * w, 8);
+			s += x;
+		}
+		memcpy(g->acc + 8 * w, &s, 8);
+	}
+	if(u->rank == 0) {
+		for(size_t b = 8 * words; b < bytes; ++b) {
+			unsigned char s = 0;
+			for(int q = 0; q < g->world; ++q) s += ((const unsigned char *) g->bufs[q])[b];
+			g->acc[b] = s;
+		}
+	}
+	pthread_barrier_wait(&g->bar);
+	memcpy(buf, g->acc, bytes);
+	pthread_barrier_wait(&g->bar);   /* acc is reused by the next call */
+	return 0;
+}
+
+static int tg_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
+	(void) stream;
+	tuser *u = user;
+	tgroup *g = u->g;
+	if(u->rank == root) g->root_buf = send;
+	pthread_barrier_wait(&g->bar);
+	if(u->rank != root || recv != send) memcpy(recv, g->root_buf, bytes);
+	pthread_barrier_wait(&g->bar);
+	return 0;
+}
+
+/* ------------------------------------------------------------------ rank threads */
+typedef struct {
+	/* shared */
+	const ccq_mgpu *cfg;
+	tgroup *tg;
+	unsigned char id[CCG_RCCL_ID_BYTES];
+	int ndev;
+	/* the work: tree of a host LT, or dist of an MSA then tree */
+	const void *D;
+	const ccg_tree_args *ta;
+	const ccg_snp_args *sa;
+	/* per rank */
+	int rank, rc, inc;
+	ccg_join *joins;
+	int nj, fn;
+	double fd;
+	int64_t st[4];
+	char err[256];
+} rank_job;
+
+static void set_err(rank_job *j, const char *what, int rc) {
+	snprintf(j->err, sizeof(j->err), "rank %d: %s: %s", j->rank, what, ccg_strerror(rc));
+	j->rc = rc ? rc : CCG_EHIP;
+}
+
+static void *rank_main(void *p) {
+	rank_job *j = p;
+	const ccq_mgpu *c = j->cfg;
+	ccg_ctx *ctx = NULL;
+	ccg_coll coll;
+	tuser tu = {j->tg, j->rank};
+	int rc = ccg_init((c->device0 + j->rank) % j->ndev, &ctx);
+	if(rc) {
+		set_err(j, "ccg_init", rc);
+		/* the other ranks wait in the transport: a host group cannot continue */
+		return NULL;
+	}
+	if(c->transport == CCQ_TRANSPORT_RCCL) {
+		if((rc = ccg_rccl_open(ctx, j->id, j->rank, c->gpus, &coll))) {
+			set_err(j, "ccg_rccl_open", rc);
+			ccg_destroy(ctx);
+			return NULL;
+		}
+	} else {
+		memset(&coll, 0, sizeof(coll));
+		coll.user = &tu;
+		coll.rank = j->rank;
+		coll.world = c->gpus;
+		coll.host_staged = 1;
+		coll.allreduce_sum_u8 = tg_allreduce;
+		coll.broadcast = tg_bcast;
+	}
+	if(!j->sa) {
+		/* tree of a host LT: the rank uploads its own row bands */
+		rc = ccg_tree_shard(ctx, j->ta, &coll, j->D, j->joins, &j->nj, &j->fn, &j->fd, j->st);
+		if(rc) set_err(j, "ccg_tree_shard", rc);
+	} else {
+		/* dist into the rank's bands, then the tree on them, all in HBM */
+		const ccg_snp_args *a = j->sa;
+		const size_t sbytes = (size_t) a->n * a->stride * sizeof(uint64_t), ibytes = (size_t) a->stride * 4;
+		const int64_t elems = ccg_shard_elems(a->n, j->rank, c->gpus);
+		void *dseq = NULL, *dinc = NULL, *dloc = NULL;
+		ccg_snp_args da = *a;
+		if((rc = ccg_malloc(ctx, &dseq, sbytes)) || (rc = ccg_malloc(ctx, &dinc, ibytes)) ||
+		   (rc = ccg_malloc(ctx, &dloc, (size_t) (elems > 0 ? elems : 1) * j->ta->etype)) ||
+		   (rc = ccg_memcpy_h2d(ctx, dseq, a->seqs, sbytes)) || (rc = ccg_memcpy_h2d(ctx, dinc, a->incs, ibytes))) {
+			set_err(j, "device buffers", rc);
+		} else {
+			da.seqs = dseq;
+			da.incs = dinc;
+			if((rc = ccg_snp_ltd_shard_dev(ctx, &da, j->rank, c->gpus, dloc, &j->inc))) {
+				set_err(j, "ccg_snp_ltd_shard_dev", rc);
+			} else {
+				ccg_free(ctx, dseq);
+				ccg_free(ctx, dinc);
+				dseq = dinc = NULL;
+				rc = ccg_tree_shard_dev(ctx, j->ta, &coll, dloc, j->joins, &j->nj, &j->fn, &j->fd, j->st);
+				if(rc) set_err(j, "ccg_tree_shard_dev", rc);
+			}
+		}
+		if(dseq) ccg_free(ctx, dseq);
+		if(dinc) ccg_free(ctx, dinc);
+		if(dloc) ccg_free(ctx, dloc);
+	}
+	if(c->transport == CCQ_TRANSPORT_RCCL) ccg_rccl_close(&coll);
+	ccg_destroy(ctx);
+	return NULL;
+}
+
+static int run_ranks(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, const ccg_snp_args *sa, int n,
+                     ccg_join *joins, int *nj, int *fn, double *fd, int *inc, char *err, size_t errlen) {
+	const int G = c->gpus;
+	int ndev = 0, rc = ccg_device_count(&ndev);
+	if(rc) {
+		snprintf(err, errlen, "no HIP device: %s", ccg_strerror(rc));
+		return rc;
+	}
+	if(c->transport == CCQ_TRANSPORT_RCCL && G > ndev) {
+		snprintf(err, errlen, "--gpus %d with RCCL needs %d devices (%d visible); --transport host runs several ranks "
+		         "per device", G, G, ndev);
+		return CCG_EINVAL;
+	}
+	tgroup tg;
+	memset(&tg, 0, sizeof(tg));
+	tg.world = G;
+	tg.bufs = calloc((size_t) G, sizeof(void *));
+	pthread_barrier_init(&tg.bar, NULL, (unsigned) G);
+	rank_job *jobs = calloc((size_t) G, sizeof(rank_job));
+	pthread_t *th = calloc((size_t) G, sizeof(pthread_t));
+	unsigned char id[CCG_RCCL_ID_BYTES];
+	/* RCCL prints its banner / debug lines on stdout, where the CLI writes
+	 * the Newick: stdout points at stderr while the ranks run */
+	int saved_out = -1;
+	if(c->transport == CCQ_TRANSPORT_RCCL) {
+		fflush(stdout);
+		saved_out = dup(1);
+		if(saved_out >= 0) dup2(2, 1);
+	}
+	if(c->transport == CCQ_TRANSPORT_RCCL && (rc = ccg_rccl_unique_id(id))) {
+		snprintf(err, errlen, "ccg_rccl_unique_id: %s", ccg_strerror(rc));
+		goto out;
+	}
+	for(int g = 0; g < G; ++g) {
+		rank_job *j = jobs + g;
+		j->cfg = c;
+		j->tg = &tg;
+		memcpy(j->id, id, sizeof(id));
+		j->ndev = ndev;
+		j->D = D;
+		j->ta = ta;
+		j->sa = sa;
+		j->rank = g;
+		j->joins = g == 0 ? joins : malloc((size_t) (n > 2 ? n : 2) * sizeof(ccg_join));
+		if(!j->joins || pthread_create(th + g, NULL, rank_main, j)) {
+			snprintf(err, errlen, "cannot start rank %d", g);
+			rc = CCG_ENOMEM;
+			for(int q = 0; q < g; ++q) pthread_join(th[q], NULL);   /* only safe when they do not wait on rank g */
+			goto out;
+		}
+	}
+	for(int g = 0; g < G; ++g) pthread_join(th[g], NULL);
+	rc = CCG_OK;
+	for(int g = 0; g < G && !rc; ++g) {
+		if(jobs[g].rc) {
+			rc = jobs[g].rc;
+			snprintf(err, errlen, "%s", jobs[g].err);
+		}
+	}
+	for(int g = 1; g < G && !rc; ++g) {   /* every rank holds the same replicated state */
+		if(jobs[g].nj != jobs[0].nj || jobs[g].fn != jobs[0].fn ||
+		   memcmp(jobs[g].joins, joins, (size_t) jobs[0].nj * sizeof(ccg_join))) {
+			snprintf(err, errlen, "rank %d's join list differs from rank 0's", g);
+			rc = CCG_EHIP;
+		}
+	}
+	if(!rc) {
+		*nj = jobs[0].nj;
+		*fn = jobs[0].fn;
+		*fd = jobs[0].fd;
+		if(inc) *inc = jobs[0].inc;
+	}
+out:
+	if(saved_out >= 0) {
+		fflush(stdout);
+		dup2(saved_out, 1);
+		close(saved_out);
+	}
+	for(int g = 1; g < G; ++g) free(jobs[g].joins);
+	free(jobs);
+	free(th);
+	pthread_barrier_destroy(&tg.bar);
+	free(tg.bufs);
+	free(tg.acc);
+	return rc;
+}
+
+int ccq_mgpu_tree(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, ccg_join *joins, int *nj, int *fn,
+                  double *fd, char *err, size_t errlen) {
+	return run_ranks(c, D, ta, NULL, ta->n, joins, nj, fn, fd, NULL, err, errlen);
+}
+
+int ccq_mgpu_dist_tree(const ccq_mgpu *c, const ccg_snp_args *sa, const ccg_tree_args *ta, ccg_join *joins, int *nj,
+                       int *fn, double *fd, int *inc, char *err, size_t errlen) {
+	return run_ranks(c, NULL, ta, sa, ta->n, joins, nj, fn, fd, inc, err, errlen);
+}

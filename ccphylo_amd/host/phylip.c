@@ -62,6 +62,7 @@ static inline void put_grow(ccq_str *s, uint32_t *w, unsigned char c) {
 	}
 }
 
+
 static int store_dist(ccq_ltd *D, int64_t f, const char *tok) {
 	char *end;
 	double v = strtod(tok, &end);
@@ -612,4 +613,36 @@ void ccq_print_phy(FILE *out, const ccq_ltd *D, char **names, const unsigned cha
 	free(jobs);
 	free(th);
 	free(idx);
+}
+
+/* the name field ccq_print_phy writes (quotes stripped, directories dropped,
+ * padded / cut to 10 unless format bit 1), stored as ccq_load_phy reads it */
+void ccq_names_set(ccq_names *T, char **names, int n, unsigned format, char sep) {
+	grow_names(T, n);
+	char cell[512];
+	for(int i = 0; i < n; ++i) {
+		const size_t L0 = strlen(names[i]);
+		char *tmp = ccq_xmalloc(L0 + 1), *name = tmp;
+		memcpy(tmp, names[i], L0 + 1);
+		if(L0 && ((name[0] == '"' && name[L0 - 1] == '"') || (name[0] == '\'' && name[L0 - 1] == '\''))) {
+			name[L0 - 1] = 0;
+			++name;
+		}
+		name = strip_dir(name);
+		const char *field = name;
+		if(!(format & 1)) {
+			snprintf(cell, sizeof(cell), "%-10.10s", name);
+			field = cell;
+		}
+		ccq_str *nm = T->names[i];
+		uint32_t w = 0;
+		for(const char *p = field; *p; ++p) put_grow(nm, &w, (unsigned char) *p);
+		put_grow(nm, &w, (unsigned char) (i ? sep : '\n'));   /* row 0 has no cells: its name ends the line */
+		while(w > 0 && isspace(nm->seq[w - 1])) --w;
+		nm->len = w;
+		nm->seq[w] = 0;
+		free(tmp);
+	}
+	T->header->len = 0;
+	T->header->seq[0] = 0;
 }

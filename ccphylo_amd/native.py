@@ -100,7 +100,7 @@ JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("L
 
 # every symbol of include/ccphylo_amd.h
 ENGINE_SYMBOLS = [
-    "ccg_init", "ccg_destroy", "ccg_strerror", "ccg_device_info",
+    "ccg_init", "ccg_device_count", "ccg_destroy", "ccg_strerror", "ccg_device_info",
     "ccg_snp_ltd", "ccg_snp_ltd_dev", "ccg_tree", "ccg_tree_dev",
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
@@ -111,7 +111,7 @@ ENGINE_SYMBOLS = [
 HOST_SYMBOLS = [
     "ccq_new", "ccq_free", "ccq_open", "ccq_close", "ccq_peek",
     "ccq_ltd_new", "ccq_ltd_free", "ccq_ltd_reserve", "ccq_ltd_get", "ccq_ltd_set",
-    "ccq_names_new", "ccq_names_free", "ccq_load_phy", "ccq_print_phy",
+    "ccq_names_new", "ccq_names_free", "ccq_names_set", "ccq_load_phy", "ccq_print_phy",
     "ccq_replay_newick", "ccq_replay_newick_strings", "ccq_newick_pair",
     "ccq_code_table", "ccq_read_fasta", "ccq_pack", "ccq_init_inc", "ccq_inc_update", "ccq_npos",
     "ccq_load_msa", "ccq_load_msa_par", "ccq_msa_free", "ccq_load_fsa_files", "ccq_load_kma", "ccq_kma_free",

@@ -46,6 +46,8 @@ typedef struct ccg_ctx ccg_ctx;
 /* Opens `device` (ordinal in HIP_VISIBLE_DEVICES numbering) and creates the
  * engine stream.  Fails with CCG_ENODEV when no gfx950 device is present. */
 int ccg_init(int device, ccg_ctx **ctx);
+/* HIP devices visible to this process (the multi-GPU CLI deals ranks over them) */
+int ccg_device_count(int *count);
 void ccg_destroy(ccg_ctx *ctx);
 const char *ccg_strerror(int code);
 /* device name + arch, for logs */

@@ -63,6 +63,14 @@ typedef struct {
 ccq_names *ccq_names_new(int n, uint32_t init_size);
 void ccq_names_free(ccq_names *T);
 
+/* Names 0..n-1 as `ccphylo dist | ccphylo tree` would hold them: the field
+ * ccq_print_phy writes for names[i] under `format` (phy.c:59), stored the
+ * way ccq_load_phy reads a row "field<sep>" (phy.c:360-379: byte by byte
+ * with capacity doubling, trailing white space trimmed), so a Newick
+ * replayed over them has that pipeline's child order (nwck.c:45 compares
+ * capacities).  Used by the fused `dist --tree` path. */
+void ccq_names_set(ccq_names *T, char **names, int n, unsigned format, char sep);
+
 /* Loads the next matrix (phy.c:251 semantics).  Returns n (0 at EOF / on a
  * malformed file, with *err set), grows D and T as needed. */
 int ccq_load_phy(ccq_reader *r, ccq_ltd *D, ccq_names *T, char sep, char quotes, int *err);
