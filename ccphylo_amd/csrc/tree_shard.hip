@@ -3,13 +3,14 @@
 //
 // Ownership: bands of CCG_SHARD_BAND (= NJ_RB) rows dealt round-robin; a rank
 // keeps its rows back to back (Shard::off).  sD and N are replicated and every
-// rank updates them identically, so the only exchanges per join are
-//   1. broadcast of row n-1 from its owner (it moves to slot i in the pop,
-//      matrix.c:518), issued first so it overlaps nothing it depends on;
-//   2. the per-rank argmin records (initQ nj.c:182): an allreduce of a
-//      world x 16-byte array in which each rank fills its own slot; every rank
-//      folds the records in rank order with initQ's total order (smaller q,
-//      then larger flat index), so all ranks pick the same (i, j);
+// rank updates them identically, so the only exchanges per join are two
+// allreduces:
+//   1. the per-rank argmin records (initQ nj.c:182): a world x 16-byte array
+//      in which each rank fills its own slot; every rank folds the records in
+//      rank order with initQ's total order (smaller q, then larger flat
+//      index), so all ranks pick the same (i, j).  Row n-1 (it moves to slot
+//      i in the pop, matrix.c:518) rides behind the records: its owner copies
+//      it there, the other ranks write zeros (k_sh_xm);
 //   3. lines i and j (D_ik, D_jk for every k): each rank contributes the
 //      entries its rows hold and zeros elsewhere, so the bytewise sum is a
 //      gather.  Every rank then computes the whole updated line j
@@ -31,6 +32,16 @@
 
 
 // ------------------------------------------------------------------ per join
+// row n-1 behind the argmin records: the owner's cells, zeros elsewhere
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_xm(const typename Elem<ET>::T *__restrict__ D, int n, Shard sh,
+                                              typename Elem<ET>::T *__restrict__ xm) {
+	const int k = blockIdx.x * TB + threadIdx.x;
+	if(k >= n - 1) return;
+	const bool own = sh.owns(n - 1);
+	xm[k] = own ? D[sh.off(n - 1) + k] : (typename Elem<ET>::T) 0;
+}
+
 // initQ over the rank's tiles: NJ_SEG-column segments x one band, segment-
 // major.  Segment s holds the local bands from global band 256 s on:
 // first(s) = ceil((256 s - rank) / world), F = prefix sums of first, so the
@@ -447,13 +458,16 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
 	size_t o_qp = take(SH_GRID * 8), o_fp = take(SH_GRID * 8);
 	size_t o_j = take((size_t) n0 * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
-	size_t o_F = take((size_t) (nseg0 + 2) * 8), o_rec = take((size_t) coll_in->world * sizeof(ShRec));
+	// the argmin records, then row n-1 (16-byte aligned), gathered by one allreduce
+	const size_t rec_b = ((size_t) coll_in->world * sizeof(ShRec) + 15) & ~(size_t) 15;
+	size_t o_F = take((size_t) (nseg0 + 2) * 8), o_rec = take(rec_b + (size_t) n0 * ET + 16);
 	size_t o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
 	size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
 	char *m;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
 	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
 	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
+	if(rec_b + (size_t) n0 * ET + 16 > hcap) hcap = rec_b + (size_t) n0 * ET + 16;
 	unsigned char *h = NULL;
 	if(coll_in->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
 		hipFree(m);
@@ -524,9 +538,8 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 		int since_check = 0;
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
-			const int root = ccg_shard_owner(n - 1, sh.world);
-			SH_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
-			                root));
+			T *Xmr = (T *) ((char *) rec + rec_b);   // row n-1, gathered with the records
+			k_sh_xm<ET><<<cdiv(n - 1, TB), TB, 0, st>>>(D, n, sh, Xmr);
 			const int nlb = sh_nlb(n, sh), nseg = (int) cdiv(n - 1, NJ_SEG);
 			int sstar = 0;
 			while(sstar < nseg && hF[sstar + 1] - hF[sstar] < nlb) ++sstar;
@@ -535,21 +548,21 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			if(G > 0) k_sh_argmin<ET><<<G, TB, 0, st>>>(D, bs, b, n, sh, F, nlb, sstar, tiles);
 			k_sh_fold<<<1, TB, 0, st>>>(b, G, sh, rec);
 			kt.mark(CCG_K_ARGMIN);
-			SH_TRY(cr.allreduce(rec, (size_t) sh.world * sizeof(ShRec)));
+			SH_TRY(cr.allreduce(rec, rec_b + (size_t) (n - 1) * ET));
 			const unsigned gn = cdiv(n, TB);
 			k_sh_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, rec, X);
 			kt.mark(CCG_K_UPDATE);
 			SH_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
-			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xm);
+			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xmr);
 			kt.mark(CCG_K_UPDATE);
 			if(a->exact) {
 				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 				kt.mark(CCG_K_XSUM);
 			}
-			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xm);
+			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xmr);
 			kt.mark(CCG_K_POP);
 			SH_HIP(hipGetLastError());
-			launches += (G > 0) + 5 + (a->exact != 0);
+			launches += (G > 0) + 5 + (a->exact != 0);   // k_sh_xm, fold, lines, join, pop
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;

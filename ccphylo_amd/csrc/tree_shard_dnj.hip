@@ -5,9 +5,10 @@
 // sD, N, Q, P and the join list are replicated and every rank updates them
 // with the same arithmetic.
 //
-// Per join at matrix size n:
-//   0. broadcast of row n-1 from its owner (the pop moves it to slot i,
-//      dnj.c:817 / matrix.c:518);
+// Per join at matrix size n (two collectives):
+//   0. row n-1 (the pop moves it to slot i, dnj.c:817 / matrix.c:518) rides
+//      in the record allreduce of step 2: its owner copies it behind the
+//      records, every other rank writes zeros there;
 //   1. minQpair's search (dnj.c:43) with the single-GPU kernels of
 //      ccg_dnj_search.h under the Shard row policy.  The candidate row, m0
 //      and the top-B rows S depend on the replicated Q only, so every rank
@@ -43,6 +44,11 @@
 // [bitmap of rows (u64 words)][f64 fresh q][i32 fresh j], laid out for size n
 static __host__ __device__ inline size_t rec_bits_bytes(int n) { return (size_t) ((n + 63) / 64) * 8; }
 static __host__ __device__ inline size_t rec_bytes(int n) { return rec_bits_bytes(n) + (size_t) n * 12; }
+// row n-1 behind the records (16-byte aligned), n-1 elements of es bytes
+static __host__ __device__ inline size_t rec_xm_off(int n) { return (rec_bytes(n) + 15) & ~(size_t) 15; }
+static __host__ __device__ inline size_t rec_all_bytes(int n, int es) {
+	return rec_xm_off(n) + (((size_t) (n - 1) * es + 15) & ~(size_t) 15);
+}
 
 struct RecView {
 	unsigned *bits;
@@ -58,10 +64,19 @@ static __host__ __device__ inline RecView rec_view(void *R, int n) {
 }
 
 // own rescans -> records: S rows from the folded S entries (k_dnj_find), the
-// rows below S by folding their units (k_dnj_scan) and setting their bit
-__global__ __launch_bounds__(TB) void k_shd_rec(TreeBufs b, int n, Shard sh, void *R) {
+// rows below S by folding their units (k_dnj_scan) and setting their bit;
+// row n-1 behind them (the owner's cells, zeros on the other ranks)
+template <int ET>
+__global__ __launch_bounds__(TB) void k_shd_rec(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
+                                                Shard sh, void *R) {
 	TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
+	{
+		typename Elem<ET>::T *xm = (typename Elem<ET>::T *) ((char *) R + rec_xm_off(n));
+		const bool own = sh.owns(n - 1);
+		const typename Elem<ET>::T *row = D + (own ? sh.off(n - 1) : 0);
+		for(int k = blockIdx.x * TB + threadIdx.x; k < n - 1; k += gridDim.x * TB) xm[k] = own ? row[k] : 0;
+	}
 	const RecView v = rec_view(R, n);
 	const int nS = ctl->nS, T = ctl->T, lane = threadIdx.x & 63;
 	for(int e = blockIdx.x * TB + threadIdx.x; e < nS; e += gridDim.x * TB) {
@@ -508,7 +523,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		sz += (bytes + 255) & ~(size_t) 255;
 		return off;
 	};
-	const size_t o_R = take(rec_bytes(n0)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	const size_t o_R = take(rec_all_bytes(n0, ET)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
 	const size_t o_Xj = take((size_t) n0 * ET + 8), o_rp = take(rp_bytes), o_xc = take(xc_bytes);
 	char *m = NULL;
 	unsigned char *h = NULL;
@@ -518,7 +533,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
 	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
-	if(rec_bytes(n0) > hcap) hcap = rec_bytes(n0);
+	if(rec_all_bytes(n0, ET) > hcap) hcap = rec_all_bytes(n0, ET);
 	if(coll->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
 		hipFree(m);
 		hipFree(w.mem);
@@ -569,10 +584,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		int since_check = 0;
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
-			const int root = ccg_shard_owner(n - 1, sh.world);
-			SD_TRY(cr.bcast(root == sh.rank ? (const void *) (D + sh.off(n - 1)) : NULL, Xm, (size_t) (n - 1) * ET,
-			                root));
 			const unsigned gn = cdiv(n, TB);
+			T *Xmr = (T *) ((char *) R + rec_xm_off(n));   // row n-1, gathered with the records
 			const unsigned gs = grid.sel(n), gc = grid.scan(n);
 			const int seg = grid.seg(n);
 			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n));
@@ -582,21 +595,21 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			kt.mark(CCG_K_FIND);
 			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg);
 			kt.mark(CCG_K_REST);
-			k_shd_rec<<<FOLD_BLOCKS, TB, 0, st>>>(b, n, sh, R);
+			k_shd_rec<ET><<<FOLD_BLOCKS, TB, 0, st>>>(D, b, n, sh, R);
 			kt.mark(CCG_K_REST);
-			SD_TRY(cr.allreduce(R, rec_bytes(n)));
+			SD_TRY(cr.allreduce(R, rec_all_bytes(n, ET)));
 			k_shd_replay<<<1, RPL_T, 0, st>>>(b, n, R);
 			k_shd_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, X);
 			kt.mark(CCG_K_UPDATE);
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
-			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xm, Xj);
+			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj);
 			kt.mark(CCG_K_UPDATE);
 			if(a->exact) {
 				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 				kt.mark(CCG_K_XSUM);
 			}
-			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
-			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xm, Xj, R);
+			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
+			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
 			launches += 8 + (a->exact != 0);
