@@ -272,6 +272,9 @@ __global__ __launch_bounds__(TB) void k_sh_join(typename Elem<ET>::T *__restrict
 		cnt = 1;
 	}
 	update_partials(b, n, s_exact, k, d, cnt, blockIdx.x);
+	// exact mode: this block's row of the serial row sum (every rank holds
+	// the whole new line j, so every rank computes the same rows)
+	if(s_exact) xs_join_row(b, n, blockIdx.x, d, xs_tag(n));
 }
 
 // row sum of j, then ltdMatrix_popArrange (matrix.c:518) + nj.c:1588-1589:
@@ -280,7 +283,7 @@ template <int ET>
 __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, Shard sh,
                                                const typename Elem<ET>::T *__restrict__ Xm) {
 	__shared__ double s_sd;
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
 	const int nn = n - 1;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -300,25 +303,27 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 		if(!done) {
 			double sd;
 			int nj;
-			bool need;
-			if(exact) {   // k_exact_sum ran
-				sd = ctl->xsum;
-				nj = ctl->xnj;
-				need = false;
-			} else {
-				fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
-			}
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, false, &sd, &nj, &need, &chain);
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
 				s_serial = need;
+				s_chain = chain;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j;
-	const double sdj = s_sd;   // exact: k_exact_sum's
+	// exact mode, a failed check of the parallel form: the serial chain (all threads)
+	if(s_chain) {
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = s_nj;
@@ -462,6 +467,9 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	const size_t rec_b = ((size_t) coll_in->world * sizeof(ShRec) + 15) & ~(size_t) 15;
 	size_t o_F = take((size_t) (nseg0 + 2) * 8), o_rec = take(rec_b + (size_t) n0 * ET + 16);
 	size_t o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	// exact row sums over the join blocks (xs_join_row / xs_walk_blocks)
+	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xcr = take(nb * XB_CAP * sizeof(XsCross));
+	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
 	size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
 	char *m;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
@@ -489,6 +497,10 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	b.fpart = (long long *) (m + o_fp);
 	b.joins = (ccg_join *) (m + o_j);
 	b.ctl = (TreeCtl *) (m + o_ctl);
+	b.xagg = (unsigned long long *) (m + o_xa);
+	b.xblk = (XsBlk *) (m + o_xb);
+	b.xcr = (XsCross *) (m + o_xcr);
+	b.xti = (XsTie *) (m + o_xt);
 	long long *F = (long long *) (m + o_F);
 	ShRec *rec = (ShRec *) (m + o_rec);
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xc = (T *) (m + o_xc);
@@ -555,14 +567,10 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			SH_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xmr);
 			kt.mark(CCG_K_UPDATE);
-			if(a->exact) {
-				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
-				kt.mark(CCG_K_XSUM);
-			}
 			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xmr);
 			kt.mark(CCG_K_POP);
 			SH_HIP(hipGetLastError());
-			launches += (G > 0) + 5 + (a->exact != 0);   // k_sh_xm, fold, lines, join, pop
+			launches += (G > 0) + 5;   // k_sh_xm, fold, lines, join, pop
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;

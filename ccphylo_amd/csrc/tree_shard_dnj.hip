@@ -91,6 +91,7 @@ __global__ __launch_bounds__(TB) void k_shd_rec(const typename Elem<ET>::T *__re
 	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
 	for(int x = w0; x < T; x += nw) {
 		const int r = b.crow[x], ua = b.coff[x], ub = b.coff[x + 1];
+		if(!sh.owns(r)) continue;   // k_dnj_plan lists every S row; its owner fills the record
 		double q = DBL_MAX;
 		int idx = 0;
 		for(int u = ua + lane; u < ub; u += 64) {
@@ -125,13 +126,15 @@ __global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R
 	if(tid < nS) ssr[tid] = b.S[tid];
 	__syncthreads();
 	// rows [1, smin) with their bit set (no rows below S unless |S| = DNJ_B;
-	// smin is 1 then)
-	const int nw = smin > 1 ? ((smin - 1) >> 5) + 1 : 0;
+	// smin is 1 then); with the one-phase plan (nS = 0) every listed row,
+	// S included, is in the bitmap: rows [1, n)
+	const int lim = nS == 0 ? n : smin;
+	const int nw = lim > 1 ? ((lim - 1) >> 5) + 1 : 0;
 	const int per = (nw + RPL_T - 1) / RPL_T;
 	auto word = [&](int w) -> unsigned {
 		unsigned x = v.bits[w];
 		if(w == 0) x &= ~1u;                                              // row 0 never qualifies
-		if(w == nw - 1 && (smin & 31)) x &= (1u << (smin & 31)) - 1u;     // rows >= smin
+		if(w == nw - 1 && (lim & 31)) x &= (1u << (lim & 31)) - 1u;       // rows >= lim
 		return x;
 	};
 	int cnt = 0;
@@ -283,6 +286,9 @@ __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restric
 		cnt = 1;
 	}
 	update_partials(b, n, s_exact, k, d, cnt, blockIdx.x);
+	// exact mode: this block's row of the serial row sum (every rank holds
+	// the whole new line j, so every rank computes the same rows)
+	if(s_exact) xs_join_row(b, n, blockIdx.x, d, xs_tag(n));
 }
 
 // Row sum of j, updateDNJ's Q/P part (dnj.c:618-709) and DNJ_popArrange
@@ -295,9 +301,9 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
                                                     int n, Shard sh, const typename Elem<ET>::T *__restrict__ Xm,
                                                     const typename Elem<ET>::T *__restrict__ Xj, void *R) {
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
-	__shared__ int si[5][TB / 64], sfp[TB / 64];
+	__shared__ int si[5][TB / 64], sfp[TB / 64], sbp[TB / 64];
 	__shared__ double s_sd;
-	__shared__ int s_nj, s_i, s_j, s_stop, s_serial;
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
 	const int nn = n - 1;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -326,25 +332,27 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 		if(!done) {
 			double sd;
 			int nj;
-			bool need;
-			if(exact) {   // k_exact_sum ran
-				sd = ctl->xsum;
-				nj = ctl->xnj;
-				need = false;
-			} else {
-				fold_update_wave(b, (int) cdiv(n, TB), exact, false, &sd, &nj, &need);
-			}
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, false, &sd, &nj, &need, &chain);
 			if(lane == 0) {
 				s_sd = sd;
 				s_nj = nj;
 				s_serial = need;
+				s_chain = chain;
 			}
 		}
 	}
 	__syncthreads();
 	if(s_stop) return;
 	const int i = s_i, j = s_j, Nj = s_nj;
-	const double sdj = s_sd;   // exact: k_exact_sum's
+	// exact mode, a failed check of the parallel form: the serial chain (all threads)
+	if(s_chain) {
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
 	if(blockIdx.x == 0 && tid == 0) {
 		b.sD[j] = sdj;
 		b.N[j] = Nj;
@@ -424,14 +432,15 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
 	// fold); only when the next S has a band part
-	double bq = DBL_MAX;
-	int bk = 0;
+	double bq = DBL_MAX, bdum = 0.0;
+	int bk = 0, bp = 0;
 	if(BANDS) {
 		if(k >= 1 && k < nn && k != i && k != j) {
 			bq = k > j ? fq : qk0;
 			bk = k;
+			bp = k > j ? fp : pkk0;   // its partner, for k_dnj_plan's partner-cell bound
 		}
-		qarg_wave_reduce(bq, bk);
+		qarg_wave_reduce_carry(bq, bk, bdum, bp);
 	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
@@ -451,23 +460,26 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 		if(BANDS) {
 			sq[4][wid] = bq;
 			si[4][wid] = bk;
+			sbp[wid] = bp;
 		}
 	}
 	__syncthreads();
 	if(tid < (BANDS ? 5 : 4)) {
 		double q = sq[tid][0], cq = sfq[0];
-		int ix = si[tid][0], cp = sfp[0];
+		int ix = si[tid][0], cp = sfp[0], xp = BANDS ? sbp[0] : 0;
 		for(int w = 1; w < TB / 64; ++w) {
 			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
 				q = sq[tid][w];
 				ix = si[tid][w];
 				cq = sfq[w];
 				cp = sfp[w];
+				if(BANDS) xp = sbp[w];
 			}
 		}
 		if(tid == 4) {
 			b.bmq[blockIdx.x] = q;
 			b.bmr[blockIdx.x] = ix;
+			b.bmp[blockIdx.x] = xp;
 		} else {
 			b.qpart[4 * blockIdx.x + tid] = q;
 			b.ipart[4 * blockIdx.x + tid] = ix;
@@ -588,10 +600,12 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			T *Xmr = (T *) ((char *) R + rec_xm_off(n));   // row n-1, gathered with the records
 			const unsigned gs = grid.sel(n), gc = grid.scan(n);
 			const int seg = grid.seg(n);
-			k_dnj_select<ET, false><<<gs, TB, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n));
-			kt.mark(CCG_K_TOP);
-			if(grid.bands(n)) k_dnj_find<Shard, true><<<1, TBF, 0, st>>>(b, n, sh, seg);
-			else k_dnj_find<Shard, false><<<1, TBF, 0, st>>>(b, n, sh, seg);
+			// one-phase search (k_dnj_plan): each rank lists the S rows and the
+			// rows below S it owns, under the bound of its own S rows' partner
+			// cells (a subset of S: looser, still exact after the replay)
+			(void) gs;
+			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_qdelay);
+			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_qdelay);
 			kt.mark(CCG_K_FIND);
 			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg);
 			kt.mark(CCG_K_REST);
@@ -604,15 +618,11 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj);
 			kt.mark(CCG_K_UPDATE);
-			if(a->exact) {
-				k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
-				kt.mark(CCG_K_XSUM);
-			}
 			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
 			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
-			launches += 8 + (a->exact != 0);
+			launches += 7;
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;
