@@ -1238,10 +1238,18 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 
 // ------------------------------------------------------------------ DNJ scan
 // Rescans of the rows found by k_dnj_find, in SEG-cell units spread over the
-// whole grid.
-template <int ET, bool GEN, class Rows>
+// whole grid.  Tail: work every block does first (begin) and the store of
+// each unit's partial (unit, thread 0), for the sharded engine's records.
+struct NoTail {
+	__device__ __forceinline__ void begin(const TreeBufs &, int) const {}
+	__device__ __forceinline__ void unit(const TreeBufs &b, int, int u, int, int, int, double q, int j) const {
+		b.cq[u] = q;
+		b.cj[u] = j;
+	}
+};
+template <int ET, bool GEN, class Rows, class Tail = NoTail>
 __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                 int n, Rows rows, int seg) {
+                                                 int n, Rows rows, int seg, Tail tail = Tail()) {
 	__shared__ int erow[REPLAY_CAP];
 	__shared__ int eoff[REPLAY_CAP + 1];
 	__shared__ double sq[TB / 64];
@@ -1253,7 +1261,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	// speculative first TB entries, then the rest once T is known
 	const int r0 = b.crow[tid], o0 = b.coff[tid];
 	const int done = ctl->done, T = ctl->T;
-	if(done || T == 0) return;
+	if(done) return;
+	tail.begin(b, n);
+	if(T == 0) return;
 	// blocks beyond the unit count leave before staging the table
 	if((int) blockIdx.x >= b.coff[T]) return;
 	// the entry table in LDS when it fits, else searched in HBM (L2-resident)
@@ -1286,10 +1296,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 		int idx = 0;
 		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
 		qarg_block_reduce1(qq, idx, sq, si);
-		if(tid == 0) {
-			b.cq[u] = qq;
-			b.cj[u] = idx;
-		}
+		if(tid == 0) tail.unit(b, n, u, off[lo], off[lo + 1], r, qq, idx);
 		if(u + (int) gridDim.x < nunits) __syncthreads();
 	}
 	TS(2, 2);
@@ -1337,10 +1344,11 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n) {
 // So: prefix-min passes that treat the undecided bad entries as rejected;
 // the first bad entry found accepted (b_e < m_e) is certainly accepted, fixes
 // m_{e+1} = f_e, and the next pass starts after it.  Without bad entries this
-// is one pass.  Accepted (Q, P) updates are applied by the writer block only.
+// is one pass.  Accepted (Q, P) updates are applied by the writer block only,
+// or, with acc_out, flagged per entry for a later kernel to apply.
 __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_row, const int *e_j, const double *e_b,
                             const double *e_f, unsigned char *e_acc, bool writer, const TreeBufs &b, int &pi,
-                            int &pj, bool *had_bad, int n) {
+                            int &pj, bool *had_bad, int n, unsigned char *acc_out = nullptr) {
 	(void) n;   // trace stamps only
 	const int lane = threadIdx.x & 63;
 	int bad = 0;
@@ -1421,7 +1429,9 @@ __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_r
 			double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
 			pre = pre < cm ? pre : cm;
 			const bool accepted = good ? bb < pre : contrib;
-			if(writer && accepted) {
+			if(writer && acc_out) {
+				if(valid) acc_out[c0 + lane] = accepted;   // applied later (k_shd_join)
+			} else if(writer && accepted) {
 				b.Q[rv[k]] = f;
 				b.P[rv[k]] = jv[k];
 			}

@@ -38,6 +38,7 @@ struct TreeCtl {
 	double xsum;
 	long long rows, cells, cells_top, cells_rest;
 	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
+	int rtotal;          // sharded DNJ: replay entries whose accept flags k_shd_join applies
 };
 
 struct XsBlk;

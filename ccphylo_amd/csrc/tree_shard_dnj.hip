@@ -5,34 +5,34 @@
 // sD, N, Q, P and the join list are replicated and every rank updates them
 // with the same arithmetic.
 //
-// Per join at matrix size n (two collectives):
-//   0. row n-1 (the pop moves it to slot i, dnj.c:817 / matrix.c:518) rides
-//      in the record allreduce of step 2: its owner copies it behind the
-//      records, every other rank writes zeros there;
-//   1. minQpair's search (dnj.c:43) with the single-GPU kernels of
-//      ccg_dnj_search.h under the Shard row policy.  The candidate row, m0
-//      and the top-B rows S depend on the replicated Q only, so every rank
-//      computes the same ones.  Each rank rescans the rows of S it owns and
-//      bounds the serial running min below S with them alone:
-//      U_r = min(m0, min over its own k in S of max(fresh_k, Q_k)) is an upper
-//      bound of that running min for ANY subset of S (a rescanned k gives
-//      m <= fresh_k, a skipped one m <= Q_k).  It then rescans its own rows
-//      below S with Q < U_r; any other row is provably skipped by dnj.c:88;
-//   2. the fresh (q, j) of the rescanned rows go into a record array indexed
-//      by row -- a bitmap of the rescanned rows below S, f64 q, i32 j -- that
-//      each rank fills for its own rows and zeroes elsewhere, so one
-//      allreduce-sum gathers it exactly (the 8 rows of a bitmap byte are one
-//      band: one owner, no carries);
-//   3. every rank replays minQpair's accept/reject decisions over S and the
-//      rescanned rows below S in descending row order (replay_wave).  Rows
-//      of the union that the serial scan would skip have bound >= running
-//      min, so the replay rejects them: Q/P and the pair (i, j) are those of
-//      the single-GPU engine, on every rank;
-//   4. lines i and j gathered as in the sharded NJ; updateD (nj.c:836) on
-//      every rank for every k, own cells stored, the new line j kept whole;
-//   5. updateDNJ's Q/P pass (dnj.c:618-709) and DNJ_popArrange (dnj.c:817)
-//      over the replicated lines, own cells stored; the record array is
-//      zeroed for the next join.
+// Per join at matrix size n: five kernels, two collectives.
+//   1. k_dnj_plan (ccg_dnj_search.h, Shard row policy): minPos, m0 and the
+//      top rows S depend on the replicated Q only, so every rank computes the
+//      same ones.  Each rank bounds minQpair's serial running min with the
+//      S rows it owns alone: max(q(k, P[k]), Q_k) over its own k in S is an
+//      upper bound of that running min for ANY subset of S (a rescanned k
+//      gives m <= fresh_k <= q(k, P[k]), a skipped one m <= Q_k).  It lists
+//      its own S rows and its own rows below S with Q under the bound; any
+//      other row is provably skipped by dnj.c:88;
+//   2. k_dnj_scan rescans the listed units; its tail (RecTail) folds each
+//      row's units into a record indexed by row -- a bitmap of the listed
+//      rows, f64 fresh q, i32 j -- and copies row n-1 (the pop moves it to
+//      slot i, dnj.c:817 / matrix.c:518) behind the records; the other ranks
+//      hold zeros in every byte they do not own;
+//      -> allreduce-sum of records + row n-1: a gather, exact (the 8 rows of
+//      a bitmap byte are one band: one owner, no carries);
+//   3. k_shd_pick: every block replays minQpair's accept/reject decisions
+//      over the listed rows in descending order (replay_wave); rows that the
+//      serial scan would skip have bound >= running min, so the replay
+//      rejects them and (i, j) is the single-GPU engine's on every rank.
+//      Then each rank's pieces of lines i and j;
+//      -> allreduce-sum of lines i and j (a gather again);
+//   4. k_shd_join: the accepted (Q, P) updates, limbLength, updateD
+//      (nj.c:836) on every rank for every k, own cells stored, the new line j
+//      kept whole (its exact row sum: xs_join_row);
+//   5. k_shd_requeue: updateDNJ's Q/P pass (dnj.c:618-709) and
+//      DNJ_popArrange (dnj.c:817) over the replicated lines, own cells
+//      stored; the records are zeroed for the next join.
 // Hence the joins are bit-identical to ccg_tree's DNJ for every world size.
 #define CCG_DNJ_NO_TRACE
 #include <stdio.h>
@@ -63,163 +63,191 @@ static __host__ __device__ inline RecView rec_view(void *R, int n) {
 	return v;
 }
 
-// own rescans -> records: S rows from the folded S entries (k_dnj_find), the
-// rows below S by folding their units (k_dnj_scan) and setting their bit;
-// row n-1 behind them (the owner's cells, zeros on the other ranks)
+// own rescans -> records, as k_dnj_scan's tail: every scan block first copies
+// a slice of row n-1 behind the records (the owner's cells, zeros on the
+// other ranks); the thread that stores a row's last unit partial folds the
+// row's units and fills its record and bit.  The hand-off needs no L2
+// write-back or invalidate (an agent-scope release / acquire costs both on
+// the per-XCD L2s): the partials are stored write-through (sc1) and drained
+// (s_waitcnt vmcnt(0)) before the relaxed per-row arrival count, and the
+// last arriver reads them with sc1 loads (cdna_hip_programming.md G16, R1
+// with sc1 loads).  The count goes back to 0 for the next join.
 template <int ET>
-__global__ __launch_bounds__(TB) void k_shd_rec(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
-                                                Shard sh, void *R) {
-	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
-	{
+struct RecTail {
+	const typename Elem<ET>::T *D;
+	Shard sh;
+	void *R;
+	unsigned *cnt;   // n0 zeros
+	__device__ void begin(const TreeBufs &, int n) const {
 		typename Elem<ET>::T *xm = (typename Elem<ET>::T *) ((char *) R + rec_xm_off(n));
 		const bool own = sh.owns(n - 1);
 		const typename Elem<ET>::T *row = D + (own ? sh.off(n - 1) : 0);
 		for(int k = blockIdx.x * TB + threadIdx.x; k < n - 1; k += gridDim.x * TB) xm[k] = own ? row[k] : 0;
 	}
-	const RecView v = rec_view(R, n);
-	const int nS = ctl->nS, T = ctl->T, lane = threadIdx.x & 63;
-	for(int e = blockIdx.x * TB + threadIdx.x; e < nS; e += gridDim.x * TB) {
-		const int r = b.S[e];
-		if(sh.owns(r)) {
-			const Entry en = b.Sent[e];
-			v.f[r] = en.f;
-			v.j[r] = en.j;
-		}
-	}
-	// rows below S: one wave per entry folds its units
-	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
-	for(int x = w0; x < T; x += nw) {
-		const int r = b.crow[x], ua = b.coff[x], ub = b.coff[x + 1];
-		if(!sh.owns(r)) continue;   // k_dnj_plan lists every S row; its owner fills the record
-		double q = DBL_MAX;
-		int idx = 0;
-		for(int u = ua + lane; u < ub; u += 64) {
-			const double oq = b.cq[u];
-			const int oi = b.cj[u];
-			if(qarg_better(oq, oi, q, idx)) {
-				q = oq;
-				idx = oi;
+	__device__ void unit(const TreeBufs &b, int n, int u, int ua, int ub, int r, double q, int j) const {
+		if(ub - ua > 1) {
+			__hip_atomic_store(b.cq + u, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(b.cj + u, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			const unsigned seen = __hip_atomic_fetch_add(cnt + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if((int) seen != ub - ua - 1) return;
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			for(int x = ua; x < ub; ++x) {
+				if(x == u) continue;
+				const double oq = __hip_atomic_load(b.cq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				const int oi = __hip_atomic_load(b.cj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				if(qarg_better(oq, oi, q, j)) {
+					q = oq;
+					j = oi;
+				}
 			}
+			__hip_atomic_store(cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
-		qarg_wave_reduce(q, idx);
-		if(lane == 0) {
-			v.f[r] = q;
-			v.j[r] = idx;
-			atomicOr(&v.bits[r >> 5], 1u << (r & 31));
-		}
+		const RecView v = rec_view(R, n);
+		v.f[r] = q;
+		v.j[r] = j;
+		atomicOr(&v.bits[r >> 5], 1u << (r & 31));
 	}
-}
+};
 
-// One block: the entries in scan order (S, then the rescanned rows below S,
-// descending), minQpair's replay (dnj.c:76-125) and the pair.  Thread t owns
-// a contiguous run of bitmap words, the highest runs first.
-#define RPL_T 1024
-__global__ __launch_bounds__(RPL_T) void k_shd_replay(TreeBufs b, int n, void *R) {
-	__shared__ int s_scan[RPL_T / 64];
-	__shared__ int ssr[DNJ_B];
+// minQpair's replay (dnj.c:76-125) fused with the gather of lines i and j.
+// Every block builds the entries in scan order from the gathered records --
+// the rows with their bit set, descending (with the one-phase plan S rows are
+// listed like any other row) -- and replays them itself, so that no block
+// waits for another: the inputs (records, Q, m0, pos) are the same in every
+// block and so are the decisions.  Q/P are not written here (another block
+// may still be reading Q as a bound): block 0 leaves the entries and their
+// accept flags for k_shd_join.  Entries live in LDS up to PICK_CAP; beyond,
+// every block writes the same values into the shared HBM arrays and keeps
+// its accept scratch in its own slice of pacc.
+#define PICK_T 1024
+#define PICK_CAP 2048
+#define PICK_MAXB 256
+template <int ET>
+__global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
+                                                     Shard sh, void *R, typename Elem<ET>::T *__restrict__ X,
+                                                     unsigned char *pacc, unsigned char *acc_out, int pstride,
+                                                     unsigned long long *dbg) {
+#define PTS(ph)                                                                                  \
+	do {                                                                                         \
+		if(dbg && blockIdx.x == 0 && threadIdx.x == 0) {                                         \
+			unsigned long long t_;                                                               \
+			asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+			dbg[(n & 1023) * 8 + (ph)] = t_;                                                     \
+		}                                                                                        \
+	} while(0)
+	PTS(0);
+	__shared__ int s_scan[PICK_T / 64];
+	__shared__ int e_row[PICK_CAP], e_j[PICK_CAP];
+	__shared__ double e_b[PICK_CAP], e_f[PICK_CAP];
+	__shared__ unsigned char e_acc[PICK_CAP];
+	__shared__ int s_i, s_j;
 	TreeCtl *ctl = b.ctl;
-	if(ctl->done) return;
+	const int tid = threadIdx.x;
 	const RecView v = rec_view(R, n);
-	const int nS = ctl->nS, ntop = ctl->ntop, smin = ctl->smin, tid = threadIdx.x;
-	const double m0 = ctl->m0;
-	if(tid < nS) ssr[tid] = b.S[tid];
-	__syncthreads();
-	// rows [1, smin) with their bit set (no rows below S unless |S| = DNJ_B;
-	// smin is 1 then); with the one-phase plan (nS = 0) every listed row,
-	// S included, is in the bitmap: rows [1, n)
-	const int lim = nS == 0 ? n : smin;
-	const int nw = lim > 1 ? ((lim - 1) >> 5) + 1 : 0;
-	const int per = (nw + RPL_T - 1) / RPL_T;
-	auto word = [&](int w) -> unsigned {
-		unsigned x = v.bits[w];
-		if(w == 0) x &= ~1u;                                              // row 0 never qualifies
-		if(w == nw - 1 && (lim & 31)) x &= (1u << (lim & 31)) - 1u;       // rows >= lim
+	// rows [1, n) with their bit set; thread t owns a contiguous run of
+	// bitmap words, the highest runs first (the first word and the replay's
+	// inputs are loaded before the stop test: one round trip fewer)
+	const int nw = n > 1 ? ((n - 1) >> 5) + 1 : 0;
+	const int per = (nw + PICK_T - 1) / PICK_T;
+	auto word = [&](int w, unsigned x) -> unsigned {
+		if(w == 0) x &= ~1u;                                          // row 0 never qualifies
+		if(w == nw - 1 && (n & 31)) x &= (1u << (n & 31)) - 1u;       // rows >= n
 		return x;
 	};
+	const int wfirst = nw - 1 - tid * per;
+	const unsigned x0 = wfirst >= 0 ? v.bits[wfirst] : 0u;
+	const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
+	const double m0 = ctl->m0;
+	if(ctl->done) return;
+	PTS(1);
 	int cnt = 0;
 	for(int q = 0; q < per; ++q) {
 		const int w = nw - 1 - (tid * per + q);
-		if(w >= 0) cnt += __popc(word(w));
+		if(w >= 0) cnt += __popc(word(w, q == 0 ? x0 : v.bits[w]));
 	}
 	int total;
-	int pos = block_excl_scan(cnt, s_scan, &total);   // among the rest rows
+	int pos = block_excl_scan(cnt, s_scan, &total);
+	PTS(2);
+	const bool lds = total <= PICK_CAP;
+	int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
+	double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
 	for(int q = 0; q < per; ++q) {
 		const int w = nw - 1 - (tid * per + q);
 		if(w < 0) break;
-		unsigned x = word(w);
+		unsigned x = word(w, q == 0 ? x0 : v.bits[w]);
 		while(x) {
 			const int bit = 31 - __clz((int) x);
 			x &= ~(1u << bit);
-			const int r = w * 32 + bit;
-			int lo = ntop, hi = nS;   // S rows above r come first in scan order
-			while(lo < hi) {
-				const int mid = (lo + hi) >> 1;
-				if(ssr[mid] > r) lo = mid + 1; else hi = mid;
-			}
-			const int s = pos + lo;
-			b.crow[pos] = r;      // the rest rows, descending (this rank's own list is spent)
-			b.erow[s] = r;
-			b.eb[s] = b.Q[r];
-			b.ef[s] = v.f[r];
-			b.ej[s] = v.j[r];
-			++pos;
+			x_row[pos++] = w * 32 + bit;
 		}
 	}
 	__syncthreads();
-	// S rows: the rest rows above each come first (none above the top part)
-	if(tid < nS) {
-		const int r = ssr[tid];
-		int lo = 0, hi = tid < ntop ? 0 : total;
-		while(lo < hi) {
-			const int mid = (lo + hi) >> 1;
-			if(b.crow[mid] > r) lo = mid + 1; else hi = mid;
-		}
-		const int s = tid + lo;
-		b.erow[s] = r;
-		b.eb[s] = b.Sb[tid];
-		b.ef[s] = v.f[r];
-		b.ej[s] = v.j[r];
+	// then every entry's loads at once (the top rows of S fill whole bitmap
+	// words: loading per bit would chain 32 round trips in one thread)
+	for(int e = tid; e < total; e += PICK_T) {
+		const int r = x_row[e];
+		x_b[e] = b.Q[r];
+		x_f[e] = v.f[r];
+		x_j[e] = v.j[r];
 	}
 	__syncthreads();
+	PTS(3);
+	const bool writer = blockIdx.x == 0;
 	if(tid < 64) {
-		int pi = ctl->pos_i, pj = ctl->pos_j;
+		int pi = pos_i, pj = pos_j;
 		bool had_bad;
-		replay_wave(nS + total, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, true, b, pi, pj, &had_bad, n);
+		if(lds) replay_wave(total, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad, n, acc_out);
+		else replay_wave(total, m0, b.erow, b.ej, b.eb, b.ef, pacc + (size_t) blockIdx.x * pstride, writer, b, pi, pj,
+		                 &had_bad, n, acc_out);
 		if(tid == 0) {
-			if(pi == 0 && pj == 0) {
-				ctl->done = 1;
-				ctl->final_n = n;
-			} else {
-				ctl->i = pi;
-				ctl->j = pj;
+			s_i = pi;
+			s_j = pj;
+			if(writer) {
+				if(pi == 0 && pj == 0) {
+					ctl->done = 1;
+					ctl->final_n = n;
+				} else {
+					ctl->i = pi;
+					ctl->j = pj;
+				}
+				ctl->rtotal = total;
+				ctl->serial_replays += had_bad;
 			}
-			ctl->serial_replays += had_bad;
 		}
 	}
-}
-
-// the pieces of lines i and j this rank's rows hold: X[k] = D(i, k),
-// X[n + k] = D(j, k) (raw elements; zeros where another rank owns the cell)
-template <int ET>
-__global__ __launch_bounds__(TB) void k_shd_lines(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
-                                                  Shard sh, typename Elem<ET>::T *__restrict__ X) {
-	const int k = blockIdx.x * TB + threadIdx.x;
-	if(b.ctl->done || k >= n) return;
-	const int i = b.ctl->i, j = b.ctl->j;
-	typename Elem<ET>::T xi = 0, xj = 0;
-	if(k > i) {
-		if(sh.owns(k)) xi = D[sh.off(k) + i];
-	} else if(k < i && sh.owns(i)) {
-		xi = D[sh.off(i) + k];
+	__syncthreads();
+	PTS(4);
+	const int i = s_i, j = s_j;
+	if(i == 0 && j == 0) return;
+	// block 0: the entries behind the accept flags, for k_shd_join
+	if(writer && lds) {
+		for(int e = tid; e < total; e += PICK_T) {
+			b.erow[e] = e_row[e];
+			b.ef[e] = e_f[e];
+			b.ej[e] = e_j[e];
+		}
 	}
-	if(k > j) {
-		if(sh.owns(k)) xj = D[sh.off(k) + j];
-	} else if(k < j && sh.owns(j)) {
-		xj = D[sh.off(j) + k];
+	// the pieces of lines i and j this rank's rows hold: X[k] = D(i, k),
+	// X[n + k] = D(j, k) (raw elements; zeros where another rank owns the cell)
+	for(int k = blockIdx.x * PICK_T + tid; k < n; k += gridDim.x * PICK_T) {
+		typename Elem<ET>::T xi = 0, xj = 0;
+		if(k > i) {
+			if(sh.owns(k)) xi = D[sh.off(k) + i];
+		} else if(k < i && sh.owns(i)) {
+			xi = D[sh.off(i) + k];
+		}
+		if(k > j) {
+			if(sh.owns(k)) xj = D[sh.off(k) + j];
+		} else if(k < j && sh.owns(j)) {
+			xj = D[sh.off(j) + k];
+		}
+		X[k] = xi;
+		X[n + k] = xj;
 	}
-	X[k] = xi;
-	X[n + k] = xj;
+	PTS(5);
+	if(dbg && blockIdx.x == 0 && threadIdx.x == 0) dbg[(n & 1023) * 8 + 6] = total;
+#undef PTS
 }
 
 // limbLength (nj.c:42/:81), the join record and updateD (nj.c:836) over the
@@ -229,7 +257,8 @@ template <int ET>
 __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
                                                  Shard sh, const typename Elem<ET>::T *__restrict__ X,
                                                  typename Elem<ET>::T *__restrict__ Xm,
-                                                 typename Elem<ET>::T *__restrict__ Xj) {
+                                                 typename Elem<ET>::T *__restrict__ Xj,
+                                                 const unsigned char *__restrict__ acc) {
 	__shared__ int s_stop, s_nj, s_neg, s_exact, s_i, s_j;
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x;
@@ -252,6 +281,13 @@ __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restric
 	}
 	__syncthreads();
 	if(s_stop) return;
+	// minQpair's accepted (Q, P) updates (dnj.c:94-99), flagged by k_shd_pick
+	for(int e = k, tot = ctl->rtotal; e < tot; e += gridDim.x * TB) {
+		if(acc[e]) {
+			b.Q[b.erow[e]] = b.ef[e];
+			b.P[b.erow[e]] = b.ej[e];
+		}
+	}
 	const int i = s_i, j = s_j;
 	const double Dij = Elem<ET>::get(X[j], bs);
 	if(blockIdx.x == 0 && tid == 0) {
@@ -536,7 +572,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		return off;
 	};
 	const size_t o_R = take(rec_all_bytes(n0, ET)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
-	const size_t o_Xj = take((size_t) n0 * ET + 8), o_rp = take(rp_bytes), o_xc = take(xc_bytes);
+	const size_t o_Xj = take((size_t) n0 * ET + 8), o_pf = take((size_t) n0), o_pa = take((size_t) PICK_MAXB * n0), o_pc = take((size_t) n0 * 4);
+	const size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
 	char *m = NULL;
 	unsigned char *h = NULL;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) {
@@ -557,6 +594,13 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	grid.load();
 	void *R = m + o_R;
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj), *Xc = (T *) (m + o_xc);
+	unsigned char *pflag = (unsigned char *) (m + o_pf), *pacc = (unsigned char *) (m + o_pa);
+	unsigned *pcnt = (unsigned *) (m + o_pc);
+	unsigned long long *dbg = NULL;
+	if(getenv("CCG_PICK_TS")) {
+		hipMalloc((void **) &dbg, 1024 * 8 * 8);
+		hipMemsetAsync(dbg, 0, 1024 * 8 * 8, st);
+	}
 	TreeCtl init, hc;
 	long long launches = 0;
 	int n = n0;
@@ -596,7 +640,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		int since_check = 0;
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
-			const unsigned gn = cdiv(n, TB);
+			const unsigned gn = cdiv(n, TB), gp = cdiv(n, PICK_T) < PICK_MAXB ? cdiv(n, PICK_T) : PICK_MAXB;
 			T *Xmr = (T *) ((char *) R + rec_xm_off(n));   // row n-1, gathered with the records
 			const unsigned gs = grid.sel(n), gc = grid.scan(n);
 			const int seg = grid.seg(n);
@@ -607,22 +651,19 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_qdelay);
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_qdelay);
 			kt.mark(CCG_K_FIND);
-			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg);
-			kt.mark(CCG_K_REST);
-			k_shd_rec<ET><<<FOLD_BLOCKS, TB, 0, st>>>(D, b, n, sh, R);
+			k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
 			kt.mark(CCG_K_REST);
 			SD_TRY(cr.allreduce(R, rec_all_bytes(n, ET)));
-			k_shd_replay<<<1, RPL_T, 0, st>>>(b, n, R);
-			k_shd_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, X);
+			k_shd_pick<ET><<<gp, PICK_T, 0, st>>>(D, b, n, sh, R, X, pacc, pflag, n0, dbg);
 			kt.mark(CCG_K_UPDATE);
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
-			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj);
+			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj, pflag);
 			kt.mark(CCG_K_UPDATE);
 			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
 			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
-			launches += 7;
+			launches += 5;
 			--n;
 			if(++since_check == 1024) {
 				since_check = 0;
@@ -634,6 +675,22 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	SD_HIP(hipEventRecord(ctx->ev1, st));
 	kt.finish();
+	if(dbg) {
+		static unsigned long long hd[1024 * 8];
+		hipMemcpy(hd, dbg, sizeof(hd), hipMemcpyDeviceToHost);
+		double acc[8] = {0};
+		int cnt = 0;
+		for(int s_ = 0; s_ < 1024; ++s_) {
+			const unsigned long long *t_ = hd + s_ * 8;
+			if(!t_[0] || !t_[5]) continue;
+			for(int p_ = 1; p_ < 6; ++p_) acc[p_] += (double) (t_[p_] - t_[p_ - 1]) * 10.0;
+			acc[6] += (double) t_[6];
+			++cnt;
+		}
+		fprintf(stderr, "pick phases over %d joins (ns): entry->loads %.0f, count+scan %.0f, entries %.0f, replay %.0f, gather %.0f; total entries %.1f\n",
+		        cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt);
+		hipFree(dbg);
+	}
 	SD_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
 	SD_HIP(hipStreamSynchronize(st));
 	SD_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
