@@ -17,24 +17,25 @@
 // ends in a "last block" ticket: every kernel writes per-block partials, and
 // the NEXT kernel folds them redundantly in each of its blocks (identical,
 // fixed-order, hence deterministic), substituting locally the few values its
-// block 0 persists for the kernels after it.  Per DNJ join:
-//   k_dnj_select  folds the previous requeue (updateDNJ + DNJ_popArrange +
-//                 minPos), picks the top-B candidate rows S (Q[r] < m0,
-//                 scanning down from n-1) and rescans them in 16384-cell
-//                 units; each unit atomically lowers the key of
-//                 U = min(m0, min_k max(fresh_k, Q_k)), an upper bound of the
-//                 serial running min m(i) for every row below S (a row k that
-//                 the serial scan rescans gives m(i) <= fresh_k, one it skips
-//                 gives m(i) <= m(k) <= Q_k; max distributes over the units'
-//                 min, so one atomicMin per unit suffices);
-//   k_dnj_rest    rescans every row below S with Q[r] < U (any other row is
-//                 provably skipped by minQpair); one extra block folds the
-//                 units of S;
-//   k_dnj_join    replays minQpair's accept/reject decisions over S then the
-//                 rest in descending row order (a parallel prefix-min when
-//                 every fresh min is >= its stale bound, serial otherwise),
-//                 records the join and runs updateD;
-//   k_dnj_requeue folds the new row sum of j and runs updateDNJ's Q/P part
+// block 0 persists for the kernels after it.  Per DNJ join
+// (ccg_dnj_search.h has the search kernels):
+//   k_dnj_plan    one block: folds the previous requeue (updateDNJ +
+//                 DNJ_popArrange partials, minPos), picks the top rows S
+//                 (Q[r] < m0, scanning down from n-1), bounds the rows below
+//                 S by max(q(k, P[k]), Q_k) over the S rows k above them (the
+//                 Q criterion at k's stored partner cell is >= k's fresh min,
+//                 so this bounds minQpair's running min as max(fresh_k, Q_k)
+//                 does) and lists S and every row under its bound, descending,
+//                 with unit offsets (any unlisted row is provably skipped);
+//   k_dnj_scan    rescans the listed rows in SEG-cell units over the grid
+//                 (k_dnj_fold folds each entry's units once for large n);
+//   k_dnj_join    replays minQpair's accept/reject decisions over the entries
+//                 in descending row order (a parallel prefix-min when every
+//                 fresh min is >= its stale bound, pass by pass otherwise),
+//                 records the join, runs updateD and, in exact mode, its
+//                 blocks' part of the serial row sum (xs_join_row);
+//   k_dnj_requeue takes the new row sum of j (tree sum, or the exact walk of
+//                 the join blocks' records) and runs updateDNJ's Q/P part
 //                 plus DNJ_popArrange.
 // NJ: k_nj_argmin (initQ over all cells), k_nj_join (fold + updateD),
 // k_nj_pop (row sum + ltdMatrix_popArrange).
