@@ -19,28 +19,24 @@ struct DenseRows {
 #define DNJ_BANDS 64     // S: the top rows with Q < m0, then the min-Q row of each
                          // of at most this many bands below them (DnjGrid::top/bands)
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
-#define SEL_BLOCKS 1024  // max grid of k_dnj_select
-#define SCAN_BLOCKS 1024 // max grid of k_dnj_scan (default; CCG_SCAN_MAX overrides)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
-#define TBF 1024         // threads of k_dnj_find (one block)
-#define FIND_RPT 16      // rows per thread per step of k_dnj_find (one step up to n = 16386)
-#define FIND_CHUNKS 2048  // 64-row chunks of k_dnj_find's S-rank table (n <= 131072; else binary searches)
+#define TBF 1024         // threads of k_dnj_plan (one block)
+#define FIND_RPT 16      // rows per thread per step of k_dnj_plan's listing (one step up to n = 15361)
+#define FIND_CHUNKS 2048  // 64-row chunks of k_dnj_plan's S-rank table (n <= 131072; else binary searches)
 #define REPLAY_CAP 2048  // rest entries staged in LDS
-#define JOIN_UPRE 1024   // rest-unit partials k_dnj_join prefetches into LDS
+#define JOIN_UPRE 2048   // rest-unit partials k_dnj_join prefetches into LDS
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
 
-// Grids of the search kernels: k_dnj_select min(DNJ_B * ceil((n-1)/SEG),
-// sel_max), k_dnj_scan min(ceil(n / scan_div), scan_max).  CCG_SEL_MAX,
-// CCG_SCAN_DIV and CCG_SCAN_MAX override them (tests shrink the grids so
-// that the unit pruning of later grid waves runs at small n).
+// Grid of k_dnj_scan: min(ceil(n / scan_div), scan_max).  CCG_SCAN_DIV and
+// CCG_SCAN_MAX override it (tests shrink the grid so that several grid
+// waves of units run at small n).
 struct DnjGrid {
-	int sel_max = SEL_BLOCKS, scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
+	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0;
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
 		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
-		if(const char *e = getenv("CCG_SEL_MAX")) sel_max = atoi(e) > 0 ? atoi(e) : SEL_BLOCKS;
 		if(const char *e = getenv("CCG_SCAN_DIV")) scan_div = atoi(e) > 0 ? atoi(e) : 4;
 		if(const char *e = getenv("CCG_SCAN_MAX")) scan_max = atoi(e) > 0 ? atoi(e) : 2048;
 		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
@@ -69,11 +65,6 @@ struct DnjGrid {
 		b = b > DNJ_BANDS ? DNJ_BANDS : b;
 		return top(n) + b > DNJ_B ? DNJ_B - top(n) : b;
 	}
-	unsigned sel(int n) const {
-		const int s = seg(n);
-		const long long g = (long long) DNJ_B * ((n - 1 + s - 1) / s);
-		return (unsigned) (g < sel_max ? g : sel_max);
-	}
 	unsigned scan(int n) const {
 		const long long g = (n + scan_div - 1) / scan_div;
 		return (unsigned) (g < scan_max ? g : scan_max);
@@ -101,6 +92,13 @@ __device__ __forceinline__ unsigned long long rt_stamp() {
 			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
 		}                                                                             \
 	} while(0)
+#define TSW(kern, ph, th)                                                             \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == (th)) {                                  \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
 #define TS_ENTRY(kern)                                                                \
 	do {                                                                              \
 		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
@@ -118,6 +116,7 @@ __device__ __forceinline__ unsigned long long rt_stamp() {
 #else
 #define TS_EXIT(kern)
 #define TS(kern, ph)
+#define TSW(kern, ph, th)
 #define TS_ENTRY(kern)
 #endif
 
@@ -268,507 +267,12 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 	}
 }
 
-// ------------------------------------------------------------------ DNJ select
-// Prologue, wave 0 only (no block barriers): the previous join's
-// updateDNJ/DNJ_popArrange fold (dnj.c:619-709, :817-975), minPos
-// (dnj.c:1026-1032), minQpair's start (dnj.c:55-60) and the top-B rows S
-// (rows n-1, n-2, ... with Q[r] < m0).  Then the whole block rescans units.
-template <int ET, bool GEN, class Rows>
-__global__ __launch_bounds__(TB) void k_dnj_select(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                    int n, int first, Rows rows, int seg, int ktop, int kbands) {
-	__shared__ int sS[DNJ_B], so[DNJ_B + 1];
-	__shared__ double sQS[DNJ_B];
-	__shared__ double sq[TB / 64];
-	__shared__ int si[TB / 64];
-	__shared__ int s_nS, s_isub, s_Nm, s_done;
-	__shared__ double s_sDm;
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-	TS_ENTRY(0);
-	TS(0, 0);
-	if(wid == 0) {
-		// ---- loads that do not depend on the previous join's outcome
-		const int done = ctl->done;
-		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
-		const int cand0 = first ? ctl->cand : 0;
-		const double cand0_q = first ? ctl->cand_q : 0.0;
-		const int cand0_p = first ? ctl->cand_p : 0;
-		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, cq1 = DBL_MAX;
-		int ix[4] = {0, -1, 0, -1}, cp1 = 0;
-		if(!first) {
-			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
-			for(int w = lane; w < G; w += 64) {
-#pragma unroll
-				for(int t = 0; t < 4; ++t) {
-					double oq = b.qpart[4 * w + t];
-					int oi = b.ipart[4 * w + t];
-					if(qarg_better(oq, oi, q[t], ix[t])) {
-						q[t] = oq;
-						ix[t] = oi;
-						if(t == 1) {
-							cq1 = b.cfq[w];
-							cp1 = b.cfp[w];
-						}
-					}
-				}
-			}
-		}
-		// band candidates: lane l holds the min-Q row of the requeue blocks
-		// [l G / 64, (l + 1) G / 64) (rows ascending with the lane)
-		double bcq = DBL_MAX;
-		int bcr = 0;
-		if(!first && lane < kbands) {
-			const int G = (int) cdiv(n + 1, TB);
-			fold_units(b.bmq, b.bmr, lane * G / kbands, (lane + 1) * G / kbands, bcq, bcr);
-		}
-		double topQ[SEL_RPL];
-#pragma unroll
-		for(int m = 0; m < SEL_RPL; ++m) {
-			int r = n - 1 - (m * 64 + lane);   // coalesced; descending = (m, lane) order
-			topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-		}
-		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
-		const int Nm = first ? 0 : b.N[n];
-		if(done) {
-			if(lane == 0) s_done = 1;
-		} else {
-			qarg_wave_reduce(q[0], ix[0]);
-			qarg_wave_reduce_carry(q[1], ix[1], cq1, cp1);
-			qarg_wave_reduce(q[2], ix[2]);
-			qarg_wave_reduce(q[3], ix[3]);
-			const int nn = n;
-			const bool move = !first && i != nn;
-			const int isub = move ? i : -1, jsub = first ? -1 : j;
-			const double Qj = q[0], Qi = q[2];
-			const int Pj = ix[0], Pi = ix[2];
-			// Q/P of the rows minPos can pick, all known without loads: j and
-			// the moved i from the fold; the row lowered through column j with
-			// its final (Q, P) carried by the requeue partials; the row lowered
-			// through the moved row keeps (q[3], i); row 0 keeps DBL_MAX.
-#define QSUB(r) ((r) == jsub ? Qj : (r) == isub ? Qi : (r) == ix[1] ? cq1 : (r) == ix[3] ? q[3] : DBL_MAX)
-#define PSUB(r) ((r) == jsub ? Pj : (r) == isub ? Pi : (r) == ix[1] ? cp1 : (r) == ix[3] ? i : 0)
-			int cand;
-			if(first) {
-				cand = cand0;
-			} else {
-				int p = j;
-				if(ix[1] >= 0 && qarg_better(q[1], ix[1], q[0], j)) p = ix[1];
-				int p2 = 0;
-				if(move) {
-					p2 = i;
-					if(ix[3] >= 0 && qarg_better(q[3], ix[3], q[2], i)) p2 = ix[3];
-				}
-				if(p2 == nn) {
-					cand = p;
-				} else if(p == nn) {
-					cand = p2;
-				} else {
-					double Qp = QSUB(p), Qp2 = QSUB(p2);
-					cand = (Qp2 < Qp || (p < p2 && Qp2 == Qp)) ? p2 : p;
-				}
-			}
-			const double Qc = !cand ? DBL_MAX : first ? cand0_q : QSUB(cand);
-			double m0 = DBL_MAX;
-			if(cand && m0 != Qc) m0 = Qc;
-			const int pos_i = (cand && m0 != DBL_MAX) ? cand : 0;
-			const int pos_j = (cand && m0 != DBL_MAX) ? (first ? cand0_p : PSUB(cand)) : 0;
-#undef QSUB
-#undef PSUB
-			TS(0, 1);
-			// ---- S, top part: ktop rows, 64*SEL_RPL rows per step; row
-			// base - (m*64 + lane), so the descending order is (m, lane) and
-			// ballots give the positions
-			int cnt = 0;
-			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop; base -= 64 * SEL_RPL, ++step) {
-#pragma unroll
-				for(int m = 0; m < SEL_RPL; ++m) {
-					const int r = base - (m * 64 + lane);
-					if(step) topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-					const double v = r == jsub ? Qj : r == isub ? Qi : topQ[m];
-					const bool f = r >= 1 && v < m0;
-					const unsigned long long bm = __ballot(f);
-					const int pos = cnt + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm >> 32),
-					                                                     __builtin_amdgcn_mbcnt_lo((unsigned) bm, 0));
-					if(f && pos < ktop) {
-						sS[pos] = r;
-						sQS[pos] = v;
-					}
-					cnt += __popcll(bm);
-				}
-			}
-			const int ntop = cnt < ktop ? cnt : ktop;
-			int nS = ntop;
-			const int smin = ntop == ktop ? sS[ktop - 1] : 1;
-			// ---- S, band part: below the top part, each band's min-Q row with
-			// Q < m0.  Any choice of S is exact (the bounds only use rows above,
-			// the replay runs in row order); spread over all depths these rows
-			// bound the rows below them far better than more top rows do
-			// (tools/sim_stages.c).  Descending rows = higher lanes first.
-			if(smin > 1 && kbands) {
-				const bool f = bcr >= 1 && bcr < smin && bcq < m0;
-				const unsigned long long bm = __ballot(f);
-				const int pos = ntop + __popcll(lane == 63 ? 0ull : bm >> (lane + 1));
-				if(f) {
-					sS[pos] = bcr;
-					sQS[pos] = bcq;
-				}
-				nS = ntop + __popcll(bm);
-			}
-			wave_sync();
-			// ---- units of seg cells per row of S (lane: rows 2*lane, 2*lane+1)
-			const int t0 = 2 * lane, t1 = 2 * lane + 1;
-			const int r0 = t0 < nS ? sS[t0] : 0, r1 = t1 < nS ? sS[t1] : 0;
-			// rows this rank does not hold get no units (their fresh min stays
-			// DBL_MAX here and comes from their owner)
-			const int u0 = rows.owns(r0) ? dcdiv(r0, seg) : 0, u1 = rows.owns(r1) ? dcdiv(r1, seg) : 0;
-			int utot;
-			const int upre = wave_excl_scan(u0 + u1, &utot);
-			if(t0 < nS) so[t0] = upre;
-			if(t1 < nS) so[t1] = upre + u0;
-			if(lane == 0) so[nS] = utot;
-			TS(0, 2);
-			if(blockIdx.x == 0) {
-				// persist the fold and the selection for the kernels that follow
-				if(t0 < nS) {
-					b.S[t0] = r0;
-					b.Sb[t0] = sQS[t0];
-					b.uoff[t0] = upre;
-				}
-				if(t1 < nS) {
-					b.S[t1] = r1;
-					b.Sb[t1] = sQS[t1];
-					b.uoff[t1] = upre + u0;
-				}
-				const long long cells = wave_sum_int((long long) (u0 ? r0 : 0) + (u1 ? r1 : 0));
-				if(lane == 0) {
-					b.uoff[nS] = utot;
-					if(!first) {
-						b.Q[j] = Qj;
-						b.P[j] = Pj;
-						if(move) {
-							b.Q[i] = Qi;
-							b.P[i] = Pi;
-							b.sD[i] = sDm;
-							b.N[i] = Nm;
-						}
-					}
-					ctl->cand = cand;
-					ctl->m0 = m0;
-					ctl->pos_i = pos_i;
-					ctl->pos_j = pos_j;
-					ctl->nS = nS;
-					ctl->ntop = ntop;
-					ctl->smin = smin;
-					ctl->rows += nS;
-					ctl->cells += cells;
-					ctl->cells_top += cells;
-				}
-			}
-			if(lane == 0) {
-				s_done = 0;
-				s_nS = nS;
-				s_isub = isub;
-				s_Nm = Nm;
-				s_sDm = sDm;
-			}
-		}
-	}
-	__syncthreads();
-	if(s_done) return;
-	TS(0, 3);
-	const int nS = s_nS, isub = s_isub, Nm = s_Nm;
-	const double sDm = s_sDm;
-	const int nunits = so[nS];
-	// ---- rescans, one unit of seg cells per block iteration
-	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
-		int lo = 0, hi = nS - 1;   // last t with so[t] <= u
-		while(lo < hi) {
-			int mid = (lo + hi + 1) >> 1;
-			if(so[mid] <= u) lo = mid; else hi = mid - 1;
-		}
-		const int r = sS[lo];
-		const int c0 = (u - so[lo]) * seg, c1 = c0 + seg < r ? c0 + seg : r;
-		const int Nr = GEN ? (r == isub ? Nm : b.N[r]) : n;
-		const double sDr = r == isub ? sDm : b.sD[r];
-		double qq = DBL_MAX;
-		int idx = 0;
-		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, sDr, isub, GEN ? Nm : n, sDm, qq,
-		                                       idx);
-		qarg_block_reduce1(qq, idx, sq, si);
-		TS(0, 4);
-		if(tid == 0) {
-			b.uq[lo * b.maxu + (u - so[lo])] = qq;
-			b.uj[lo * b.maxu + (u - so[lo])] = idx;
-		}
-		if(u + (int) gridDim.x < nunits) __syncthreads();
-	}
-	TS(0, 5);
-	TS_EXIT(0);
-}
-
-// ------------------------------------------------------------------ DNJ find
-// One block: the fresh mins of S (fold of k_dnj_select's units), the bound
-// U = min(m0, min_k max(fresh_k, Q_k)) and the rows below S with Q[r] < U in
-// descending order (any other row is provably skipped by minQpair, see the
-// file comment) with their SEG-cell unit offsets, for k_dnj_scan/k_dnj_join.
-template <class Rows, bool BANDS>
-__global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, int seg) {
-	constexpr int NW = TBF / 64, FR = FIND_RPT;
-	__shared__ double sq[NW];
-	__shared__ double s_U;
-	__shared__ int s_mw[FR * NW], s_cnt, s_scan[NW];
-	__shared__ int lrow[REPLAY_CAP];
-	__shared__ double spm[DNJ_B];
-	__shared__ int ssr[DNJ_B];
-	__shared__ int sch[FIND_CHUNKS];
-	TreeCtl *ctl = b.ctl;
-	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-	TS_ENTRY(1);
-	TS(1, 0);
-	// ---- loads that do not depend on U (rows n-2 down; rows >= smin masked)
-	const int done = ctl->done, nS = ctl->nS, smin = ctl->smin, ntop = ctl->ntop;
-	const double m0 = ctl->m0;
-	int sr = 0, su = 0;
-	double sb = DBL_MAX;
-	// the first UPRE units of each S row, loaded before their count is known
-	constexpr int UPRE = 8;
-	double uqv[UPRE];
-	int ujv[UPRE];
-	if(tid < DNJ_B) {
-		sr = b.S[tid];
-		sb = b.Sb[tid];
-		su = b.uoff[tid + 1] - b.uoff[tid];
-		const int lim = b.maxu < UPRE ? b.maxu : UPRE;
-#pragma unroll
-		for(int u = 0; u < UPRE; ++u) {
-			const int v = u < lim ? u : lim - 1;
-			uqv[u] = b.uq[tid * b.maxu + v];
-			ujv[u] = b.uj[tid * b.maxu + v];
-		}
-	}
-	const int top = n - 2;
-	double qv[FR];
-#pragma unroll
-	for(int m = 0; m < FR; ++m) {
-		const int r = top - (m * TBF + tid);   // coalesced; descending = (m, tid) order
-		qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-	}
-	if(done) return;
-	// ---- fresh mins of S and U
-	double fq = DBL_MAX;
-	int fj = 0;
-	if(tid < nS) {
-#pragma unroll
-		for(int u = 0; u < UPRE; ++u) {
-			if(u < su && qarg_better(uqv[u], ujv[u], fq, fj)) {
-				fq = uqv[u];
-				fj = ujv[u];
-			}
-		}
-		if(su > UPRE) fold_units(b.uq + tid * b.maxu, b.uj + tid * b.maxu, UPRE, su, fq, fj);
-		Entry e;
-		e.f = fq;
-		e.bnd = sb;
-		e.row = sr;
-		e.j = fj;
-		b.Sent[tid] = e;
-	}
-	if(BANDS) {
-		// bound of the rows below S row t: min(m0, max(fresh, Q) over S rows
-		// 0..t), a prefix min in scan order (S spans at most 2 waves)
-		const double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
-		const double x = wave_incl_min(v);
-		if(lane == 63) sq[wid] = x;
-		__syncthreads();
-		double c = m0;
-		for(int w = 0; w < wid && w < 2; ++w) c = sq[w] < c ? sq[w] : c;
-		if(tid < nS) {
-			spm[tid] = x < c ? x : c;
-			ssr[tid] = sr;
-		}
-		__syncthreads();
-		// every row below the top part is under the bound after it
-		if(tid == 0) s_U = smin > 1 ? spm[ntop - 1] : m0;
-		__syncthreads();
-	} else {
-		// S all on top: one bound for every row below it
-		double v = tid < nS ? (fq > sb ? fq : sb) : DBL_MAX;
-		v = readlane_d(wave_incl_min(v), 63);
-		if(lane == 0) sq[wid] = v;
-		__syncthreads();
-		if(tid == 0) {
-			double U = m0;
-			for(int w = 0; w < NW; ++w) U = sq[w] < U ? sq[w] : U;
-			s_U = U;
-		}
-		__syncthreads();
-	}
-	const double U = s_U;
-	// S rows above row r: a table over 64-row chunks (the S rows above the
-	// chunk), then the at most two band rows inside the chunk (band rows come
-	// from distinct 256-row requeue blocks).  No dependent LDS chains per row.
-	const bool bands = BANDS && nS > ntop;   // else S is all above the listed rows (k_dnj_join's plain slots)
-	const int nch0 = smin > 1 && bands ? ((smin - 1) >> 6) + 1 : 0;
-	const bool table = nch0 <= FIND_CHUNKS;   // else (n > 2^20) a binary search per row
-	const int nch = table ? nch0 : 0;
-	for(int c = tid; c < nch; c += TBF) {
-		int lo = ntop, hi = nS;   // S rows at or above row 64 (c + 1)
-		while(lo < hi) {
-			const int mid = (lo + hi) >> 1;
-			if(ssr[mid] >= 64 * (c + 1)) lo = mid + 1; else hi = mid;
-		}
-		sch[c] = lo;
-	}
-	if(nch) __syncthreads();   // uniform
-	auto s_above = [&](int r) {
-		int k;
-		if(table) {
-			k = sch[r >> 6];
-			while(k < nS && ssr[k] > r) ++k;
-		} else {
-			int lo = ntop, hi = nS;
-			while(lo < hi) {
-				const int mid = (lo + hi) >> 1;
-				if(ssr[mid] > r) lo = mid + 1; else hi = mid;
-			}
-			k = lo;
-		}
-		return k;
-	};
-	TS(1, 1);
-	// ---- rows [1, smin) with Q[r] < U, descending: per (m, wave) ballot
-	// counts, one prefix over them, then mbcnt within the wave
-	int T = 0;
-	if(smin > 1) {
-		for(int base = top; base >= 1; base -= TBF * FR) {
-			if(base != top) {
-#pragma unroll
-				for(int m = 0; m < FR; ++m) {
-					const int r = base - (m * TBF + tid);
-					qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-				}
-			}
-			unsigned long long bm[FR];
-			int above[FR];
-#pragma unroll
-			for(int m = 0; m < FR; ++m) {
-				const int r = base - (m * TBF + tid);
-				bool f = r >= 1 && r < smin && qv[m] < U && rows.owns(r);
-				above[m] = ntop;
-				if(bands && f) {
-					// its own bound (the S rows above it), and not an S row itself
-					const int t = s_above(r);
-					f = qv[m] < spm[t - 1] && !(t < nS && ssr[t] == r);
-					above[m] = t;
-				}
-				bm[m] = __ballot(f);
-				if(lane == 0) s_mw[m * NW + wid] = __popcll(bm[m]);
-			}
-			__syncthreads();
-			if(wid == 0) {
-				// exclusive prefix over the FR*NW counts in (m, wave) order
-				constexpr int NC = FR * NW, PER = (NC + 63) / 64;
-				int c[PER], sum = 0;
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					c[k] = x < NC ? s_mw[x] : 0;
-					sum += c[k];
-				}
-				int tot;
-				int pre = wave_excl_scan(sum, &tot);
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					if(x < NC) s_mw[x] = pre;
-					pre += c[k];
-				}
-				if(lane == 0) s_cnt = tot;
-			}
-			__syncthreads();
-#pragma unroll
-			for(int m = 0; m < FR; ++m) {
-				if((bm[m] >> lane) & 1ull) {
-					const int r = base - (m * TBF + tid);
-					const int pos = T + s_mw[m * NW + wid] +
-					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
-					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
-					if(pos < REPLAY_CAP) lrow[pos] = r;
-					b.crow[pos] = r;
-					b.cbnd[pos] = qv[m];
-					if(bands) b.cslot[pos] = pos + above[m];
-				}
-			}
-			T += s_cnt;
-			__syncthreads();
-			if(base - TBF * FR < 1) break;
-		}
-	}
-	if(tid == 0) ctl->T = T;
-	// slots of the S rows in scan order: the rest rows above each come first
-	// (stored last: a store before a barrier would make the barrier wait for it)
-	int spos = tid;
-	if(bands && tid < nS) {
-		int lo = 0, hi = tid < ntop ? 0 : T;   // first rest entry below S row tid (none above the top part)
-		const int r = ssr[tid];
-		if(T <= REPLAY_CAP) {   // the list in LDS (kept apart: no flat loads)
-			while(lo < hi) {
-				const int mid = (lo + hi) >> 1;
-				if(lrow[mid] > r) lo = mid + 1; else hi = mid;
-			}
-		} else {
-			while(lo < hi) {
-				const int mid = (lo + hi) >> 1;
-				if(b.crow[mid] > r) lo = mid + 1; else hi = mid;
-			}
-		}
-		spos = tid + lo;
-	}
-	if(T == 0) {
-		if(bands && tid < nS) b.Spos[tid] = spos;
-		return;
-	}
-	// ---- SEG-cell units per entry (thread: a contiguous run of entries)
-	const int K = dcdiv(T, TBF);
-	int mysum = 0;
-	long long cells = 0;
-	for(int k = 0; k < K; ++k) {
-		const int e = tid * K + k;
-		if(e < T) {
-			const int r = e < REPLAY_CAP ? lrow[e] : b.crow[e];   // past the LDS copy: HBM
-			mysum += dcdiv(r, seg);
-			cells += r;
-		}
-	}
-	int utot;
-	int pre = block_excl_scan(mysum, s_scan, &utot);
-	for(int k = 0; k < K; ++k) {
-		const int e = tid * K + k;
-		if(e < T) {
-			b.coff[e] = pre;
-			pre += dcdiv(e < REPLAY_CAP ? lrow[e] : b.crow[e], seg);
-		}
-	}
-	cells = wave_sum_int(cells);
-	if(lane == 0 && cells) {
-		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) cells);
-		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) cells);
-	}
-	if(tid == 0) {
-		b.coff[T] = utot;
-		ctl->rows += T;
-	}
-	if(bands && tid < nS) b.Spos[tid] = spos;
-	TS(1, 2);
-	TS_EXIT(1);
-}
-
 // ------------------------------------------------------------------ DNJ plan (one-phase search)
-// One block of TBF threads, before any rescan of the join; it replaces
-// k_dnj_select's prologue + k_dnj_find, so S and the rows below it are
-// rescanned in ONE phase (k_dnj_scan):
+// One block of TBF threads, before any rescan of the join, so S and the rows
+// below it are rescanned in ONE phase (k_dnj_scan):
 //   wave 0: the previous join's updateDNJ / DNJ_popArrange fold, minPos and
-//   minQpair's start (dnj.c:1026-1032, :55-60), S (as k_dnj_select);
+//   minQpair's start (dnj.c:1026-1032, :55-60), S: the top rows with Q < m0,
+//   plus band-minimum rows for large n;
 //   the bound of the rows below S, from each S row k's Q criterion at its
 //   stored partner column P[k] evaluated now: fresh_k is the minimum over all
 //   of row k's columns, so q(k, P[k]) >= fresh_k and max(q(k, P[k]), Q_k)
@@ -778,9 +282,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_find(TreeBufs b, int n, Rows rows, 
 //   in ~94% of S rows and the same rows qualify (tools/sim_bound.c, N=10k:
 //   120.0 rest rows per join either way);
 //   the entry list in scan order (descending rows: S, then the rows below
-//   with Q < their bound, band rows of S merged in) with SEG-cell unit
-//   offsets (crow / cbnd / coff, ctl->T), read by k_dnj_scan and k_dnj_join
-//   (which sees nS = 0: every entry is an "rest" entry).
+//   with Q < their bound, band rows of S merged in: crow / cbnd, ctl->T),
+//   read by k_dnj_scan and k_dnj_join (which sees nS = 0: every entry is a
+//   "rest" entry); entry e's rescan units are [e umax, (e + 1) umax).
 // Rows j and i of the previous join have their Q/P in the requeue partials
 // (substituted here, persisted by thread 0); the moved row i's sD/N (row n's)
 // are substituted as column and persisted for the kernels after.
@@ -796,9 +300,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	__shared__ double sQS[DNJ_B], sQP[DNJ_B];   // S rows: Q, and the Q criterion at the partner cell (band rows)
 	__shared__ double spq[NSP];                 // the Q criterion at the partner cell of row top - t
 	__shared__ double spm[DNJ_B + 2];           // bound below S row t (prefix over S in scan order)
-	__shared__ int s_mw[FR * LW], s_mu[FR * LW], s_cnt, s_ucnt;
+	__shared__ int s_mw[FR * LW], s_cnt;
 	__shared__ int sch[FIND_CHUNKS];
-	__shared__ int s_done, s_isub, s_jsub, s_nS, s_ntop, s_smin, s_Nm, s_utop;
+	__shared__ int s_done, s_isub, s_jsub, s_nS, s_ntop, s_smin, s_Nm;
 	__shared__ double s_m0, s_Qj, s_Qi, s_sDm;
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -835,7 +339,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
 		}
 	} else {
-		// ---- k_dnj_select's prologue: fold, minPos, m0, S
+		// ---- prologue: fold, minPos, m0, S
 		const int done = ctl->done;
 		const int i = first ? -1 : ctl->i, j = first ? -1 : ctl->j;
 		const int cand0 = first ? ctl->cand : 0;
@@ -919,10 +423,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			if(lane == 0) s_done = 1;
 		} else {
 			TS(1, 5);
-			qarg_wave_reduce(q[0], ix[0]);
-			qarg_wave_reduce_carry(q[1], ix[1], cq1, cp1);
-			qarg_wave_reduce(q[2], ix[2]);
-			qarg_wave_reduce(q[3], ix[3]);
+			qarg_wave_reduce4(q, ix, cq1, cp1);
 			const int nn = n;
 			const bool move = !first && i != nn;
 			const int isub = move ? i : -1, jsub = first ? -1 : j;
@@ -1002,21 +503,17 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// ---- the top part is the head of the entry list: rows, bounds, units
 			const int t0 = 2 * lane, t1 = 2 * lane + 1;
 			const int r0 = t0 < ntop ? sS[t0] : 0, r1 = t1 < ntop ? sS[t1] : 0;
-			const int u0 = t0 < ntop && rows.owns(r0) ? dcdiv(r0, seg) : 0;
-			const int u1 = t1 < ntop && rows.owns(r1) ? dcdiv(r1, seg) : 0;
-			int utot;
-			const int upre = wave_excl_scan(u0 + u1, &utot);
+			const bool o0 = t0 < ntop && rows.owns(r0), o1 = t1 < ntop && rows.owns(r1);
 			if(t0 < ntop) {
 				b.crow[t0] = r0;
 				b.cbnd[t0] = sQS[t0];
-				b.coff[t0] = upre;
 			}
 			if(t1 < ntop) {
 				b.crow[t1] = r1;
 				b.cbnd[t1] = sQS[t1];
-				b.coff[t1] = upre + u0;
 			}
-			const long long ctop = wave_sum_int((long long) (u0 ? r0 : 0) + (u1 ? r1 : 0));
+			const long long ctop = wave_sum_int((long long) (o0 ? r0 : 0) + (o1 ? r1 : 0));
+			TS(1, 8);
 			if(lane == 0) {
 				if(!first) {   // persist the fold for the kernels after
 					b.Q[j] = Qj;
@@ -1050,13 +547,14 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				s_m0 = m0;
 				s_Nm = Nm;
 				s_sDm = sDm;
-				s_utop = utot;
 			}
+			TS(1, 9);
 		}
 		__builtin_amdgcn_s_setprio(0);
 #pragma unroll
 		for(int m = 0; m < FR; ++m) qv[m] = DBL_MAX;   // wave 0 lists no rows
 	}
+	TSW(1, 10, 64);
 	__syncthreads();
 	TS(1, 1);
 	if(s_done) return;
@@ -1073,6 +571,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		}
 		spq[lt] = qp;
 	}
+	TSW(1, 11, 64);
 	__syncthreads();
 	// ---- the bound below each S row: prefix min over S in scan order of
 	// max(q at the partner, Q), starting at m0 (S spans at most 2 waves)
@@ -1095,7 +594,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		U = ntop ? spm[ntop - 1] : m0;   // every row below the top part is under it
 	}
 	TS(1, 2);
-	// ---- S rows above row r (band mode): chunk table, as k_dnj_find
+	// ---- S rows above row r (band mode): chunk table
 	const bool bands = BANDS && nS > ntop;
 	const int nch0 = smin > 1 && bands ? ((smin - 1) >> 6) + 1 : 0;
 	const bool table = nch0 <= FIND_CHUNKS;
@@ -1127,7 +626,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// ---- the rest of the entry list, after the top part: rows [1, smin) that
 	// are band rows of S or have Q < their bound, with positions and unit
 	// offsets from one prefix over (step, wave) counts
-	int T = ntop, UT = s_utop;
+	int T = ntop;
 	long long mycells = 0;
 	if(smin > 1) {
 		for(int base = top; base >= 1; base -= LT * FR) {
@@ -1158,45 +657,34 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 				mycells += f ? r : 0;
 				bm[m] = __ballot(f);
-				const int ut = bm[m] ? wave_sum_int(f ? dcdiv(r, seg) : 0) : 0;   // uniform branch
-				if(lane == 0 && wid > 0) {
-					s_mw[m * LW + wid - 1] = __popcll(bm[m]);
-					s_mu[m * LW + wid - 1] = ut;
-				}
+				if(lane == 0 && wid > 0) s_mw[m * LW + wid - 1] = __popcll(bm[m]);
 			}
 			if(lane == 0 && wid > 0) {
 #pragma unroll
 				for(int m = 0; m < FR; ++m)
-					if(m >= mlim) s_mw[m * LW + wid - 1] = s_mu[m * LW + wid - 1] = 0;
+					if(m >= mlim) s_mw[m * LW + wid - 1] = 0;
 			}
+			TSW(1, 12, 64);
 			__syncthreads();
 			if(wid == 0) {
 				constexpr int NC = FR * LW, PER = (NC + 63) / 64;
-				int c[PER], cu[PER], sum = 0, usum = 0;
+				int c[PER], sum = 0;
 #pragma unroll
 				for(int k = 0; k < PER; ++k) {
 					const int x = lane * PER + k;
 					c[k] = x < NC ? s_mw[x] : 0;
-					cu[k] = x < NC ? s_mu[x] : 0;
 					sum += c[k];
-					usum += cu[k];
 				}
-				int tot, utot;
-				int pre = wave_excl_scan(sum, &tot), upre = wave_excl_scan(usum, &utot);
+				int tot;
+				int pre = wave_excl_scan(sum, &tot);
 #pragma unroll
 				for(int k = 0; k < PER; ++k) {
 					const int x = lane * PER + k;
-					if(x < NC) {
-						s_mw[x] = pre;
-						s_mu[x] = upre;
-					}
+					if(x < NC) s_mw[x] = pre;
 					pre += c[k];
-					upre += cu[k];
 				}
-				if(lane == 0) {
-					s_cnt = tot;
-					s_ucnt = utot;
-				}
+				if(lane == 0) s_cnt = tot;
+				TS(1, 13);
 			}
 			__syncthreads();
 #pragma unroll
@@ -1204,21 +692,17 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				if(bm[m] == 0ull) continue;   // uniform (always for wave 0)
 				const int r = base - (m * LT + lt);
 				const bool f = (bm[m] >> lane) & 1ull;
-				int ut;
-				const int uex = wave_excl_scan(f ? dcdiv(r, seg) : 0, &ut);   // recomputed: no registers held across the barriers
 				if(f) {
 					const int pos = T + s_mw[m * LW + wid - 1] +
 					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
 					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
 					b.crow[pos] = r;
 					b.cbnd[pos] = qv[m];
-					b.coff[pos] = UT + s_mu[m * LW + wid - 1] + uex;
 				}
 			}
 			T += s_cnt;
-			UT += s_ucnt;
 			if(base - LT * FR < 1) break;
-			__syncthreads();   // s_mw / s_mu are reused by the next step
+			__syncthreads();   // s_mw is reused by the next step
 		}
 	}
 	TS(1, 3);
@@ -1229,17 +713,22 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	}
 	if(tid == 0) {
 		ctl->T = T;
-		b.coff[T] = UT;
-		ctl->rows += T;
+		atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) T);   // no read: nothing waits
 	}
 	TS(1, 4);
 	TS_EXIT(1);
 }
 
 // ------------------------------------------------------------------ DNJ scan
-// Rescans of the rows found by k_dnj_find, in SEG-cell units spread over the
-// whole grid.  Tail: work every block does first (begin) and the store of
-// each unit's partial (unit, thread 0), for the sharded engine's records.
+// Rescans of the rows listed by k_dnj_plan, in seg-cell units spread over the
+// whole grid.  Entry e owns the fixed unit range [e umax, (e + 1) umax) (umax
+// = dnj_umax(n, seg), the units of the longest row); a row of r cells uses
+// the first dcdiv(r, seg) of them, so no prefix over the entries is needed
+// anywhere (the plan lists rows only).  Tail: work every block does first
+// (begin) and the store of each unit's partial (unit, thread 0), for the
+// sharded engine's records.
+__host__ __device__ __forceinline__ int dnj_umax(int n, int seg) { return n > 2 ? (n - 2) / seg + 1 : 1; }
+
 struct NoTail {
 	__device__ __forceinline__ void begin(const TreeBufs &, int) const {}
 	__device__ __forceinline__ void unit(const TreeBufs &b, int, int u, int, int, int, double q, int j) const {
@@ -1251,7 +740,6 @@ template <int ET, bool GEN, class Rows, class Tail = NoTail>
 __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                  int n, Rows rows, int seg, Tail tail = Tail()) {
 	__shared__ int erow[REPLAY_CAP];
-	__shared__ int eoff[REPLAY_CAP + 1];
 	__shared__ double sq[TB / 64];
 	__shared__ int si[TB / 64];
 	TreeCtl *ctl = b.ctl;
@@ -1259,44 +747,34 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	TS_ENTRY(2);
 	TS(2, 0);
 	// speculative first TB entries, then the rest once T is known
-	const int r0 = b.crow[tid], o0 = b.coff[tid];
+	const int r0 = b.crow[tid];
 	const int done = ctl->done, T = ctl->T;
 	if(done) return;
 	tail.begin(b, n);
 	if(T == 0) return;
+	const int umax = dnj_umax(n, seg), nunits = T * umax;
 	// blocks beyond the unit count leave before staging the table
-	if((int) blockIdx.x >= b.coff[T]) return;
-	// the entry table in LDS when it fits, else searched in HBM (L2-resident)
+	if((int) blockIdx.x >= nunits) return;
+	// the entry rows in LDS when they fit, else read from HBM (L2-resident)
 	const bool lds = T <= REPLAY_CAP;
 	if(lds) {
-		if(tid < T) {
-			erow[tid] = r0;
-			eoff[tid] = o0;
-		}
-		for(int e = TB + tid; e < T; e += TB) {
-			erow[e] = b.crow[e];
-			eoff[e] = b.coff[e];
-		}
-		if(tid == 0) eoff[T] = b.coff[T];
+		if(tid < T) erow[tid] = r0;
+		for(int e = TB + tid; e < T; e += TB) erow[e] = b.crow[e];
 	}
 	__syncthreads();
 	TS(2, 1);
-	const int *off = lds ? eoff : b.coff;
-	const int nunits = off[T];
 	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
-		int lo = 0, hi = T - 1;   // last e with off[e] <= u
-		while(lo < hi) {
-			int mid = (lo + hi + 1) >> 1;
-			if(off[mid] <= u) lo = mid; else hi = mid - 1;
-		}
-		const int r = lds ? erow[lo] : b.crow[lo];
-		const int c0 = (u - off[lo]) * seg, c1 = c0 + seg < r ? c0 + seg : r;
+		const int e = u / umax, ua = e * umax;
+		const int r = lds ? erow[e] : b.crow[e];
+		const int c0 = (u - ua) * seg;
+		if(c0 >= r || !rows.owns(r)) continue;   // past the row's end, or another rank's S row (uniform)
+		const int c1 = c0 + seg < r ? c0 + seg : r;
 		const int Nr = GEN ? b.N[r] : n;
 		double qq = DBL_MAX;
 		int idx = 0;
 		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
 		qarg_block_reduce1(qq, idx, sq, si);
-		if(tid == 0) tail.unit(b, n, u, off[lo], off[lo + 1], r, qq, idx);
+		if(tid == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, qq, idx);
 		if(u + (int) gridDim.x < nunits) __syncthreads();
 	}
 	TS(2, 2);
@@ -1308,13 +786,13 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 // one wave per entry, into (rf, rj); k_dnj_join then reads one pair per entry
 // instead of folding every entry's units in each of its blocks.
 template <int UNUSED = 0>
-__global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n) {
+__global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
 	const TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
-	const int T = ctl->T, lane = threadIdx.x & 63;
+	const int T = ctl->T, lane = threadIdx.x & 63, umax = dnj_umax(n, seg);
 	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
 	for(int e = w0; e < T; e += nw) {
-		const int ua = b.coff[e], ub = b.coff[e + 1];
+		const int ua = e * umax, ub = ua + dcdiv(b.crow[e], seg);
 		double q = DBL_MAX;
 		int idx = 0;
 		for(int u = ua + lane; u < ub; u += 64) {

@@ -220,6 +220,40 @@ __device__ __forceinline__ void qarg_wave_reduce_carry(double &q, int &idx, doub
 	cp = __builtin_amdgcn_readlane(cp, 63);
 }
 
+// four independent wave-wide (q, idx) reduces in lockstep (four dependency
+// chains interleaved step by step), the second carrying a payload (cq, cp)
+__device__ __forceinline__ void qarg_wave_reduce4(double (&q)[4], int (&idx)[4], double &cq, int &cp) {
+#define S_(C, R)                                              \
+	{                                                         \
+		double oq_[4];                                        \
+		int oi_[4];                                           \
+		_Pragma("unroll") for(int t = 0; t < 4; ++t) {        \
+			oq_[t] = dpp_d<C, R>(DBL_MAX, q[t]);              \
+			oi_[t] = dpp_i<C, R>(INT32_MIN, idx[t]);          \
+		}                                                     \
+		const double ocq_ = dpp_d<C, R>(DBL_MAX, cq);         \
+		const int ocp_ = dpp_i<C, R>(0, cp);                  \
+		_Pragma("unroll") for(int t = 0; t < 4; ++t) {        \
+			const bool b_ = qarg_better(oq_[t], oi_[t], q[t], idx[t]); \
+			q[t] = b_ ? oq_[t] : q[t];                        \
+			idx[t] = b_ ? oi_[t] : idx[t];                    \
+			if(t == 1) {                                      \
+				cq = b_ ? ocq_ : cq;                          \
+				cp = b_ ? ocp_ : cp;                          \
+			}                                                 \
+		}                                                     \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+#pragma unroll
+	for(int t = 0; t < 4; ++t) {
+		q[t] = readlane_d(q[t], 63);
+		idx[t] = __builtin_amdgcn_readlane(idx[t], 63);
+	}
+	cq = readlane_d(cq, 63);
+	cp = __builtin_amdgcn_readlane(cp, 63);
+}
+
 // block-wide (q, idx) reduce; result valid in every thread.  `sq`/`si` are
 // LDS scratch of blockDim/64 entries.
 __device__ __forceinline__ void qarg_block_reduce(double &q, int &idx, double *sq, int *si) {

@@ -137,7 +137,7 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 // replay; then limbLength, the join record and updateD with the whole grid.
 template <int ET, bool GEN>
 __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
-                                                 int general, int prefold) {
+                                                 int general, int prefold, int seg) {
 	__shared__ int e_row[DNJ_B + REPLAY_CAP], e_j[DNJ_B + REPLAY_CAP];
 	__shared__ double e_b[DNJ_B + REPLAY_CAP], e_f[DNJ_B + REPLAY_CAP];
 	__shared__ unsigned char e_acc[DNJ_B + REPLAY_CAP];
@@ -176,16 +176,15 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		se0 = b.Sent[lane];
 		se1 = b.Sent[lane + 64];
 		const int sp0 = merged ? b.Spos[lane] : lane, sp1 = merged ? b.Spos[lane + 64] : lane + 64;
-		int rr[4], c0[4], c1[4], cs[4];
+		int rr[4], cs[4];
 		double bb[4];
 #pragma unroll
 		for(int m = 0; m < 4; ++m) {
 			cs[m] = merged ? b.cslot[lane + 64 * m] : nS + lane + 64 * m;
 			rr[m] = b.crow[lane + 64 * m];
 			bb[m] = b.cbnd[lane + 64 * m];
-			c0[m] = b.coff[lane + 64 * m];
-			c1[m] = b.coff[lane + 64 * m + 1];
 		}
+		const int umax = dnj_umax(n, seg);   // entry e's units: [e umax, e umax + dcdiv(row, seg))
 		if(lane == 0) {
 			s_nj = ctl->njoins;
 			s_neg = ctl->neg;
@@ -220,7 +219,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			for(int m = 0; m < 4; ++m) {
 				const int e = lane + 64 * m;
 				if(e >= T) continue;
-				const int ua = c0[m], ub = c1[m];
+				const int ua = e * umax, ub = ua + dcdiv(rr[m], seg);
 				double q = DBL_MAX;
 				int idx = 0;
 				if(prefold) {
@@ -268,8 +267,8 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				if(prefold) {
 					q = e < JOIN_UPRE ? lq[e] : b.rf[e];
 					idx = e < JOIN_UPRE ? lj[e] : b.rj[e];
-				} else if(b.coff[e + 1] <= JOIN_UPRE) {
-					const int ua = b.coff[e], ub = b.coff[e + 1];
+				} else if(e * dnj_umax(n, seg) + dcdiv(r, seg) <= JOIN_UPRE) {
+					const int ua = e * dnj_umax(n, seg), ub = ua + dcdiv(r, seg);
 					for(int u = ua; u < ub; ++u) {
 						if(qarg_better(lq[u], lj[u], q, idx)) {
 							q = lq[u];
@@ -277,7 +276,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 						}
 					}
 				} else {
-					fold_units(b.cq, b.cj, b.coff[e], b.coff[e + 1], q, idx);
+					fold_units(b.cq, b.cj, e * dnj_umax(n, seg), e * dnj_umax(n, seg) + dcdiv(r, seg), q, idx);
 				}
 				const int s = s_merged ? b.cslot[e] : s_nS + e;
 				x_row[s] = r;
@@ -1180,7 +1179,17 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t maxu = cdiv(n, SEG) + 1;
 	// every row below S may qualify: room for n entries and their units
 	const size_t ncand = (size_t) n + 257;
-	size_t cunits = (size_t) n * ((size_t) n / SEG + 1) / 2 + (size_t) n + 256;
+	// entry e's rescan units are [e umax, (e + 1) umax) (k_dnj_scan): room for
+	// ncand entries at the largest umax of the run (seg grows with n in steps
+	// at n = 16384 m, so the maximum is at n or just below a step)
+	DnjGrid g;
+	g.load();
+	int umax = dnj_umax(n, g.seg(n));
+	for(int m = 2; m <= 9; ++m) {
+		const int k = 16384 * m - 1;
+		if(k <= n && dnj_umax(k, g.seg(k)) > umax) umax = dnj_umax(k, g.seg(k));
+	}
+	size_t cunits = ncand * (size_t) umax;
 	if(cunits < JOIN_UPRE) cunits = JOIN_UPRE;
 	const size_t nq = (size_t) nj_blocks(n) + 1;
 	size_t sz = 0;
@@ -1269,18 +1278,17 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	const int general = GEN;
 	const int xs = 0;   // exact row sums: split over the join kernel and its consumer (xs_join_row, xs_walk_blocks)
 	if(method == CCG_TREE_DNJ) {
-		const unsigned gs = g_grid.sel(n), gc = g_grid.scan(n);
+		const unsigned gc = g_grid.scan(n);
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
 		// one-phase search: k_dnj_plan lists S and the rows below it under the
 		// partner-cell bound, k_dnj_scan rescans them all
-		(void) gs;
 		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
 		else k_dnj_plan<ET, GEN, DenseRows, false><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
 		kt.mark(CCG_K_FIND);
 		k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n);
+		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
 		kt.mark(CCG_K_REST);
-		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold);
+		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold, seg);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_UPDATE);
 		if(xs) {
@@ -1435,7 +1443,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		for(int k = 0; k < nk && cnt; ++k) {
 			if(!present[k]) continue;
 			fprintf(stderr, "  %-14s gap-before %6.2f  span %6.2f  block0:", kn[k], gap[k] / cnt, acc[k][14] / cnt);
-			for(int p = 0; p < 9; ++p) fprintf(stderr, " %6.2f", acc[k][p] / cnt);
+			for(int p = 0; p < 14; ++p) fprintf(stderr, " %6.2f", acc[k][p] / cnt);
 			fprintf(stderr, "\n");
 		}
 	}

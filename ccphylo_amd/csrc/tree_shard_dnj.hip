@@ -642,12 +642,11 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		while(n > stop_n) {
 			const unsigned gn = cdiv(n, TB), gp = cdiv(n, PICK_T) < PICK_MAXB ? cdiv(n, PICK_T) : PICK_MAXB;
 			T *Xmr = (T *) ((char *) R + rec_xm_off(n));   // row n-1, gathered with the records
-			const unsigned gs = grid.sel(n), gc = grid.scan(n);
+			const unsigned gc = grid.scan(n);
 			const int seg = grid.seg(n);
 			// one-phase search (k_dnj_plan): each rank lists the S rows and the
 			// rows below S it owns, under the bound of its own S rows' partner
 			// cells (a subset of S: looser, still exact after the replay)
-			(void) gs;
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_qdelay);
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_qdelay);
 			kt.mark(CCG_K_FIND);

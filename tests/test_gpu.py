@@ -262,8 +262,8 @@ def _clade_ltd(n, seed, L=3000, clades=16):
 def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
     """The large-n settings of the DNJ search at small n: rescan units of
     several SEG (CCG_SEG_MUL), each rest row's units folded once by k_dnj_fold
-    (CCG_PREFOLD_N=0) and grids far smaller than the units (CCG_SEL_MAX,
-    CCG_SCAN_MAX: many grid waves).  Joins bit-identical to the serial
+    (CCG_PREFOLD_N=0) and scan grids far smaller than the units
+    (CCG_SCAN_MAX: many grid waves).  Joins bit-identical to the serial
     reference (exact row sums), single GPU and sharded."""
     from oracle import pyoracle
     if kind == "euc":
@@ -273,8 +273,7 @@ def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
         D = np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
     else:
         D = _clade_ltd(n, n)
-    sel, scan, segm, pf = env.split(",")
-    monkeypatch.setenv("CCG_SEL_MAX", sel)
+    _, scan, segm, pf = env.split(",")
     monkeypatch.setenv("CCG_SCAN_MAX", scan)
     monkeypatch.setenv("CCG_SEG_MUL", segm)
     monkeypatch.setenv("CCG_PREFOLD_N", pf)
