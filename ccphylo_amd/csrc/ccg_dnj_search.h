@@ -71,54 +71,7 @@ struct DnjGrid {
 	}
 };
 
-// ---- diagnostic build only (make trace): s_memrealtime stamps (100 MHz) of
-// block 0's entry and phases and of the last block exit, for the joins at
-// n in (g_trace_hi - 256, g_trace_hi]; dumped to stderr by tree_run_t.
-#if defined(CCG_TRACE) && !defined(CCG_DNJ_NO_TRACE)
-#define NKT 5
-__device__ unsigned long long g_trace[256 * NKT * 16];
-__device__ int g_trace_hi;
-__device__ __forceinline__ unsigned long long rt_stamp() {
-	unsigned long long t;
-	__builtin_amdgcn_sched_barrier(0);
-	asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-	__builtin_amdgcn_sched_barrier(0);
-	return t;
-}
-#define TS(kern, ph)                                                                  \
-	do {                                                                              \
-		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
-		}                                                                             \
-	} while(0)
-#define TSW(kern, ph, th)                                                             \
-	do {                                                                              \
-		if(blockIdx.x == 0 && threadIdx.x == (th)) {                                  \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
-		}                                                                             \
-	} while(0)
-#define TS_ENTRY(kern)                                                                \
-	do {                                                                              \
-		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + 15] = ~rt_stamp(); \
-		}                                                                             \
-	} while(0)
-#define TS_EXIT(kern)                                                                 \
-	do {                                                                              \
-		if(threadIdx.x == 0) {                                                        \
-			int s_ = g_trace_hi - n;                                                  \
-			if(s_ >= 0 && s_ < 256) atomicMax(&g_trace[(s_ * NKT + (kern)) * 16 + 14], rt_stamp()); \
-		}                                                                             \
-	} while(0)
-#else
-#define TS_EXIT(kern)
-#define TS(kern, ph)
-#define TSW(kern, ph, th)
-#define TS_ENTRY(kern)
-#endif
+// (trace stamps TS / TSW / TS_ENTRY / TS_EXIT / TS_SAMP: ccg_tree_common.h)
 
 // ------------------------------------------------------------------ helpers
 // (q, j) min of LT row r over columns [c0, c1), whole block of NT threads,
@@ -746,6 +699,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	const int tid = threadIdx.x;
 	TS_ENTRY(2);
 	TS(2, 0);
+	TS_SAMP(0);
 	// speculative first TB entries, then the rest once T is known
 	const int r0 = b.crow[tid];
 	const int done = ctl->done, T = ctl->T;
@@ -763,6 +717,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	}
 	__syncthreads();
 	TS(2, 1);
+	TS_SAMP(1);
 	for(int u = blockIdx.x; u < nunits; u += gridDim.x) {
 		const int e = u / umax, ua = e * umax;
 		const int r = lds ? erow[e] : b.crow[e];
@@ -778,6 +733,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 		if(u + (int) gridDim.x < nunits) __syncthreads();
 	}
 	TS(2, 2);
+	TS_SAMP(2);
 	TS_EXIT(2);
 }
 

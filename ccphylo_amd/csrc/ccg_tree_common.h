@@ -304,6 +304,65 @@ static __device__ double serial_sum_t(const double *__restrict__ c, int n) {
 	return s_sd;
 }
 
+// ---- diagnostic build only (make trace): s_memrealtime stamps (100 MHz) of
+// block 0's entry and phases and of the last block exit, for the joins at
+// n in (g_trace_hi - 256, g_trace_hi]; dumped to stderr by tree_run_t.
+#if defined(CCG_TRACE) && !defined(CCG_DNJ_NO_TRACE)
+#define NKT 5
+__device__ unsigned long long g_trace[256 * NKT * 16];
+__device__ int g_trace_hi;
+__device__ __forceinline__ unsigned long long rt_stamp() {
+	unsigned long long t;
+	__builtin_amdgcn_sched_barrier(0);
+	asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+	__builtin_amdgcn_sched_barrier(0);
+	return t;
+}
+#define TS(kern, ph)                                                                  \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
+#define TSW(kern, ph, th)                                                             \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == (th)) {                                  \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + (ph)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
+#define TS_ENTRY(kern)                                                                \
+	do {                                                                              \
+		if(blockIdx.x == 0 && threadIdx.x == 0) {                                     \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_trace[(s_ * NKT + (kern)) * 16 + 15] = ~rt_stamp(); \
+		}                                                                             \
+	} while(0)
+// every 32nd block of the scan: entry / table staged / exit stamps (no atomics)
+__device__ unsigned long long g_samp[256 * 64 * 3];
+#define TS_SAMP(ph)                                                                   \
+	do {                                                                              \
+		if(threadIdx.x == 0 && (blockIdx.x & 31) == 0 && (blockIdx.x >> 5) < 64) {    \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_samp[(s_ * 64 + (blockIdx.x >> 5)) * 3 + (ph)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
+#define TS_EXIT(kern)                                                                 \
+	do {                                                                              \
+		if(threadIdx.x == 0) {                                                        \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) atomicMax(&g_trace[(s_ * NKT + (kern)) * 16 + 14], rt_stamp()); \
+		}                                                                             \
+	} while(0)
+#else
+#define TS_EXIT(kern)
+#define TS(kern, ph)
+#define TSW(kern, ph, th)
+#define TS_SAMP(ph)
+#define TS_ENTRY(kern)
+#endif
+
 // ------------------------------------------------------------------ exact row sum, in parallel
 // The reference's serial sum s_k = fl(s_{k-1} + c_k) (nj.c:911 / :1002) of
 // the new row of j, computed without its dependent chain.  Every c_k >= 0
@@ -841,7 +900,27 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 
 // wave 0 of a consumer block: the serial sum from the G join blocks'
 // records; false when a check fails (the caller then runs the chain)
-__device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
+// the walk's first loads, issued before the consumer knows it needs them
+// (with the fold's partials, one round trip instead of three): lane g < 64
+// holds block g's summary, its first XS_PRE_C crossings and first tie
+#define XS_PRE_C 2
+struct XsPre {
+	XsBlk blk;
+	XsCross cr[XS_PRE_C];
+	XsTie ti;
+};
+__device__ __forceinline__ void xs_prefetch(const TreeBufs &b, int G, XsPre &p) {
+	const int g = threadIdx.x & 63;
+	if(g < G) {
+		p.blk = b.xblk[g];
+#pragma unroll
+		for(int c = 0; c < XS_PRE_C; ++c) p.cr[c] = b.xcr[(size_t) g * XB_CAP + c];
+		p.ti = b.xti[(size_t) g * XB_CAP];
+	}
+}
+
+__device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPre *pre, int n) {
+	(void) n;   // trace stamps only
 	__shared__ XsCross lc[XS_CAP];
 	__shared__ int lcR[XS_CAP], lcT[XS_CAP];   // the crossing's block: Rw, global index of its first tie
 	__shared__ XsTie lt[XS_CAP];
@@ -858,7 +937,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 		const int g = g0 + lane;
 		XsBlk s;
 		if(g < G) {
-			s = b.xblk[g];
+			s = pre && g0 == 0 ? pre->blk : b.xblk[g];
 		} else {
 			s.tail = 0;
 			s.nc = s.nt = s.tp = s.ex0 = s.bad = 0;
@@ -870,14 +949,14 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 		const int Rw = Rwb + wave_excl_scan(s.tp, &tr);
 		for(int c = 0; c < s.nc && c < XB_CAP; ++c) {
 			if(co + c < XS_CAP) {
-				lc[co + c] = b.xcr[(size_t) g * XB_CAP + c];
+				lc[co + c] = pre && g0 == 0 && c < XS_PRE_C ? pre->cr[c < XS_PRE_C ? c : 0] : b.xcr[(size_t) g * XB_CAP + c];
 				lcR[co + c] = Rw;
 				lcT[co + c] = to;
 			}
 		}
 		for(int t = 0; t < s.nt && t < XB_CAP; ++t) {
 			if(to + t < XS_CAP) {
-				lt[to + t] = b.xti[(size_t) g * XB_CAP + t];
+				lt[to + t] = pre && g0 == 0 && t == 0 ? pre->ti : b.xti[(size_t) g * XB_CAP + t];
 				ltR[to + t] = Rw;
 			}
 		}
@@ -898,6 +977,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 	bad = __any(bad) || nx > XS_CAP - 1 || ntot > XS_CAP;
 	if(bad) return false;
 	wave_sync();
+	TS(4, 7);
 	// ---- per segment: its increment for an even / odd start (ties rounded to even)
 	double A0[2], A1[2], cvA[2];
 	int exA[2], cxA[2];
@@ -938,6 +1018,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 			A1[h] = seg - (double) dn1;
 		}
 	}
+	TS(4, 8);
 	// ---- the walk
 	double S = SH;
 	bool ok = (eH > 0 && eH < 0x7FF) || (SH == 0.0 && lseg[0] == 0.0);
@@ -959,6 +1040,17 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 			S = Sn;
 		}
 	}
+	TS(4, 9);
+#if defined(CCG_TRACE) && !defined(CCG_DNJ_NO_TRACE)
+	if(blockIdx.x == 0 && threadIdx.x == 0) {   // counts in the stamp columns 10 / 11 (printed as "us")
+		const int s_ = g_trace_hi - n;
+		if(s_ >= 0 && s_ < 256) {
+			const unsigned long long t0 = ~g_trace[(s_ * NKT + 4) * 16 + 15];
+			g_trace[(s_ * NKT + 4) * 16 + 10] = t0 + (unsigned long long) nx * 100;     // crossings
+			g_trace[(s_ * NKT + 4) * 16 + 11] = t0 + (unsigned long long) ntot * 100;   // ties
+		}
+	}
+#endif
 	*out = S;
 	return ok;
 }
@@ -969,11 +1061,15 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out) {
 __device__ void row_sum_j_wave(const TreeBufs &b, int n, bool exact, bool general, double *sd, int *nj, bool *need,
                                bool *chain) {
 	const int G = (int) cdiv(n, TB);
+	XsPre pre;
+	if(exact) xs_prefetch(b, G, pre);
+	TS(4, 5);
 	fold_update_wave(b, G, exact, general, sd, nj, need);
+	TS(4, 6);
 	*chain = false;
 	if(*need) {
 		double r;
-		if(xs_walk_blocks(b, G, &r)) *sd = r;
+		if(xs_walk_blocks(b, G, &r, exact ? &pre : nullptr, n)) *sd = r;
 		else *chain = true;
 	}
 }

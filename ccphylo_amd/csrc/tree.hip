@@ -485,7 +485,7 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 // the next k_dnj_select folds.
 template <int ET, bool BANDS>
 __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                    int n, int general) {
+                                                    int n, int general, int exact_arg) {
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
 	__shared__ int si[5][TB / 64], sfp[TB / 64], sbp[TB / 64];
 	__shared__ double s_sd;
@@ -510,13 +510,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	const double sDm0 = b.sD[nn];
 	if(wid == 0) {
 		const int done = ctl->done;
-		const bool exact = ctl->exact;
+		const bool exact = exact_arg != 0;   // a launch argument: the row sum's loads wait for no ctl load
 		if(lane == 0) {
 			s_i = ctl->i;
 			s_j = ctl->j;
 			s_stop = done;
 		}
-		if(!done) {
+		{   // also once the loop stopped (the result is unused then): nothing waits for `done`
 			double sd;
 			int nj;
 			bool need, chain;
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(TB) void k_nj_join(typename Elem<ET>::T *__restrict
 
 // row sum of j, then matrix.c:518 ltdMatrix_popArrange + nj.c:1588-1589
 template <int ET>
-__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, int general) {
+__global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n, int general, int exact_arg) {
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
@@ -869,13 +869,13 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 	const int Nm = b.N[nn];
 	if(wid == 0) {
 		const int done = ctl->done;
-		const bool exact = ctl->exact;
+		const bool exact = exact_arg != 0;   // a launch argument: the row sum's loads wait for no ctl load
 		if(lane == 0) {
 			s_i = ctl->i;
 			s_j = ctl->j;
 			s_stop = done;
 		}
-		if(!done) {
+		{   // also once the loop stopped (the result is unused then): nothing waits for `done`
 			double sd;
 			int nj;
 			bool need, chain;
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(TB) void k_hnj_argmin(TreeBufs b, int n) {
 
 template <int ET>
 __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                   int n, int general) {
+                                                   int n, int general, int exact_arg) {
 	__shared__ double s_sd, sq[TB / 64], sq2[TB / 64];
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain, sk[TB / 64], sk2[TB / 64];
 	TreeCtl *ctl = b.ctl;
@@ -1047,13 +1047,13 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 	const int k = (int) blockIdx.x * TB + tid;
 	if(wid == 0) {
 		const int done = ctl->done;
-		const bool exact = ctl->exact;
+		const bool exact = exact_arg != 0;   // a launch argument: the row sum's loads wait for no ctl load
 		if(lane == 0) {
 			s_i = ctl->i;
 			s_j = ctl->j;
 			s_stop = done;
 		}
-		if(!done) {
+		{   // also once the loop stopped (the result is unused then): nothing waits for `done`
 			double sd;
 			int nj;
 			bool need, chain;
@@ -1295,8 +1295,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 			k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 			kt.mark(CCG_K_XSUM);
 		}
-		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general);
-		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general);
+		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
+		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		kt.mark(CCG_K_REQUEUE);
 		return (GEN ? 5 : 4) + prefold + xs;
 	}
@@ -1310,7 +1310,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 			k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 			kt.mark(CCG_K_XSUM);
 		}
-		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general);   // updateHNJ's Q/P pass + HNJ_popArrange
+		k_hnj_update<ET><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);   // updateHNJ's Q/P pass + HNJ_popArrange
 		kt.mark(CCG_K_POP);
 		return (GEN ? 4 : 3) + xs;
 	}
@@ -1324,7 +1324,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 		kt.mark(CCG_K_XSUM);
 	}
-	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general);
+	k_nj_pop<ET><<<gn, TB, 0, st>>>(D, b, n, general, exact);
 	kt.mark(CCG_K_POP);
 	return (GEN ? 4 : 3) + xs;
 }
@@ -1440,6 +1440,37 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		const char *kn[NKT] = {"select", "plan/find", "scan", "join", "requeue"};
 		fprintf(stderr, "trace: %d joins at n <= %d; iteration %.2f us; serial replays %d, serial sums %d\n", cnt,
 		        trace_hi, cnt ? itv / (cnt - 1) : 0, h.serial_replays, h.serial_sums);
+		{
+			// sampled scan blocks (every 32nd): start and end relative to the kernel's first entry
+			static unsigned long long sp[256 * 64 * 3];
+			CCG_CHECK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_samp), sizeof(sp), 0, hipMemcpyDeviceToHost));
+			double st_max = 0, en_max = 0, dur = 0, st_med = 0;
+			int sc = 0, jc = 0;
+			for(int s = 0; s < 256; ++s) {
+				const unsigned long long t0 = ~tr[(s * NKT + 2) * 16 + 15];
+				if(!tr[(s * NKT + 2) * 16 + 15]) continue;
+				double smax = 0, emax = 0;
+				int any = 0;
+				for(int q = 0; q < 64; ++q) {
+					const unsigned long long *e = sp + (s * 64 + q) * 3;
+					if(!e[0] || !e[2] || e[0] < t0) continue;
+					const double a = (e[0] - t0) / 100.0, z = (e[2] - t0) / 100.0;
+					smax = a > smax ? a : smax;
+					emax = z > emax ? z : emax;
+					dur += z - a;
+					st_med += a;
+					++sc;
+					any = 1;
+				}
+				if(any) {
+					st_max += smax;
+					en_max += emax;
+					++jc;
+				}
+			}
+			if(jc) fprintf(stderr, "  scan samples: %d joins, %.1f working blocks sampled/join; last start %.2f us, last end %.2f us, mean start %.2f, mean duration %.2f us\n",
+			                jc, (double) sc / jc, st_max / jc, en_max / jc, st_med / sc, dur / sc);
+		}
 		for(int k = 0; k < nk && cnt; ++k) {
 			if(!present[k]) continue;
 			fprintf(stderr, "  %-14s gap-before %6.2f  span %6.2f  block0:", kn[k], gap[k] / cnt, acc[k][14] / cnt);

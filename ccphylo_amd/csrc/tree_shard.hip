@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <rccl/rccl.h>
+#define CCG_DNJ_NO_TRACE
 #include "ccg_tree_common.h"
 #include "ccg_shard.h"
 
