@@ -254,6 +254,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	__shared__ double spq[NSP];                 // the Q criterion at the partner cell of row top - t
 	__shared__ double spm[DNJ_B + 2];           // bound below S row t (prefix over S in scan order)
 	__shared__ int s_mw[FR * LW], s_cnt;
+	__shared__ double s_sb[FR * LW];          // band mode: the bound of slot (m, wave)'s 64 rows ...
+	__shared__ unsigned char s_sf[FR * LW];   // ... unless an S row falls among them (then per row)
 	__shared__ int sch[FIND_CHUNKS];
 	__shared__ int s_done, s_isub, s_jsub, s_nS, s_ntop, s_smin, s_Nm;
 	__shared__ double s_m0, s_Qj, s_Qi, s_sDm;
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		if(done) {
 			if(lane == 0) s_done = 1;
 		} else {
-			TS(1, 5);
+			
 			qarg_wave_reduce4(q, ix, cq1, cp1);
 			const int nn = n;
 			const bool move = !first && i != nn;
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			const int pos_j = (cand && m0 != DBL_MAX) ? (first ? cand0_p : PSUB(cand)) : 0;
 #undef QSUB
 #undef PSUB
-			TS(1, 6);
+			
 			// ---- S, top part: ktop rows with Q < m0 from the top
 			int cnt = 0;
 			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop; base -= 64 * SEL_RPL, ++step) {
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				nS = ntop + __popcll(bm);
 			}
 			wave_sync();
-			TS(1, 7);
+			
 			// ---- the top part is the head of the entry list: rows, bounds, units
 			const int t0 = 2 * lane, t1 = 2 * lane + 1;
 			const int r0 = t0 < ntop ? sS[t0] : 0, r1 = t1 < ntop ? sS[t1] : 0;
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				b.cbnd[t1] = sQS[t1];
 			}
 			const long long ctop = wave_sum_int((long long) (o0 ? r0 : 0) + (o1 ? r1 : 0));
-			TS(1, 8);
+			
 			if(lane == 0) {
 				if(!first) {   // persist the fold for the kernels after
 					b.Q[j] = Qj;
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				s_Nm = Nm;
 				s_sDm = sDm;
 			}
-			TS(1, 9);
+			
 		}
 		__builtin_amdgcn_s_setprio(0);
 #pragma unroll
@@ -582,14 +584,32 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	int T = ntop;
 	long long mycells = 0;
 	if(smin > 1) {
+		double qn[FR];   // the next step's Q, loaded while this step runs
 		for(int base = top; base >= 1; base -= LT * FR) {
 			if(base != top && wid > 0) {
 #pragma unroll
+				for(int m = 0; m < FR; ++m) qv[m] = qn[m];
+			}
+			if(wid > 0 && base - LT * FR >= 1) {
+#pragma unroll
 				for(int m = 0; m < FR; ++m) {
-					const int r = base - (m * LT + lt);
-					qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+					const int r = base - LT * FR - (m * LT + lt);
+					qn[m] = r >= 1 ? b.Q[r] : DBL_MAX;
 				}
 			}
+			if(bands) {
+				// each slot's bound with one S search per slot, not per row
+				if(tid < FR * LW) {
+					const int m = tid / LW, w = tid - (tid / LW) * LW;
+					const int rhi = base - (m * LT + w * 64);
+					const int t0 = rhi >= 1 ? s_above(rhi) : nS;
+					s_sb[tid] = t0 ? spm[t0 - 1] : m0;
+					s_sf[tid] = t0 < nS && sS[t0] >= rhi - 63;
+				}
+				__syncthreads();
+			}
+			if(base == top) TS(1, 5);
+			if(base == top - LT * FR) TS(1, 9);
 			unsigned long long bm[FR];
 #pragma unroll
 			for(int m = 0; m < FR; ++m) bm[m] = 0ull;
@@ -598,17 +618,26 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			for(int m = 0; m < FR; ++m) {
 				if(m >= mlim) continue;   // uniform; no break: the loop stays unrolled (registers, not scratch)
 				const int r = wid > 0 ? base - (m * LT + lt) : 0;
-				qv[m] = r == jsub ? s_Qj : r == isub ? s_Qi : qv[m];
-				bool f = false;
-				if(r >= 1 && r < smin && rows.owns(r)) {
-					if(bands) {
+				const int rhi = base - (m * LT + (wid - 1) * 64);   // the wave's rows: [rhi - 63, rhi]
+				if((jsub <= rhi && jsub >= rhi - 63) || (isub <= rhi && isub >= rhi - 63))   // uniform, rare
+					qv[m] = r == jsub ? s_Qj : r == isub ? s_Qi : qv[m];
+				// band mode: the wave's 64 rows [rhi - 63, rhi] mostly hold no S
+				// row, so one wave-uniform lookup gives every lane's bound
+				// (the per-row search only where an S row falls inside)
+				double bnd = U;
+				bool srow = false;
+				if(bands && wid > 0) {
+					const int x = m * LW + wid - 1;
+					if(s_sf[x]) {   // uniform branch
 						const int t = s_above(r);
-						f = (t < nS && sS[t] == r) || qv[m] < (t ? spm[t - 1] : m0);
+						srow = t < nS && sS[t] == r;
+						bnd = t ? spm[t - 1] : m0;
 					} else {
-						f = qv[m] < U;
+						bnd = s_sb[x];
 					}
 				}
-				mycells += f ? r : 0;
+				bool f = false;
+				if(r >= 1 && r < smin && rows.owns(r)) f = srow || qv[m] < bnd;
 				bm[m] = __ballot(f);
 				if(lane == 0 && wid > 0) s_mw[m * LW + wid - 1] = __popcll(bm[m]);
 			}
@@ -618,6 +647,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 					if(m >= mlim) s_mw[m * LW + wid - 1] = 0;
 			}
 			TSW(1, 12, 64);
+			if(base == top) TSW(1, 6, 64);
 			__syncthreads();
 			if(wid == 0) {
 				constexpr int NC = FR * LW, PER = (NC + 63) / 64;
@@ -638,6 +668,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 				if(lane == 0) s_cnt = tot;
 				TS(1, 13);
+				if(base == top) TS(1, 7);
 			}
 			__syncthreads();
 #pragma unroll
@@ -645,6 +676,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				if(bm[m] == 0ull) continue;   // uniform (always for wave 0)
 				const int r = base - (m * LT + lt);
 				const bool f = (bm[m] >> lane) & 1ull;
+				mycells += f ? r : 0;
 				if(f) {
 					const int pos = T + s_mw[m * LW + wid - 1] +
 					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
@@ -654,6 +686,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 			}
 			T += s_cnt;
+			if(base == top) TSW(1, 8, 64);
 			if(base - LT * FR < 1) break;
 			__syncthreads();   // s_mw is reused by the next step
 		}
