@@ -254,8 +254,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	__shared__ double spq[NSP];                 // the Q criterion at the partner cell of row top - t
 	__shared__ double spm[DNJ_B + 2];           // bound below S row t (prefix over S in scan order)
 	__shared__ int s_mw[FR * LW], s_cnt;
-	__shared__ double s_sb[FR * LW];          // band mode: the bound of slot (m, wave)'s 64 rows ...
-	__shared__ unsigned char s_sf[FR * LW];   // ... unless an S row falls among them (then per row)
+	__shared__ double s_sb[LW * FR];          // band mode: the bound of slot (wave, m)'s 64 rows ...
+	__shared__ __attribute__((aligned(16))) unsigned char s_sf[LW * FR];   // ... unless an S row falls among them
 	__shared__ int sch[FIND_CHUNKS];
 	__shared__ int s_done, s_isub, s_jsub, s_nS, s_ntop, s_smin, s_Nm;
 	__shared__ double s_m0, s_Qj, s_Qi, s_sDm;
@@ -590,23 +590,25 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 #pragma unroll
 				for(int m = 0; m < FR; ++m) qv[m] = qn[m];
 			}
-			if(wid > 0 && base - LT * FR >= 1) {
-#pragma unroll
-				for(int m = 0; m < FR; ++m) {
-					const int r = base - LT * FR - (m * LT + lt);
-					qn[m] = r >= 1 ? b.Q[r] : DBL_MAX;
-				}
-			}
 			if(bands) {
 				// each slot's bound with one S search per slot, not per row
-				if(tid < FR * LW) {
-					const int m = tid / LW, w = tid - (tid / LW) * LW;
-					const int rhi = base - (m * LT + w * 64);
+				if(tid < FR * LW) {   // slot (wave w + 1, m) at w FR + m: a wave reads its flags in one 16-byte load
+					const int w = tid / FR, m = tid - (tid / FR) * FR;
+					// rows >= smin are S's top part (never listed; s_above's chunk
+					// table covers rows < smin only): the slot's highest listable row
+					const int rh0 = base - (m * LT + w * 64), rhi = rh0 < smin - 1 ? rh0 : smin - 1;
 					const int t0 = rhi >= 1 ? s_above(rhi) : nS;
 					s_sb[tid] = t0 ? spm[t0 - 1] : m0;
-					s_sf[tid] = t0 < nS && sS[t0] >= rhi - 63;
+					s_sf[tid] = t0 < nS && sS[t0] >= rh0 - 63;
 				}
 				__syncthreads();
+			}
+			unsigned sfm = 0;   // bit m: slot m of this wave holds an S row
+			if(bands && wid > 0) {
+				const uint4 f4 = *(const uint4 *) (s_sf + (wid - 1) * FR);
+				const unsigned fw[4] = {f4.x, f4.y, f4.z, f4.w};
+#pragma unroll
+				for(int m = 0; m < FR; ++m) sfm |= ((fw[m >> 2] >> (8 * (m & 3))) & 1u) << m;
 			}
 			if(base == top) TS(1, 5);
 			if(base == top - LT * FR) TS(1, 9);
@@ -627,13 +629,12 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				double bnd = U;
 				bool srow = false;
 				if(bands && wid > 0) {
-					const int x = m * LW + wid - 1;
-					if(s_sf[x]) {   // uniform branch
+					if((sfm >> m) & 1u) {   // uniform branch (rare)
 						const int t = s_above(r);
 						srow = t < nS && sS[t] == r;
 						bnd = t ? spm[t - 1] : m0;
 					} else {
-						bnd = s_sb[x];
+						bnd = s_sb[(wid - 1) * FR + m];
 					}
 				}
 				bool f = false;
@@ -645,6 +646,16 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 #pragma unroll
 				for(int m = 0; m < FR; ++m)
 					if(m >= mlim) s_mw[m * LW + wid - 1] = 0;
+			}
+			// the next step's Q, issued after this step's compares (a wait for
+			// them must not hold up the compares) and in flight through the
+			// prefix and the writes
+			if(wid > 0 && base - LT * FR >= 1) {
+#pragma unroll
+				for(int m = 0; m < FR; ++m) {
+					const int r = base - LT * FR - (m * LT + lt);
+					qn[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+				}
 			}
 			TSW(1, 12, 64);
 			if(base == top) TSW(1, 6, 64);

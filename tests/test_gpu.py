@@ -285,6 +285,32 @@ def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
     assert (sh == got).all()
 
 
+@pytest.mark.parametrize("kind,n,top,bands", [("euc", 2000, 16, 64), ("clade", 2500, 8, 32), ("euc", 3000, 1, 127),
+                                               ("clade", 1800, 16, 64)])
+def test_dnj_band_mode_small_n(dev, monkeypatch, kind, n, top, bands):
+    """The large-n choice of S (top rows + one min-Q row per band, per-slot
+    bounds in k_dnj_plan's listing, CCG_S_SPLIT_N) at small n: joins
+    bit-identical to the serial reference (exact row sums), single GPU and
+    sharded at world 1."""
+    from oracle import pyoracle
+    if kind == "euc":
+        rng = np.random.default_rng(n + top)
+        pts = rng.random((n, 8))
+        i, j = np.tril_indices(n, -1)
+        D = np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
+    else:
+        D = _clade_ltd(n, n + 7)
+    monkeypatch.setenv("CCG_S_SPLIT_N", "100")
+    monkeypatch.setenv("CCG_S_TOP", str(top))
+    monkeypatch.setenv("CCG_S_BANDS", str(bands))
+    got, fn, fd, st = dev.tree(D, n, method=1, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=1)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
+    sh = dev.tree_shard(D, n, None, method=1, exact=True)[0]
+    assert (sh == got).all()
+
+
 def _missing_ltd(n, seed, frac=0.05):
     """Euclidean distances with a fraction of cells set to -1 (missing,
     nj.c:111 initSummaD skips them; updateD's quirky branches run)."""
