@@ -59,6 +59,14 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # alone as in the mix, so their ceiling is half the nominal: 256 x 4 x 16 x
 # 2.4e9 = 3.93e13 (`int32_wave64_ceiling`, `frac_of_int32_ceiling`).
 VALU_NOMINAL_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# Non-pair dist runs on the matrix cores (k_snp_mfma, the default): a code is
+# the tetrahedron vector (+-1)^3 in MX-fp4, 3 MACs = 6 flops per position pair
+# (dist = (3 L - dot) / 4, exact).  Peak: the MX-fp4 dense rate, ~10 PF
+# (MI355X_MICROARCH.md); tools/micro/mfma_fp4 (profiles/r02_mfma_fp4.txt)
+# issues 3.55e15 MAC/s = 7.1 PF from registers on this box.
+MFMA_FP4_DENSE_TFLOPS = 10000.0
+MFMA_FP4_MEASURED_TFLOPS = 7098.0
+FLOPS_PER_POSITION_PAIR = 6.0
 VALU_INT32_CEILING = 256 * 4 * 16 * 2.4e9
 OPS_PER_WORD_PAIR = 3.0
 OPS_PER_WORD_PAIR_PAIRMODE = 6.0   # v_and (masks), v_xor, v_bitop3, v_and, 2x v_bcnt (dist and n)
@@ -288,11 +296,25 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     words = (L + 31) // 32
     opw = OPS_PER_WORD_PAIR_PAIRMODE if pair else OPS_PER_WORD_PAIR
     ops = m * words * opw / world   # per GPU
+    mfma = not pair and os.environ.get("CCG_DIST_MFMA", "1") != "0"
     del seqs, incs, Dd, Nd
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "roofline": valu_roofline(ops, dt, opw)}
+            "kernel": "k_snp_mfma" if mfma else ("k_snp_tile_pair" if pair else "k_snp_tile"),
+            "roofline": mfma_roofline(m * L / world, dt) if mfma else valu_roofline(ops, dt, opw)}
+
+
+def mfma_roofline(position_pairs, dt):
+    """dist on the matrix cores: 6 flops (3 MX-fp4 MACs) per position pair
+    against the MX-fp4 dense peak, and beside it the register-fed issue rate
+    measured on this box."""
+    tf = FLOPS_PER_POSITION_PAIR * position_pairs / dt / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4), "measured_issue_peak": MFMA_FP4_MEASURED_TFLOPS,
+            "frac_of_measured_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
+            "form": "tetrahedron (+-1)^3 MX-fp4 operands, v_mfma_scale_f32_32x32x64_f8f6f4, dist = (3 L - dot) / 4",
+            "evidence": "profiles/r02_mfma_fp4.txt (tools/micro/mfma_fp4: lane map, register-fed rate)"}
 
 
 def valu_roofline(ops, dt, opw):
@@ -426,7 +448,8 @@ def config3_leg(dev, torch, tmpdir, n=50_000, L=5_000_000, steps=1, cpu=True):
            "taxa_pairs_per_s": round(m / dist_s, 1), "nt_comparisons_per_s": m * L / dist_s,
            "joins_per_s": round(joins / tree_s, 1), "joins": joins, "rows_rescanned": rows,
            "cells_rescanned": cells, "included_positions": inc, "row_sums": "exact",
-           "roofline": {"dist": valu_roofline(ops, dist_s, OPS_PER_WORD_PAIR),
+           "roofline": {"dist": mfma_roofline(m * L, dist_s) if os.environ.get("CCG_DIST_MFMA", "1") != "0"
+                        else valu_roofline(ops, dist_s, OPS_PER_WORD_PAIR),
                         "tree": {"bound": "hbm", "achieved": round(tree_bytes / tree_s / 1e9, 1),
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(tree_bytes / tree_s / 1e9 / HBM_PEAK_GBS, 4),

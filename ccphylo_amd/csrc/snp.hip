@@ -205,6 +205,158 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile(const uint2 *__restrict__ P
 	}
 }
 
+// ------------------------------------------------------------------ MFMA tiles (non-pair)
+// fsacmp's count as a dot product on the matrix cores, exactly.  A 2-bit code
+// (hi, lo) becomes the tetrahedron vector (s_hi, s_lo, s_hi s_lo) of +-1
+// (s = 1 - 2 bit): equal codes dot to 3, different ones to -1, so over the
+// L positions of a word slice (padding and the pre-masked positions are code
+// 0 in every row: "equal")  dist = (3 L - dot) / 4.  The three components are
+// MX-fp4 operands of v_mfma_scale_f32_32x32x64_f8f6f4 (e2m1 +1 = 0x2,
+// -1 = 0xA, unit scales); f32 accumulation of the +-1 products is exact while
+// |dot| <= 3 L < 2^24 (the host splits K beyond that).  A lane's operand for
+// one 32x32x64 step is one 32-position plane word expanded to 32 nibbles
+// (tools/micro/mfma_fp4: row = lane & 31, and A's (lane, nibble) meets B's
+// (lane, nibble), so any fixed spread of the word's bits over the nibbles
+// works if both panels use it): dword q holds bits q, q+4, ..., q+28 at the
+// nibbles' sign bits, (x << (3 - q)) & 0x88888888 | 0x22222222, 2 VALU ops.
+// Block = 4 waves on a 128x128 pair tile, each wave 64x64 (2x2 MFMA tiles,
+// 3 components x 2 words of 32 positions per step); raw words staged through
+// LDS as in k_snp_tile (double-buffered KC-word chunks, XCD-contiguous tile
+// order, split-K over word slices).
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+#define MFMA_FP4 4
+#define MFMA_SCALE1 127
+#define MFMA_KMAX 174762   // words per slice: 3 * 32 * Wk < 2^24
+
+__device__ __forceinline__ v8i_t fp4_spread(uint32_t x) {
+	v8i_t v;
+	v[0] = (int) (((x << 3) & 0x88888888u) | 0x22222222u);
+	v[1] = (int) (((x << 2) & 0x88888888u) | 0x22222222u);
+	v[2] = (int) (((x << 1) & 0x88888888u) | 0x22222222u);
+	v[3] = (int) ((x & 0x88888888u) | 0x22222222u);
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+template <int ET, bool SPLIT>
+__global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P, int Wp, int n, long long t0,
+                                                     long long items, int S, int Wk, double nFactor, double bs,
+                                                     typename Elem<ET>::T *__restrict__ D, long long rowBegin,
+                                                     long long rowEnd, unsigned *__restrict__ cnt, long long cbase) {
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
+	int I, J;
+	const long long item = t0 + xcd_tile(blockIdx.x, items);
+	tile_ij(item / S, I, J);
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int wr = wid >> 1, wc = wid & 1;   // this wave's 64x64 quarter
+	const uint2 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint2 *Bp = P + (size_t) J * TILE * Wp + wb;
+	const int Wl = we - wb;   // words of this slice (a multiple of KC)
+	v16f_t acc[2][2];
+#pragma unroll
+	for(int a = 0; a < 2; ++a)
+#pragma unroll
+		for(int c = 0; c < 2; ++c)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[a][c][r] = 0.0f;
+	uint4 va[4], vb[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + 2 * wp);
+		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+		As[0][(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+		Bs[0][(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+		Bs[0][(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+	}
+	__syncthreads();
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 64 * wr + l32, rb0 = 64 * wc + l32;
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KC, buf ^= 1) {
+		const bool more = w0 + KC < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + KC + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
+			}
+		}
+		const uint2 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 2
+		for(int s = 0; s < KC / 2; ++s) {
+			const int w = 2 * s + h;   // this lane's word: its half of the step's 64 positions
+			uint2 a[2], b[2];
+#pragma unroll
+			for(int t = 0; t < 2; ++t) {
+				a[t] = Ac[w * RS + ra0 + 32 * t];
+				b[t] = Bc[w * RS + rb0 + 32 * t];
+			}
+#pragma unroll
+			for(int comp = 0; comp < 3; ++comp) {
+				v8i_t fa[2], fb[2];
+#pragma unroll
+				for(int t = 0; t < 2; ++t) {
+					fa[t] = fp4_spread(comp == 0 ? a[t].x : comp == 1 ? a[t].y : a[t].x ^ a[t].y);
+					fb[t] = fp4_spread(comp == 0 ? b[t].x : comp == 1 ? b[t].y : b[t].x ^ b[t].y);
+				}
+#pragma unroll
+				for(int ta = 0; ta < 2; ++ta)
+#pragma unroll
+					for(int tb = 0; tb < 2; ++tb)
+						acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+						    fa[ta], fb[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+			}
+		}
+		if(more) {
+			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+				Bn[(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+			}
+		}
+		__syncthreads();
+	}
+	// epilogue: C/D of 32x32 (col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5));
+	// dist = (3 L - dot) / 4 over the slice's L = 32 Wl positions
+	const int L3 = 3 * 32 * Wl;
+#pragma unroll
+	for(int ta = 0; ta < 2; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const long long i = (long long) I * TILE + 64 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			if(i >= n || i < rowBegin || i >= rowEnd) continue;
+			const long long base = tri(i);
+#pragma unroll
+			for(int tb = 0; tb < 2; ++tb) {
+				const long long j = (long long) J * TILE + 64 * wc + 32 * tb + l32;
+				if(j < i) {
+					const unsigned d = (unsigned) ((L3 - (int) acc[ta][tb][r]) >> 2);
+					if(SPLIT) {
+						atomicAdd(&cnt[base + j - cbase], d);
+					} else {
+						const double v = nFactor * (double) d;
+						D[base + j] = Elem<ET>::put(v, 0.5, bs);
+					}
+				}
+			}
+		}
+	}
+}
+
 // The same tiles for one rank of the row-sharded layout (ccg_shard.h): the A
 // panel gathers the rank's owned rows, so a rank computes only its own rows
 // and writes them where ccg_tree_shard_dev reads them.
@@ -694,14 +846,37 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 		}
 		return CCG_OK;
 	}
+	// MFMA form (k_snp_mfma, the default; CCG_DIST_MFMA=0 selects the VALU
+	// tiles): f32-exact while a slice holds < MFMA_KMAX words
+	const char *mf = getenv("CCG_DIST_MFMA");
+	const int use_mfma = mf ? atoi(mf) : 1;
+	int Sm = S, Wkm = Wk;
+	if(use_mfma && Wkm > MFMA_KMAX) {
+		Wkm = (MFMA_KMAX / kc) * kc;
+		Sm = (int) cdivll(Wp, Wkm);
+	}
+	if(use_mfma) {
+		S = Sm;
+	}
+	const long long mi_begin = t_begin * S, mi_end = t_end * S;
 	unsigned *cnt = NULL;
 	if(S > 1) {
 		CCG_CHECK(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)));
 		CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
 	}
-	for(long long t = i_begin; t < i_end; t += batch) {
-		long long items = i_end - t < batch ? i_end - t : batch;
-		if(S > 1) {
+	for(long long t = use_mfma ? mi_begin : i_begin; t < (use_mfma ? mi_end : i_end); t += batch) {
+		const long long iend = use_mfma ? mi_end : i_end;
+		long long items = iend - t < batch ? iend - t : batch;
+		if(use_mfma) {
+			if(S > 1)
+				k_snp_mfma<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, items,
+				                                                             S, Wkm, nFactor, a->byteScale, (T *) D, rb,
+				                                                             re, cnt, f0);
+			else
+				k_snp_mfma<ET, false><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t,
+				                                                              items, 1, Wp, nFactor, a->byteScale,
+				                                                              (T *) D, rb, re, cnt, f0);
+		} else if(S > 1) {
 			k_snp_tile<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, a->n, t, items, S,
 			                                                             Wk, nFactor, a->byteScale, (T *) D, rb, re,
 			                                                             cnt, f0);

@@ -175,6 +175,41 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
     return seqs, incs.astype(np.uint32)
 
 
+@pytest.mark.parametrize("n,L,et,rows", [(300, 1000, 8, None), (1000, 20000, 4, None), (777, 4097, 2, (100, 650)),
+                                         (2100, 33, 1, None), (129, 700000, 8, (5, 129))])
+def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows):
+    """The MFMA form of fsacmp (k_snp_mfma: tetrahedron +-1 vectors in
+    MX-fp4, dist = (3 L - dot) / 4) gives the VALU tile kernel's matrix bit
+    for bit: odd sizes, row ranges, split-K slices, every element type (the
+    default path, MFMA, is checked against the oracle by the tests above)."""
+    import torch
+    rng = np.random.default_rng(n + L)
+    W = L // 32 + 1
+    seqs = rng.integers(-2**62, 2**62, (n, W), dtype=np.int64)
+    seqs[:, : W // 3] = seqs[0, : W // 3]
+    inc = np.full(W, -1, dtype=np.int32)
+    inc[(L + 31) // 32:] = 0
+    if L % 32:
+        inc[(L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    inc[W // 2] &= 0x0F0F0F0F
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CCG_DIST_MFMA", mode)
+        s_d = torch.from_numpy(seqs).cuda()
+        i_d = torch.from_numpy(inc).cuda()
+        m = n * (n - 1) // 2
+        D = torch.zeros(m, dtype={8: torch.float64, 4: torch.float32, 2: torch.int16, 1: torch.uint8}[et],
+                        device="cuda")
+        kw = dict(etype=et)
+        if rows:
+            kw["row_range"] = rows
+        dev.snp_ltd_dev(s_d.data_ptr(), i_d.data_ptr(), n, L, W, D.data_ptr(), **kw)
+        torch.cuda.synchronize()
+        out[mode] = D.cpu().numpy()
+    assert (out["0"].view(np.uint8) == out["1"].view(np.uint8)).all()
+    assert out["1"].any()
+
+
 @pytest.mark.parametrize("n,L,proxi,rate,et,norm", [(70, 3000, 10, 0.05, 8, 0), (65, 4097, 2, 0.3, 8, 1000),
                                                     (40, 20000, 40, 0.01, 4, 0), (33, 2048, 100, 0.02, 2, 100),
                                                     (50, 9000, 1, 0.7, 1, 100), (20, 70000, 33, 0.002, 8, 0),
