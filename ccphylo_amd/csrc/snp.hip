@@ -466,6 +466,130 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restric
 	}
 }
 
+// k_snp_mfma for one rank of the row-sharded layout (as k_snp_tile_band):
+// A panel = the rank's owned rows, rows stored at Shard::off(i).  No split-K:
+// the host takes this path only while Wp < MFMA_KMAX.
+template <int ET>
+__global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restrict__ P, int Wp, int n,
+                                                          const long long *__restrict__ pfx, int npanels, long long t0,
+                                                          long long items, double nFactor, double bs,
+                                                          typename Elem<ET>::T *__restrict__ Dloc, int rank, int world) {
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
+	const long long t = t0 + xcd_tile(blockIdx.x, items);
+	int lo = 0, hi = npanels - 1;
+	while(lo < hi) {
+		const int mid = (lo + hi + 1) >> 1;
+		if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
+	}
+	const int I = lo, J = (int) (t - pfx[lo]);
+	const Shard sh{rank, world};
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE + l, lb = L / SB, g = lb * world + rank, r = g * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const uint2 *Bp = P + (size_t) J * TILE * Wp;
+	const int Wl = Wp;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int wr = wid >> 1, wc = wid & 1;
+	v16f_t acc[2][2];
+#pragma unroll
+	for(int a = 0; a < 2; ++a)
+#pragma unroll
+		for(int c = 0; c < 2; ++c)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[a][c][r] = 0.0f;
+	uint4 va[4], vb[4];
+	long long ar[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		ar[q] = arow(row);
+		va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + 2 * wp);
+		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+		As[0][(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+		Bs[0][(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+		Bs[0][(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+	}
+	__syncthreads();
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 64 * wr + l32, rb0 = 64 * wc + l32;
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KC, buf ^= 1) {
+		const bool more = w0 + KC < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + w0 + KC + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
+			}
+		}
+		const uint2 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 2
+		for(int s = 0; s < KC / 2; ++s) {
+			const int w = 2 * s + h;
+			uint2 a[2], b[2];
+#pragma unroll
+			for(int tt = 0; tt < 2; ++tt) {
+				a[tt] = Ac[w * RS + ra0 + 32 * tt];
+				b[tt] = Bc[w * RS + rb0 + 32 * tt];
+			}
+#pragma unroll
+			for(int comp = 0; comp < 3; ++comp) {
+				v8i_t fa[2], fb[2];
+#pragma unroll
+				for(int tt = 0; tt < 2; ++tt) {
+					fa[tt] = fp4_spread(comp == 0 ? a[tt].x : comp == 1 ? a[tt].y : a[tt].x ^ a[tt].y);
+					fb[tt] = fp4_spread(comp == 0 ? b[tt].x : comp == 1 ? b[tt].y : b[tt].x ^ b[tt].y);
+				}
+#pragma unroll
+				for(int ta = 0; ta < 2; ++ta)
+#pragma unroll
+					for(int tb = 0; tb < 2; ++tb)
+						acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+						    fa[ta], fb[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+			}
+		}
+		if(more) {
+			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
+				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
+				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
+				Bn[(2 * wp + 1) * RS + row] = make_uint2(vb[q].z, vb[q].w);
+			}
+		}
+		__syncthreads();
+	}
+	const int L3 = 3 * 32 * Wl;
+#pragma unroll
+	for(int ta = 0; ta < 2; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const int l = 64 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			const long long L = (long long) I * TILE + l, lb = L / SB, i = (lb * world + rank) * SB + (L - lb * SB);
+			if(i >= n) continue;
+			const long long base = sh.off(i);
+#pragma unroll
+			for(int tb = 0; tb < 2; ++tb) {
+				const long long j = (long long) J * TILE + 64 * wc + 32 * tb + l32;
+				if(j < i) {
+					const unsigned d = (unsigned) ((L3 - (int) acc[ta][tb][r]) >> 2);
+					Dloc[base + j] = Elem<ET>::put(nFactor * (double) d, 0.5, bs);
+				}
+			}
+		}
+	}
+}
+
 // split-K epilogue: D[f] = nFactor * count (fsacmpthrd.c:247-255)
 template <int ET>
 __global__ void k_snp_finish(const unsigned *__restrict__ cnt, long long cbase, long long f0, long long f1,
@@ -929,11 +1053,19 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	CCG_CHECK(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
 	                         ctx->stream));
 	const long long total = pfx[npanels], batch = 1 << 16;
+	// the MFMA form unless disabled or a row's words exceed its exact f32 range
+	const char *mf = getenv("CCG_DIST_MFMA");
+	const bool use_mfma_b = (mf ? atoi(mf) : 1) && Wp < MFMA_KMAX;
 	for(long long t = 0; t < total; t += batch) {
 		const long long items = total - t < batch ? total - t : batch;
-		k_snp_tile_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
-		                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
-		                                                             rank, world);
+		if(use_mfma_b)
+			k_snp_mfma_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
+			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
+			                                                             rank, world);
+		else
+			k_snp_tile_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
+			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
+			                                                             rank, world);
 		CCG_CHECK(hipGetLastError());
 	}
 	CCG_CHECK(hipStreamSynchronize(ctx->stream));
