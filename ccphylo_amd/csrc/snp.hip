@@ -228,6 +228,9 @@ typedef float v16f_t __attribute__((ext_vector_type(16)));
 #define MFMA_FP4 4
 #define MFMA_SCALE1 127
 #define MFMA_KMAX 174762   // words per slice: 3 * 32 * Wk < 2^24
+#ifndef MFMA_UNROLL
+#define MFMA_UNROLL 2
+#endif
 
 __device__ __forceinline__ v8i_t fp4_spread(uint32_t x) {
 	v8i_t v;
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P
 			}
 		}
 		const uint2 *Ac = As[buf], *Bc = Bs[buf];
-#pragma unroll 2
+#pragma unroll MFMA_UNROLL
 		for(int s = 0; s < KC / 2; ++s) {
 			const int w = 2 * s + h;   // this lane's word: its half of the step's 64 positions
 			uint2 a[2], b[2];
