@@ -296,20 +296,21 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     words = (L + 31) // 32
     opw = OPS_PER_WORD_PAIR_PAIRMODE if pair else OPS_PER_WORD_PAIR
     ops = m * words * opw / world   # per GPU
-    mfma = not pair and os.environ.get("CCG_DIST_MFMA", "1") != "0"
+    mfma = os.environ.get("CCG_DIST_MFMA", "1") != "0"
     del seqs, incs, Dd, Nd
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "kernel": "k_snp_mfma" if mfma else ("k_snp_tile_pair" if pair else "k_snp_tile"),
-            "roofline": mfma_roofline(m * L / world, dt) if mfma else valu_roofline(ops, dt, opw)}
+            "kernel": ("k_snp_mfma_pair" if pair else "k_snp_mfma") if mfma else ("k_snp_tile_pair" if pair else "k_snp_tile"),
+            "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
+            else valu_roofline(ops, dt, opw)}
 
 
-def mfma_roofline(position_pairs, dt):
+def mfma_roofline(position_pairs, dt, flops_per_pp=FLOPS_PER_POSITION_PAIR):
     """dist on the matrix cores: 6 flops (3 MX-fp4 MACs) per position pair
-    against the MX-fp4 dense peak, and beside it the register-fed issue rate
-    measured on this box."""
-    tf = FLOPS_PER_POSITION_PAIR * position_pairs / dt / 1e12
+    (pair mode: 8, the mask is a fourth component) against the MX-fp4 dense
+    peak, and beside it the register-fed issue rate measured on this box."""
+    tf = flops_per_pp * position_pairs / dt / 1e12
     return {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4), "measured_issue_peak": MFMA_FP4_MEASURED_TFLOPS,
             "frac_of_measured_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),

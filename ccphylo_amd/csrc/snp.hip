@@ -751,6 +751,158 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 	}
 }
 
+// Pair mode (fsacmpair fsacmp.c:587: dist and n over inc_a & inc_b) on the
+// matrix cores: each component nibble is zeroed where the row's mask bit is
+// 0, so over the positions both rows include, equal codes dot to 3 and
+// different ones to -1 (dot = 3 n - 4 dist), and a fourth component, the
+// mask itself (+1 / 0), dots to n = popc(m_a & m_b).  Same tiles, staging
+// (uint4 {hi, lo, m, 0} words, KCP-word chunks) and split-K as
+// k_snp_tile_pair; exact while 3 L < 2^24 per slice.
+// one pair-mode operand: component comp (0 hi, 1 lo, 2 hi ^ lo: masked +-1;
+// 3: the mask as +1 / 0) of a lane's word, from its mask spread mq
+__device__ __forceinline__ v8i_t fp4_pair_comp(uint32_t hi, uint32_t lo, const uint32_t (&mq)[4], int comp) {
+	v8i_t v;
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		if(comp == 3) {
+			v[q] = (int) (mq[q] >> 2);   // +1.0 where included
+		} else {
+			const uint32_t x = comp == 0 ? hi : comp == 1 ? lo : hi ^ lo;
+			const uint32_t xs = q < 3 ? x << (3 - q) : x;
+			const uint32_t mf = mq[q] | (mq[q] >> 1) | (mq[q] >> 2) | (mq[q] >> 3);   // 0xF where included
+			v[q] = (int) (((xs & 0x88888888u) | 0x22222222u) & mf);
+		}
+	}
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+template <int ET, bool SPLIT>
+__global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
+                                                          long long items, int S, int Wk, unsigned norm,
+                                                          unsigned minLength, double bs,
+                                                          typename Elem<ET>::T *__restrict__ D,
+                                                          typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
+                                                          long long rowEnd, unsigned *__restrict__ cd,
+                                                          unsigned *__restrict__ cn, long long cbase) {
+	__shared__ __attribute__((aligned(16))) uint4 As[2][KCP * RSP];
+	__shared__ __attribute__((aligned(16))) uint4 Bs[2][KCP * RSP];
+	int I, J;
+	const long long item = t0 + xcd_tile(blockIdx.x, items);
+	tile_ij(item / S, I, J);
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	const int Wl = we - wb;   // a multiple of KCP
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int wr = wid >> 1, wc = wid & 1;
+	const uint4 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint4 *Bp = P + (size_t) J * TILE * Wp + wb;
+	v16f_t acc[2][2], accn[2][2];
+#pragma unroll
+	for(int a = 0; a < 2; ++a)
+#pragma unroll
+		for(int c = 0; c < 2; ++c)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[a][c][r] = accn[a][c][r] = 0.0f;
+	uint4 va[4], vb[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		va[q] = Ap[(size_t) row * Wp + wp];
+		vb[q] = Bp[(size_t) row * Wp + wp];
+	}
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+		As[0][wp * RSP + row] = va[q];
+		Bs[0][wp * RSP + row] = vb[q];
+	}
+	__syncthreads();
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 64 * wr + l32, rb0 = 64 * wc + l32;
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KCP, buf ^= 1) {
+		const bool more = w0 + KCP < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				va[q] = Ap[(size_t) row * Wp + w0 + KCP + wp];
+				vb[q] = Bp[(size_t) row * Wp + w0 + KCP + wp];
+			}
+		}
+		const uint4 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll 1
+		for(int s = 0; s < KCP / 2; ++s) {
+			const int w = 2 * s + h;
+			uint4 a[2], b[2];
+			uint32_t ma[2][4], mb[2][4];
+#pragma unroll
+			for(int t = 0; t < 2; ++t) {
+				a[t] = Ac[w * RSP + ra0 + 32 * t];
+				b[t] = Bc[w * RSP + rb0 + 32 * t];
+#pragma unroll
+				for(int q = 0; q < 4; ++q) {
+					ma[t][q] = (q < 3 ? a[t].z << (3 - q) : a[t].z) & 0x88888888u;
+					mb[t][q] = (q < 3 ? b[t].z << (3 - q) : b[t].z) & 0x88888888u;
+				}
+			}
+#pragma unroll
+			for(int comp = 0; comp < 4; ++comp) {
+				v8i_t fa[2], fb[2];
+#pragma unroll
+				for(int t = 0; t < 2; ++t) {
+					fa[t] = fp4_pair_comp(a[t].x, a[t].y, ma[t], comp);
+					fb[t] = fp4_pair_comp(b[t].x, b[t].y, mb[t], comp);
+				}
+#pragma unroll
+				for(int ta = 0; ta < 2; ++ta)
+#pragma unroll
+					for(int tb = 0; tb < 2; ++tb) {
+						if(comp < 3)
+							acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+							    fa[ta], fb[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+						else
+							accn[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+							    fa[ta], fb[tb], accn[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+					}
+			}
+		}
+		if(more) {
+			uint4 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+				An[wp * RSP + row] = va[q];
+				Bn[wp * RSP + row] = vb[q];
+			}
+		}
+		__syncthreads();
+	}
+#pragma unroll
+	for(int ta = 0; ta < 2; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const long long i = (long long) I * TILE + 64 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			if(i >= n || i < rowBegin || i >= rowEnd) continue;
+			const long long base = tri(i);
+#pragma unroll
+			for(int tb = 0; tb < 2; ++tb) {
+				const long long j = (long long) J * TILE + 64 * wc + 32 * tb + l32;
+				if(j < i) {
+					const int nn = (int) accn[ta][tb][r];
+					const unsigned d = (unsigned) ((3 * nn - (int) acc[ta][tb][r]) >> 2);
+					if(SPLIT) {
+						atomicAdd(&cd[base + j - cbase], d);
+						atomicAdd(&cn[base + j - cbase], (unsigned) nn);
+					} else {
+						pair_store<ET>(D, Nm, base + j, d, (uint32_t) nn, norm, minLength, bs);
+					}
+				}
+			}
+		}
+	}
+}
+
 // split-K epilogue of pair mode: the A7 store of the summed (dist, n)
 template <int ET>
 __global__ void k_snp_pair_finish(const unsigned *__restrict__ cd, const unsigned *__restrict__ cn, long long f0,
@@ -950,9 +1102,21 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 			cn = cd + (f1 - f0);
 			CCG_CHECK(hipMemsetAsync(cd, 0, (size_t) (f1 - f0) * 2 * sizeof(unsigned), ctx->stream));
 		}
+		// the MFMA form (default; CCG_DIST_MFMA=0: VALU tiles) while a slice is f32-exact
+		const char *mfp = getenv("CCG_DIST_MFMA");
+		const bool pmfma = (mfp ? atoi(mfp) : 1) && Wk < MFMA_KMAX;
 		for(long long t = i_begin; t < i_end; t += batch) {
 			long long items = i_end - t < batch ? i_end - t : batch;
-			if(S > 1) {
+			if(pmfma) {
+				if(S > 1)
+					k_snp_mfma_pair<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    (const uint4 *) planes, Wp, a->n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D,
+					    (T *) N, rb, re, cd, cn, f0);
+				else
+					k_snp_mfma_pair<ET, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    (const uint4 *) planes, Wp, a->n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+					    (T *) N, rb, re, cd, cn, f0);
+			} else if(S > 1) {
 				k_snp_tile_pair<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
 				    (const uint4 *) planes, Wp, a->n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D,
 				    (T *) N, rb, re, cd, cn, f0);

@@ -175,23 +175,29 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
     return seqs, incs.astype(np.uint32)
 
 
-@pytest.mark.parametrize("n,L,et,rows", [(300, 1000, 8, None), (1000, 20000, 4, None), (777, 4097, 2, (100, 650)),
-                                         (2100, 33, 1, None), (129, 700000, 8, (5, 129))])
-def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows):
-    """The MFMA form of fsacmp (k_snp_mfma: tetrahedron +-1 vectors in
-    MX-fp4, dist = (3 L - dot) / 4) gives the VALU tile kernel's matrix bit
-    for bit: odd sizes, row ranges, split-K slices, every element type (the
+@pytest.mark.parametrize("n,L,et,rows,pair", [(300, 1000, 8, None, False), (1000, 20000, 4, None, False),
+                                              (777, 4097, 2, (100, 650), False), (2100, 33, 1, None, False),
+                                              (129, 700000, 8, (5, 129), False), (300, 1000, 8, None, True),
+                                              (900, 30000, 4, None, True), (555, 4100, 2, (50, 400), True),
+                                              (1100, 65, 8, None, True)])
+def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
+    """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma, k_snp_mfma_pair:
+    tetrahedron +-1 vectors in MX-fp4, dist = (3 L - dot) / 4, in pair mode
+    masked with n from a fourth component) give the VALU tile kernels'
+    matrices (and N) bit for bit: odd sizes, row ranges, split-K slices, every element type (the
     default path, MFMA, is checked against the oracle by the tests above)."""
     import torch
     rng = np.random.default_rng(n + L)
     W = L // 32 + 1
     seqs = rng.integers(-2**62, 2**62, (n, W), dtype=np.int64)
     seqs[:, : W // 3] = seqs[0, : W // 3]
-    inc = np.full(W, -1, dtype=np.int32)
-    inc[(L + 31) // 32:] = 0
+    inc = np.full((n, W) if pair else W, -1, dtype=np.int32)
+    inc[..., (L + 31) // 32:] = 0
     if L % 32:
-        inc[(L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
-    inc[W // 2] &= 0x0F0F0F0F
+        inc[..., (L + 31) // 32 - 1] = ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    inc[..., W // 2] &= 0x0F0F0F0F
+    if pair:   # per-taxon masks: ~1/8 of the positions excluded, differently per taxon
+        inc &= (rng.integers(-2**31, 2**31, inc.shape, dtype=np.int64) | 0x77777777).astype(np.int32)
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("CCG_DIST_MFMA", mode)
@@ -200,14 +206,17 @@ def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows):
         m = n * (n - 1) // 2
         D = torch.zeros(m, dtype={8: torch.float64, 4: torch.float32, 2: torch.int16, 1: torch.uint8}[et],
                         device="cuda")
-        kw = dict(etype=et)
+        Nd = torch.zeros_like(D) if pair else None
+        kw = dict(etype=et, pair=pair, N_ptr=Nd.data_ptr() if pair else None)
         if rows:
             kw["row_range"] = rows
         dev.snp_ltd_dev(s_d.data_ptr(), i_d.data_ptr(), n, L, W, D.data_ptr(), **kw)
         torch.cuda.synchronize()
-        out[mode] = D.cpu().numpy()
-    assert (out["0"].view(np.uint8) == out["1"].view(np.uint8)).all()
-    assert out["1"].any()
+        out[mode] = (D.cpu().numpy(), Nd.cpu().numpy() if pair else None)
+    assert (out["0"][0].view(np.uint8) == out["1"][0].view(np.uint8)).all()
+    if pair:
+        assert (out["0"][1].view(np.uint8) == out["1"][1].view(np.uint8)).all()
+    assert out["1"][0].any()
 
 
 @pytest.mark.parametrize("n,L,proxi,rate,et,norm", [(70, 3000, 10, 0.05, 8, 0), (65, 4097, 2, 0.3, 8, 1000),
