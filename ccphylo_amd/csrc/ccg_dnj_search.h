@@ -86,20 +86,30 @@ __device__ __forceinline__ void row_segment_min(const Rows &rows, const typename
                                                 int c0, int c1, int Nr, double sDr, int isub, int Nm, double sDm,
                                                 double &q, int &idx) {
 	const typename Elem<ET>::T *row = D + rows.row(r);
-	for(int base = c0; base < c1; base += UNR * NT) {
-		typename Elem<ET>::T v[UNR];
-		int nk[UNR];
-		double sk[UNR];
+	typename Elem<ET>::T v[UNR];
+	int nk[UNR];
+	double sk[UNR];
+	// clamped (always valid) addresses: no branches between the loads, so all
+	// of them are in flight before the first wait
+	auto load = [&](int base, typename Elem<ET>::T (&lv)[UNR], int (&lk)[UNR], double (&ls)[UNR]) {
 #pragma unroll
 		for(int m = 0; m < UNR; ++m) {
-			// clamped (always valid) addresses: no branches between the loads,
-			// so all of them are in flight before the first wait
 			int c = base + m * NT + (int) threadIdx.x;
 			c = c < c1 ? c : c1 - 1;
-			v[m] = row[c];
-			nk[m] = GEN ? N[c] : Nr;
-			sk[m] = sD[c];
+			lv[m] = row[c];
+			lk[m] = GEN ? N[c] : Nr;
+			ls[m] = sD[c];
 		}
+	};
+	load(c0, v, nk, sk);
+	for(int base = c0; base < c1; base += UNR * NT) {
+		// software pipeline (segments of several UNR * NT cells, large n): the
+		// next step's loads are in flight while this step's cells are compared
+		typename Elem<ET>::T vn[UNR];
+		int nkn[UNR];
+		double skn[UNR];
+		const bool more = base + UNR * NT < c1;   // uniform
+		if(more) load(base + UNR * NT, vn, nkn, skn);
 		// branch-free (no use of a loaded value under a condition, so the
 		// compiler cannot sink a load behind the first wait)
 #pragma unroll
@@ -112,6 +122,14 @@ __device__ __forceinline__ void row_segment_min(const Rows &rows, const typename
 			const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
 			q = take ? x : q;
 			idx = take ? c : idx;
+		}
+		if(more) {
+#pragma unroll
+			for(int m = 0; m < UNR; ++m) {
+				v[m] = vn[m];
+				nk[m] = nkn[m];
+				sk[m] = skn[m];
+			}
 		}
 	}
 }
@@ -771,7 +789,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 		const int Nr = GEN ? b.N[r] : n;
 		double qq = DBL_MAX;
 		int idx = 0;
-		row_segment_min<ET, GEN, TB, SEG / TB>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
+		row_segment_min<ET, GEN, TB, SEG / TB / 2>(rows, D, bs, b.sD, b.N, r, c0, c1, Nr, b.sD[r], -1, 0, 0.0, qq, idx);
 		qarg_block_reduce1(qq, idx, sq, si);
 		if(tid == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, qq, idx);
 		if(u + (int) gridDim.x < nunits) __syncthreads();
