@@ -36,6 +36,7 @@
 // Hence the joins are bit-identical to ccg_tree's DNJ for every world size.
 #define CCG_DNJ_NO_TRACE
 #include <stdio.h>
+#include <string.h>
 #include <stdlib.h>
 #include "ccg_dnj_search.h"
 #include "ccg_shard.h"
@@ -597,9 +598,13 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	unsigned char *pflag = (unsigned char *) (m + o_pf), *pacc = (unsigned char *) (m + o_pa);
 	unsigned *pcnt = (unsigned *) (m + o_pc);
 	unsigned long long *dbg = NULL;
+	// diagnostic: k_shd_pick's phase stamps (s_memrealtime), averaged to stderr
 	if(getenv("CCG_PICK_TS")) {
-		hipMalloc((void **) &dbg, 1024 * 8 * 8);
-		hipMemsetAsync(dbg, 0, 1024 * 8 * 8, st);
+		if(hipMalloc((void **) &dbg, 1024 * 8 * 8) != hipSuccess) dbg = NULL;
+		else if(hipMemsetAsync(dbg, 0, 1024 * 8 * 8, st) != hipSuccess) {
+			hipFree(dbg);
+			dbg = NULL;
+		}
 	}
 	TreeCtl init, hc;
 	long long launches = 0;
@@ -675,8 +680,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	SD_HIP(hipEventRecord(ctx->ev1, st));
 	kt.finish();
 	if(dbg) {
-		static unsigned long long hd[1024 * 8];
-		hipMemcpy(hd, dbg, sizeof(hd), hipMemcpyDeviceToHost);
+		static thread_local unsigned long long hd[1024 * 8];
+		if(hipMemcpy(hd, dbg, sizeof(hd), hipMemcpyDeviceToHost) != hipSuccess) memset(hd, 0, sizeof(hd));
 		double acc[8] = {0};
 		int cnt = 0;
 		for(int s_ = 0; s_ < 1024; ++s_) {
@@ -686,8 +691,9 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			acc[6] += (double) t_[6];
 			++cnt;
 		}
-		fprintf(stderr, "pick phases over %d joins (ns): entry->loads %.0f, count+scan %.0f, entries %.0f, replay %.0f, gather %.0f; total entries %.1f\n",
-		        cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt);
+		if(cnt)
+			fprintf(stderr, "pick phases over %d joins (ns): entry->loads %.0f, count+scan %.0f, entries %.0f, replay %.0f, gather %.0f; total entries %.1f\n",
+			        cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt);
 		hipFree(dbg);
 	}
 	SD_HIP(hipMemcpyAsync(&hc, b.ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
