@@ -20,6 +20,7 @@ struct DenseRows {
                          // of at most this many bands below them (DnjGrid::top/bands)
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
+#define SEL_STEPS 8      // steps of the S scan at most (then the listing takes over)
 #define TBF 1024         // threads of k_dnj_plan (one block)
 #define FIND_RPT 16      // rows per thread per step of k_dnj_plan's listing (one step up to n = 15361)
 #define FIND_CHUNKS 2048  // 64-row chunks of k_dnj_plan's S-rank table (n <= 131072; else binary searches)
@@ -432,14 +433,23 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 #undef QSUB
 #undef PSUB
 			
-			// ---- S, top part: ktop rows with Q < m0 from the top
-			int cnt = 0;
-			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop; base -= 64 * SEL_RPL, ++step) {
+			// ---- S, top part: ktop rows with Q < m0 from the top, examining at
+			// most SEL_STEPS steps of 64 SEL_RPL rows (any S is exact: when the
+			// scan stops short, the rows below the examined ones are left to the
+			// listing under its bound, which never exceeds m0)
+			int cnt = 0, low = n;   // rows >= low examined
+			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop && step < SEL_STEPS; base -= 64 * SEL_RPL, ++step) {
+				if(step) {
+#pragma unroll
+					for(int m = 0; m < SEL_RPL; ++m) {   // all of the step's loads in flight at once
+						const int r = base - (m * 64 + lane);
+						topQ[m] = b.Q[r >= 1 ? r : 1];
+					}
+				}
 #pragma unroll
 				for(int m = 0; m < SEL_RPL; ++m) {
 					if(cnt >= ktop) continue;   // uniform
 					const int r = base - (m * 64 + lane);
-					if(step) topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
 					const double v = r == jsub ? Qj : r == isub ? Qi : topQ[m];
 					const bool f = r >= 1 && v < m0;
 					const unsigned long long bm = __ballot(f);
@@ -450,11 +460,13 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 						sQS[pos] = v;
 					}
 					cnt += __popcll(bm);
+					low = base - (m * 64 + 63) > 1 ? base - (m * 64 + 63) : 1;
 				}
 			}
 			const int ntop = cnt < ktop ? cnt : ktop;
 			int nS = ntop;
-			const int smin = ntop == ktop ? sS[ktop - 1] : 1;
+			// full: below S's last row; short: below the examined rows (1: all)
+			const int smin = ntop == ktop ? sS[ktop - 1] : low;
 			// ---- S, band part (large n): each band's min-Q row below the top
 			// part, with the Q criterion at its partner cell (rows j and i of the
 			// previous join are never band candidates)
