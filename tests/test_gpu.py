@@ -179,7 +179,8 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
                                               (777, 4097, 2, (100, 650), False), (2100, 33, 1, None, False),
                                               (129, 700000, 8, (5, 129), False), (300, 1000, 8, None, True),
                                               (900, 30000, 4, None, True), (555, 4100, 2, (50, 400), True),
-                                              (1100, 65, 8, None, True)])
+                                              (1100, 65, 8, None, True), (70, 6_000_000, 8, None, False),
+                                              (40, 5_800_000, 4, None, True)])
 def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
     """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma, k_snp_mfma_pair:
     tetrahedron +-1 vectors in MX-fp4, dist = (3 L - dot) / 4, in pair mode
