@@ -231,6 +231,15 @@ typedef float v16f_t __attribute__((ext_vector_type(16)));
 #ifndef MFMA_UNROLL
 #define MFMA_UNROLL 2
 #endif
+// k_snp_mfma's LDS chunk (words) and blocks per CU: 8-word chunks keep a
+// block's double-buffered panels at 33 KB, so 3 blocks fit a CU's LDS
+#ifndef KCM
+#define KCM 8
+#endif
+#ifndef MFMA_BLOCKS
+#define MFMA_BLOCKS 3
+#endif
+#define QS (TILE * KCM / 2 / 256)   // uint4 staged per thread per panel
 
 __device__ __forceinline__ v8i_t fp4_spread(uint32_t x) {
 	v8i_t v;
@@ -243,12 +252,12 @@ __device__ __forceinline__ v8i_t fp4_spread(uint32_t x) {
 }
 
 template <int ET, bool SPLIT>
-__global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P, int Wp, int n, long long t0,
+__global__ __launch_bounds__(256, MFMA_BLOCKS) void k_snp_mfma(const uint2 *__restrict__ P, int Wp, int n, long long t0,
                                                      long long items, int S, int Wk, double nFactor, double bs,
                                                      typename Elem<ET>::T *__restrict__ D, long long rowBegin,
                                                      long long rowEnd, unsigned *__restrict__ cnt, long long cbase) {
-	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
-	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KCM * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KCM * RS];
 	int I, J;
 	const long long item = t0 + xcd_tile(blockIdx.x, items);
 	tile_ij(item / S, I, J);
@@ -265,16 +274,16 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P
 		for(int c = 0; c < 2; ++c)
 #pragma unroll
 			for(int r = 0; r < 16; ++r) acc[a][c][r] = 0.0f;
-	uint4 va[4], vb[4];
+	uint4 va[QS], vb[QS];
 #pragma unroll
-	for(int q = 0; q < 4; ++q) {
-		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+	for(int q = 0; q < QS; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e / (KCM / 2), wp = e % (KCM / 2);
 		va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + 2 * wp);
 		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
 	}
 #pragma unroll
-	for(int q = 0; q < 4; ++q) {
-		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+	for(int q = 0; q < QS; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e / (KCM / 2), wp = e % (KCM / 2);
 		As[0][(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
 		As[0][(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
 		Bs[0][(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
@@ -284,19 +293,19 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P
 	const int h = lane >> 5, l32 = lane & 31;
 	const int ra0 = 64 * wr + l32, rb0 = 64 * wc + l32;
 	int buf = 0;
-	for(int w0 = 0; w0 < Wl; w0 += KC, buf ^= 1) {
-		const bool more = w0 + KC < Wl;
+	for(int w0 = 0; w0 < Wl; w0 += KCM, buf ^= 1) {
+		const bool more = w0 + KCM < Wl;
 		if(more) {
 #pragma unroll
-			for(int q = 0; q < 4; ++q) {
-				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-				va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + KC + 2 * wp);
-				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
+			for(int q = 0; q < QS; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e / (KCM / 2), wp = e % (KCM / 2);
+				va[q] = *(const uint4 *) (Ap + (size_t) row * Wp + w0 + KCM + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KCM + 2 * wp);
 			}
 		}
 		const uint2 *Ac = As[buf], *Bc = Bs[buf];
 #pragma unroll MFMA_UNROLL
-		for(int s = 0; s < KC / 2; ++s) {
+		for(int s = 0; s < KCM / 2; ++s) {
 			const int w = 2 * s + h;   // this lane's word: its half of the step's 64 positions
 			uint2 a[2], b[2];
 #pragma unroll
@@ -323,8 +332,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma(const uint2 *__restrict__ P
 		if(more) {
 			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
 #pragma unroll
-			for(int q = 0; q < 4; ++q) {
-				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+			for(int q = 0; q < QS; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e / (KCM / 2), wp = e % (KCM / 2);
 				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
 				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
 				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
@@ -368,8 +377,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restric
                                                           const long long *__restrict__ pfx, int npanels, long long t0,
                                                           long long items, double nFactor, double bs,
                                                           typename Elem<ET>::T *__restrict__ Dloc, int rank, int world) {
-	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
-	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KCM * RS];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KCM * RS];
 	// tile t of the rank's list: panel I = last with pfx[I] <= t, J = t - pfx[I]
 	const long long t = t0 + xcd_tile(blockIdx.x, items);
 	int lo = 0, hi = npanels - 1;
@@ -394,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restric
 #pragma unroll
 		for(int c = 0; c < 8; ++c) acc[a][c] = 0;
 	// this thread's staging slots: rows e>>3, word pairs 2*(e&7), e = q*256 + tid
-	uint4 va[4], vb[4];
+	uint4 va[QS], vb[QS];
 #pragma unroll
 	for(int q = 0; q < 4; ++q) {
 		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
@@ -444,8 +453,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restric
 		if(more) {
 			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
 #pragma unroll
-			for(int q = 0; q < 4; ++q) {
-				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
+			for(int q = 0; q < QS; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e / (KCM / 2), wp = e % (KCM / 2);
 				An[(2 * wp) * RS + row] = make_uint2(va[q].x, va[q].y);
 				An[(2 * wp + 1) * RS + row] = make_uint2(va[q].z, va[q].w);
 				Bn[(2 * wp) * RS + row] = make_uint2(vb[q].x, vb[q].y);
