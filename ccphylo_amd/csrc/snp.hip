@@ -656,24 +656,49 @@ __device__ __forceinline__ void pair_store(typename Elem<ET>::T *D, typename Ele
 // (uint4 {hi, lo, m, 0} per word): double-buffered KCP-word chunks of both
 // 128-row panels, XCD-contiguous tile order, and split-K over word slices when
 // the tiles do not fill the chip (exact u32 atomics of dist and n, then
-// k_snp_pair_finish applies the A7 epilogue).
-template <int ET, bool SPLIT>
+// k_snp_pair_finish applies the A7 epilogue).  BAND: one rank of the
+// row-sharded layout, as k_snp_tile_band (A panel = the rank's owned rows,
+// tile t of the rank's list found in pfx, rows stored at Shard::off(i), no
+// split-K, no N).
+template <int ET, bool SPLIT, bool BAND = false>
 __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
                                                           long long items, int S, int Wk, unsigned norm,
                                                           unsigned minLength, double bs,
                                                           typename Elem<ET>::T *__restrict__ D,
                                                           typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
                                                           long long rowEnd, unsigned *__restrict__ cd,
-                                                          unsigned *__restrict__ cn, long long cbase) {
+                                                          unsigned *__restrict__ cn, long long cbase,
+                                                          const long long *__restrict__ pfx = nullptr, int npanels = 0,
+                                                          int rank = 0, int world = 1) {
 	__shared__ __attribute__((aligned(16))) uint4 As[2][KCP * RSP];
 	__shared__ __attribute__((aligned(16))) uint4 Bs[2][KCP * RSP];
 	int I, J;
 	const long long item = t0 + xcd_tile(blockIdx.x, items);
-	tile_ij(item / S, I, J);
-	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	if(BAND) {
+		int lo = 0, hi = npanels - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if(pfx[mid] <= item) lo = mid; else hi = mid - 1;
+		}
+		I = lo;
+		J = (int) (item - pfx[lo]);
+	} else {
+		tile_ij(item / S, I, J);
+	}
+	// global row of A-panel row l (band: the rank's owned row I*TILE + l; rows
+	// past n read row 0)
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE + l;
+		if(!BAND) return L;
+		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const int wb = BAND ? 0 : (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
 	const int Wl = we - wb;   // a multiple of KCP
 	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-	const uint4 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint4 *Aq[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) Aq[q] = P + (size_t) arow((q * 256 + threadIdx.x) >> 3) * Wp + wb;
 	const uint4 *Bp = P + (size_t) J * TILE * Wp + wb;
 	uint32_t ad[8][8], an[8][8];
 #pragma unroll
@@ -687,7 +712,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 #pragma unroll
 	for(int q = 0; q < 4; ++q) {
 		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-		va[q] = Ap[(size_t) row * Wp + wp];
+		va[q] = Aq[q][wp];
 		vb[q] = Bp[(size_t) row * Wp + wp];
 	}
 #pragma unroll
@@ -704,7 +729,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
 				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-				va[q] = Ap[(size_t) row * Wp + w0 + KCP + wp];
+				va[q] = Aq[q][w0 + KCP + wp];
 				vb[q] = Bp[(size_t) row * Wp + w0 + KCP + wp];
 			}
 		}
@@ -742,9 +767,18 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 	}
 #pragma unroll
 	for(int a = 0; a < 8; ++a) {
-		long long i = (long long) I * TILE + 2 * ty + 32 * (a >> 1) + (a & 1);
-		if(i >= n || i < rowBegin || i >= rowEnd) continue;
-		long long base = tri(i);
+		const int l = 2 * ty + 32 * (a >> 1) + (a & 1);
+		long long i = (long long) I * TILE + l;
+		long long base;
+		if(BAND) {
+			const long long lb = i / SB;
+			i = (lb * world + rank) * SB + (i - lb * SB);
+			if(i >= n) continue;
+			base = Shard{rank, world}.off(i);
+		} else {
+			if(i >= n || i < rowBegin || i >= rowEnd) continue;
+			base = tri(i);
+		}
 #pragma unroll
 		for(int c = 0; c < 8; ++c) {
 			long long j = (long long) J * TILE + 2 * tx + 32 * (c >> 1) + (c & 1);
@@ -1215,6 +1249,30 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 		const long long owned = (nb - 1 - rank) / world + 1, last = (owned - 1) * world + rank;
 		nloc = (owned - 1) * SB + (n - last * SB < SB ? n - last * SB : SB);
 	}
+	if(a->pair && a->proxi) {
+		// maskProxi pairs: an owned band's rows are contiguous in both the full
+		// LT and the rank's buffer with the same relative offsets, so each run of
+		// consecutive owned bands is k_snp_pair_proxi over its LT range with D
+		// shifted by off(first row) - tri(first row)
+		const int W32 = (a->len + 31) / 32;
+		const Shard sh{rank, world};
+		for(long long g = rank; g < nb;) {
+			long long g2 = g;
+			while(world == 1 && g2 + 1 < nb) ++g2;   // world 1 owns every band
+			const long long r0 = g * SB, r1 = (g2 + 1) * SB < n ? (g2 + 1) * SB : n;
+			const long long f0 = tri(r0), f1 = tri(r1), gr = cdivll(f1 - f0, 4);
+			T *Dg = (T *) D + (sh.off(r0) - f0);
+			if(f1 > f0) {
+				k_snp_pair_proxi<ET><<<(unsigned) (gr < 16384 ? gr : 16384), 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, W32, a->len, (int) a->proxi, f0, f1, a->norm, a->minLength,
+				    a->byteScale, Dg, (T *) NULL);
+				CCG_CHECK(hipGetLastError());
+			}
+			g = g2 + world;
+		}
+		CCG_CHECK(hipStreamSynchronize(ctx->stream));
+		return CCG_OK;
+	}
 	// tiles per panel (column tiles with a cell j < i), prefix-summed so that a
 	// launch spans many panels and fills the chip
 	const int npanels = (int) cdivll(nloc, TILE);
@@ -1234,7 +1292,11 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	const bool use_mfma_b = (mf ? atoi(mf) : 1) && Wp < MFMA_KMAX;
 	for(long long t = 0; t < total; t += batch) {
 		const long long items = total - t < batch ? total - t : batch;
-		if(use_mfma_b)
+		if(a->pair)   // fsacmpair per cell (VALU pair tiles in the band form)
+			k_snp_tile_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+			    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+			    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
+		else if(use_mfma_b)
 			k_snp_mfma_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
 			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
 			                                                             rank, world);
@@ -1257,7 +1319,6 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 
 int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
 	if(!a || world < 1 || rank < 0 || rank >= world) return CCG_EINVAL;
-	if(a->pair) return CCG_EUNSUP;
 	if(a->row_begin || a->row_end) return CCG_EINVAL;
 	return snp_run(ctx, a, Dloc, NULL, inc_out, rank, world);
 }

@@ -603,10 +603,6 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline shards nj and dnj.\n", tmethod);
 		return 1;
 	}
-	if(flag & 2) {
-		fprintf(stderr, "ccphylo_amd: --tree needs the non-pair distances (-f without 2).\n");
-		return 1;
-	}
 	FILE *tout = (treename[0] == '-' && treename[1] == 0) ? stdout : fopen(treename, "wb");
 	if(!tout) {
 		fprintf(stderr, "Error: %d (%s)\n", errno, strerror(errno));
@@ -628,7 +624,7 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 		fprintf(stderr, "ccphylo_amd: --tree needs at least 3 included sequences (%d).\n", n);
 		return 1;
 	}
-	fprintf(stderr, "# %d / %d bases included in distance matrix.\n", ccq_npos(M->incs, M->len), M->len);
+	if(!M->pair) fprintf(stderr, "# %d / %d bases included in distance matrix.\n", ccq_npos(M->incs, M->len), M->len);
 	ccg_snp_args sa;
 	memset(&sa, 0, sizeof(sa));
 	sa.n = n;
@@ -636,7 +632,8 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 	sa.stride = M->W;
 	sa.seqs = M->seqs;
 	sa.incs = M->incs;
-	sa.pair = 0;
+	sa.pair = M->pair;   /* -f 2: per-taxon masks, fsacmpair per cell (and -P maskProxi) */
+	sa.proxi = M->pair ? proxi : 0;
 	sa.norm = norm;
 	sa.minLength = M->minLength;
 	sa.etype = et;

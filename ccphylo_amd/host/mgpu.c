@@ -151,7 +151,7 @@ static void *rank_main(void *p) {
 	} else {
 		/* dist into the rank's bands, then the tree on them, all in HBM */
 		const ccg_snp_args *a = j->sa;
-		const size_t sbytes = (size_t) a->n * a->stride * sizeof(uint64_t), ibytes = (size_t) a->stride * 4;
+		const size_t sbytes = (size_t) a->n * a->stride * sizeof(uint64_t), ibytes = (size_t) a->stride * 4 * (a->pair ? a->n : 1);
 		const int64_t elems = ccg_shard_elems(a->n, j->rank, c->gpus);
 		void *dseq = NULL, *dinc = NULL, *dloc = NULL;
 		ccg_snp_args da = *a;

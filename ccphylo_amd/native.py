@@ -430,10 +430,12 @@ class Device:
 
 
     def snp_ltd_shard_dev(self, seqs_ptr, incs_ptr, n, length, stride, Dloc_ptr, rank, world, norm=0, etype=8,
-                          byte_scale=1.0):
+                          byte_scale=1.0, pair=False, min_length=1, proxi=0):
         """ccg_snp_ltd_shard_dev: the rank's rows of the band layout, straight
-        into its shard buffer (device pointers).  Returns getNpos(mask)."""
-        a = SnpArgs(n, length, stride, seqs_ptr, incs_ptr, 0, norm, 1, 0, etype, byte_scale, 0, 0)
+        into its shard buffer (device pointers).  Returns getNpos(mask) (0 in
+        pair mode, where incs holds one mask per taxon)."""
+        a = SnpArgs(n, length, stride, seqs_ptr, incs_ptr, int(pair), norm, min_length, proxi if pair else 0, etype,
+                    byte_scale, 0, 0)
         inc = C.c_int(0)
         self._check(self.lib.ccg_snp_ltd_shard_dev(self.h, C.byref(a), rank, world, C.c_void_p(Dloc_ptr),
                                                    C.byref(inc)), "ccg_snp_ltd_shard_dev")

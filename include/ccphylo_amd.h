@@ -251,11 +251,12 @@ int ccg_tree_shard(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, c
                    ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
 
 /* dist straight into one rank's shard ("dist writes the
- * shards that DNJ consumes in place"): non-pair ccg_snp_ltd_dev semantics
+ * shards that DNJ consumes in place"): ccg_snp_ltd_dev semantics
  * (a->row_begin = a->row_end = 0), but only the rank's owned rows are
  * computed, stored as ccg_tree_shard_dev reads them (ccg_shard_row_offset);
  * Dloc_dev holds ccg_shard_elems(n, rank, world) elements.  seqs / incs are
- * device pointers holding every taxon.  CCG_EUNSUP for pair mode. */
+ * device pointers holding every taxon.  Pair mode (a->pair, incs = one mask
+ * per taxon, -P via a->proxi) stores D only (cmpairFsaThrd semantics). */
 int ccg_snp_ltd_shard_dev(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc_dev, int *inc_out);
 
 /* ------------------------------------------------------------------ */

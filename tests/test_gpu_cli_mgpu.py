@@ -101,3 +101,19 @@ def test_cli_dist_tree_fused_large(tmp_path):
     out = tmp_path / "t.nwk"
     cli(["dist", "-i", str(src), "--tree", str(out), "--gpus", "3", "--transport", "host"])
     assert out.read_bytes() == two_step
+
+
+@pytest.mark.parametrize("msa,extra", [("msa64.fsa", ["-f", "3"]), ("msa_odd.fsa", ["-f", "3", "-P", "2"]),
+                                       ("msa_word.fsa", ["-f", "3"]), ("msa64.fsa", ["-f", "3", "-P", "10"])])
+@pytest.mark.parametrize("gpus,transport", [(1, "rccl"), (3, "host")])
+def test_cli_dist_tree_fused_pair(tmp_path, msa, extra, gpus, transport):
+    """Pair-mode distances (-f 2: cmpairFsaThrd, fsacmp.c:587; -P maskProxi)
+    written into the rank bands: the same Newick as `dist -f 3 | tree`."""
+    src = os.path.join(GOLDEN, msa)
+    phy = tmp_path / "d.phy"
+    with open(phy, "wb") as f:
+        f.write(cli(["dist", "-i", src] + extra))
+    two_step = cli(["tree", "-i", str(phy)])
+    out = tmp_path / "t.nwk"
+    cli(["dist", "-i", src, "--tree", str(out), "--gpus", str(gpus), "--transport", transport] + extra)
+    assert out.read_bytes() == two_step

@@ -262,3 +262,40 @@ def test_dist_shard_to_tree_in_place(dev):
     for p in (ps, pi, pd):
         dev.free(p)
     _same(got, ref)
+
+
+@pytest.mark.parametrize("n,L,et,proxi", [(300, 4000, 8, 0), (517, 2049, 4, 0), (129, 1000, 2, 0), (260, 3000, 8, 20),
+                                          (75, 700, 4, 5)])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_dist_shard_layout_pair(dev, n, L, et, proxi, world):
+    """Pair mode (cmpairFsaThrd, fsacmp.c:587; -P: maskProxi fsacmp.c:355)
+    into the band shards: each rank's buffer equals the band extract of the
+    full pair-mode LT (itself checked against the oracle and goldens)."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    seqs, inc1, W = _rand_msa(n, L, 7 * n + world + proxi)
+    rng = np.random.default_rng(n + proxi)
+    incs = np.tile(inc1, (n, 1))
+    drop = rng.random((n, W, 32)) < 0.1        # per-taxon exclusions
+    bits = (drop.astype(np.uint64) << np.arange(31, -1, -1, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
+    incs &= ~bits
+    ml = int(0.8 * L)
+    dt = cg.ETYPES[et]
+    full, _, _ = dev.snp_ltd(seqs, incs, n, L, pair=True, min_length=ml, proxi=proxi, etype=et, byte_scale=2.0)
+    ps, pi = dev.malloc(seqs.nbytes), dev.malloc(incs.nbytes)
+    dev.h2d(ps, seqs)
+    dev.h2d(pi, incs)
+    try:
+        for rank in range(world):
+            m = nt.shard_elems(n, rank, world)
+            pd = dev.malloc(max(m, 1) * et)
+            dev.snp_ltd_shard_dev(ps, pi, n, L, W, pd, rank, world, etype=et, byte_scale=2.0, pair=True,
+                                  min_length=ml, proxi=proxi)
+            got = np.empty(m, dtype=dt)
+            if m:
+                dev.d2h(got, pd)
+            dev.free(pd)
+            assert (got == nt.shard_extract(full, n, rank, world)).all()
+    finally:
+        dev.free(ps)
+        dev.free(pi)
