@@ -820,24 +820,44 @@ __device__ __forceinline__ v8i_t fp4_pair_comp(uint32_t hi, uint32_t lo, const u
 	return v;
 }
 
-template <int ET, bool SPLIT>
+template <int ET, bool SPLIT, bool BAND = false>
 __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
                                                           long long items, int S, int Wk, unsigned norm,
                                                           unsigned minLength, double bs,
                                                           typename Elem<ET>::T *__restrict__ D,
                                                           typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
                                                           long long rowEnd, unsigned *__restrict__ cd,
-                                                          unsigned *__restrict__ cn, long long cbase) {
+                                                          unsigned *__restrict__ cn, long long cbase,
+                                                          const long long *__restrict__ pfx = nullptr, int npanels = 0,
+                                                          int rank = 0, int world = 1) {
 	__shared__ __attribute__((aligned(16))) uint4 As[2][KCP * RSP];
 	__shared__ __attribute__((aligned(16))) uint4 Bs[2][KCP * RSP];
 	int I, J;
 	const long long item = t0 + xcd_tile(blockIdx.x, items);
-	tile_ij(item / S, I, J);
-	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	if(BAND) {   // as k_snp_tile_pair's band form
+		int lo = 0, hi = npanels - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if(pfx[mid] <= item) lo = mid; else hi = mid - 1;
+		}
+		I = lo;
+		J = (int) (item - pfx[lo]);
+	} else {
+		tile_ij(item / S, I, J);
+	}
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE + l;
+		if(!BAND) return L;
+		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const int wb = BAND ? 0 : (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
 	const int Wl = we - wb;   // a multiple of KCP
 	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	const int wr = wid >> 1, wc = wid & 1;
-	const uint4 *Ap = P + (size_t) I * TILE * Wp + wb;
+	const uint4 *Aq[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) Aq[q] = P + (size_t) arow((q * 256 + threadIdx.x) >> 3) * Wp + wb;
 	const uint4 *Bp = P + (size_t) J * TILE * Wp + wb;
 	v16f_t acc[2][2], accn[2][2];
 #pragma unroll
@@ -850,7 +870,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 #pragma unroll
 	for(int q = 0; q < 4; ++q) {
 		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-		va[q] = Ap[(size_t) row * Wp + wp];
+		va[q] = Aq[q][wp];
 		vb[q] = Bp[(size_t) row * Wp + wp];
 	}
 #pragma unroll
@@ -869,7 +889,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
 				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-				va[q] = Ap[(size_t) row * Wp + w0 + KCP + wp];
+				va[q] = Aq[q][w0 + KCP + wp];
 				vb[q] = Bp[(size_t) row * Wp + w0 + KCP + wp];
 			}
 		}
@@ -925,9 +945,17 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 	for(int ta = 0; ta < 2; ++ta) {
 #pragma unroll
 		for(int r = 0; r < 16; ++r) {
-			const long long i = (long long) I * TILE + 64 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
-			if(i >= n || i < rowBegin || i >= rowEnd) continue;
-			const long long base = tri(i);
+			long long i = (long long) I * TILE + 64 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			long long base;
+			if(BAND) {
+				const long long lb = i / SB;
+				i = (lb * world + rank) * SB + (i - lb * SB);
+				if(i >= n) continue;
+				base = Shard{rank, world}.off(i);
+			} else {
+				if(i >= n || i < rowBegin || i >= rowEnd) continue;
+				base = tri(i);
+			}
 #pragma unroll
 			for(int tb = 0; tb < 2; ++tb) {
 				const long long j = (long long) J * TILE + 64 * wc + 32 * tb + l32;
@@ -1292,7 +1320,11 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	const bool use_mfma_b = (mf ? atoi(mf) : 1) && Wp < MFMA_KMAX;
 	for(long long t = 0; t < total; t += batch) {
 		const long long items = total - t < batch ? total - t : batch;
-		if(a->pair)   // fsacmpair per cell (VALU pair tiles in the band form)
+		if(a->pair && use_mfma_b)   // fsacmpair per cell, the pair tiles in the band form
+			k_snp_mfma_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+			    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+			    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
+		else if(a->pair)
 			k_snp_tile_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
 			    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
 			    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);

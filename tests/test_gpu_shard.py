@@ -267,11 +267,14 @@ def test_dist_shard_to_tree_in_place(dev):
 @pytest.mark.parametrize("n,L,et,proxi", [(300, 4000, 8, 0), (517, 2049, 4, 0), (129, 1000, 2, 0), (260, 3000, 8, 20),
                                           (75, 700, 4, 5)])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_dist_shard_layout_pair(dev, n, L, et, proxi, world):
+@pytest.mark.parametrize("mfma", ["1", "0"])
+def test_dist_shard_layout_pair(dev, monkeypatch, n, L, et, proxi, world, mfma):
     """Pair mode (cmpairFsaThrd, fsacmp.c:587; -P: maskProxi fsacmp.c:355)
     into the band shards: each rank's buffer equals the band extract of the
-    full pair-mode LT (itself checked against the oracle and goldens)."""
+    full pair-mode LT (itself checked against the oracle and goldens), with
+    the MFMA (k_snp_mfma_pair) and VALU (k_snp_tile_pair) band forms."""
     import ccphylo_amd as cg
+    monkeypatch.setenv("CCG_DIST_MFMA", mfma)
     from ccphylo_amd import native as nt
     seqs, inc1, W = _rand_msa(n, L, 7 * n + world + proxi)
     rng = np.random.default_rng(n + proxi)
