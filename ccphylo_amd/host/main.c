@@ -648,6 +648,9 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 	int rc = ccq_mgpu_dist_tree(&mc, &sa, &ta, joins, &nj, &fn, &fd, &inc, emsg, sizeof(emsg));
 	if(rc) {
 		fprintf(stderr, "ccphylo_amd: dist --tree failed: %s\n", emsg);
+		if(rc == CCG_EUNSUP)
+			fprintf(stderr, "ccphylo_amd: the matrix has missing entries (pairs below the minimum length); "
+			                "their updateD rules run on one GPU: use `ccphylo dist ... | ccphylo tree`.\n");
 		return 1;
 	}
 	fprintf(stderr, "# Total time used computing distances and tree: %.2f s.\n", (double) (clock() - t0) / 1000000);

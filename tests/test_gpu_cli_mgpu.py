@@ -104,7 +104,7 @@ def test_cli_dist_tree_fused_large(tmp_path):
 
 
 @pytest.mark.parametrize("msa,extra", [("msa64.fsa", ["-f", "3"]), ("msa_odd.fsa", ["-f", "3", "-P", "2"]),
-                                       ("msa_word.fsa", ["-f", "3"]), ("msa64.fsa", ["-f", "3", "-P", "10"])])
+                                       ("msa_word.fsa", ["-f", "3"]), ("msa_crlf.fsa", ["-f", "3", "-P", "100"])])
 @pytest.mark.parametrize("gpus,transport", [(1, "rccl"), (3, "host")])
 def test_cli_dist_tree_fused_pair(tmp_path, msa, extra, gpus, transport):
     """Pair-mode distances (-f 2: cmpairFsaThrd, fsacmp.c:587; -P maskProxi)
@@ -117,3 +117,13 @@ def test_cli_dist_tree_fused_pair(tmp_path, msa, extra, gpus, transport):
     out = tmp_path / "t.nwk"
     cli(["dist", "-i", src, "--tree", str(out), "--gpus", str(gpus), "--transport", transport] + extra)
     assert out.read_bytes() == two_step
+
+
+def test_cli_dist_tree_fused_pair_missing(tmp_path):
+    """msa64 with -f 3 -P 10 leaves pairs below the minimum length (-1
+    entries): the sharded tree refuses them (CCG_EUNSUP) and says how to run
+    them on one GPU, rather than building a different tree."""
+    import ccphylo_amd as cg
+    p = subprocess.run([cg.CLI_PATH, "dist", "-i", os.path.join(GOLDEN, "msa64.fsa"), "-f", "3", "-P", "10", "--tree",
+                        str(tmp_path / "t.nwk")], capture_output=True, timeout=120)
+    assert p.returncode == 1 and b"missing entries" in p.stderr
