@@ -104,7 +104,7 @@ def test_cli_dist_tree_fused_large(tmp_path):
 
 
 @pytest.mark.parametrize("msa,extra", [("msa64.fsa", ["-f", "3"]), ("msa_odd.fsa", ["-f", "3", "-P", "2"]),
-                                       ("msa_word.fsa", ["-f", "3"]), ("msa_crlf.fsa", ["-f", "3", "-P", "100"])])
+                                       ("msa_word.fsa", ["-f", "3"]), ("msa_crlf.fsa", ["-f", "3"])])
 @pytest.mark.parametrize("gpus,transport", [(1, "rccl"), (3, "host")])
 def test_cli_dist_tree_fused_pair(tmp_path, msa, extra, gpus, transport):
     """Pair-mode distances (-f 2: cmpairFsaThrd, fsacmp.c:587; -P maskProxi)
