@@ -659,7 +659,7 @@ __device__ __forceinline__ void pair_store(typename Elem<ET>::T *D, typename Ele
 // k_snp_pair_finish applies the A7 epilogue).  BAND: one rank of the
 // row-sharded layout, as k_snp_tile_band (A panel = the rank's owned rows,
 // tile t of the rank's list found in pfx, rows stored at Shard::off(i), no
-// split-K, no N).
+// N); split-K counts are indexed by the rank's local element.
 template <int ET, bool SPLIT, bool BAND = false>
 __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
                                                           long long items, int S, int Wk, unsigned norm,
@@ -675,13 +675,14 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 	int I, J;
 	const long long item = t0 + xcd_tile(blockIdx.x, items);
 	if(BAND) {
+		const long long tile = item / S;
 		int lo = 0, hi = npanels - 1;
 		while(lo < hi) {
 			const int mid = (lo + hi + 1) >> 1;
-			if(pfx[mid] <= item) lo = mid; else hi = mid - 1;
+			if(pfx[mid] <= tile) lo = mid; else hi = mid - 1;
 		}
 		I = lo;
-		J = (int) (item - pfx[lo]);
+		J = (int) (tile - pfx[lo]);
 	} else {
 		tile_ij(item / S, I, J);
 	}
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_pair(const uint4 *__restric
 		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
 		return r < n ? r : 0;
 	};
-	const int wb = BAND ? 0 : (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
 	const int Wl = we - wb;   // a multiple of KCP
 	const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
 	const uint4 *Aq[4];
@@ -835,13 +836,14 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 	int I, J;
 	const long long item = t0 + xcd_tile(blockIdx.x, items);
 	if(BAND) {   // as k_snp_tile_pair's band form
+		const long long tile = item / S;
 		int lo = 0, hi = npanels - 1;
 		while(lo < hi) {
 			const int mid = (lo + hi + 1) >> 1;
-			if(pfx[mid] <= item) lo = mid; else hi = mid - 1;
+			if(pfx[mid] <= tile) lo = mid; else hi = mid - 1;
 		}
 		I = lo;
-		J = (int) (item - pfx[lo]);
+		J = (int) (tile - pfx[lo]);
 	} else {
 		tile_ij(item / S, I, J);
 	}
@@ -851,7 +853,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
 		return r < n ? r : 0;
 	};
-	const int wb = BAND ? 0 : (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
+	const int wb = (int) (item % S) * Wk, we = wb + Wk < Wp ? wb + Wk : Wp;
 	const int Wl = we - wb;   // a multiple of KCP
 	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	const int wr = wid >> 1, wc = wid & 1;
@@ -1318,17 +1320,64 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	// the MFMA form unless disabled or a row's words exceed its exact f32 range
 	const char *mf = getenv("CCG_DIST_MFMA");
 	const bool use_mfma_b = (mf ? atoi(mf) : 1) && Wp < MFMA_KMAX;
+	if(a->pair) {
+		// fsacmpair per cell, the pair tiles in the band form; split-K over word
+		// slices (as snp_launch) when the rank's tiles do not fill the chip, the
+		// u32 counts indexed by local element and finished in place
+		hipDeviceProp_t prop;
+		CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+		const long long slots = 2LL * prop.multiProcessorCount;
+		const int chunks = Wp / KCP;
+		int S = 1;
+		if(total < 16 * slots) {
+			S = (int) cdivll(16 * slots, total);
+			if(S > chunks / 4) S = chunks / 4;
+			if(S < 1) S = 1;
+		}
+		const int Wk = (int) cdivll(chunks, S) * KCP;
+		S = (int) cdivll(Wp, Wk);
+		const bool pm = (mf ? atoi(mf) : 1) && Wk < MFMA_KMAX;
+		const long long elems = ccg_shard_elems(n, rank, world);
+		unsigned *cd = NULL, *cn = NULL;
+		if(S > 1) {
+			CCG_CHECK(hipMalloc(&cd, (size_t) elems * 2 * sizeof(unsigned)));
+			cn = cd + elems;
+			CCG_CHECK(hipMemsetAsync(cd, 0, (size_t) elems * 2 * sizeof(unsigned), ctx->stream));
+		}
+		for(long long t = 0; t < total * S; t += batch) {
+			const long long items = total * S - t < batch ? total * S - t : batch;
+			if(pm && S > 1)
+				k_snp_mfma_pair<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, (int) n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) NULL, 0, n, cd, cn, 0, d_pfx, npanels, rank, world);
+			else if(pm)
+				k_snp_mfma_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
+			else if(S > 1)
+				k_snp_tile_pair<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, (int) n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) NULL, 0, n, cd, cn, 0, d_pfx, npanels, rank, world);
+			else
+				k_snp_tile_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
+				    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
+			CCG_CHECK(hipGetLastError());
+		}
+		if(S > 1) {
+			const long long g = cdivll(elems, 256);
+			k_snp_pair_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(
+			    cd, cn, 0, elems, a->norm, a->minLength, a->byteScale, (T *) D, (T *) NULL);
+			CCG_CHECK(hipGetLastError());
+		}
+		CCG_CHECK(hipStreamSynchronize(ctx->stream));
+		if(cd) CCG_CHECK(hipFree(cd));
+		CCG_CHECK(hipFree(d_pfx));
+		return CCG_OK;
+	}
 	for(long long t = 0; t < total; t += batch) {
 		const long long items = total - t < batch ? total - t : batch;
-		if(a->pair && use_mfma_b)   // fsacmpair per cell, the pair tiles in the band form
-			k_snp_mfma_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
-			    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
-			    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
-		else if(a->pair)
-			k_snp_tile_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
-			    (const uint4 *) planes, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D,
-			    (T *) NULL, 0, n, NULL, NULL, 0, d_pfx, npanels, rank, world);
-		else if(use_mfma_b)
+		if(use_mfma_b)
 			k_snp_mfma_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
 			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
 			                                                             rank, world);
