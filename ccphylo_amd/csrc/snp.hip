@@ -479,16 +479,21 @@ __global__ __launch_bounds__(256, 2) void k_snp_tile_band(const uint2 *__restric
 }
 
 // k_snp_mfma for one rank of the row-sharded layout (as k_snp_tile_band):
-// A panel = the rank's owned rows, rows stored at Shard::off(i).  No split-K:
-// the host takes this path only while Wp < MFMA_KMAX.
-template <int ET>
+// A panel = the rank's owned rows, rows stored at Shard::off(i).  SPLIT: word
+// slice item % S of Wk (< MFMA_KMAX) words, u32 counts added by local element
+// (k_snp_finish stores them), when the rank's tiles do not fill the chip or a
+// row exceeds the f32-exact slice length.
+template <int ET, bool SPLIT = false>
 __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restrict__ P, int Wp, int n,
                                                           const long long *__restrict__ pfx, int npanels, long long t0,
                                                           long long items, double nFactor, double bs,
-                                                          typename Elem<ET>::T *__restrict__ Dloc, int rank, int world) {
+                                                          typename Elem<ET>::T *__restrict__ Dloc, int rank, int world,
+                                                          int S = 1, int Wk = 0, unsigned *__restrict__ cnt = nullptr) {
 	__shared__ __attribute__((aligned(16))) uint2 As[2][KC * RS];
 	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC * RS];
-	const long long t = t0 + xcd_tile(blockIdx.x, items);
+	const long long item = t0 + xcd_tile(blockIdx.x, items), t = SPLIT ? item / S : item;
+	// SPLIT: word slice item % S of Wk words (counts added into cnt by local element)
+	const int wb = SPLIT ? (int) (item % S) * Wk : 0;
 	int lo = 0, hi = npanels - 1;
 	while(lo < hi) {
 		const int mid = (lo + hi + 1) >> 1;
@@ -500,8 +505,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 		const long long L = (long long) I * TILE + l, lb = L / SB, g = lb * world + rank, r = g * SB + (L - lb * SB);
 		return r < n ? r : 0;
 	};
-	const uint2 *Bp = P + (size_t) J * TILE * Wp;
-	const int Wl = Wp;
+	const uint2 *Bp = P + (size_t) J * TILE * Wp + wb;
+	const int Wl = SPLIT ? (wb + Wk < Wp ? Wk : Wp - wb) : Wp;
 	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 	const int wr = wid >> 1, wc = wid & 1;
 	v16f_t acc[2][2];
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 	for(int q = 0; q < 4; ++q) {
 		const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
 		ar[q] = arow(row);
-		va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + 2 * wp);
+		va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + 2 * wp);
 		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
 	}
 #pragma unroll
@@ -538,7 +543,7 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 #pragma unroll
 			for(int q = 0; q < 4; ++q) {
 				const int e = q * 256 + threadIdx.x, row = e >> 3, wp = e & 7;
-				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + w0 + KC + 2 * wp);
+				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + w0 + KC + 2 * wp);
 				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC + 2 * wp);
 			}
 		}
@@ -595,7 +600,8 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 				const long long j = (long long) J * TILE + 64 * wc + 32 * tb + l32;
 				if(j < i) {
 					const unsigned d = (unsigned) ((L3 - (int) acc[ta][tb][r]) >> 2);
-					Dloc[base + j] = Elem<ET>::put(nFactor * (double) d, 0.5, bs);
+					if(SPLIT) atomicAdd(&cnt[base + j], d);
+					else Dloc[base + j] = Elem<ET>::put(nFactor * (double) d, 0.5, bs);
 				}
 			}
 		}
@@ -1372,6 +1378,52 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 		}
 		CCG_CHECK(hipStreamSynchronize(ctx->stream));
 		if(cd) CCG_CHECK(hipFree(cd));
+		CCG_CHECK(hipFree(d_pfx));
+		return CCG_OK;
+	}
+	if(use_mfma_b || (mf ? atoi(mf) : 1)) {
+		// the MFMA form with snp_launch's split-K over word slices when the
+		// rank's tiles do not fill the chip, or when a row exceeds the f32-exact
+		// slice length; u32 counts by local element, k_snp_finish in place
+		hipDeviceProp_t prop;
+		CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+		const long long slots = 2LL * prop.multiProcessorCount;
+		const int chunks = Wp / KC;
+		int S = 1;
+		if(total < 16 * slots) {
+			S = (int) cdivll(16 * slots, total);
+			if(S > chunks / 4) S = chunks / 4;
+			if(S < 1) S = 1;
+		}
+		int Wk = (int) cdivll(chunks, S) * KC;
+		if(Wk > MFMA_KMAX) Wk = (MFMA_KMAX / KC) * KC;
+		S = (int) cdivll(Wp, Wk);
+		const long long elems = ccg_shard_elems(n, rank, world);
+		unsigned *cnt = NULL;
+		if(S > 1) {
+			CCG_CHECK(hipMalloc(&cnt, (size_t) elems * sizeof(unsigned)));
+			CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) elems * sizeof(unsigned), ctx->stream));
+		}
+		for(long long t = 0; t < total * S; t += batch) {
+			const long long items = total * S - t < batch ? total * S - t : batch;
+			if(S > 1)
+				k_snp_mfma_band<ET, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    (const uint2 *) planes, Wp, (int) n, d_pfx, npanels, t, items, nFactor, a->byteScale, (T *) D, rank,
+				    world, S, Wk, cnt);
+			else
+				k_snp_mfma_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n,
+				                                                             d_pfx, npanels, t, items, nFactor,
+				                                                             a->byteScale, (T *) D, rank, world);
+			CCG_CHECK(hipGetLastError());
+		}
+		if(S > 1) {
+			const long long g = cdivll(elems, 256);
+			k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, 0, 0, elems, nFactor,
+			                                                                                a->byteScale, (T *) D);
+			CCG_CHECK(hipGetLastError());
+		}
+		CCG_CHECK(hipStreamSynchronize(ctx->stream));
+		if(cnt) CCG_CHECK(hipFree(cnt));
 		CCG_CHECK(hipFree(d_pfx));
 		return CCG_OK;
 	}

@@ -215,7 +215,7 @@ def _rand_msa(n, L, seed):
 
 
 @pytest.mark.parametrize("n,L,et,norm", [(300, 4000, 8, 0), (1000, 3000, 4, 0), (517, 2049, 2, 100), (129, 1000, 1, 0),
-                                         (2300, 1500, 8, 1000)])
+                                         (2300, 1500, 8, 1000), (70, 6_000_000, 8, 0)])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_dist_shard_layout(dev, n, L, et, norm, world):
     """ccg_snp_ltd_shard_dev writes each rank's rows exactly where
