@@ -4,8 +4,9 @@
 #include <stdlib.h>
 #include "ccg_internal.h"
 
-int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out);
-int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out);
+int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, bool host_in);
+int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out,
+                           bool host_in);
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
                   double *final_d, int64_t *stats);
 int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel);
@@ -94,14 +95,21 @@ int ccg_snp_ltd_dev(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *in
 	if(!c || !a || !D) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
 	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
-	return ccg_snp_dev_impl(c, a, D, N, inc_out);
+	return ccg_snp_dev_impl(c, a, D, N, inc_out, false);
 }
 
 int ccg_snp_ltd_shard_dev(ccg_ctx *c, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
 	if(!c || !a || !Dloc) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
 	CCG_CHECK(hipDeviceSynchronize());
-	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out);
+	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out, false);
+}
+
+int ccg_snp_ltd_shard(ccg_ctx *c, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
+	if(!c || !a || !Dloc || !a->seqs || !a->incs) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());
+	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out, true);
 }
 
 int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
@@ -109,20 +117,11 @@ int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_ou
 	if(a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
 	size_t n = (size_t) a->n;
-	size_t seq_bytes = n * (size_t) a->stride * 8;
-	size_t inc_bytes = (a->pair ? n : 1) * (size_t) a->stride * 4;
 	size_t lt = n > 1 ? n * (n - 1) / 2 * (size_t) a->etype : 0;
-	void *d_seq = NULL, *d_inc = NULL, *d_D = NULL, *d_N = NULL;
+	void *d_D = NULL, *d_N = NULL;
 	int rc = CCG_OK;
-	ccg_snp_args da = *a;
-	if(hipMalloc(&d_seq, seq_bytes ? seq_bytes : 8) != hipSuccess || hipMalloc(&d_inc, inc_bytes ? inc_bytes : 4) != hipSuccess ||
-	   hipMalloc(&d_D, lt ? lt : 8) != hipSuccess || (N && a->pair && hipMalloc(&d_N, lt ? lt : 8) != hipSuccess)) {
+	if(hipMalloc(&d_D, lt ? lt : 8) != hipSuccess || (N && a->pair && hipMalloc(&d_N, lt ? lt : 8) != hipSuccess)) {
 		rc = CCG_ENOMEM;
-		goto done;
-	}
-	if(hipMemcpyAsync(d_seq, a->seqs, seq_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-	   hipMemcpyAsync(d_inc, a->incs, inc_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-		rc = CCG_EHIP;
 		goto done;
 	}
 	// untouched cells (outside a row range) keep the caller's contents
@@ -133,9 +132,8 @@ int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_ou
 			goto done;
 		}
 	}
-	da.seqs = (const uint64_t *) d_seq;
-	da.incs = (const uint32_t *) d_inc;
-	rc = ccg_snp_dev_impl(c, &da, d_D, d_N, inc_out);
+	// the packed sequences stream from host memory into the bit planes
+	rc = ccg_snp_dev_impl(c, a, d_D, d_N, inc_out, true);
 	if(rc == CCG_OK && lt) {
 		if(hipMemcpyAsync(D, d_D, lt, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
 		   (d_N && hipMemcpyAsync(N, d_N, lt, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
@@ -145,8 +143,6 @@ int ccg_snp_ltd(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_ou
 	}
 done:
 	hipStreamSynchronize(c->stream);
-	if(d_seq) hipFree(d_seq);
-	if(d_inc) hipFree(d_inc);
 	if(d_D) hipFree(d_D);
 	if(d_N) hipFree(d_N);
 	return rc;

@@ -1323,9 +1323,9 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	CCG_CHECK(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
 	                         ctx->stream));
 	const long long total = pfx[npanels], batch = 1 << 16;
-	// the MFMA form unless disabled or a row's words exceed its exact f32 range
+	// the MFMA form unless disabled (CCG_DIST_MFMA=0); a row longer than the
+	// f32-exact slice is split over word slices
 	const char *mf = getenv("CCG_DIST_MFMA");
-	const bool use_mfma_b = (mf ? atoi(mf) : 1) && Wp < MFMA_KMAX;
 	if(a->pair) {
 		// fsacmpair per cell, the pair tiles in the band form; split-K over word
 		// slices (as snp_launch) when the rank's tiles do not fill the chip, the
@@ -1381,7 +1381,7 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 		CCG_CHECK(hipFree(d_pfx));
 		return CCG_OK;
 	}
-	if(use_mfma_b || (mf ? atoi(mf) : 1)) {
+	if(mf ? atoi(mf) : 1) {
 		// the MFMA form with snp_launch's split-K over word slices when the
 		// rank's tiles do not fill the chip, or when a row exceeds the f32-exact
 		// slice length; u32 counts by local element, k_snp_finish in place
@@ -1429,12 +1429,7 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	}
 	for(long long t = 0; t < total; t += batch) {
 		const long long items = total - t < batch ? total - t : batch;
-		if(use_mfma_b)
-			k_snp_mfma_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
-			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
-			                                                             rank, world);
-		else
-			k_snp_tile_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
+		k_snp_tile_band<ET><<<(unsigned) items, 256, 0, ctx->stream>>>((const uint2 *) planes, Wp, (int) n, d_pfx,
 			                                                             npanels, t, items, nFactor, a->byteScale, (T *) D,
 			                                                             rank, world);
 		CCG_CHECK(hipGetLastError());
@@ -1444,23 +1439,83 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	return CCG_OK;
 }
 
-static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world);
+static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world,
+                   bool host_in);
 
-int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
-	return snp_run(ctx, a, D, N, inc_out, 0, 0);
+int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, bool host_in) {
+	return snp_run(ctx, a, D, N, inc_out, 0, 0, host_in);
 }
 
-int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
+int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out,
+                           bool host_in) {
 	if(!a || world < 1 || rank < 0 || rank >= world) return CCG_EINVAL;
 	if(a->row_begin || a->row_end) return CCG_EINVAL;
-	return snp_run(ctx, a, Dloc, NULL, inc_out, rank, world);
+	return snp_run(ctx, a, Dloc, NULL, inc_out, rank, world, host_in);
 }
 
-static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world) {
+// the bit planes of every taxon.  host_in: a->seqs / a->incs are host memory,
+// streamed through a bounded staging buffer, so HBM holds the planes and the
+// LT only (configs[4]: 25 GB of planes beside a 250 GB shard, where a device
+// copy of the packed MSA would add another 25 GB).  *mask = the device copy of
+// the non-pair include mask (k_popsum reads it), or NULL.
+static int snp_planes(ccg_ctx *ctx, const ccg_snp_args *a, int W32, int Wp, void *planes, bool host_in,
+                      uint32_t **mask) {
+	*mask = NULL;
+	if(!host_in) {
+		const long long total = (long long) a->n * Wp, pg = cdivll(total, 256);
+		k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(
+		    a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair, (uint2 *) planes, (uint4 *) planes);
+		CCG_CHECK(hipGetLastError());
+		return CCG_OK;
+	}
+	const size_t row_b = (size_t) a->stride * 8 + (a->pair ? (size_t) a->stride * 4 : 0);
+	long long R = (long long) (((size_t) 256 << 20) / row_b);
+	if(R < 1) R = 1;
+	if(R > a->n) R = a->n;
+	void *stage = NULL;
+	CCG_CHECK(hipMalloc(&stage, (size_t) R * row_b));
+	if(!a->pair) {
+		if(hipMalloc((void **) mask, (size_t) a->stride * 4) != hipSuccess) {
+			hipFree(stage);
+			*mask = NULL;
+			return CCG_ENOMEM;
+		}
+		CCG_CHECK(hipMemcpyAsync(*mask, a->incs, (size_t) a->stride * 4, hipMemcpyHostToDevice, ctx->stream));
+	}
+	uint64_t *sseq = (uint64_t *) stage;
+	uint32_t *sinc = (uint32_t *) ((char *) stage + (size_t) R * a->stride * 8);
+	int rc = CCG_OK;
+	for(long long t0 = 0; t0 < a->n && rc == CCG_OK; t0 += R) {
+		const long long rows = a->n - t0 < R ? a->n - t0 : R;
+		// stream-ordered: the copy into the stage waits for the previous chunk's k_planes
+		if(hipMemcpyAsync(sseq, a->seqs + (size_t) t0 * a->stride, (size_t) rows * a->stride * 8,
+		                  hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+		   (a->pair && hipMemcpyAsync(sinc, a->incs + (size_t) t0 * a->stride, (size_t) rows * a->stride * 4,
+		                              hipMemcpyHostToDevice, ctx->stream) != hipSuccess)) {
+			rc = CCG_EHIP;
+			break;
+		}
+		const long long pg = cdivll(rows * Wp, 256);
+		k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(
+		    sseq, a->pair ? sinc : *mask, (int) rows, a->stride, W32, Wp, a->pair, (uint2 *) planes + t0 * Wp,
+		    (uint4 *) planes + t0 * Wp);
+		if(hipGetLastError() != hipSuccess) rc = CCG_EHIP;
+	}
+	hipStreamSynchronize(ctx->stream);
+	hipFree(stage);
+	return rc;
+}
+
+static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, int rank, int world,
+                   bool host_in) {
 	if(!a || a->n < 0 || a->len <= 0 || a->stride < (a->len + 31) / 32) return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if(a->n < 2) {
-		if(inc_out && !a->pair) {
+		if(inc_out && !a->pair && host_in) {
+			int s = 0;
+			for(int w = 0; w < (a->len + 31) / 32; ++w) s += __builtin_popcount(a->incs[w]);
+			*inc_out = s;
+		} else if(inc_out && !a->pair) {
 			int *d_inc;
 			CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
 			k_popsum<<<1, 256, 0, ctx->stream>>>(a->incs, (a->len + 31) / 32, d_inc);
@@ -1480,17 +1535,20 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	CCG_CHECK(hipMalloc(&planes, (size_t) npad * Wp * esz));
 	CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
 	CCG_CHECK(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream));
-	long long total = (long long) a->n * Wp;
-	const long long pg = cdivll(total, 256);
-	k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair,
-	                                                                (uint2 *) planes, (uint4 *) planes);
-	CCG_CHECK(hipGetLastError());
+	uint32_t *mask = NULL;
+	if(int prc = snp_planes(ctx, a, W32, Wp, planes, host_in, &mask)) {
+		hipFree(planes);
+		hipFree(d_inc);
+		hipFree(mask);
+		return prc;
+	}
 	int inc = 0;
 	if(!a->pair) {
-		k_popsum<<<1, 1024, 0, ctx->stream>>>(a->incs, W32, d_inc);
+		k_popsum<<<1, 1024, 0, ctx->stream>>>(mask ? mask : a->incs, W32, d_inc);
 		CCG_CHECK(hipMemcpyAsync(&inc, d_inc, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
 		CCG_CHECK(hipStreamSynchronize(ctx->stream));
 	}
+	if(mask) CCG_CHECK(hipFree(mask));
 	double nFactor = 1.0;
 	if(!a->pair && a->norm) {
 		nFactor = a->norm;
@@ -1524,4 +1582,58 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	CCG_CHECK(hipFree(d_inc));
 	if(inc_out) *inc_out = inc;
 	return rc;
+}
+
+// ------------------------------------------------------------------ Phylip round trip
+// `ccphylo dist -W ... | ccphylo tree` passes each cell through text: printphy
+// (phy.c:59-123) writes an integral d as "%d" and any other as "%.*f" with -x
+// digits, and loadPhy (phy.c:469) reads it back with strtod (then the cast to
+// the matrix type).  The fused `dist --tree` stores the same values in place:
+// K = round-half-even(d * 10^p) exactly (d * 10^p = hi + lo without error),
+// then K / 10^p is one correctly rounded division of exact operands, which is
+// strtod's result for the printed decimal.  Cells whose product reaches 2^52
+// (more digits than a double carries) set *bad; the caller refuses them.
+template <typename T>
+__global__ void k_round_decimal(T *__restrict__ D, long long elems, double P, int *__restrict__ bad) {
+	for(long long e = (long long) blockIdx.x * blockDim.x + threadIdx.x; e < elems;
+	    e += (long long) gridDim.x * blockDim.x) {
+		const double x = (double) D[e];
+		if(x == trunc(x)) continue;   // "%d" or the integer's exact digits
+		const double hi = x * P, lo = fma(x, P, -hi);
+		if(!(fabs(hi) < 4503599627370496.0)) {
+			atomicOr(bad, 1);
+			continue;
+		}
+		double K = rint(hi);   // half-even on hi; the exact tie needs lo == 0
+		const double d = hi - K;
+		if(d == 0.5 && lo > 0) K += 1.0;
+		else if(d == -0.5 && lo < 0) K -= 1.0;
+		D[e] = (T) (K / P);
+	}
+}
+
+extern "C" int ccg_round_decimal_dev(ccg_ctx *ctx, void *D, int64_t elems, int etype, int precision) {
+	if(!ctx || (!D && elems) || elems < 0 || precision < 0 || precision > 22) return CCG_EINVAL;
+	if(etype != 8 && etype != 4) return CCG_EUNSUP;
+	CCG_CHECK(hipSetDevice(ctx->device));
+	CCG_CHECK(hipDeviceSynchronize());
+	if(!elems) return CCG_OK;
+	double P = 1.0;
+	for(int k = 0; k < precision; ++k) P *= 10.0;   // exact up to 10^22
+	int *d_bad = NULL, bad = 0;
+	CCG_CHECK(hipMalloc(&d_bad, sizeof(int)));
+	CCG_CHECK(hipMemsetAsync(d_bad, 0, sizeof(int), ctx->stream));
+	const long long g = cdivll(elems, 256);
+	const unsigned grid = (unsigned) (g < 65536 ? g : 65536);
+	if(etype == 8) k_round_decimal<double><<<grid, 256, 0, ctx->stream>>>((double *) D, elems, P, d_bad);
+	else k_round_decimal<float><<<grid, 256, 0, ctx->stream>>>((float *) D, elems, P, d_bad);
+	CCG_CHECK(hipGetLastError());
+	CCG_CHECK(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+	CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	CCG_CHECK(hipFree(d_bad));
+	if(bad) {
+		ccg_set_last_msg("ccg_round_decimal_dev: a cell needs more than 15 significant digits at this precision");
+		return CCG_EUNSUP;
+	}
+	return CCG_OK;
 }

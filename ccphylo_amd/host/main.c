@@ -259,12 +259,12 @@ static int main_tree(int argc, char **argv) {
 			ccg_tree_args ta = {n, et, bs, m, flag, !fast, 0, 0};
 			int nj = 0, fn = 0;
 			double fd = 0;
-			int64_t st[6 + 2 * CCG_NKSTAT];
+			int64_t st[8 + 2 * CCG_NKSTAT];
 			memset(st, 0, sizeof(st));
 			int rc;
 			if(gpus) {
 				/* one matrix over G ranks, one thread per rank (host/mgpu.c) */
-				ccq_mgpu mc = {gpus, device, transport};
+				ccq_mgpu mc = {gpus, device, transport, -1};
 				char emsg[320] = "";
 				rc = ccq_mgpu_tree(&mc, D->mat, &ta, joins, &nj, &fn, &fd, emsg, sizeof(emsg));
 				if(rc) {
@@ -326,7 +326,7 @@ static int dist_help(FILE *out) {
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree", "Also build the tree in HBM, Newick to FILE", "off");
-	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_method", "nj / dnj for --tree", "dnj");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_method", "nj / dnj (/ hnj, 1 GPU) for --tree", "dnj");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_flag", "tree -f flags for --tree", "0");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "gpus", "Shard --tree over G GPUs", "1");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "transport", "rccl / host collectives for --gpus", "rccl");
@@ -587,20 +587,29 @@ static int dist_fsa_files(char **files, int nfiles, const char *tmpl, const char
 }
 
 /* `dist --tree FILE`: the MSA's distances and the tree in HBM, without the
- * Phylip text (configs[4]: a 1e6-taxon matrix has no text form).  The LT is
- * written straight into the ranks' row bands (ccg_snp_ltd_shard_dev) and the
- * sharded tree consumes it there; the Newick equals `ccphylo dist | ccphylo
- * tree` for the same MSA (integer SNP counts print exactly; taxon names as
- * that pipeline's reader holds them, ccq_names_set).  -W normalised
- * distances are used unrounded (the pipeline rounds them to -x digits). */
+ * Phylip text (configs[4]: a 1e6-taxon matrix has no text form).  With
+ * --gpus G > 1 the LT is written straight into the ranks' row bands
+ * (ccg_snp_ltd_shard) and the sharded tree consumes it there; with one GPU
+ * the single-GPU engine runs on the full LT.  The Newick equals `ccphylo
+ * dist | ccphylo tree` for the same MSA: integer SNP counts print exactly,
+ * -W normalised distances are rounded to -x digits as the text would round
+ * them (ccg_round_decimal_dev), taxon names as that pipeline's reader holds
+ * them (ccq_names_set). */
 static int dist_tree(const char *in, const char *treename, const char *tmethod, int tflag, unsigned flag,
                      unsigned norm, unsigned minLength, double minCov, unsigned proxi, int precision, int et,
                      double bs, unsigned threads, int device, int gpus, int transport, int fast) {
 	int m;
 	if(!strcmp(tmethod, "dnj")) m = CCG_TREE_DNJ;
 	else if(!strcmp(tmethod, "nj")) m = CCG_TREE_NJ;
+	else if(!strcmp(tmethod, "hnj") && gpus <= 1) m = CCG_TREE_HNJ;
 	else {
-		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline shards nj and dnj.\n", tmethod);
+		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline runs nj and dnj (hnj with --gpus 1).\n",
+		        tmethod);
+		return 1;
+	}
+	if(norm && (et == 2 || et == 1)) {
+		/* the pipeline's text round trip of -W cells through dtouc is not restated */
+		fprintf(stderr, "ccphylo_amd: -W with -s / -b and --tree: use `ccphylo dist ... | ccphylo tree`.\n");
 		return 1;
 	}
 	FILE *tout = (treename[0] == '-' && treename[1] == 0) ? stdout : fopen(treename, "wb");
@@ -642,15 +651,37 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 	ccg_join *joins = malloc((size_t) n * sizeof(ccg_join));
 	int nj = 0, fn = 0, inc = 0;
 	double fd = 0;
-	ccq_mgpu mc = {gpus > 0 ? gpus : 1, device, transport};
+	/* -W distances are not integral: the Phylip text of `dist | tree` rounds
+	 * them to -x digits, and so does this path (ccg_round_decimal_dev) */
+	const int rp = norm ? precision : -1;
 	char emsg[320] = "";
 	clock_t t0 = clock();
-	int rc = ccq_mgpu_dist_tree(&mc, &sa, &ta, joins, &nj, &fn, &fd, &inc, emsg, sizeof(emsg));
-	if(rc) {
-		fprintf(stderr, "ccphylo_amd: dist --tree failed: %s\n", emsg);
+	int rc;
+	if(gpus <= 1) {
+		/* one GPU: the full LT (the world-1 band layout) and the single-GPU
+		 * engine, which also runs the missing-entry rules of updateD
+		 * (nj.c:1021-1030) and -m hnj, exactly as `dist | tree` would */
+		ccg_ctx *ctx = open_gpu(device);
+		void *dD = NULL;
+		const size_t lt = (size_t) n * (size_t) (n - 1) / 2 * (size_t) et;
+		if((rc = ccg_malloc(ctx, &dD, lt))) snprintf(emsg, sizeof(emsg), "LT buffer: %s", ccg_strerror(rc));
+		else if((rc = ccg_snp_ltd_shard(ctx, &sa, 0, 1, dD, &inc)))
+			snprintf(emsg, sizeof(emsg), "ccg_snp_ltd_shard: %s", ccg_strerror(rc));
+		else if(rp >= 0 && (rc = ccg_round_decimal_dev(ctx, dD, (int64_t) n * (n - 1) / 2, et, rp)))
+			snprintf(emsg, sizeof(emsg), "ccg_round_decimal_dev: %s", ccg_strerror(rc));
+		else if((rc = ccg_tree_dev(ctx, &ta, dD, joins, &nj, &fn, &fd, NULL)))
+			snprintf(emsg, sizeof(emsg), "ccg_tree_dev: %s", ccg_strerror(rc));
+		if(dD) ccg_free(ctx, dD);
+		ccg_destroy(ctx);
+	} else {
+		ccq_mgpu mc = {gpus, device, transport, rp};
+		rc = ccq_mgpu_dist_tree(&mc, &sa, &ta, joins, &nj, &fn, &fd, &inc, emsg, sizeof(emsg));
 		if(rc == CCG_EUNSUP)
 			fprintf(stderr, "ccphylo_amd: the matrix has missing entries (pairs below the minimum length); "
-			                "their updateD rules run on one GPU: use `ccphylo dist ... | ccphylo tree`.\n");
+			                "their updateD rules run on one GPU: use --gpus 1.\n");
+	}
+	if(rc) {
+		fprintf(stderr, "ccphylo_amd: dist --tree failed: %s\n", emsg);
 		return 1;
 	}
 	fprintf(stderr, "# Total time used computing distances and tree: %.2f s.\n", (double) (clock() - t0) / 1000000);

@@ -29,13 +29,22 @@
 #include "mgpu.h"
 
 /* ------------------------------------------------------------------ host transport */
+/* An abortable barrier: a rank that fails (setup, an engine error, a
+ * collective it cannot serve) calls tg_abort, and every rank waiting in the
+ * group -- or arriving later -- leaves its collective with an error instead
+ * of waiting for a peer that will never come. */
 typedef struct {
 	int world;
-	pthread_barrier_t bar;
+	pthread_mutex_t mu;
+	pthread_cond_t cv;
+	int count, aborted, fail;
+	unsigned gen;
 	void **bufs;          /* each rank's buffer of the current call */
 	const void *root_buf;
 	unsigned char *acc;   /* the allreduce result */
 	size_t acap;
+	int acc_fail;         /* rank 0 could not grow acc: every rank fails the call */
+	int first_fail;       /* the rank that aborted the group first (its error is the one reported) */
 } tgroup;
 
 typedef struct {
@@ -43,18 +52,69 @@ typedef struct {
 	int rank;
 } tuser;
 
+/* 0, or -1 when the group was aborted before every rank arrived */
+static int tg_wait(tgroup *g) {
+	pthread_mutex_lock(&g->mu);
+	if(g->aborted) {
+		pthread_mutex_unlock(&g->mu);
+		return -1;
+	}
+	const unsigned gen = g->gen;
+	if(++g->count == g->world) {
+		g->count = 0;
+		++g->gen;
+		pthread_cond_broadcast(&g->cv);
+		pthread_mutex_unlock(&g->mu);
+		return 0;
+	}
+	while(gen == g->gen && !g->aborted) pthread_cond_wait(&g->cv, &g->mu);
+	const int rc = gen == g->gen ? -1 : 0;
+	pthread_mutex_unlock(&g->mu);
+	return rc;
+}
+
+static void tg_abort(tgroup *g, int rank) {
+	pthread_mutex_lock(&g->mu);
+	if(!g->aborted) g->first_fail = rank;
+	g->aborted = 1;
+	pthread_cond_broadcast(&g->cv);
+	pthread_mutex_unlock(&g->mu);
+}
+
+/* every rank states whether its setup succeeded; 1 when all did (the same
+ * answer on every rank), 0 otherwise */
+static int tg_agree(tgroup *g, int rank, int ok) {
+	pthread_mutex_lock(&g->mu);
+	if(!ok && !g->fail) {
+		g->fail = 1;
+		g->first_fail = rank;
+	}
+	pthread_mutex_unlock(&g->mu);
+	if(tg_wait(g)) return 0;
+	pthread_mutex_lock(&g->mu);
+	const int all = !g->fail;
+	pthread_mutex_unlock(&g->mu);
+	/* nobody may change fail again before every rank has read it */
+	if(tg_wait(g)) return 0;
+	return all;
+}
+
 static int tg_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 	(void) stream;
 	tuser *u = user;
 	tgroup *g = u->g;
 	g->bufs[u->rank] = buf;
-	if(u->rank == 0 && g->acap < bytes) {
-		free(g->acc);
-		g->acc = malloc(bytes ? bytes : 1);
-		g->acap = g->acc ? bytes : 0;
+	if(u->rank == 0) {
+		g->acc_fail = 0;
+		if(g->acap < bytes) {
+			free(g->acc);
+			g->acc = malloc(bytes ? bytes : 1);
+			g->acap = g->acc ? bytes : 0;
+			g->acc_fail = !g->acc;
+		}
 	}
-	pthread_barrier_wait(&g->bar);
-	if(!g->acc && bytes) return -1;
+	if(tg_wait(g)) return -1;
+	if(g->acc_fail) return -1;   /* the same on every rank: they all leave here */
 	/* rank r sums slice r of every rank's buffer (one non-zero contributor
 	 * per byte: 64-bit adds never carry between bytes) */
 	const size_t words = bytes / 8, per = (words + g->world - 1) / g->world;
@@ -75,10 +135,9 @@ static int tg_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 			g->acc[b] = s;
 		}
 	}
-	pthread_barrier_wait(&g->bar);
+	if(tg_wait(g)) return -1;
 	memcpy(buf, g->acc, bytes);
-	pthread_barrier_wait(&g->bar);   /* acc is reused by the next call */
-	return 0;
+	return tg_wait(g);   /* acc is reused by the next call */
 }
 
 static int tg_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
@@ -86,10 +145,9 @@ static int tg_bcast(void *user, const void *send, void *recv, size_t bytes, int 
 	tuser *u = user;
 	tgroup *g = u->g;
 	if(u->rank == root) g->root_buf = send;
-	pthread_barrier_wait(&g->bar);
+	if(tg_wait(g)) return -1;
 	if(u->rank != root || recv != send) memcpy(recv, g->root_buf, bytes);
-	pthread_barrier_wait(&g->bar);
-	return 0;
+	return tg_wait(g);
 }
 
 /* ------------------------------------------------------------------ rank threads */
@@ -122,18 +180,42 @@ static void *rank_main(void *p) {
 	const ccq_mgpu *c = j->cfg;
 	ccg_ctx *ctx = NULL;
 	ccg_coll coll;
+	int have_coll = 0;
+	void *dloc = NULL;
 	tuser tu = {j->tg, j->rank};
+	/* local setup first (device, shard buffer); the ranks agree on it before
+	 * any of them enters a collective, so one rank's failure ends them all */
 	int rc = ccg_init((c->device0 + j->rank) % j->ndev, &ctx);
-	if(rc) {
-		set_err(j, "ccg_init", rc);
-		/* the other ranks wait in the transport: a host group cannot continue */
-		return NULL;
+	if(rc) set_err(j, "ccg_init", rc);
+	/* test hook: CCQ_MGPU_FAIL=setup:<rank> or run:<rank> makes that rank fail
+	 * its setup, or leave instead of running the tree (its peers are then in
+	 * their collectives), so the tests can check that the CLI exits */
+	const char *inj = getenv("CCQ_MGPU_FAIL");
+	const int inj_setup = inj && !strncmp(inj, "setup:", 6) && atoi(inj + 6) == j->rank;
+	const int inj_run = inj && !strncmp(inj, "run:", 4) && atoi(inj + 4) == j->rank;
+	if(!rc && inj_setup) {
+		rc = CCG_EHIP;
+		snprintf(j->err, sizeof(j->err), "rank %d: injected setup failure (CCQ_MGPU_FAIL)", j->rank);
+		j->rc = rc;
+	}
+	if(!rc && j->sa) {
+		const int64_t elems = ccg_shard_elems(j->sa->n, j->rank, c->gpus);
+		if((rc = ccg_malloc(ctx, &dloc, (size_t) (elems > 0 ? elems : 1) * j->ta->etype))) set_err(j, "shard buffer", rc);
+	}
+	if(!tg_agree(j->tg, j->rank, !rc)) {
+		if(!rc) snprintf(j->err, sizeof(j->err), "rank %d: stopped: another rank failed its setup", j->rank);
+		if(!j->rc) j->rc = CCG_EHIP;
+		goto out;
 	}
 	if(c->transport == CCQ_TRANSPORT_RCCL) {
-		if((rc = ccg_rccl_open(ctx, j->id, j->rank, c->gpus, &coll))) {
-			set_err(j, "ccg_rccl_open", rc);
-			ccg_destroy(ctx);
-			return NULL;
+		/* a rank whose ncclCommInitRank fails leaves the others waiting in
+		 * theirs (RCCL has no cancellable init here); every earlier failure is
+		 * caught by the agreement above */
+		if((rc = ccg_rccl_open(ctx, j->id, j->rank, c->gpus, &coll))) set_err(j, "ccg_rccl_open", rc);
+		else have_coll = 1;
+		if(!tg_agree(j->tg, j->rank, !rc)) {
+			if(!j->rc) j->rc = CCG_EHIP;
+			goto out;
 		}
 	} else {
 		memset(&coll, 0, sizeof(coll));
@@ -144,40 +226,33 @@ static void *rank_main(void *p) {
 		coll.allreduce_sum_u8 = tg_allreduce;
 		coll.broadcast = tg_bcast;
 	}
-	if(!j->sa) {
+	if(inj_run) {
+		rc = CCG_EHIP;
+		snprintf(j->err, sizeof(j->err), "rank %d: injected failure before the tree (CCQ_MGPU_FAIL)", j->rank);
+		j->rc = rc;
+	} else if(!j->sa) {
 		/* tree of a host LT: the rank uploads its own row bands */
 		rc = ccg_tree_shard(ctx, j->ta, &coll, j->D, j->joins, &j->nj, &j->fn, &j->fd, j->st);
 		if(rc) set_err(j, "ccg_tree_shard", rc);
+	} else if((rc = ccg_snp_ltd_shard(ctx, j->sa, j->rank, c->gpus, dloc, &j->inc))) {
+		/* dist into the rank's bands (the packed MSA streams from host memory
+		 * into the bit planes: HBM holds the planes and the shard only), then
+		 * the tree on them, all in HBM */
+		set_err(j, "ccg_snp_ltd_shard", rc);
+	} else if(c->round_precision >= 0 &&
+	          (rc = ccg_round_decimal_dev(ctx, dloc, ccg_shard_elems(j->sa->n, j->rank, c->gpus), j->ta->etype,
+	                                      c->round_precision))) {
+		set_err(j, "ccg_round_decimal_dev", rc);
 	} else {
-		/* dist into the rank's bands, then the tree on them, all in HBM */
-		const ccg_snp_args *a = j->sa;
-		const size_t sbytes = (size_t) a->n * a->stride * sizeof(uint64_t), ibytes = (size_t) a->stride * 4 * (a->pair ? a->n : 1);
-		const int64_t elems = ccg_shard_elems(a->n, j->rank, c->gpus);
-		void *dseq = NULL, *dinc = NULL, *dloc = NULL;
-		ccg_snp_args da = *a;
-		if((rc = ccg_malloc(ctx, &dseq, sbytes)) || (rc = ccg_malloc(ctx, &dinc, ibytes)) ||
-		   (rc = ccg_malloc(ctx, &dloc, (size_t) (elems > 0 ? elems : 1) * j->ta->etype)) ||
-		   (rc = ccg_memcpy_h2d(ctx, dseq, a->seqs, sbytes)) || (rc = ccg_memcpy_h2d(ctx, dinc, a->incs, ibytes))) {
-			set_err(j, "device buffers", rc);
-		} else {
-			da.seqs = dseq;
-			da.incs = dinc;
-			if((rc = ccg_snp_ltd_shard_dev(ctx, &da, j->rank, c->gpus, dloc, &j->inc))) {
-				set_err(j, "ccg_snp_ltd_shard_dev", rc);
-			} else {
-				ccg_free(ctx, dseq);
-				ccg_free(ctx, dinc);
-				dseq = dinc = NULL;
-				rc = ccg_tree_shard_dev(ctx, j->ta, &coll, dloc, j->joins, &j->nj, &j->fn, &j->fd, j->st);
-				if(rc) set_err(j, "ccg_tree_shard_dev", rc);
-			}
-		}
-		if(dseq) ccg_free(ctx, dseq);
-		if(dinc) ccg_free(ctx, dinc);
-		if(dloc) ccg_free(ctx, dloc);
+		rc = ccg_tree_shard_dev(ctx, j->ta, &coll, dloc, j->joins, &j->nj, &j->fn, &j->fd, j->st);
+		if(rc) set_err(j, "ccg_tree_shard_dev", rc);
 	}
-	if(c->transport == CCQ_TRANSPORT_RCCL) ccg_rccl_close(&coll);
-	ccg_destroy(ctx);
+	/* host transport: the others leave their next (or current) collective */
+	if(rc) tg_abort(j->tg, j->rank);
+out:
+	if(dloc) ccg_free(ctx, dloc);
+	if(have_coll) ccg_rccl_close(&coll);
+	if(ctx) ccg_destroy(ctx);
 	return NULL;
 }
 
@@ -198,7 +273,8 @@ static int run_ranks(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, 
 	memset(&tg, 0, sizeof(tg));
 	tg.world = G;
 	tg.bufs = calloc((size_t) G, sizeof(void *));
-	pthread_barrier_init(&tg.bar, NULL, (unsigned) G);
+	pthread_mutex_init(&tg.mu, NULL);
+	pthread_cond_init(&tg.cv, NULL);
 	rank_job *jobs = calloc((size_t) G, sizeof(rank_job));
 	pthread_t *th = calloc((size_t) G, sizeof(pthread_t));
 	unsigned char id[CCG_RCCL_ID_BYTES];
@@ -228,12 +304,18 @@ static int run_ranks(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, 
 		if(!j->joins || pthread_create(th + g, NULL, rank_main, j)) {
 			snprintf(err, errlen, "cannot start rank %d", g);
 			rc = CCG_ENOMEM;
-			for(int q = 0; q < g; ++q) pthread_join(th[q], NULL);   /* only safe when they do not wait on rank g */
+			tg_abort(&tg, g);   /* the started ranks leave their setup agreement */
+			for(int q = 0; q < g; ++q) pthread_join(th[q], NULL);
 			goto out;
 		}
 	}
 	for(int g = 0; g < G; ++g) pthread_join(th[g], NULL);
 	rc = CCG_OK;
+	/* the error of the rank that failed first (the others only stopped) */
+	if(tg.aborted || tg.fail) {
+		rc = jobs[tg.first_fail].rc ? jobs[tg.first_fail].rc : CCG_EHIP;
+		snprintf(err, errlen, "%s", jobs[tg.first_fail].err);
+	}
 	for(int g = 0; g < G && !rc; ++g) {
 		if(jobs[g].rc) {
 			rc = jobs[g].rc;
@@ -262,7 +344,8 @@ out:
 	for(int g = 1; g < G; ++g) free(jobs[g].joins);
 	free(jobs);
 	free(th);
-	pthread_barrier_destroy(&tg.bar);
+	pthread_mutex_destroy(&tg.mu);
+	pthread_cond_destroy(&tg.cv);
 	free(tg.bufs);
 	free(tg.acc);
 	return rc;

@@ -12,6 +12,8 @@ typedef struct {
 	int gpus;        /* ranks */
 	int device0;     /* rank g runs on device (device0 + g) mod the device count */
 	int transport;   /* CCQ_TRANSPORT_* */
+	int round_precision;   /* dist --tree: >= 0 rounds each shard cell as the Phylip text would
+	                          (ccg_round_decimal_dev, -W with -x digits); < 0: none */
 } ccq_mgpu;
 
 /* ccg_tree_shard on every rank from the full host LT D (ta->n taxa); the

@@ -105,7 +105,8 @@ ENGINE_SYMBOLS = [
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
-    "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_selftest_row_sum",
+    "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
+    "ccg_round_decimal_dev",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -439,6 +440,20 @@ class Device:
         inc = C.c_int(0)
         self._check(self.lib.ccg_snp_ltd_shard_dev(self.h, C.byref(a), rank, world, C.c_void_p(Dloc_ptr),
                                                    C.byref(inc)), "ccg_snp_ltd_shard_dev")
+        return inc.value
+
+    def snp_ltd_shard(self, seqs, incs, n, length, Dloc_ptr, rank, world, norm=0, etype=8, byte_scale=1.0,
+                      pair=False, min_length=1, proxi=0):
+        """ccg_snp_ltd_shard: as snp_ltd_shard_dev with the packed MSA in host
+        memory (numpy uint64[n, stride] / uint32 masks), streamed into the bit
+        planes; Dloc_ptr is the rank's device shard."""
+        seqs = np.ascontiguousarray(seqs, dtype=np.uint64)
+        incs = np.ascontiguousarray(incs, dtype=np.uint32)
+        a = SnpArgs(n, length, seqs.shape[1], seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length,
+                    proxi if pair else 0, etype, byte_scale, 0, 0)
+        inc = C.c_int(0)
+        self._check(self.lib.ccg_snp_ltd_shard(self.h, C.byref(a), rank, world, C.c_void_p(Dloc_ptr), C.byref(inc)),
+                    "ccg_snp_ltd_shard")
         return inc.value
 
 

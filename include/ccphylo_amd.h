@@ -258,6 +258,22 @@ int ccg_tree_shard(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, c
  * device pointers holding every taxon.  Pair mode (a->pair, incs = one mask
  * per taxon, -P via a->proxi) stores D only (cmpairFsaThrd semantics). */
 int ccg_snp_ltd_shard_dev(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc_dev, int *inc_out);
+/* Same with a->seqs / a->incs in HOST memory (Dloc_dev still a device
+ * buffer): the packed rows stream through a 256 MB staging buffer into the
+ * bit planes, so the rank's HBM holds the planes and its shard only (at
+ * configs[4], n = 1e6 x 100 kbp: 25 GB + 250 GB, where a device copy of the
+ * packed MSA would add 25 GB).  ccg_snp_ltd streams the same way. */
+int ccg_snp_ltd_shard(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc_dev, int *inc_out);
+
+/* The text round trip of `ccphylo dist | ccphylo tree` applied in place to
+ * `elems` cells of a device LT (etype 8 or 4): an integral cell is kept
+ * (printphy's "%d", phy.c:115), any other becomes strtod("%.*f" of it) with
+ * `precision` digits (phy.c:117, loadPhy's strtod phy.c:469), computed exactly
+ * (round-half-even of d * 10^p, then one correctly rounded division).  Used by
+ * the fused `dist -W ... --tree`, whose normalised distances the pipeline
+ * would round.  CCG_EUNSUP for etype 2/1, or for a cell with more significant
+ * digits than a double holds at that precision. */
+int ccg_round_decimal_dev(ccg_ctx *ctx, void *D_dev, int64_t elems, int etype, int precision);
 
 /* ------------------------------------------------------------------ */
 /* device memory helpers (for callers that keep the pipeline in HBM)   */

@@ -121,9 +121,115 @@ def test_cli_dist_tree_fused_pair(tmp_path, msa, extra, gpus, transport):
 
 def test_cli_dist_tree_fused_pair_missing(tmp_path):
     """msa64 with -f 3 -P 10 leaves pairs below the minimum length (-1
-    entries): the sharded tree refuses them (CCG_EUNSUP) and says how to run
-    them on one GPU, rather than building a different tree."""
+    entries).  With one GPU the fused path runs the single-GPU engine, whose
+    updateD keeps the missing-entry quirks (nj.c:1021-1030): the Newick of
+    `dist -f 3 -P 10 | tree`.  The sharded tree (--gpus > 1) still refuses
+    such matrices (CCG_EUNSUP) and says to use one GPU."""
     import ccphylo_amd as cg
-    p = subprocess.run([cg.CLI_PATH, "dist", "-i", os.path.join(GOLDEN, "msa64.fsa"), "-f", "3", "-P", "10", "--tree",
-                        str(tmp_path / "t.nwk")], capture_output=True, timeout=120)
+    src = os.path.join(GOLDEN, "msa64.fsa")
+    extra = ["-f", "3", "-P", "10"]
+    phy = tmp_path / "d.phy"
+    with open(phy, "wb") as f:
+        f.write(cli(["dist", "-i", src] + extra))
+    assert b"-1" in phy.read_bytes()
+    for method in ("dnj", "nj", "hnj"):
+        two_step = cli(["tree", "-i", str(phy), "-m", method])
+        out = tmp_path / f"t_{method}.nwk"
+        cli(["dist", "-i", src, "--tree", str(out), "--tree_method", method, "--gpus", "1"] + extra)
+        assert out.read_bytes() == two_step, method
+    p = subprocess.run([cg.CLI_PATH, "dist", "-i", src, "--tree", str(tmp_path / "t.nwk"), "--gpus", "2",
+                        "--transport", "host"] + extra, capture_output=True, timeout=120)
     assert p.returncode == 1 and b"missing entries" in p.stderr
+
+
+@pytest.mark.parametrize("msa,extra", [("msa64.fsa", ["-W", "1000"]), ("msa300.fsa", ["-W", "7", "-x", "4"]),
+                                       ("msa64.fsa", ["-W", "1000", "-p"]), ("msa_odd.fsa", ["-f", "3", "-W", "3"])])
+@pytest.mark.parametrize("gpus", [1, 3])
+def test_cli_dist_tree_fused_norm(tmp_path, msa, extra, gpus):
+    """-W normalised distances are not integral: `dist -W | tree` rounds them
+    to -x digits in the Phylip text (printphy phy.c:117, strtod phy.c:469);
+    the fused path rounds them in HBM the same way (ccg_round_decimal_dev)."""
+    src = os.path.join(GOLDEN, msa)
+    phy = tmp_path / "d.phy"
+    with open(phy, "wb") as f:
+        f.write(cli(["dist", "-i", src] + extra))
+    tx = ["-x", extra[extra.index("-x") + 1]] if "-x" in extra else []
+    tp = ["-p"] if "-p" in extra else []
+    two_step = cli(["tree", "-i", str(phy)] + tx + tp)
+    out = tmp_path / "t.nwk"
+    cli(["dist", "-i", src, "--tree", str(out), "--gpus", str(gpus), "--transport", "host"] + extra)
+    assert out.read_bytes() == two_step
+
+
+def test_round_decimal_dev():
+    """ccg_round_decimal_dev against Python's own %.*f / float() round trip
+    (correctly rounded both ways, as glibc's printf / strtod are)."""
+    import torch
+    import ccphylo_amd as cg
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.random(20000) * 10 ** rng.integers(-6, 6, 20000), np.arange(50.0),
+                        np.array([0.5e-9, 1.5e-9, 2.5e-9, 0.1, 0.7, 123456.7890123455, 1e-12, 4.4e5])])
+    dev = cg.Device(0)
+    try:
+        for p in (9, 4, 0, 12):
+            for dt, et in ((np.float64, 8), (np.float32, 4)):
+                h = x.astype(dt)
+                h = h[(h == np.trunc(h)) | (np.abs(h.astype(np.float64)) * 10.0 ** p < 2.0 ** 51)]
+                t = torch.from_numpy(h.copy()).cuda()
+                rc = dev.lib.ccg_round_decimal_dev(dev.h, C_void(t.data_ptr()), C_i64(len(h)), et, p)
+                assert rc == 0, (p, et)
+                torch.cuda.synchronize()
+                want = np.array([v if v == int(v) else dt(float("%.*f" % (p, v))) for v in h.astype(np.float64)],
+                                dtype=dt)
+                assert (t.cpu().numpy() == want).all(), (p, et)
+        # more significant digits than a double holds: refused, not rounded wrongly
+        t = torch.tensor([123456.5, 1.25], dtype=torch.float64, device="cuda")
+        assert dev.lib.ccg_round_decimal_dev(dev.h, C_void(t.data_ptr()), C_i64(2), 8, 15) == -5
+    finally:
+        dev.close()
+
+
+def C_void(p):
+    import ctypes
+    return ctypes.c_void_p(p)
+
+
+def C_i64(v):
+    import ctypes
+    return ctypes.c_int64(v)
+
+
+@pytest.mark.parametrize("where", ["setup:1", "run:2"])
+def test_cli_mgpu_rank_failure_exits(tmp_path, where):
+    """One rank failing -- in its setup, or leaving instead of running its
+    tree while its peers sit in their collectives -- makes the CLI exit with
+    an error instead of hanging (host transport)."""
+    import ccphylo_amd as cg
+    env = dict(os.environ, CCQ_MGPU_FAIL=where)
+    p = subprocess.run([cg.CLI_PATH, "dist", "-i", os.path.join(GOLDEN, "msa300.fsa"), "--tree",
+                        str(tmp_path / "t.nwk"), "--gpus", "3", "--transport", "host"], capture_output=True,
+                       timeout=120, env=env)
+    assert p.returncode == 1, p.stderr.decode()[-1000:]
+    assert b"injected" in p.stderr
+    p = subprocess.run([cg.CLI_PATH, "tree", "-i", os.path.join(GOLDEN, "test.phy.gz"), "--gpus", "3",
+                        "--transport", "host"], capture_output=True, timeout=120, env=env)
+    assert p.returncode == 1 and b"injected" in p.stderr
+
+
+@pytest.mark.parametrize("method", ["dnj", "nj"])
+def test_cli_dist_tree_world8_20k(tmp_path, method):
+    """configs[4] rehearsal on one GPU (formerly
+    tools/rehearse_world8.py): a clade-structured 20k x 3 kbp MSA through
+    `dist --tree --gpus 8 --transport host` (8 rank threads, dist straight into
+    the band shards, the sharded tree) against `--gpus 1` (the single-GPU
+    engine on the full LT): the same Newick bytes."""
+    from tools.rehearse_world8 import write_fasta
+    fa = tmp_path / "m.fsa"
+    write_fasta(str(fa), 20000, 3000)
+    outs = {}
+    for g in (1, 8):
+        out = tmp_path / f"{method}{g}.nwk"
+        cli(["dist", "-i", str(fa), "--tree", str(out), "--tree_method", method, "--gpus", str(g), "--transport",
+             "host"])
+        outs[g] = out.read_bytes()
+    assert outs[8] == outs[1] and len(outs[1]) > 20000

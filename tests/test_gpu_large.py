@@ -179,3 +179,46 @@ def test_config3_sharded_dnj_prefix(dev):
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "sharded dnj 200k float exact prefix")
+
+
+def test_config4_pipeline_200k_world1_exact(dev):
+    """configs[4]'s pipeline at n = 200k x 100 kbp, world 1: the
+    tree-like packed alignment in host memory -> ccg_snp_ltd_shard (planes
+    streamed into HBM, float band shard = the packed LT at world 1): sampled
+    cells against the oracle's fsacmp; then ccg_tree_shard_dev DNJ with EXACT
+    row sums in place, a join prefix against the oracle on a host copy.
+    Reference: cdist.c:196-390 (dist), dnj.c:985 (the DNJ loop)."""
+    import torch
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    from oracle import pyoracle
+    from tools.config5_rank import make_packed_host
+    n, L, k = 200_000, 100_000, 400
+    W = L // 32 + 1
+    seqs = make_packed_host(torch, n, W)
+    incs = np.full(W, 0xFFFFFFFF, dtype=np.uint32)
+    incs[::10] = 0
+    incs[(L + 31) // 32:] = 0
+    if L % 32:
+        incs[(L + 31) // 32 - 1] &= (0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF
+    elems = nt.shard_elems(n, 0, 1)
+    assert elems == n * (n - 1) // 2
+    D = torch.empty(elems, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    inc = dev.snp_ltd_shard(seqs, incs, n, L, D.data_ptr(), 0, 1, etype=4)
+    assert inc == int(np.unpackbits(incs.view(np.uint8)).sum())
+    lib = pyoracle.lib()
+    rng = np.random.default_rng(4)
+    pairs = [(1, 0), (n - 1, 0), (n - 1, n - 2), (n // 2, n // 3)] + \
+            [tuple(sorted(rng.choice(n, 2, replace=False).tolist(), reverse=True)) for _ in range(16)]
+    for i, j in pairs:
+        want = lib.orc_fsacmp(seqs[i].ctypes.data, seqs[j].ctypes.data, incs.ctypes.data, L)
+        assert float(D[i * (i - 1) // 2 + j].item()) == float(want), (i, j)
+    del seqs
+    host = D.cpu().numpy()
+    got = dev.tree_shard_dev(D.data_ptr(), n, None, etype=4, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
+    del D
+    torch.cuda.empty_cache()
+    ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
+    assert len(ref[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "configs[4] pipeline 200k exact prefix")
