@@ -351,6 +351,8 @@ struct RcclApi {
 	ncclResult_t (*init_rank)(ncclComm_t *, int, ncclUniqueId, int);
 	ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
 	ncclResult_t (*bcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+	ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+	ncclResult_t (*abort_comm)(ncclComm_t);
 	ncclResult_t (*destroy)(ncclComm_t);
 	const char *(*err)(ncclResult_t);
 };
@@ -368,9 +370,12 @@ static int rccl_load() {
 	a.init_rank = (decltype(a.init_rank)) dlsym(h, "ncclCommInitRank");
 	a.all_reduce = (decltype(a.all_reduce)) dlsym(h, "ncclAllReduce");
 	a.bcast = (decltype(a.bcast)) dlsym(h, "ncclBroadcast");
+	a.all_gather = (decltype(a.all_gather)) dlsym(h, "ncclAllGather");
+	a.abort_comm = (decltype(a.abort_comm)) dlsym(h, "ncclCommAbort");
 	a.destroy = (decltype(a.destroy)) dlsym(h, "ncclCommDestroy");
 	a.err = (decltype(a.err)) dlsym(h, "ncclGetErrorString");
-	if(!a.get_id || !a.init_rank || !a.all_reduce || !a.bcast || !a.destroy || !a.err) return CCG_EUNSUP;
+	if(!a.get_id || !a.init_rank || !a.all_reduce || !a.bcast || !a.all_gather || !a.destroy || !a.err)
+		return CCG_EUNSUP;
 	g_rccl = a;
 	return CCG_OK;
 }
@@ -418,6 +423,20 @@ static int rccl_bcast(void *user, const void *send, void *recv, size_t bytes, in
 	return r != ncclSuccess;
 }
 
+static int rccl_allgather(void *user, const void *send, void *recv, size_t bytes, void *stream) {
+	ncclDataType_t t;
+	size_t cnt;
+	// the widest element tiling both buffers and the slot size
+	rccl_type((const void *) ((uintptr_t) send | (uintptr_t) recv), bytes, &t, &cnt);
+	ncclResult_t r = g_rccl.all_gather(send, recv, cnt, t, ((RcclUser *) user)->comm, (hipStream_t) stream);
+	if(r != ncclSuccess) {
+		char m[160];
+		snprintf(m, sizeof(m), "ncclAllGather: %s", g_rccl.err(r));
+		ccg_set_last_msg(m);
+	}
+	return r != ncclSuccess;
+}
+
 // ------------------------------------------------------------------ host driver
 static long long sh_first(int s, const Shard &sh) {
 	if(s == 0) return 0;
@@ -447,12 +466,6 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	// device state: the single-GPU TreeBufs subset this loop uses
 	const size_t nb = (size_t) cdiv(n0, TB) + 1;
 	const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
-	long long K = 0;
-	{
-		const int rk = sh_init_chunk(n0, ET, coll_in->host_staged != 0, &K);
-		if(rk) return rk;
-	}
-	const size_t xc_bytes = (size_t) K * (size_t) n0 * ET;
 	const size_t rp_bytes = sh_rp_bytes(n0);
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
@@ -471,10 +484,10 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	// exact row sums over the join blocks (xs_join_row / xs_walk_blocks)
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xcr = take(nb * XB_CAP * sizeof(XsCross));
 	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
-	size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
+	size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll_in->world));
 	char *m;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
-	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
+	size_t hcap = sh_init_host_bytes(n0, coll_in->world);
 	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
 	if(rec_b + (size_t) n0 * ET + 16 > hcap) hcap = rec_b + (size_t) n0 * ET + 16;
 	unsigned char *h = NULL;
@@ -504,8 +517,9 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	b.xti = (XsTie *) (m + o_xt);
 	long long *F = (long long *) (m + o_F);
 	ShRec *rec = (ShRec *) (m + o_rec);
-	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xc = (T *) (m + o_xc);
+	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm);
 	void *rp = m + o_rp;
+	ShInitStat istat = {0, 0};
 	long long *hF = (long long *) malloc((size_t) (nseg0 + 2) * 8);
 	TreeCtl init, hc;
 	long long launches = 0;
@@ -534,14 +548,14 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	}
 	hF[0] = 0;
 	for(int s = 0; s <= nseg0; ++s) hF[s + 1] = hF[s] + sh_first(s, sh);
-	SH_HIP(hipMemsetAsync(m, 0, sz - xc_bytes, st));
+	SH_HIP(hipMemsetAsync(m, 0, sz, st));
 	SH_HIP(hipMemcpyAsync(F, hF, (size_t) (nseg0 + 2) * 8, hipMemcpyHostToDevice, st));
 	SH_HIP(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	SH_HIP(hipEventRecord(ctx->ev0, st));
 	kt.init(st, a->profile != 0);
 	{
 		int missing = 0;
-		SH_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, rp, Xc, K, b, &launches, &missing));
+		SH_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, rp, m + o_is, b, &launches, &missing, &istat));
 		if(missing) {
 			rc = CCG_EUNSUP;   // the missing-entry quirks of updateD run on one GPU only
 			goto out;
@@ -612,6 +626,10 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			}
 			stats[4 + 2 * CCG_NKSTAT] = 0;
 			stats[5 + 2 * CCG_NKSTAT] = 0;
+			stats[6 + 2 * CCG_NKSTAT] = 0;
+			stats[7 + 2 * CCG_NKSTAT] = 0;
+			stats[8 + 2 * CCG_NKSTAT] = istat.coll_bytes;
+			stats[9 + 2 * CCG_NKSTAT] = istat.hard;
 		}
 	}
 out:
@@ -685,7 +703,14 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 	out->host_staged = 0;
 	out->allreduce_sum_u8 = rccl_allreduce;
 	out->broadcast = rccl_bcast;
+	out->allgather = rccl_allgather;
 	return CCG_OK;
+}
+
+int ccg_rccl_abort(ccg_coll *c) {
+	if(!c || !c->user) return CCG_EINVAL;
+	if(!g_rccl.abort_comm) return CCG_EUNSUP;
+	return g_rccl.abort_comm(((RcclUser *) c->user)->comm) == ncclSuccess ? CCG_OK : CCG_EHIP;
 }
 
 int ccg_rccl_close(ccg_coll *c) {

@@ -558,14 +558,12 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	const double bs = a->byteScale;
 	hipStream_t st = ctx->stream;
 	const Shard sh = {coll->rank, coll->world};
-	long long K = 0;
-	int rc = sh_init_chunk(n0, ET, coll->host_staged != 0, &K);
-	if(rc) return rc;
+	int rc;
 	TreeWork w;
 	if((rc = ccg_tree_alloc(&w, n0, st))) return rc;
 	TreeBufs b = w.b;
 	// shard buffers: records, lines i/j, row n-1, new line j, init gathers
-	const size_t xc_bytes = (size_t) K * (size_t) n0 * ET, rp_bytes = sh_rp_bytes(n0);
+	const size_t rp_bytes = sh_rp_bytes(n0);
 	size_t sz = 0;
 	auto take = [&](size_t bytes) {
 		size_t off = sz;
@@ -574,14 +572,14 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	};
 	const size_t o_R = take(rec_all_bytes(n0, ET)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
 	const size_t o_Xj = take((size_t) n0 * ET + 8), o_pf = take((size_t) n0), o_pa = take((size_t) PICK_MAXB * n0), o_pc = take((size_t) n0 * 4);
-	const size_t o_rp = take(rp_bytes), o_xc = take(xc_bytes);
+	const size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll->world));
 	char *m = NULL;
 	unsigned char *h = NULL;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) {
 		hipFree(w.mem);
 		return CCG_ENOMEM;
 	}
-	size_t hcap = xc_bytes > rp_bytes ? xc_bytes : rp_bytes;
+	size_t hcap = sh_init_host_bytes(n0, coll->world);
 	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
 	if(rec_all_bytes(n0, ET) > hcap) hcap = rec_all_bytes(n0, ET);
 	if(coll->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
@@ -594,7 +592,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	DnjGrid grid;
 	grid.load();
 	void *R = m + o_R;
-	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj), *Xc = (T *) (m + o_xc);
+	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj);
+	ShInitStat istat = {0, 0};
 	unsigned char *pflag = (unsigned char *) (m + o_pf), *pacc = (unsigned char *) (m + o_pa);
 	unsigned *pcnt = (unsigned *) (m + o_pc);
 	unsigned long long *dbg = NULL;
@@ -627,13 +626,13 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			goto out;                                                \
 		}                                                            \
 	} while(0)
-	SD_HIP(hipMemsetAsync(m, 0, sz - xc_bytes, st));
+	SD_HIP(hipMemsetAsync(m, 0, sz, st));
 	SD_HIP(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	SD_HIP(hipEventRecord(ctx->ev0, st));
 	kt.init(st, a->profile != 0);
 	{
 		int missing = 0;
-		SD_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, m + o_rp, Xc, K, b, &launches, &missing));
+		SD_TRY(sh_init_summad<ET>(D, n0, bs, sh, cr, st, m + o_rp, m + o_is, b, &launches, &missing, &istat));
 		if(missing) {
 			rc = CCG_EUNSUP;   // the missing-entry quirks of updateD run on one GPU only
 			goto out;
@@ -725,6 +724,10 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			}
 			stats[4 + 2 * CCG_NKSTAT] = hc.cells_top;
 			stats[5 + 2 * CCG_NKSTAT] = hc.cells_rest;
+			stats[6 + 2 * CCG_NKSTAT] = hc.serial_sums;
+			stats[7 + 2 * CCG_NKSTAT] = hc.chain_sums;
+			stats[8 + 2 * CCG_NKSTAT] = istat.coll_bytes;
+			stats[9 + 2 * CCG_NKSTAT] = istat.hard;
 		}
 	}
 out:

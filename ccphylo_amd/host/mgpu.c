@@ -45,6 +45,8 @@ typedef struct {
 	size_t acap;
 	int acc_fail;         /* rank 0 could not grow acc: every rank fails the call */
 	int first_fail;       /* the rank that aborted the group first (its error is the one reported) */
+	ccg_coll **rccl;      /* each rank's open RCCL communicator (NULL once closed or aborted) */
+	int *rccl_aborted;
 } tgroup;
 
 typedef struct {
@@ -78,7 +80,32 @@ static void tg_abort(tgroup *g, int rank) {
 	if(!g->aborted) g->first_fail = rank;
 	g->aborted = 1;
 	pthread_cond_broadcast(&g->cv);
+	/* RCCL: the peers wait inside their collectives on the device; aborting
+	 * every open communicator makes those calls return */
+	for(int r = 0; g->rccl && r < g->world; ++r) {
+		if(g->rccl[r]) {
+			ccg_rccl_abort(g->rccl[r]);
+			g->rccl[r] = NULL;
+			g->rccl_aborted[r] = 1;
+		}
+	}
 	pthread_mutex_unlock(&g->mu);
+}
+
+/* RCCL communicator registry (tg_abort's targets) */
+static void tg_rccl_set(tgroup *g, int rank, ccg_coll *c) {
+	pthread_mutex_lock(&g->mu);
+	g->rccl[rank] = c;
+	pthread_mutex_unlock(&g->mu);
+}
+
+/* 1 when the rank still owns its communicator (and now closes it itself) */
+static int tg_rccl_take(tgroup *g, int rank) {
+	pthread_mutex_lock(&g->mu);
+	const int own = g->rccl[rank] != NULL && !g->rccl_aborted[rank];
+	g->rccl[rank] = NULL;
+	pthread_mutex_unlock(&g->mu);
+	return own;
 }
 
 /* every rank states whether its setup succeeded; 1 when all did (the same
@@ -138,6 +165,20 @@ static int tg_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 	if(tg_wait(g)) return -1;
 	memcpy(buf, g->acc, bytes);
 	return tg_wait(g);   /* acc is reused by the next call */
+}
+
+static int tg_allgather(void *user, const void *send, void *recv, size_t bytes, void *stream) {
+	(void) stream;
+	tuser *u = user;
+	tgroup *g = u->g;
+	g->bufs[u->rank] = (void *) send;
+	if(tg_wait(g)) return -1;
+	/* every rank copies the others' slots (its own may alias recv's) */
+	for(int q = 0; q < g->world; ++q) {
+		unsigned char *dst = (unsigned char *) recv + (size_t) q * bytes;
+		if(dst != g->bufs[q]) memcpy(dst, g->bufs[q], bytes);
+	}
+	return tg_wait(g);
 }
 
 static int tg_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
@@ -212,7 +253,10 @@ static void *rank_main(void *p) {
 		 * theirs (RCCL has no cancellable init here); every earlier failure is
 		 * caught by the agreement above */
 		if((rc = ccg_rccl_open(ctx, j->id, j->rank, c->gpus, &coll))) set_err(j, "ccg_rccl_open", rc);
-		else have_coll = 1;
+		else {
+			have_coll = 1;
+			tg_rccl_set(j->tg, j->rank, &coll);
+		}
 		if(!tg_agree(j->tg, j->rank, !rc)) {
 			if(!j->rc) j->rc = CCG_EHIP;
 			goto out;
@@ -225,6 +269,7 @@ static void *rank_main(void *p) {
 		coll.host_staged = 1;
 		coll.allreduce_sum_u8 = tg_allreduce;
 		coll.broadcast = tg_bcast;
+		coll.allgather = tg_allgather;
 	}
 	if(inj_run) {
 		rc = CCG_EHIP;
@@ -247,11 +292,11 @@ static void *rank_main(void *p) {
 		rc = ccg_tree_shard_dev(ctx, j->ta, &coll, dloc, j->joins, &j->nj, &j->fn, &j->fd, j->st);
 		if(rc) set_err(j, "ccg_tree_shard_dev", rc);
 	}
-	/* host transport: the others leave their next (or current) collective */
+	/* the others leave their next (or current) collective */
 	if(rc) tg_abort(j->tg, j->rank);
 out:
+	if(have_coll && tg_rccl_take(j->tg, j->rank)) ccg_rccl_close(&coll);
 	if(dloc) ccg_free(ctx, dloc);
-	if(have_coll) ccg_rccl_close(&coll);
 	if(ctx) ccg_destroy(ctx);
 	return NULL;
 }
@@ -273,6 +318,8 @@ static int run_ranks(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, 
 	memset(&tg, 0, sizeof(tg));
 	tg.world = G;
 	tg.bufs = calloc((size_t) G, sizeof(void *));
+	tg.rccl = calloc((size_t) G, sizeof(ccg_coll *));
+	tg.rccl_aborted = calloc((size_t) G, sizeof(int));
 	pthread_mutex_init(&tg.mu, NULL);
 	pthread_cond_init(&tg.cv, NULL);
 	rank_job *jobs = calloc((size_t) G, sizeof(rank_job));
@@ -347,6 +394,8 @@ out:
 	pthread_mutex_destroy(&tg.mu);
 	pthread_cond_destroy(&tg.cv);
 	free(tg.bufs);
+	free(tg.rccl);
+	free(tg.rccl_aborted);
 	free(tg.acc);
 	return rc;
 }

@@ -89,11 +89,12 @@ class Join(C.Structure):
 # ccg_coll (include/ccphylo_amd.h): the sharded tree loop's collectives
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 BROADCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
 class Coll(C.Structure):
     _fields_ = [("user", C.c_void_p), ("rank", C.c_int), ("world", C.c_int), ("host_staged", C.c_int),
-                ("allreduce_sum_u8", ALLREDUCE_FN), ("broadcast", BROADCAST_FN)]
+                ("allreduce_sum_u8", ALLREDUCE_FN), ("broadcast", BROADCAST_FN), ("allgather", ALLGATHER_FN)]
 
 
 JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("Lj", np.float64)])
@@ -104,7 +105,7 @@ ENGINE_SYMBOLS = [
     "ccg_snp_ltd", "ccg_snp_ltd_dev", "ccg_tree", "ccg_tree_dev",
     "ccg_malloc", "ccg_free", "ccg_memcpy_h2d", "ccg_memcpy_d2h", "ccg_synchronize",
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
-    "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_tree_shard", "ccg_tree_shard_dev",
+    "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
     "ccg_round_decimal_dev",
 ]
@@ -170,6 +171,7 @@ def engine_lib():
         lib.ccg_rccl_unique_id.argtypes = [C.c_void_p]
         lib.ccg_rccl_open.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(Coll)]
         lib.ccg_rccl_close.argtypes = [C.POINTER(Coll)]
+        lib.ccg_rccl_abort.argtypes = [C.POINTER(Coll)]
         lib.ccg_tree_shard.argtypes = [C.c_void_p, C.POINTER(TreeArgs), C.POINTER(Coll), C.c_void_p, C.c_void_p,
                                        C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int64)]
@@ -324,7 +326,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (8 + 2 * NKSTAT))()
+        st = (C.c_int64 * (10 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         rc = fn_(self.h, C.byref(a), C.c_void_p(dptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd), st)
         self._check(rc, "ccg_tree")
@@ -351,7 +353,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (8 + 2 * NKSTAT))()
+        st = (C.c_int64 * (10 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         cp = C.byref(coll.c) if coll is not None else None
         rc = fn_(self.h, C.byref(a), cp, C.c_void_p(ptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd),
@@ -490,7 +492,9 @@ class HostColl:
     each exchange to host memory and calls back here.  For tests and for
     transports without GPU-direct collectives."""
 
-    def __init__(self, dist, group=None):
+    def __init__(self, dist, group=None, allgather_native=True):
+        """allgather_native=False leaves ccg_coll.allgather NULL, so the engine
+        emulates it with the allreduce (tests both paths)."""
         import torch
         self._torch = torch
         self.dist = dist
@@ -532,9 +536,25 @@ class HostColl:
                 self.errors.append(repr(e))
                 return 1
 
+        def allgather(user, send, recv, nbytes, stream):
+            try:
+                self.calls += 1
+                self.bytes += nbytes * self.world
+                if nbytes:
+                    mine = _arr(send, nbytes).clone()   # send may alias this rank's slot of recv
+                    out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+                    dist.all_gather(out, mine, group=group)
+                    C.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * self.world)
+                return 0
+            except Exception as e:
+                self.errors.append(repr(e))
+                return 1
+
         self._ar = ALLREDUCE_FN(allreduce)   # keep the thunks alive
         self._bc = BROADCAST_FN(broadcast)
-        self.c = Coll(None, self.rank, self.world, 1, self._ar, self._bc)
+        self._ag = ALLGATHER_FN(allgather)
+        self.c = Coll(None, self.rank, self.world, 1, self._ar, self._bc,
+                      self._ag if allgather_native else ALLGATHER_FN())
 
 
 class RcclColl:

@@ -161,13 +161,17 @@ typedef struct {
 	                          prefix of a large tree); 0: run to n = 2 */
 } ccg_tree_args;
 
-/* stats layout (ccg_tree / ccg_tree_dev, 8 + 2*CCG_NKSTAT entries when
- * profile = 1, else 4): [0] rows rescanned, [1] cells rescanned, [2] kernel
- * launches, [3] device time (us); then for kernel class c: [4+2c] launches,
- * [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT] cells rescanned by
- * CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST; [6+2*CCG_NKSTAT] exact row
- * sums that needed the serial order, [7+2*CCG_NKSTAT] of those computed by
- * the serial chain (the parallel form declined).  Classes: */
+/* stats layout (ccg_tree / ccg_tree_dev / ccg_tree_shard*, 10 + 2*CCG_NKSTAT
+ * entries when profile = 1, else 4): [0] rows rescanned, [1] cells
+ * rescanned, [2] kernel launches, [3] device time (us); then for kernel class
+ * c: [4+2c] launches, [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT]
+ * cells rescanned by CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST;
+ * [6+2*CCG_NKSTAT] exact row sums that needed the serial order,
+ * [7+2*CCG_NKSTAT] of those computed by the serial chain (the parallel form
+ * declined); sharded engines only: [8+2*CCG_NKSTAT] bytes this rank put into
+ * the initSummaD collectives, [9+2*CCG_NKSTAT] columns whose column part
+ * went through the serial gather (the rest are exact sums of per-rank
+ * statistics).  Classes: */
 #define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
 #define CCG_K_TOP      1   /* sharded DNJ k_dnj_select: requeue fold, top rows S, their rescans */
 #define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the listed rows (one GPU: S and the rows below it) */
@@ -220,13 +224,18 @@ int64_t ccg_shard_elems(int64_t n, int rank, int world);
  *     in which at most one rank holds a non-zero byte, so the sum is a gather
  *     of owned pieces, exact for every element type.
  *   broadcast: `bytes` from `send` on rank `root` into `recv` on every rank
- *     (root included); `send` is ignored elsewhere. */
+ *     (root included); `send` is ignored elsewhere.
+ *   allgather (may be NULL): `bytes` from `send` on every rank r land at
+ *     recv + r * bytes on every rank (`send` may alias that slot).  NULL: the
+ *     engine emulates it with allreduce_sum_u8 over a zeroed world x bytes
+ *     buffer (twice the ring bytes). */
 typedef struct {
 	void *user;
 	int rank, world;
 	int host_staged;
 	int (*allreduce_sum_u8)(void *user, void *buf, size_t bytes, void *stream);
 	int (*broadcast)(void *user, const void *send, void *recv, size_t bytes, int root, void *stream);
+	int (*allgather)(void *user, const void *send, void *recv, size_t bytes, void *stream);
 } ccg_coll;
 
 /* RCCL transport (librccl.so.1 is loaded on first use).  Rank 0 makes the
@@ -236,6 +245,9 @@ typedef struct {
 int ccg_rccl_unique_id(void *id);
 int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *out);
 int ccg_rccl_close(ccg_coll *coll);
+/* ncclCommAbort: unblocks this rank's pending collectives after a peer failed
+ * (the multi-GPU CLI calls it on every rank's communicator when one fails). */
+int ccg_rccl_abort(ccg_coll *coll);
 
 /* NJ (a->method = CCG_TREE_NJ, nj_thread nj.c:1612) or DNJ (CCG_TREE_DNJ,
  * dnj_thread dnj.c:1054) on the rank's rows.  Every rank returns the full

@@ -131,8 +131,9 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir
     dist.init_process_group("gloo", rank=rank, world_size=world)
     D, bs = _typed(_data(kind, n), et)
     dev = cg.Device(0)
-    coll = nt.HostColl(dist) if transport == "gloo" else nt.RcclColl(dev, dist)
-    if transport == "gloo":
+    coll = nt.HostColl(dist, allgather_native=transport != "gloo-noag") if transport.startswith("gloo") \
+        else nt.RcclColl(dev, dist)
+    if transport.startswith("gloo"):
         joins, fn, fd, st = dev.tree_shard(D, n, coll, etype=et, byte_scale=bs, method=method, exact=exact)
     else:
         loc = nt.shard_extract(D, n, rank, world)
@@ -156,6 +157,9 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir
                                                                     (3, 500, "snp", 8, True, "gloo", 1),
                                                                     (2, 400, "snp", 2, False, "gloo", 1),
                                                                     (3, 1200, "clade", 4, True, "gloo", 1),
+                                                                    # ccg_coll.allgather NULL: emulated by the allreduce
+                                                                    (3, 600, "euc", 4, True, "gloo-noag", 1),
+                                                                    (2, 700, "euc", 8, True, "gloo-noag", 0),
                                                                     (1, 900, "euc", 8, True, "rccl", 1),
                                                                     # world 8, the driver's node size, rehearsed as 8
                                                                     # processes on the one GPU
@@ -171,6 +175,26 @@ def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport,
         fn, fd = np.load(tmp_path / f"f{r}.npy")
         assert (int(fn), fd) == (ref_fn, ref_fd)
         assert len(j) == len(ref_j) and (j == ref_j).all()
+
+
+@pytest.mark.parametrize("kind,et,n,max_hard", [("snp", 8, 1500, 0), ("clade", 4, 1200, 0), ("snp", 2, 900, 0),
+                                                 ("euc", 4, 2000, 100), ("euc", 8, 1600, 1600)])
+@pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
+def test_shard_init_exact_columns(dev, kind, et, n, max_hard, method):
+    """initSummaD's column parts (nj.c:111) without gathering the matrix:
+    integer SNP counts and float distances take the exact per-rank
+    statistics path (stats[9+2N]: columns left for the serial gather), only
+    %.9f-like doubles need the serial gather; the joins equal the single-GPU
+    engine's (exact row sums) either way."""
+    import ccphylo_amd as cg
+    D, bs = _typed(_data(kind, n), et)
+    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=method, exact=True)[:3]
+    j, fn, fd, st = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=method, exact=True, profile=True)
+    _same((j, fn, fd), ref)
+    hard, init_bytes = st[9 + 2 * cg.native.NKSTAT], st[8 + 2 * cg.native.NKSTAT]
+    assert hard <= max_hard, hard
+    if hard == 0:
+        assert init_bytes == 28 * n + 16, init_bytes   # row parts + one n x 16 B statistics slot
 
 
 def test_max_joins_prefix(dev):
