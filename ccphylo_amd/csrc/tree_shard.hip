@@ -647,6 +647,20 @@ out:
 int ccg_tree_shard_dnj_impl(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
                             int *njoins, int *final_n, double *final_d, int64_t *stats);
 
+// tree.hip: the single-GPU engine
+int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
+                  double *final_d, int64_t *stats);
+
+// world 1 holds the whole matrix in the band layout, which is the packed LT
+// the single-GPU engine consumes: with nothing to exchange it runs that engine
+// (missing entries and -m hnj included).  CCG_SHARD_FORCE=1 keeps the sharded
+// kernels at world 1 (their tests compare them with the single engine).
+static bool shard_world1_single(const ccg_coll *coll) {
+	if(coll && coll->world != 1) return false;
+	const char *f = getenv("CCG_SHARD_FORCE");
+	return !(f && atoi(f));
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -736,6 +750,16 @@ static int shard_check(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll)
 
 int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
                        int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	if(c && a && shard_world1_single(coll) && (!coll || coll->rank == 0)) {
+		if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
+		if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ && a->method != CCG_TREE_HNJ))
+			return CCG_EINVAL;
+		if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
+		if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
+		CCG_CHECK(hipSetDevice(c->device));
+		CCG_CHECK(hipDeviceSynchronize());
+		return ccg_tree_impl(c, a, Dloc, joins, njoins, final_n, final_d, stats);
+	}
 	int rc = shard_check(c, a, coll);
 	if(rc) return rc;
 	if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
@@ -759,7 +783,7 @@ int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll,
 
 int ccg_tree_shard(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, const void *D, ccg_join *joins,
                    int *njoins, int *final_n, double *final_d, int64_t *stats) {
-	int rc = shard_check(c, a, coll);
+	int rc = c && a && shard_world1_single(coll) ? CCG_OK : shard_check(c, a, coll);
 	if(rc) return rc;
 	if(!D) return CCG_EINVAL;
 	const int rank = coll ? coll->rank : 0, world = coll ? coll->world : 1;

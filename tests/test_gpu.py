@@ -275,7 +275,7 @@ def test_dist_row_range(dev):
 @pytest.mark.parametrize("et", [8, 4, 2, 1])
 @pytest.mark.parametrize("n", [70, 300])
 @pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
-def test_tree_all_ties(dev, et, n, method):
+def test_tree_all_ties(dev, monkeypatch, et, n, method):
     """A matrix of one repeated value: every Q and every D ties, so only the
     reference's tie rules (initHNJ hclust.c:110-115, initQ `<=`, minQpair) pick
     the joins.  Guards the tie branch ROCm 7.2 miscompiled in k_init_hnj for
@@ -288,6 +288,7 @@ def test_tree_all_ties(dev, et, n, method):
     assert (fn, fd) == (rfn, rfd)
     assert len(got) == len(ref) and (got["i"] == ref["i"]).all() and (got["j"] == ref["j"]).all()
     assert (got["Li"] == ref["Li"]).all() and (got["Lj"] == ref["Lj"]).all()
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")   # the sharded kernels, not the world-1 single engine
     sh, sfn, sfd, _ = dev.tree_shard(D, n, None, etype=et, byte_scale=1.0, method=method, exact=True)
     assert (sfn, sfd) == (rfn, rfd) and (sh == got).all()
 
@@ -326,6 +327,7 @@ def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
     ref, rfn, rfd = pyoracle.tree(D, n, method=1)
     assert (fn, fd) == (rfn, rfd)
     assert len(got) == len(ref) and (got == ref).all()
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")   # the sharded kernels, not the world-1 single engine
     sh = dev.tree_shard(D, n, None, method=1, exact=True)[0]
     assert (sh == got).all()
 
@@ -352,6 +354,7 @@ def test_dnj_band_mode_small_n(dev, monkeypatch, kind, n, top, bands):
     ref, rfn, rfd = pyoracle.tree(D, n, method=1)
     assert (fn, fd) == (rfn, rfd)
     assert len(got) == len(ref) and (got == ref).all()
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")   # the sharded kernels, not the world-1 single engine
     sh = dev.tree_shard(D, n, None, method=1, exact=True)[0]
     assert (sh == got).all()
 

@@ -162,10 +162,11 @@ def test_config2_dist_and_dnj_prefix(dev):
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "dnj configs[2] exact prefix")
 
 
-def test_config3_sharded_dnj_prefix(dev):
+def test_config3_sharded_dnj_prefix(dev, monkeypatch):
     """configs[3]: N = 200k Euclidean (seed 4), float (`-p`, 80 GB), through
-    the row-sharded engine at world 1 (band layout = the packed LT), exact
+    the row-sharded kernels at world 1 (band layout = the packed LT), exact
     DNJ, the first 500 joins against the oracle's prefix."""
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")
     import torch
     import ccphylo_amd as cg
     from oracle import pyoracle
@@ -181,7 +182,7 @@ def test_config3_sharded_dnj_prefix(dev):
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "sharded dnj 200k float exact prefix")
 
 
-def test_config4_pipeline_200k_world1_exact(dev):
+def test_config4_pipeline_200k_world1_exact(dev, monkeypatch):
     """configs[4]'s pipeline at n = 200k x 100 kbp, world 1: the
     tree-like packed alignment in host memory -> ccg_snp_ltd_shard (planes
     streamed into HBM, float band shard = the packed LT at world 1): sampled
@@ -193,6 +194,7 @@ def test_config4_pipeline_200k_world1_exact(dev):
     from ccphylo_amd import native as nt
     from oracle import pyoracle
     from tools.config5_rank import make_packed_host
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")   # the sharded kernels (world 1 would run the single engine)
     n, L, k = 200_000, 100_000, 400
     W = L // 32 + 1
     seqs = make_packed_host(torch, n, W)

@@ -27,6 +27,13 @@ def dev():
     d.close()
 
 
+@pytest.fixture(autouse=True)
+def _sharded_kernels_at_world1(monkeypatch):
+    """World 1 normally runs the single-GPU engine (nothing to exchange);
+    these tests compare the sharded kernels with it, so they force them."""
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")
+
+
 def _euclid(n, seed, dim=8):
     rng = np.random.default_rng(seed)
     pts = rng.random((n, dim))
@@ -128,6 +135,7 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir
     from ccphylo_amd import native as nt
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["CCG_SHARD_FORCE"] = "1"   # world 1 over RCCL: the sharded kernels, not the single engine
     dist.init_process_group("gloo", rank=rank, world_size=world)
     D, bs = _typed(_data(kind, n), et)
     dev = cg.Device(0)
@@ -215,11 +223,25 @@ def test_max_joins_prefix(dev):
 
 
 def test_shard_hnj_unsupported(dev):
-    """HNJ runs on one GPU: the sharded entry point says so (CCG_EUNSUP)."""
+    """HNJ runs on one GPU: the sharded kernels say so (CCG_EUNSUP)."""
     import ccphylo_amd as cg
     D = np.arange(10 * 9 // 2, dtype=np.float64)
     with pytest.raises(cg.CcgError, match="not supported"):
         dev.tree_shard(D, 10, None, method=cg.CCG_TREE_HNJ)
+
+
+@pytest.mark.parametrize("method", [0, 1, 2], ids=["nj", "dnj", "hnj"])
+def test_shard_world1_runs_single_engine(dev, monkeypatch, method):
+    """Without CCG_SHARD_FORCE, world 1 (no transport) is the single-GPU
+    engine on the same buffer: missing entries (updateD's quirks,
+    nj.c:1021-1030) and -m hnj work, with its joins."""
+    monkeypatch.delenv("CCG_SHARD_FORCE")
+    n = 300
+    D = _euclid(n, 9)
+    D[[17, 4000, 9000]] = -1.0
+    ref = dev.tree(D, n, method=method, exact=True)[:3]
+    got = dev.tree_shard(D, n, None, method=method, exact=True)[:3]
+    _same(got, ref)
 
 
 def _rand_msa(n, L, seed):
