@@ -31,6 +31,7 @@ struct ccg_ctx {
 	hipStream_t stream;
 	hipEvent_t ev0, ev1;
 	char name[256];
+	float dist_ms;   // the last dist call's pair kernels (HIP events on the engine stream)
 };
 
 // ---------------------------------------------------------------- numerics

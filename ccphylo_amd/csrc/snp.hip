@@ -1562,6 +1562,8 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 		return CCG_EINVAL;
 	}
 	int rc = CCG_OK;
+	ctx->dist_ms = 0;
+	CCG_CHECK(hipEventRecord(ctx->ev0, ctx->stream));
 	if(world > 0) {
 		switch(a->etype) {
 			case 8: rc = snp_launch_band<8>(ctx, a, planes, Wp, nFactor, D, rank, world); break;
@@ -1577,11 +1579,19 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 			default: rc = snp_launch<1>(ctx, a, planes, Wp, nFactor, D, N, rb, re); break;
 		}
 	}
+	CCG_CHECK(hipEventRecord(ctx->ev1, ctx->stream));
 	CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	if(rc == CCG_OK) CCG_CHECK(hipEventElapsedTime(&ctx->dist_ms, ctx->ev0, ctx->ev1));
 	CCG_CHECK(hipFree(planes));
 	CCG_CHECK(hipFree(d_inc));
 	if(inc_out) *inc_out = inc;
 	return rc;
+}
+
+extern "C" int ccg_last_dist_ms(ccg_ctx *ctx, double *ms) {
+	if(!ctx || !ms) return CCG_EINVAL;
+	*ms = ctx->dist_ms;
+	return CCG_OK;
 }
 
 // ------------------------------------------------------------------ Phylip round trip

@@ -107,7 +107,7 @@ ENGINE_SYMBOLS = [
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
-    "ccg_round_decimal_dev",
+    "ccg_round_decimal_dev", "ccg_last_dist_ms",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -391,6 +391,12 @@ class Device:
                                              C.c_void_p(N_ptr) if N_ptr else None, C.byref(fatal)),
                     "ccg_kma_ltd_dev")
         return fatal.value
+
+    def last_dist_ms(self):
+        """HIP-event duration of the last dist call's pair kernels (ccg_last_dist_ms)."""
+        ms = C.c_double(0)
+        self._check(self.lib.ccg_last_dist_ms(self.h, C.byref(ms)), "ccg_last_dist_ms")
+        return ms.value
 
     def selftest_row_sum(self, c):
         """The engine's exact-mode row sum of c (ccg_selftest_row_sum): returns

@@ -82,6 +82,11 @@ int ccg_snp_ltd(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_
  * pipeline: dist writes the LT that ccg_tree_dev consumes in place). */
 int ccg_snp_ltd_dev(ccg_ctx *ctx, const ccg_snp_args *a, void *D_dev, void *N_dev, int *inc_out);
 
+/* Duration of the last dist call's pair kernels on this context (the
+ * compare and epilogue launches, without the bit-plane build), from HIP
+ * events on the engine stream; benchmarks use it for the roofline. */
+int ccg_last_dist_ms(ccg_ctx *ctx, double *ms);
+
 /* ------------------------------------------------------------------ */
 /* dist on KMA count matrices (matcmp.c:448 cmpMats per pair)          */
 /* ------------------------------------------------------------------ */
