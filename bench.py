@@ -2,38 +2,36 @@
 """bench.py -- headline benchmark of ccphylo_amd (driver contract).
 
 Metric (BASELINE.json): "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa".
-`value` is NJ iterations (joins) per second of `ccphylo tree -m dnj` (the
-reference's default method, which yields the exact NJ join sequence) on
-configs[1]: an N=10,000-taxon distance matrix, one full tree per step, the
-packed LT already resident in HBM when the timed region starts (one fresh
-device copy per step; the engine consumes its input).  Row sums are exact
-(the CLI default): the join list and the Newick bytes equal the reference's,
-checked in the cpu_baseline leg against the reference binary's own output.
-extras.dnj_fast_sums is the non-default --fast_sums mode with its parity
-status at this config (join list identical or not, splits differing).
+The headline workload is configs[2], the largest single-GPU configuration
+with both halves of the metric: a 50k-taxon x 5 Mbp synthetic tree-like
+alignment, packed in HBM, -> `ccphylo dist` (all-pairs SNP counts, the full
+LT) -> `ccphylo tree -m dnj` with exact row sums (bit-identical to the
+reference), in place.  A step is the whole pipeline on the resident packed
+alignment (the tree consumes the LT, so every step recomputes it); `value`
+is taxa pairs per second of that pipeline, n(n-1)/2 / step time, and the
+line carries its split (dist taxa-pairs/s, NJ iterations/s).
 
-extras.config3: configs[2], the largest single-GPU configuration: a 50k taxa
-x 5 Mbp synthetic tree-like alignment, packed in HBM -> dist -> exact DNJ in
-place, steps-timed, with its own roofline (dist: VALU issue; tree: HBM) and
-cpu_baseline (the reference's `dist -t <threads>` on row subsamples of the
-same alignment written as FASTA, whose distances are also compared with the
-GPU's cells).
+Multi-GPU (torchrun, one process per GPU, N > 1): the SAME matrix sharded:
+dist writes each rank's LT row bands (ccg_snp_ltd_shard_dev) and the sharded
+DNJ (ccg_tree_shard_dev, exact) consumes them over RCCL -- strong scaling of
+one pipeline, `scaling: "strong"`.  `joins_sha256` is the hash of the join
+list, identical for every N when the sharded tree equals the single-GPU one.
 
-Multi-GPU (torchrun, one process per GPU): every rank builds its own N=10k
-tree on its own GPU ("replicas") -> scaling "weak", value = all ranks' joins
-divided by the max over ranks of the timed span.  One N=10k tree does not
-gain from more GPUs (a join is ~35 us of dependent steps); the sharded path is
-measured where it pays, in extras.nj_sharded: ONE N=100k matrix (40 GB) with
-its LT row bands dealt over all ranks, NJ joins with RCCL exchanges
-(ccg_tree_shard_dev), strong scaling; and extras.dnj_sharded,
-configs[3]: ONE N=200k matrix (float, 80 GB) sharded the same way, DNJ joins.
+Roofline: the dominant kernel by device time of the step (the MFMA dist
+kernel at N = 1; its duration from HIP events on the engine stream,
+ccg_last_dist_ms), with every tree kernel class beside it (HIP events of a
+profiled step); `traffic` from the committed rocprofv3 PMC summary.
+cpu_baseline: the reference binary (oracle/_ref, built from the reference's
+sources) running the same pipeline (`dist -t <nproc>` then `tree`) on the
+first taxa of the same alignment, whose distances and Newick are compared
+with the GPU's.
 
-Also reported: the dominant kernel's roofline (HIP-event timing of every
-kernel in one profiled extra step on the engine stream; algorithmic bytes as
-defined in DESIGN.md; `traffic` from the committed rocprofv3 PMC summary of
-the same kernel, profiles/r02_pmc.json, when present), the reference CPU path
-on the same matrix (rank 0, N=1), and extras (exact-row-sum mode, -m nj, and
-SNP `dist` throughput).
+extras: configs[1] (N = 10k Phylip matrix: DNJ exact and fast, NJ, HNJ, with
+the reference's DNJ and NJ on the host), the reference-rule rescanned cells
+ against the engine's at configs[1] and on a configs[2] prefix,
+dist alone at 8192 x 1 Mbp (non-pair and pair mode), KMA `cos`, configs[3]
+(one 200k float matrix, the whole exact DNJ tree: the single-GPU engine at
+N = 1, sharded over RCCL at N > 1) and the sharded NJ.
 """
 import argparse
 import json
@@ -72,8 +70,36 @@ OPS_PER_WORD_PAIR = 3.0
 OPS_PER_WORD_PAIR_PAIRMODE = 6.0   # v_and (masks), v_xor, v_bitop3, v_and, 2x v_bcnt (dist and n)
 KNAMES = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll",
           "exact_sum"]
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc.json")
-SHARD_LEG_TIMEOUT_S = 480
+def _latest(*names):
+    """The newest committed profile of a kind (this round's, else the last)."""
+    for nm in names:
+        p = os.path.join(ROOT, "profiles", nm)
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", names[-1])
+
+
+PMC_SUMMARY = _latest("r03_pmc.json", "r02_pmc.json")
+PMC_HEADLINE = _latest("r03_pmc_headline.json")
+SHARD_LEG_TIMEOUT_S = 600
+
+
+def host_cpus():
+    """CPUs this process may run on, and the cgroup CPU quota (cpu.max) when
+    one limits it (the GPU box reports every host CPU but grants a share)."""
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return ncpu, quota
 
 
 from tools.synth import euclid as euclid_ltd  # noqa: E402
@@ -118,7 +144,7 @@ def pmc_traffic(kernel):
         return None, None
 
 
-KERNEL_STATS = os.path.join(ROOT, "profiles", "r02_kernel_stats.csv")
+KERNEL_STATS = _latest("r03_kernel_stats.csv", "r02_kernel_stats.csv")
 KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
         "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop", "exact_sum": "k_exact_sum"}
 
@@ -184,11 +210,13 @@ def roofline(stats, n, s):
     return out
 
 
-def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
+def cpu_baseline(D, n, tmpdir, threads=None, method="dnj"):
     """The reference binary (oracle/_ref, built from /root/reference by
-    oracle/Makefile) on the same matrix written as Phylip, with 1 and 16
-    pthreads (`-t`, the box's CPU share); the faster is the baseline.  Falls
-    back to the oracle's C restatement in-process."""
+    oracle/Makefile) on the same matrix written as Phylip, with 1 and all
+    host pthreads (`-t`); the faster is the baseline.  Falls back to the
+    oracle's C restatement in-process."""
+    if threads is None:
+        threads = sorted({1, host_cpus()[0]})
     ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
     if os.path.exists(ref):
         from ccphylo_amd import native
@@ -197,8 +225,9 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
         runs = {}
         for t in threads:
             t0 = time.perf_counter()
-            p = subprocess.run([ref, "tree", "-i", path, "-m", "dnj", "-t", str(t), "-o",
-                                os.path.join(tmpdir, "ref.nwk")], capture_output=True, text=True, timeout=900)
+            p = subprocess.run([ref, "tree", "-i", path, "-m", method, "-t", str(t), "-o",
+                                os.path.join(tmpdir, "ref.nwk" if method == "dnj" else f"ref_{method}.nwk")],
+                               capture_output=True, text=True, timeout=900)
             wall = time.perf_counter() - t0
             # the reference reports clock() (CPU time summed over threads), so
             # the construction rate uses the process wall clock minus its load
@@ -214,8 +243,10 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
         cons, wall, load = runs[best]
         desc = "; ".join(f"-t {t}: construction {c:.2f} s, load {l:.2f} s, wall {w:.2f} s"
                          for t, (c, w, l) in sorted(runs.items()))
+        ncpu, quota = host_cpus()
         return {"value": round((n - 2) / cons, 2), "unit": "NJ joins/s", "cores": best, "kind": "reference",
-                "sample": f"full N={n} DNJ tree, reference ccphylo 0.8.5 `tree -m dnj` on the same matrix "
+                "host_cpus": ncpu, "cgroup_cpu_quota": quota,
+                "sample": f"full N={n} {method.upper()} tree, reference ccphylo 0.8.5 `tree -m {method}` on the same matrix "
                           f"(Phylip %.9f), best of {list(threads)} pthreads ({desc}); 1-thread time is the "
                           f"reference's own 'Constructing tree' report, multi-thread time is process wall "
                           f"minus its 'loading matrix' report"}
@@ -227,8 +258,8 @@ def cpu_baseline(D, n, tmpdir, threads=(1, 16)):
             "sample": f"full N={n} DNJ tree with the oracle's serial C restatement (reference binary absent)"}
 
 
-def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=16):
-    """The reference's `ccphylo dist` (oracle/_ref, -t 16) on random MSAs of
+def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=None):
+    """The reference's `ccphylo dist` (oracle/_ref, -t <host CPUs>) on random MSAs of
     `sizes` taxa x L bp (FASTA text, seeded; the data of the GPU dist leg).  The process wall time is
     parse + compare; with two sizes, t = a n + b n^2 separates the quadratic
     (compare) term, whose rate is reported as nt-comparisons/s."""
@@ -236,6 +267,8 @@ def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=16):
     ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
     if not os.path.exists(ref):
         return None
+    ncpu, quota = host_cpus()
+    threads = threads or ncpu
     rng = np.random.default_rng(11)
     lut = np.frombuffer(b"ACGT", dtype=np.uint8)
     walls = {}
@@ -254,6 +287,7 @@ def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=16):
     pairs_s = 0.5 / b if b > 0 else None         # pairs ~ n^2 / 2
     return {"value": round(pairs_s * L, 1) if pairs_s else None, "unit": "nt-comparisons/s",
             "taxa_pairs_per_s": round(pairs_s, 1) if pairs_s else None, "cores": threads, "kind": "reference",
+            "host_cpus": ncpu, "cgroup_cpu_quota": quota,
             "sample": f"reference ccphylo 0.8.5 `dist -t {threads}` on random MSAs of {list(sizes)} taxa x {L} "
                       f"bp (FASTA); walls " + ", ".join(f"n={n}: {w:.2f} s" for n, w in sorted(walls.items())) +
                       "; the rate is the quadratic (compare) term of t = a n + b n^2"}
@@ -360,116 +394,153 @@ def read_phylip_values(path):
     return n, np.array(vals)
 
 
-def config3_cpu_baseline(seqs_host, L, masked_words, tmpdir, gpu_cells, sizes=(96, 192), threads=16):
-    """The reference's `ccphylo dist -t <threads>` (oracle/_ref, built from
-    the reference's sources) on the first 96 and 192 taxa of the configs[2]
-    alignment written as FASTA.  Wall = parse + compare; t = a n + b n^2
-    separates the compare term.  The reference's distances for those taxa are
-    compared with the GPU's LT cells (same rows)."""
+def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256):
+    """The reference binary's own pipeline on the first `m` taxa of the
+    headline alignment (written as FASTA): `ccphylo dist -t <host CPUs>`
+    then `ccphylo tree` (DNJ; its threads do not speed DNJ up, so -t 1).
+    value = m(m-1)/2 / (dist wall + tree wall).  The reference's distances
+    are compared with the GPU's LT cells of those taxa, and its Newick with
+    the Newick the GPU builds from the same sub-matrix."""
+    import ccphylo_amd as cg
+    from ccphylo_amd import native
     ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
     if not os.path.exists(ref):
         return {"error": "reference binary absent (oracle/_ref not built)"}
-    walls, mism = {}, 0
-    for m in sizes:
-        path = os.path.join(tmpdir, f"c3_{m}.fsa")
-        packed_rows_to_fasta(path, seqs_host[:m], L, masked_words)
-        out = os.path.join(tmpdir, f"c3_{m}.phy")
-        t0 = time.perf_counter()
-        subprocess.run([ref, "dist", "-i", path, "-t", str(threads), "-o", out], capture_output=True, timeout=900,
-                       check=True)
-        walls[m] = time.perf_counter() - t0
-        os.unlink(path)
-        nn, vals = read_phylip_values(out)
-        os.unlink(out)
-        k = m * (m - 1) // 2
-        mism += int(nn != m) + int((vals != gpu_cells[:k]).sum())
-    (n1, t1), (n2, t2) = sorted(walls.items())
-    b = (t2 / n2 - t1 / n1) / (n2 - n1)          # t / n = a + b n
-    pairs_s = 0.5 / b if b > 0 else None
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count()
-    return {"value": round(pairs_s, 2) if pairs_s else None, "unit": "taxa-pairs/s", "cores": threads,
-            "host_cpus_available": ncpu, "kind": "reference",
-            "nt_comparisons_per_s": round(pairs_s * L, 1) if pairs_s else None,
-            "parity_mismatched_cells": mism,
-            "sample": f"reference ccphylo 0.8.5 `dist -t {threads}` on the first {list(sizes)} taxa of the same "
-                      f"{L / 1e6:g} Mbp alignment (FASTA); walls " +
-                      ", ".join(f"{m} taxa: {w:.2f} s" for m, w in sorted(walls.items())) +
-                      "; the rate is the quadratic (compare) term of t = a n + b n^2; its distances equal the GPU's "
-                      "LT cells of the same taxa when parity_mismatched_cells is 0"}
+    ncpu, quota = host_cpus()
+    masked = [w for w in range((L + 31) // 32) if incs_host[w] == 0]
+    fa = os.path.join(tmpdir, "head.fsa")
+    phy = os.path.join(tmpdir, "head.phy")
+    nwk = os.path.join(tmpdir, "head.nwk")
+    packed_rows_to_fasta(fa, seqs_host[:m], L, masked)
+    t0 = time.perf_counter()
+    subprocess.run([ref, "dist", "-i", fa, "-t", str(ncpu), "-o", phy], capture_output=True, timeout=900, check=True)
+    t1 = time.perf_counter()
+    subprocess.run([ref, "tree", "-i", phy, "-o", nwk], capture_output=True, timeout=900, check=True)
+    t2 = time.perf_counter()
+    os.unlink(fa)
+    nn, vals = read_phylip_values(phy)
+    k = m * (m - 1) // 2
+    mism = int(nn != m) + int((vals != gpu_cells[:k]).sum())
+    # the GPU tree of the same sub-matrix (its LT block is the first m rows)
+    trees = cg.newick_from_phylip(phy, lambda D_, n_: dev.tree(np.asarray(gpu_cells[:k], dtype=np.float64), n_,
+                                                              method=cg.CCG_TREE_DNJ, exact=True)[:3])
+    with open(nwk, "rb") as f:
+        same_tree = ("\n".join(trees) + "\n").encode() == f.read()
+    os.unlink(phy)
+    os.unlink(nwk)
+    pairs = m * (m - 1) / 2
+    return {"value": round(pairs / (t2 - t0), 2), "unit": "taxa-pairs/s (dist + DNJ tree, end to end)",
+            "cores": ncpu, "host_cpus": ncpu, "cgroup_cpu_quota": quota, "kind": "reference",
+            "dist_s": round(t1 - t0, 3), "tree_s": round(t2 - t1, 3),
+            "dist_nt_comparisons_per_s": round(pairs * L / (t1 - t0), 1),
+            "parity_mismatched_cells": mism, "parity_newick_identical": same_tree,
+            "sample": f"reference ccphylo 0.8.5 `dist -t {ncpu}` + `tree` (DNJ) on the first {m} taxa of the same "
+                      f"{L / 1e6:g} Mbp alignment (FASTA, parse included); the GPU's LT cells and Newick for the same "
+                      f"taxa are compared with the reference's"}
 
 
-def config3_leg(dev, torch, tmpdir, n=50_000, L=5_000_000, steps=1, cpu=True):
-    """configs[2]: N=50k taxa x L=5 Mbp synthetic tree-like alignment on one
-    GPU, end to end in HBM: packed sequences (62.5 GB) -> ccg_snp_ltd_dev
-    (double LT, 10 GB) -> ccg_tree_dev DNJ with exact row sums, in place.  A
-    step = dist + tree (steps-timed); the alignment is generated once."""
-    import ccphylo_amd as cg
+def make_headline_alignment(torch, n, L):
+    """configs[2]: tools/config3.make_packed's tree-like alignment (512 clades,
+    ~0.8% of codes flipped per taxon) on this GPU, every 10th word excluded
+    (the 'N columns'); the same bytes on every rank."""
     from tools.config3 import make_packed
     W = L // 32 + 1
     seqs = make_packed(torch, n, W)
     incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
-    masked_words = list(range(0, (L + 31) // 32, 10))
     incs[::10] = 0
     incs[(L + 31) // 32:] = 0
+    if L % 32:
+        incs[(L + 31) // 32 - 1] &= ((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF) - (1 << 32)
+    torch.cuda.synchronize()
+    return seqs, incs, W
+
+
+def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0):
+    """The headline: dist + exact DNJ of one n x L alignment per step.
+    world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
+    world > 1: ccg_snp_ltd_shard_dev into this rank's band shard,
+    ccg_tree_shard_dev over `coll` (RCCL).  Returns (timed result, the last
+    step's joins, profiled-step stats or None, alignment, the first capture_k
+    LT cells of the first step (world 1))."""
+    import hashlib
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    seqs, incs, W = make_headline_alignment(torch, n, L)
+    m = n * (n - 1) // 2
+    elems = m if world == 1 else nt.shard_elems(n, rank, world)
+    D = torch.empty(max(elems, 1), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    cap = []
+
+    def step(profile=False):
+        t0 = time.perf_counter()
+        if world == 1:
+            inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
+        else:
+            inc = dev.snp_ltd_shard_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr(), rank, world)
+        dms = dev.last_dist_ms()
+        t1 = time.perf_counter()
+        if capture_k and not cap and world == 1:   # untimed: only in the first (warmup) step
+            cap.append(D[:capture_k].cpu().numpy())
+            t1 = time.perf_counter()
+        if world == 1:
+            j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, profile=profile)
+        else:
+            j, fn, fd, st = dev.tree_shard_dev(D.data_ptr(), n, coll, method=cg.CCG_TREE_DNJ, exact=True,
+                                               profile=profile)
+        t2 = time.perf_counter()
+        return t1 - t0, t2 - t1, dms, (j, fn, fd), st, inc
+
+    for _ in range(warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    parts = []
+    for _ in range(steps):
+        parts.append(step())
+    barrier()
+    dt = shard_max(time.perf_counter() - t0, dist)
+    dist_s = shard_max(sum(p[0] for p in parts) / steps, dist)
+    tree_s = shard_max(sum(p[1] for p in parts) / steps, dist)
+    dist_kernel_ms = shard_max(sum(p[2] for p in parts) / steps, dist)
+    joins, st, inc = parts[-1][3], parts[-1][4], parts[-1][5]
+    jj, fn, fd = joins
+    sha = hashlib.sha256(np.ascontiguousarray(jj).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+    pst = None
+    if profile_tree:
+        pst = step(profile=True)[4]   # HIP events around every tree kernel (an extra, untimed step)
+    res = {"dt": dt, "dist_s": dist_s, "tree_s": tree_s, "dist_kernel_ms": dist_kernel_ms, "joins": len(jj),
+           "joins_sha256": sha, "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]),
+           "included_positions": inc}
+    del D
+    torch.cuda.empty_cache()
+    return res, joins, pst, (seqs, incs, W), (cap[0] if cap else None)
+
+
+def refrule_cells(dev, torch, seqs, incs, n, L, W, prefix, threads):
+    """DNJ's algorithmic bytes count the cells the REFERENCE's
+    minQpair rescans (dnj.c:43-128), not the engine's speculative ones.  The
+    oracle (the reference's rule, serial) and the engine run the same first
+    `prefix` joins of the headline matrix; their rescanned rows / cells."""
+    import ccphylo_amd as cg
+    from oracle import pyoracle
     m = n * (n - 1) // 2
     D = torch.empty(m, dtype=torch.float64, device="cuda")
-    torch.cuda.synchronize()
-    t_dist, t_tree, joins, cells, rows = [], [], 0, 0, 0
-    first_cells = None
-    for k in range(steps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if first_cells is None:   # the LT block of the first 192 taxa, for the reference check
-            first_cells = D[:192 * 191 // 2].cpu().numpy()
-            torch.cuda.synchronize()
-            t1b = time.perf_counter()
-        else:
-            t1b = t1
-        j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        t_dist.append(t1 - t0)
-        t_tree.append(t2 - t1b)
-        joins, rows, cells = len(j), int(st[0]), int(st[1])
-    dist_s, tree_s = sum(t_dist) / steps, sum(t_tree) / steps
-    words = (L + 31) // 32
-    ops = m * words * OPS_PER_WORD_PAIR
-    # tree HBM bytes: initSummaD + initHNJ (two LT passes), the rescanned cells,
-    # and per join the O(n) update / requeue / row-sum traffic (DESIGN.md 4)
-    sizes_sum = n * (n + 1) / 2.0
-    tree_bytes = 2.0 * 8 * m + 8.0 * cells + (7 * 8 + 48) * sizes_sum
-    res = {"n": n, "L": L, "steps": steps, "ms_per_step": round(1000 * (dist_s + tree_s), 1),
-           "dist_s": round(dist_s, 3), "tree_s": round(tree_s, 3),
-           "taxa_pairs_per_s": round(m / dist_s, 1), "nt_comparisons_per_s": m * L / dist_s,
-           "joins_per_s": round(joins / tree_s, 1), "joins": joins, "rows_rescanned": rows,
-           "cells_rescanned": cells, "included_positions": inc, "row_sums": "exact",
-           "roofline": {"dist": mfma_roofline(m * L, dist_s) if os.environ.get("CCG_DIST_MFMA", "1") != "0"
-                        else valu_roofline(ops, dist_s, OPS_PER_WORD_PAIR),
-                        "tree": {"bound": "hbm", "achieved": round(tree_bytes / tree_s / 1e9, 1),
-                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(tree_bytes / tree_s / 1e9 / HBM_PEAK_GBS, 4),
-                                 "algorithmic_bytes": tree_bytes,
-                                 "note": "2 LT passes (init) + 8 B per rescanned cell + ~104 B per active taxon per "
-                                         "join; latency-bound joins, see DESIGN.md 4"}},
-           "tree_parity": "exact row sums; tests/test_gpu_large.py::test_config2_dist_and_dnj_prefix pins this "
-                          "configuration's dist cells (fsacmp) and DNJ join prefix against the oracle"}
-    del D, incs
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
+    host = D.cpu().numpy()
+    j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=prefix)
+    del D
     torch.cuda.empty_cache()
-    if cpu:
-        try:
-            host = seqs[:192].cpu().numpy().view(np.uint64)
-            res["cpu_baseline"] = config3_cpu_baseline(host, L, masked_words, tmpdir, first_cells)
-        except Exception as e:  # noqa: BLE001
-            res["cpu_baseline"] = {"error": str(e)}
-    del seqs
-    torch.cuda.empty_cache()
-    return res
+    t0 = time.perf_counter()
+    rj, _, _, rst = pyoracle.tree(host, n, method=cg.CCG_TREE_DNJ, max_joins=prefix, threads=threads, copy=False,
+                                  stats=True)
+    dt = time.perf_counter() - t0
+    same = len(rj) == len(j) and bool((rj == j).all())
+    del host
+    return {"joins": prefix, "engine_rows": int(st[0]), "engine_cells": int(st[1]),
+            "reference_rule_rows": int(rst[0]), "reference_rule_cells": int(rst[1]),
+            "engine_over_reference_cells": round(int(st[1]) / max(int(rst[1]), 1), 3),
+            "joins_identical_to_oracle": same, "oracle_s": round(dt, 1)}
 
 
 def kma_extra(dev, torch, n=1024, L=50_000, reps=3, metric="cos"):
@@ -508,19 +579,15 @@ def kma_extra(dev, torch, n=1024, L=50_000, reps=3, metric="cos"):
             "config": f"{n} KMA count matrices x {L} positions, -d {metric}, double, views in HBM"}
 
 
-def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, transport="rccl"):
-    """NJ with the LT rows sharded over the ranks (ccg_tree_shard_dev; SURVEY
-    8(e)): rank g holds the row bands g, g + world, ... of ONE n-taxon matrix
-    (n = 100k, double: 40 GB in all), collectives over RCCL (world > 1) --
-    strong scaling of one tree.  Timed: the first `joins` joins (each a full
-    initQ scan of the whole matrix), as time(joins + 1) - time(1) so the exact
-    initSummaD and the setup are excluded.  Every rank takes part."""
+def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=100_000, joins=64):
+    """NJ on ONE n-taxon matrix (n = 100k, double: 40 GB): world 1 the
+    single-GPU engine; world > 1 the row-sharded engine (rank g holds the row
+    bands g, g + world, ...; ccg_tree_shard_dev) over `coll`
+    (RCCL) -- strong scaling of one tree.  Timed: the first `joins` joins
+    (each a full initQ scan of the whole matrix), as time(joins + 1) -
+    time(1) so the exact initSummaD and the setup are excluded."""
     import ccphylo_amd as cg
-    from ccphylo_amd import native as nt
     from tools.synth import euclid_shard_dev
-    coll = None
-    if world > 1:
-        coll = nt.RcclColl(dev, dist) if transport == "rccl" else nt.HostColl(dist)
     loc = euclid_shard_dev(torch, n, rank, world)
     work = torch.empty_like(loc)
 
@@ -537,13 +604,9 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, 
         dt = shard_max(dt, dist)
         return dt, st
 
-    try:
-        t1, _ = run(1)
-        tk, _ = run(joins + 1)
-        _, pst = run(joins + 1, profile=True)
-    finally:
-        if coll is not None and transport == "rccl":
-            coll.close()
+    t1, _ = run(1)
+    tk, _ = run(joins + 1)
+    _, pst = run(joins + 1, profile=True)
     dt = tk - t1
     # algorithmic bytes of the argmin of the timed joins: every LT cell once (s = 8) + sD
     cells = sum((m * (m - 1) // 2) for m in range(n - joins, n))
@@ -554,57 +617,42 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=100_000, joins=64, 
     torch.cuda.empty_cache()
     return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 3), "joins": joins,
             "n": n, "world": world, "seconds": round(dt, 4),
-            "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, {8 * n * (n - 1) / 2 / 1e9:.1f} GB) with "
-                      f"its LT row bands dealt over {world} GPU(s) ({transport if world > 1 else 'no'} transport); "
-                      f"first {joins} joins; fast row sums",
+            "config": f"NJ (-m nj) on one N={n} Euclidean matrix (double, {8 * n * (n - 1) / 2 / 1e9:.1f} GB), " +
+                      ("the single-GPU engine" if world == 1 else f"its LT row bands dealt over {world} GPUs") +
+                      f"; first {joins} joins; fast row sums",
             "hbm_GBps_aggregate": round(gb, 1), "hbm_frac_aggregate": round(gb / (HBM_PEAK_GBS * world), 4),
             "argmin_kernel_GBps_per_gpu": round(kern_gb, 1) if kern_gb else None,
             "coll_us_per_join": round(pst[5 + 2 * 8] / 1e3 / (joins + 1), 2) if pst[4 + 2 * 8] else 0.0}
 
 
-def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, n=200_000, joins=4000, transport="rccl"):
-    """configs[3]: DNJ with the LT rows sharded over the ranks (ccg_tree_shard_dev
-    with CCG_TREE_DNJ): ONE n-taxon Euclidean matrix (n = 200k,
-    float = `-p`: 80 GB in all), rank g holding the row bands g, g + world, ...;
-    collectives over RCCL (world > 1).  Timed: the first `joins` joins, as
-    time(joins + 1) - time(1), so the exact initSummaD, initHNJ and the setup
-    are excluded.  Every rank takes part."""
+def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=200_000, joins=0, exact=True):
+    """configs[3]: DNJ on ONE n-taxon Euclidean matrix (n = 200k, float =
+    `-p`: 80 GB), the WHOLE tree (joins = 0) with exact row sums.  world 1:
+    the single-GPU engine on the packed LT (ccg_tree_shard_dev at world 1);
+    world > 1: rank g holds the row bands g, g + world, ... and the ranks
+    exchange over `coll` (RCCL) -- strong scaling of one tree."""
+    import hashlib
     import ccphylo_amd as cg
-    from ccphylo_amd import native as nt
     from tools.synth import euclid_shard_dev
-    coll = None
-    if world > 1:
-        coll = nt.RcclColl(dev, dist) if transport == "rccl" else nt.HostColl(dist)
     loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
-    work = torch.empty_like(loc)
-
-    def run(k):
-        work.copy_(loc)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        t0 = time.perf_counter()
-        j, fn, fd, st = dev.tree_shard_dev(work.data_ptr(), n, coll, etype=4, method=cg.CCG_TREE_DNJ, exact=False,
-                                           max_joins=k)
-        dt = time.perf_counter() - t0
-        assert len(j) == k, (len(j), k)
-        return shard_max(dt, dist), st
-
-    try:
-        t1, _ = run(1)
-        tk, st = run(joins + 1)
-    finally:
-        if coll is not None and transport == "rccl":
-            coll.close()
-    dt = tk - t1
-    del loc, work
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    j, fn, fd, st = dev.tree_shard_dev(loc.data_ptr(), n, coll, etype=4, method=cg.CCG_TREE_DNJ, exact=exact,
+                                       max_joins=joins)
+    dt = shard_max(time.perf_counter() - t0, dist)
+    del loc
     torch.cuda.empty_cache()
-    return {"joins_per_s": round(joins / dt, 2), "ms_per_join": round(1000 * dt / joins, 4), "joins": joins,
-            "n": n, "world": world, "seconds": round(dt, 4),
+    sha = hashlib.sha256(np.ascontiguousarray(j).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+    return {"joins_per_s": round(len(j) / dt, 2), "ms_per_join": round(1000 * dt / max(len(j), 1), 4),
+            "joins": len(j), "n": n, "world": world, "seconds": round(dt, 3), "joins_sha256": sha,
             "rows_rescanned_rank0": int(st[0]), "cells_rescanned_rank0": int(st[1]),
+            "row_sums": "exact" if exact else "fast",
             "config": f"configs[3]: DNJ (-m dnj) on one N={n} Euclidean matrix (float, "
-                      f"{4 * n * (n - 1) / 2 / 1e9:.0f} GB) with its LT row bands dealt over {world} GPU(s) "
-                      f"({transport if world > 1 else 'no'} transport); first {joins} joins; fast row sums"}
+                      f"{4 * n * (n - 1) / 2 / 1e9:.0f} GB), " +
+                      ("the single-GPU engine" if world == 1 else f"its LT row bands dealt over {world} GPUs (RCCL)") +
+                      f"; {'the whole tree' if not joins else f'first {joins} joins'}, init included"}
 
 
 def shard_max(x, dist):
@@ -640,21 +688,175 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
     return out
 
 
+HEADLINE_STATS = _latest("r03_kernel_stats_headline.csv")
+HSYM = {"dist": "k_snp_mfma", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
+        "dnj_requeue": "k_dnj_requeue", "exact_sum": "k_exact_sum", "dnj_select": "k_dnj_select",
+        "init": "k_init_rows"}
+
+
+def headline_profile_evidence(kernel):
+    """rocprofv3 mean duration (us) and PMC HBM bytes per launch of a headline
+    kernel, from the committed profiles of the same workload (if present)."""
+    import csv
+    out = {}
+    sym = HSYM.get(kernel, kernel)
+    try:
+        with open(HEADLINE_STATS) as f:
+            for r in csv.DictReader(f):
+                if r["Name"].replace("void ", "").startswith(sym + "<") or r["Name"] == sym:
+                    out["rocprof_mean_us"] = round(float(r["AverageNs"]) / 1e3, 3)
+                    out["rocprof_calls"] = int(r["Calls"])
+                    break
+    except (OSError, KeyError, ValueError):
+        pass
+    try:
+        with open(PMC_HEADLINE) as f:
+            d = json.load(f)
+        k = d["kernels"].get(sym)
+        if k:
+            out["traffic"] = k["hbm_bytes_per_launch"]
+            out["traffic_source"] = d.get("source")
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
+
+
+def headline_roofline(n, L, elems, dist_kernel_ms, dist_launches, pst, world):
+    """Every kernel of the headline step with its roofline; the dominant one
+    (largest device time per step) is the line's `roofline`.
+    dist: 6 flops (3 MX-fp4 MACs) per position pair, this rank's cells x L,
+    against the MX-fp4 dense peak; tree kernels: SURVEY 8(d) bytes (the
+    engine's own rescanned cells for the scans), against 8 TB/s."""
+    kernels = {}
+    tf = FLOPS_PER_POSITION_PAIR * elems * float(L) / (dist_kernel_ms / 1e3) / 1e12
+    d = {"kernel": "k_snp_mfma" if world == 1 else "k_snp_mfma_band", "bound": "mfma", "achieved": round(tf, 1),
+         "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4),
+         "frac_of_measured_issue_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
+         "step_ms": round(dist_kernel_ms, 2), "launches": dist_launches,
+         "avg_launch_ms": round(dist_kernel_ms / dist_launches, 3),
+         "flops_per_launch": FLOPS_PER_POSITION_PAIR * elems * float(L) / dist_launches,
+         "algorithm": "6 flops per position pair (tetrahedron MX-fp4 form, dist = (3 L - dot) / 4), "
+                      "position pairs = LT cells x L"}
+    d.update(headline_profile_evidence("dist"))
+    kernels["dist"] = d
+    if pst is not None:
+        cs, cr = pst[4 + 2 * len(KNAMES)], pst[5 + 2 * len(KNAMES)]
+        for c, name in enumerate(KNAMES):
+            cnt, ns = pst[4 + 2 * c], pst[5 + 2 * c]
+            if not cnt or name == "coll":
+                continue
+            ab = algorithmic_bytes_total(name, n, 8, cs, cr) / (world if name in ("init",) else 1)
+            gbs = ab / (ns / 1e9) / 1e9
+            k = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 5), "step_ms": round(ns / 1e6, 2), "launches": cnt,
+                 "avg_launch_us": round(ns / cnt / 1e3, 3), "algorithmic_bytes_per_launch": round(ab / cnt, 1)}
+            k.update(headline_profile_evidence(name))
+            kernels[name] = k
+        if pst[4 + 2 * 8]:
+            kernels["coll"] = {"step_ms": round(pst[5 + 2 * 8] / 1e6, 2), "launches": pst[4 + 2 * 8],
+                               "note": "collective enqueue / host-staged round trips"}
+    dom = max((k for k in kernels if k != "coll"), key=lambda k: kernels[k]["step_ms"])
+    out = {key: kernels[dom][key] for key in ("bound", "achieved", "peak", "unit", "frac")}
+    out["traffic"] = kernels[dom].get("traffic")
+    out["kernel"] = kernels[dom].get("kernel", KSYM.get(dom, dom))
+    out["step_ms"] = kernels[dom]["step_ms"]
+    for key in ("rocprof_mean_us", "traffic_source", "avg_launch_ms", "avg_launch_us", "flops_per_launch",
+                "algorithmic_bytes_per_launch"):
+        if key in kernels[dom]:
+            out[key] = kernels[dom][key]
+    out["timing"] = "HIP events on the engine stream (dist: ccg_last_dist_ms; tree: a profiled step)"
+    out["kernels"] = kernels
+    return out
+
+
+def config1_extras(dev, torch, td, n=10_000, steps=3, cpu=True, threads=16):
+    """configs[1]: an N=10k synthetic Phylip matrix (Euclidean U[0,1)^8, seed
+    1, %.9f-quantized), `tree -m dnj` exact (steps-timed, one fresh device
+    copy per tree), fast sums, NJ, HNJ; the reference binary's DNJ on the
+    same matrix and its NJ on the first 4000 taxa (NJ is O(n^3) on the CPU);
+    the reference-rule rescanned cells (oracle) vs the engine's."""
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    D = euclid_ltd(n, seed=1)
+    nbytes = D.nbytes
+    bufs = [dev.malloc(nbytes) for _ in range(steps + 1)]
+    for b in bufs:
+        dev.h2d(b, D)
+    dev.tree_dev(bufs[0], n, method=cg.CCG_TREE_DNJ, exact=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    joins = 0
+    for k in range(steps):
+        j, fn, fd, st = dev.tree_dev(bufs[1 + k], n, method=cg.CCG_TREE_DNJ, exact=True)
+        joins += len(j)
+    dt = time.perf_counter() - t0
+    for b in bufs:
+        dev.free(b)
+    exact_joins = (j, fn, fd)
+    out = {"config": f"configs[1]: N={n} Euclidean Phylip matrix (%.9f), f64, one GPU",
+           "dnj_exact": {"joins_per_s": round(joins / dt, 2), "ms_per_tree": round(1000 * dt / steps, 2),
+                         "steps": steps, "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1])}}
+    pb = dev.malloc(nbytes)
+    fast_joins = None
+    for label, method, ex in (("dnj_fast_sums", cg.CCG_TREE_DNJ, False), ("nj", cg.CCG_TREE_NJ, True),
+                              ("hnj", cg.CCG_TREE_HNJ, True)):
+        dev.h2d(pb, D)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        j2, fn2, fd2, _ = dev.tree_dev(pb, n, method=method, exact=ex)
+        t2 = time.perf_counter() - t1
+        out[label] = {"joins_per_s": round(len(j2) / t2, 2), "seconds": round(t2, 4),
+                      "row_sums": "exact" if ex else "fast"}
+        if label == "dnj_fast_sums":
+            fast_joins = (j2, fn2, fd2)
+    dev.h2d(pb, D)
+    _, _, _, pst = dev.tree_dev(pb, n, method=cg.CCG_TREE_DNJ, exact=True, profile=True)
+    out["dnj_exact"]["roofline"] = roofline(pst, n, 8)
+    dev.h2d(pb, D)
+    _, _, _, nst = dev.tree_dev(pb, n, method=cg.CCG_TREE_NJ, exact=True, profile=True)
+    out["nj"]["roofline"] = roofline(nst, n, 8)
+    dev.free(pb)
+    # the reference rule's rescans on the same tree (the oracle, serial)
+    rj, _, _, rst = pyoracle.tree(D, n, method=cg.CCG_TREE_DNJ, stats=True, threads=threads)
+    out["dnj_exact"]["reference_rule"] = {
+        "rows_rescanned": int(rst[0]), "cells_rescanned": int(rst[1]),
+        "engine_over_reference_cells": round(out["dnj_exact"]["cells_rescanned"] / max(int(rst[1]), 1), 3),
+        "joins_identical_to_oracle": bool(len(rj) == len(j) and (rj == j).all())}
+    if cpu:
+        out["dnj_exact"]["cpu_baseline"] = cpu_baseline(D, n, td)
+        try:
+            par = reference_tree_parity(D, n, exact_joins, fast_joins, td)
+            out["dnj_exact"]["cpu_baseline"]["parity"] = par
+            out["dnj_fast_sums"]["parity_vs_exact"] = {k: v for k, v in par.items() if k.startswith("fast")}
+        except Exception as e:  # noqa: BLE001
+            out["dnj_exact"]["cpu_baseline"]["parity"] = {"error": str(e)}
+        # NJ on the host: the reference's -m nj on the first 4000 taxa, the GPU on the same matrix
+        m4 = 4000
+        D4 = D[:m4 * (m4 - 1) // 2].copy()
+        nj_cpu = cpu_baseline(D4, m4, td, threads=[1], method="nj")
+        t1 = time.perf_counter()
+        dev.tree(D4, m4, method=cg.CCG_TREE_NJ, exact=True)
+        t2 = time.perf_counter() - t1
+        nj_cpu["gpu_joins_per_s_same_matrix"] = round((m4 - 2) / t2, 2)
+        out["nj"]["cpu_baseline"] = nj_cpu
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=10000)
-    ap.add_argument("--sums", choices=["fast", "exact"], default="exact")
+    ap.add_argument("--n", type=int, default=50_000, help="headline taxa (configs[2])")
+    ap.add_argument("--L", type=int, default=5_000_000, help="headline alignment length (configs[2])")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--no-config3", action="store_true", help="skip the 50k x 5M dist+tree leg (~1 min)")
-    ap.add_argument("--c3-steps", type=int, default=1)
+    ap.add_argument("--c1-n", type=int, default=10_000)
+    ap.add_argument("--refrule-prefix", type=int, default=150)
     ap.add_argument("--shard-n", type=int, default=100_000)
     ap.add_argument("--shard-joins", type=int, default=64)
     ap.add_argument("--dnj-shard-n", type=int, default=200_000)
-    ap.add_argument("--dnj-shard-joins", type=int, default=4000)
+    ap.add_argument("--dnj-shard-joins", type=int, default=0, help="0: the whole configs[3] tree")
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
     args = ap.parse_args()
@@ -671,18 +873,10 @@ def main():
     gpu = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     import ccphylo_amd as cg
-
-    n = args.n
-    s = 8
-    D = euclid_ltd(n, seed=1)
+    from ccphylo_amd import native as nt
+    ncpu, quota = host_cpus()
+    oracle_threads = max(1, min(16, int(quota) if quota else ncpu))
     dev = cg.Device(gpu)
-    exact = args.sums == "exact"
-    nbytes = D.nbytes
-    bufs = [dev.malloc(nbytes) for _ in range(args.steps + args.warmup)]
-    for b in bufs:
-        dev.h2d(b, D)
-    for w in range(args.warmup):
-        dev.tree_dev(bufs[w], n, method=cg.CCG_TREE_DNJ, exact=exact)
 
     def barrier():
         torch.cuda.synchronize()
@@ -690,150 +884,127 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    joins = 0
-    for k in range(args.steps):
-        j, fn, fd, st = dev.tree_dev(bufs[args.warmup + k], n, method=cg.CCG_TREE_DNJ, exact=exact)
-        joins += len(j)
-    barrier()
-    dt = time.perf_counter() - t0
-    main_joins = (j, fn, fd)
+    coll, transport = None, "none (one GPU)"
     if world > 1:
-        t = torch.tensor([dt])
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
-        jt = torch.tensor([joins], dtype=torch.float64)
-        dist.all_reduce(jt, op=dist.ReduceOp.SUM)
-        joins_all = float(jt[0])
-    else:
-        joins_all = float(joins)
-    for b in bufs:
-        dev.free(b)
+        try:
+            coll = nt.RcclColl(dev, dist) if args.shard_transport == "rccl" else nt.HostColl(dist)
+            transport = args.shard_transport
+        except Exception as e:  # noqa: BLE001
+            coll, transport = nt.HostColl(dist), f"gloo (host-staged; RCCL unavailable: {e})"
 
-    # one profiled extra step (HIP events around every kernel, engine stream)
-    pb = dev.malloc(nbytes)
-    dev.h2d(pb, D)
-    _, _, _, pst = dev.tree_dev(pb, n, method=cg.CCG_TREE_DNJ, exact=exact, profile=True)
-    dev.free(pb)
-    roof = roofline(pst, n, s)
-    roof["row_sums_serial_order"] = int(pst[6 + 2 * len(KNAMES)])
-    roof["row_sums_by_serial_chain"] = int(pst[7 + 2 * len(KNAMES)])
-
+    n, L = args.n, args.L
+    m = n * (n - 1) // 2
+    elems = m if world == 1 else nt.shard_elems(n, rank, world)
+    head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
+        dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
+        capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0)
+    dt = head["dt"]
+    # dist launches per call (snp_launch: batches of 16384 (tile, slice) items)
+    tiles = (-(-n // 128)) * (-(-n // 128) + 1) // 2
+    roof = headline_roofline(n, L, elems, head["dist_kernel_ms"], max(1, -(-tiles // 16384)) if world == 1 else 1,
+                             pst, world)
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
-        "value": round(joins_all / dt, 2),
-        "unit": "NJ iterations (joins)/s",
+        "value": round(m * args.steps / dt, 1),
+        "unit": "taxa-pairs/s (dist + exact DNJ tree of the same matrix, end to end)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1000.0 * dt / args.steps, 3),
+        "ms_per_step": round(1000.0 * dt / args.steps, 1),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64",
-        "data": f"synthetic: N={n} Euclidean distances of U[0,1)^8 points (seed 1), quantized to 9 decimals "
-                f"as a %.9f Phylip would be; one full tree per step per GPU",
-        "config": {"workload": f"ccphylo tree -m dnj (configs[1]: N={n} synthetic Phylip matrix, NJ/DNJ on 1 "
-                               f"MI355X per rank)", "n_taxa": n, "method": "dnj", "elem": "double",
-                   "row_sums": args.sums, "parallelism": f"replicas x{world}"},
+        "dtype": "u2 packed codes -> MX-fp4 MFMA (exact integer counts), f64 LT and tree",
+        "data": f"synthetic: {n} taxa x {L} bp tree-like alignment (512 clades, ~0.8% of codes flipped per taxon, "
+                f"every 10th 32-position word excluded), generated packed in HBM",
+        "config": {"workload": f"configs[2]: ccphylo dist (MSA, non-pair) + ccphylo tree -m dnj (exact row sums) "
+                               f"on {n} taxa x {L / 1e6:g} Mbp, one matrix per step",
+                   "n_taxa": n, "alignment_length": L, "lt": "double",
+                   "parallelism": "one GPU" if world == 1 else f"LT row bands over {world} GPUs ({transport})"},
+        "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
+                  "dist_taxa_pairs_per_s": round(m / head["dist_s"], 1),
+                  "dist_nt_comparisons_per_s": m * float(L) / head["dist_s"],
+                  "tree_nj_iterations_per_s": round(head["joins"] / head["tree_s"], 1),
+                  "joins": head["joins"], "joins_sha256": head["joins_sha256"],
+                  "rows_rescanned": head["rows_rescanned"], "cells_rescanned": head["cells_rescanned"],
+                  "included_positions": head["included_positions"]},
         "roofline": roof,
     }
-    fast_joins = None
-    if rank == 0 and world == 1 and not args.no_extras:
-        extras = {}
-        pb = dev.malloc(nbytes)
-        other = "dnj_exact_sums" if not exact else "dnj_fast_sums"
-        for label, method, ex in ((other, cg.CCG_TREE_DNJ, not exact),
-                                  ("nj", cg.CCG_TREE_NJ, exact), ("hnj", cg.CCG_TREE_HNJ, exact)):
-            dev.h2d(pb, D)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            j2, fn2, fd2, st = dev.tree_dev(pb, n, method=method, exact=ex)
-            t2 = time.perf_counter() - t1
-            extras[label] = {"joins_per_s": round(len(j2) / t2, 2), "seconds": round(t2, 4),
-                             "row_sums": "exact" if ex else "fast"}
-            if label == "dnj_fast_sums":
-                fast_joins = (j2, fn2, fd2)
-        dev.h2d(pb, D)
-        _, _, _, nst = dev.tree_dev(pb, n, method=cg.CCG_TREE_NJ, exact=exact, profile=True)
-        extras["nj"]["roofline"] = roofline(nst, n, s)
-        dev.free(pb)
-        result["extras"] = extras
-    if not args.no_extras:
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            with tempfile.TemporaryDirectory(dir="/tmp") as td:
+                host = seqs[:256].cpu().numpy().view(np.uint64)
+                result["cpu_baseline"] = headline_cpu_baseline(dev, host, incs.cpu().numpy().view(np.uint32), L,
+                                                               cells, td)
+        except Exception as e:  # noqa: BLE001
+            result["cpu_baseline"] = {"error": str(e)}
+    extras = result.setdefault("extras", {}) if not args.no_extras else None
+    if extras is not None and rank == 0 and world == 1:
+        try:
+            extras["refrule_config2_prefix"] = refrule_cells(dev, torch, seqs, incs, n, L, W, args.refrule_prefix,
+                                                             oracle_threads)
+        except Exception as e:  # noqa: BLE001
+            extras["refrule_config2_prefix"] = {"error": str(e)}
+    del seqs, incs
+    torch.cuda.empty_cache()
+    if extras is not None:
+        if rank == 0 and world == 1:
+            try:
+                with tempfile.TemporaryDirectory(dir="/tmp") as td:
+                    extras["config1"] = config1_extras(dev, torch, td, n=args.c1_n, cpu=not args.no_cpu,
+                                                       threads=oracle_threads)
+            except Exception as e:  # noqa: BLE001
+                extras["config1"] = {"error": str(e)}
+            try:
+                extras["dist_pair"] = dist_extra(dev, torch, pair=True)
+            except Exception as e:  # noqa: BLE001
+                extras["dist_pair"] = {"error": str(e)}
+            try:
+                extras["kma_cos"] = kma_extra(dev, torch)
+            except Exception as e:  # noqa: BLE001
+                extras["kma_cos"] = {"error": str(e)}
+            torch.cuda.empty_cache()
         # every rank takes part (row-sharded dist); rank 0 reports
         try:
-            d = dist_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None)
+            extras["dist"] = dist_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None)
         except Exception as e:  # noqa: BLE001
-            d = {"error": str(e)}
-        result.setdefault("extras", {})["dist"] = d
-        if world == 1:
+            extras["dist"] = {"error": str(e)}
+        if rank == 0 and world == 1 and not args.no_cpu:
             try:
-                result["extras"]["dist_pair"] = dist_extra(dev, torch, pair=True)
+                with tempfile.TemporaryDirectory(dir="/tmp") as td:
+                    extras["dist"]["cpu_baseline"] = cpu_baseline_dist(td)
             except Exception as e:  # noqa: BLE001
-                result["extras"]["dist_pair"] = {"error": str(e)}
-            try:
-                result["extras"]["kma_cos"] = kma_extra(dev, torch)
-            except Exception as e:  # noqa: BLE001
-                result["extras"]["kma_cos"] = {"error": str(e)}
-            if not args.no_config3:
-                # configs[2]: N=50k x L=5M tree-like alignment -> dist -> exact DNJ, all in HBM
-                try:
-                    torch.cuda.empty_cache()
-                    with tempfile.TemporaryDirectory(dir="/tmp") as td:
-                        c3 = config3_leg(dev, torch, td, steps=args.c3_steps, cpu=not args.no_cpu)
-                    c3["config"] = ("configs[2]: 50k taxa x 5 Mbp synthetic tree-like alignment (512 clades, ~0.8% "
-                                    "codes flipped per taxon), packed in HBM -> ccg_snp_ltd_dev (double LT, 10 GB) "
-                                    "-> ccg_tree_dev DNJ with exact row sums")
-                    result["extras"]["config3"] = c3
-                except Exception as e:  # noqa: BLE001
-                    result["extras"]["config3"] = {"error": str(e)}
-                torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_cpu:
-        with tempfile.TemporaryDirectory(dir="/tmp") as td:
-            result["cpu_baseline"] = cpu_baseline(D, n, td)
-            if exact:
-                try:
-                    par = reference_tree_parity(D, n, main_joins, fast_joins, td)
-                    result["cpu_baseline"]["parity"] = par
-                    if "dnj_fast_sums" in result.get("extras", {}):
-                        result["extras"]["dnj_fast_sums"]["parity_vs_exact"] = {
-                            k: v for k, v in par.items() if k.startswith("fast")}
-                except Exception as e:  # noqa: BLE001
-                    result["cpu_baseline"]["parity"] = {"error": str(e)}
-            if not args.no_extras and isinstance(result.get("extras", {}).get("dist"), dict):
-                try:
-                    result["extras"]["dist"]["cpu_baseline"] = cpu_baseline_dist(td)
-                except Exception as e:  # noqa: BLE001
-                    result["extras"]["dist"]["cpu_baseline"] = {"error": str(e)}
-    if not args.no_extras:
-        # last, under a watchdog: a collective that never completes (e.g. an
-        # RCCL bootstrap failure on one rank) must not cost the whole line
+                extras["dist"]["cpu_baseline"] = {"error": str(e)}
+        torch.cuda.empty_cache()
+        # the sharded legs last, under a watchdog: a collective that never
+        # completes must not cost the whole line
         import threading
 
         def _timeout():
             if rank == 0:
-                for leg in ("nj_sharded", "dnj_sharded"):
-                    result["extras"].setdefault(leg, {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"})
+                for leg in ("dnj_sharded", "nj_sharded"):
+                    extras.setdefault(leg, {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"})
                 print(json.dumps(result), flush=True)
             os._exit(0)
         wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
         wd.daemon = True
         wd.start()
         try:
-            d = nj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None, n=args.shard_n,
-                               joins=args.shard_joins, transport=args.shard_transport)
+            extras["dnj_sharded"] = dnj_shard_extra(dev, torch, rank=rank, world=world,
+                                                    dist=dist if world > 1 else None, coll=coll,
+                                                    n=args.dnj_shard_n, joins=args.dnj_shard_joins)
         except Exception as e:  # noqa: BLE001
-            d = {"error": str(e)}
-        result["extras"]["nj_sharded"] = d
+            extras["dnj_sharded"] = {"error": str(e)}
         torch.cuda.empty_cache()
         try:
-            d = dnj_shard_extra(dev, torch, rank=rank, world=world, dist=dist if world > 1 else None,
-                                n=args.dnj_shard_n, joins=args.dnj_shard_joins, transport=args.shard_transport)
+            extras["nj_sharded"] = nj_shard_extra(dev, torch, rank=rank, world=world,
+                                                  dist=dist if world > 1 else None, coll=coll, n=args.shard_n,
+                                                  joins=args.shard_joins)
         except Exception as e:  # noqa: BLE001
-            d = {"error": str(e)}
+            extras["nj_sharded"] = {"error": str(e)}
         wd.cancel()
-        result["extras"]["dnj_sharded"] = d
+    if coll is not None and hasattr(coll, "close"):
+        coll.close()
     dev.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
