@@ -167,7 +167,7 @@ def test_round_decimal_dev():
     import torch
     import ccphylo_amd as cg
     rng = np.random.default_rng(5)
-    x = np.concatenate([rng.random(20000) * 10 ** rng.integers(-6, 6, 20000), np.arange(50.0),
+    x = np.concatenate([rng.random(20000) * 10.0 ** rng.integers(-6, 6, 20000), np.arange(50.0),
                         np.array([0.5e-9, 1.5e-9, 2.5e-9, 0.1, 0.7, 123456.7890123455, 1e-12, 4.4e5])])
     dev = cg.Device(0)
     try:
