@@ -550,7 +550,8 @@ class HostColl:
                     mine = _arr(send, nbytes).clone()   # send may alias this rank's slot of recv
                     out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
                     dist.all_gather(out, mine, group=group)
-                    C.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * self.world)
+                    allb = torch.cat(out).numpy()   # keep it alive across the copy
+                    C.memmove(recv, allb.ctypes.data, nbytes * self.world)
                 return 0
             except Exception as e:
                 self.errors.append(repr(e))
