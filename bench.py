@@ -84,6 +84,28 @@ PMC_HEADLINE = _latest("r03_pmc_headline.json")
 SHARD_LEG_TIMEOUT_S = 600
 
 
+_LEG = ["start"]
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout)."""
+    _LEG[0] = msg
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
+def start_heartbeat(every=45.0):
+    """A line every `every` seconds while a long leg runs (a single call such
+    as the oracle's prefix or a whole tree may take minutes)."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print(f"[bench {time.perf_counter() - _T0:7.1f} s] ... {_LEG[0]}", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def host_cpus():
     """CPUs this process may run on, and the cgroup CPU quota (cpu.max) when
     one limits it (the GPU box reports every host CPU but grants a share)."""
@@ -491,13 +513,15 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1, dms, (j, fn, fd), st, inc
 
-    for _ in range(warmup):
-        step()
+    for w in range(warmup):
+        r = step()
+        log(f"  warmup step {w}: dist {r[0]:.2f} s, tree {r[1]:.2f} s")
     barrier()
     t0 = time.perf_counter()
     parts = []
-    for _ in range(steps):
+    for k in range(steps):
         parts.append(step())
+        log(f"  step {k}: dist {parts[-1][0]:.2f} s, tree {parts[-1][1]:.2f} s")
     barrier()
     dt = shard_max(time.perf_counter() - t0, dist)
     dist_s = shard_max(sum(p[0] for p in parts) / steps, dist)
@@ -892,9 +916,12 @@ def main():
         except Exception as e:  # noqa: BLE001
             coll, transport = nt.HostColl(dist), f"gloo (host-staged; RCCL unavailable: {e})"
 
+    if rank == 0:
+        start_heartbeat()
     n, L = args.n, args.L
     m = n * (n - 1) // 2
     elems = m if world == 1 else nt.shard_elems(n, rank, world)
+    log(f"headline: configs[2] pipeline {n} x {L}, world {world}, {args.warmup} warmup + {args.steps} steps")
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0)
@@ -930,7 +957,9 @@ def main():
                   "included_positions": head["included_positions"]},
         "roofline": roof,
     }
+    log(f"headline: {result['value']:.4g} taxa-pairs/s, {result['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("headline cpu_baseline (reference dist + tree on 256 taxa)")
         try:
             with tempfile.TemporaryDirectory(dir="/tmp") as td:
                 host = seqs[:256].cpu().numpy().view(np.uint64)
@@ -940,6 +969,7 @@ def main():
             result["cpu_baseline"] = {"error": str(e)}
     extras = result.setdefault("extras", {}) if not args.no_extras else None
     if extras is not None and rank == 0 and world == 1:
+        log(f"reference-rule cells on a {args.refrule_prefix}-join prefix of the headline tree (oracle)")
         try:
             extras["refrule_config2_prefix"] = refrule_cells(dev, torch, seqs, incs, n, L, W, args.refrule_prefix,
                                                              oracle_threads)
@@ -949,12 +979,14 @@ def main():
     torch.cuda.empty_cache()
     if extras is not None:
         if rank == 0 and world == 1:
+            log("configs[1] extras")
             try:
                 with tempfile.TemporaryDirectory(dir="/tmp") as td:
                     extras["config1"] = config1_extras(dev, torch, td, n=args.c1_n, cpu=not args.no_cpu,
                                                        threads=oracle_threads)
             except Exception as e:  # noqa: BLE001
                 extras["config1"] = {"error": str(e)}
+            log("dist / kma extras")
             try:
                 extras["dist_pair"] = dist_extra(dev, torch, pair=True)
             except Exception as e:  # noqa: BLE001
@@ -989,6 +1021,7 @@ def main():
         wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
         wd.daemon = True
         wd.start()
+        log("configs[3]: the whole DNJ tree of one 200k float matrix")
         try:
             extras["dnj_sharded"] = dnj_shard_extra(dev, torch, rank=rank, world=world,
                                                     dist=dist if world > 1 else None, coll=coll,
@@ -996,6 +1029,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             extras["dnj_sharded"] = {"error": str(e)}
         torch.cuda.empty_cache()
+        log("NJ on one 100k matrix")
         try:
             extras["nj_sharded"] = nj_shard_extra(dev, torch, rank=rank, world=world,
                                                   dist=dist if world > 1 else None, coll=coll, n=args.shard_n,
@@ -1003,6 +1037,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             extras["nj_sharded"] = {"error": str(e)}
         wd.cancel()
+    log("done")
     if coll is not None and hasattr(coll, "close"):
         coll.close()
     dev.close()
