@@ -437,7 +437,11 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
     t0 = time.perf_counter()
     subprocess.run([ref, "dist", "-i", fa, "-t", str(ncpu), "-o", phy], capture_output=True, timeout=900, check=True)
     t1 = time.perf_counter()
-    subprocess.run([ref, "tree", "-i", phy, "-o", nwk], capture_output=True, timeout=900, check=True)
+    # -x 3: the reference's formNode (nwck.c:52-53, :75) reserves 32 bytes for
+    # "(" + two ":%.*f" lengths + ",)"; at the default 9 digits a length of
+    # 1000 or more overruns the buffer (heap corruption, glibc aborts on this
+    # alignment's SNP counts), so both Newicks are written with 3 digits
+    subprocess.run([ref, "tree", "-i", phy, "-o", nwk, "-x", "3"], capture_output=True, timeout=900, check=True)
     t2 = time.perf_counter()
     os.unlink(fa)
     nn, vals = read_phylip_values(phy)
@@ -445,7 +449,7 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
     mism = int(nn != m) + int((vals != gpu_cells[:k]).sum())
     # the GPU tree of the same sub-matrix (its LT block is the first m rows)
     trees = cg.newick_from_phylip(phy, lambda D_, n_: dev.tree(np.asarray(gpu_cells[:k], dtype=np.float64), n_,
-                                                              method=cg.CCG_TREE_DNJ, exact=True)[:3])
+                                                              method=cg.CCG_TREE_DNJ, exact=True)[:3], precision=3)
     with open(nwk, "rb") as f:
         same_tree = ("\n".join(trees) + "\n").encode() == f.read()
     os.unlink(phy)
@@ -456,7 +460,7 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
             "dist_s": round(t1 - t0, 3), "tree_s": round(t2 - t1, 3),
             "dist_nt_comparisons_per_s": round(pairs * L / (t1 - t0), 1),
             "parity_mismatched_cells": mism, "parity_newick_identical": same_tree,
-            "sample": f"reference ccphylo 0.8.5 `dist -t {ncpu}` + `tree` (DNJ) on the first {m} taxa of the same "
+            "sample": f"reference ccphylo 0.8.5 `dist -t {ncpu}` + `tree -x 3` (DNJ) on the first {m} taxa of the same "
                       f"{L / 1e6:g} Mbp alignment (FASTA, parse included); the GPU's LT cells and Newick for the same "
                       f"taxa are compared with the reference's"}
 
