@@ -20,7 +20,16 @@ import numpy as np  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 method = cg.CCG_TREE_NJ if (len(sys.argv) > 2 and sys.argv[2] == "nj") else cg.CCG_TREE_DNJ
 dev = cg.Device(0)
-if "--clade" in sys.argv:   # config-3-like clade data (tools/config3.py) through the GPU dist
+if "--c2" in sys.argv:   # the bench headline's alignment (configs[2] data at this n, 5 Mbp)
+    import torch
+    from bench import make_headline_alignment
+    seqs, incs, W = make_headline_alignment(torch, n, 5_000_000)
+    Dd = torch.empty(n * (n - 1) // 2, dtype=torch.float64, device="cuda")
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, 5_000_000, W, Dd.data_ptr())
+    D = Dd.cpu().numpy()
+    del seqs, Dd
+    torch.cuda.empty_cache()
+elif "--clade" in sys.argv:   # config-3-like clade data (tools/config3.py) through the GPU dist
     import torch
     from tools.config3 import make_packed
     L = 1_000_000
@@ -34,6 +43,6 @@ if "--clade" in sys.argv:   # config-3-like clade data (tools/config3.py) throug
     del seqs, Dd
 else:
     D = euclid(n)
-for exact in (False, True):
+for exact in ((True,) if "--exact" in sys.argv else (False, True)):
     joins, fn, fd, st = dev.tree(D, n, method=method, exact=exact)
     print(f"exact={exact}: {len(joins)} joins, device {st[3] / 1e3:.1f} ms", flush=True)
