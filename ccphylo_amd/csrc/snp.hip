@@ -608,6 +608,196 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 	}
 }
 
+// ------------------------------------------------------------------ MFMA, 256 x 256 tiles
+// k_snp_mfma2: the same exact MX-fp4 form on 256 x 256 pair tiles, one block of
+// 4 waves per CU, each wave 128 x 128 (4 x 4 MFMA tiles, 256 accumulator
+// VGPRs).  Per 64-position step a lane spreads its 4 A and 4 B plane words
+// once per component and feeds 16 MFMAs with them (k_snp_mfma: 4 spreads per
+// 4 MFMAs), and the third component (hi ^ lo) comes from the first two
+// spreads in one v_bitop3 per dword ((a ^ b) | 0x22222222: the sign bits
+// xor, the 0x2 exponent bits cancel and are set again), so the VALU work per
+// MFMA drops about 3x and each staged panel byte feeds twice the position
+// pairs (half the panel traffic into the CUs).  BAND: the A panel gathers
+// one rank's owned rows of the band layout (k_snp_mfma_band), D indexed by
+// Shard::off.  SPLIT: word slice item % S of Wk words, exact u32 counts.
+#define TILE2 256
+#define KC2 8                          // words per LDS chunk
+#define RS2 260                        // LDS row stride (uint2): 16-byte aligned rows of 256 + pad
+#define QS2 (TILE2 * KC2 / 2 / 256)    // uint4 staged per thread per panel (4)
+
+__device__ __forceinline__ v8i_t fp4_xor_spread(const v8i_t &a, const v8i_t &b) {
+	v8i_t v;
+#pragma unroll
+	for(int q = 0; q < 4; ++q) v[q] = (int) xor_or((uint32_t) a[q], (uint32_t) b[q], 0x22222222u);
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+template <int ET, bool SPLIT, bool BAND>
+__global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ P, int Wp, int n, long long t0,
+                                                      long long items, int S, int Wk, double nFactor, double bs,
+                                                      typename Elem<ET>::T *__restrict__ D, long long rowBegin,
+                                                      long long rowEnd, unsigned *__restrict__ cnt, long long cbase,
+                                                      const long long *__restrict__ pfx, int npanels, int rank,
+                                                      int world) {
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KC2 * RS2];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC2 * RS2];
+	const long long item = t0 + xcd_tile(blockIdx.x, items), t = SPLIT ? item / S : item;
+	int I, J;
+	if(BAND) {   // tile t of the rank's list: panel I = last with pfx[I] <= t, J = t - pfx[I]
+		int lo = 0, hi = npanels - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
+		}
+		I = lo;
+		J = (int) (t - pfx[lo]);
+	} else {
+		tile_ij(t, I, J);
+	}
+	const int wb = SPLIT ? (int) (item % S) * Wk : 0;
+	const int Wl = SPLIT ? (wb + Wk < Wp ? Wk : Wp - wb) : Wp;
+	const Shard sh{rank, world};
+	// the A panel's row l: I * TILE2 + l, or the rank's owned row of that local
+	// index (rows past n stage row 0 and are never stored)
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE2 + l;
+		if(!BAND) return L;
+		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const uint2 *Bp = P + (size_t) J * TILE2 * Wp + wb;
+	long long ar[QS2];
+	uint4 va[QS2], vb[QS2];
+#pragma unroll
+	for(int q = 0; q < QS2; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+		ar[q] = arow(row);
+		va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + 2 * wp);
+		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
+	}
+#pragma unroll
+	for(int q = 0; q < QS2; ++q) {
+		const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+		As[0][(2 * wp) * RS2 + row] = make_uint2(va[q].x, va[q].y);
+		As[0][(2 * wp + 1) * RS2 + row] = make_uint2(va[q].z, va[q].w);
+		Bs[0][(2 * wp) * RS2 + row] = make_uint2(vb[q].x, vb[q].y);
+		Bs[0][(2 * wp + 1) * RS2 + row] = make_uint2(vb[q].z, vb[q].w);
+	}
+	__syncthreads();
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int wr = wid >> 1, wc = wid & 1;
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 128 * wr + l32, rb0 = 128 * wc + l32;
+	v16f_t acc[4][4];
+#pragma unroll
+	for(int a = 0; a < 4; ++a)
+#pragma unroll
+		for(int c = 0; c < 4; ++c)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[a][c][r] = 0.0f;
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KC2, buf ^= 1) {
+		const bool more = w0 + KC2 < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < QS2; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + w0 + KC2 + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC2 + 2 * wp);
+			}
+		}
+		const uint2 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll
+		for(int s = 0; s < KC2 / 2; ++s) {
+			const int w = 2 * s + h;   // this lane's word: its half of the step's 64 positions
+			uint2 a[4], b[4];
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				a[x] = Ac[w * RS2 + ra0 + 32 * x];
+				b[x] = Bc[w * RS2 + rb0 + 32 * x];
+			}
+			v8i_t f0[4], g0[4], f1[4], g1[4];
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				f0[x] = fp4_spread(a[x].x);
+				g0[x] = fp4_spread(b[x].x);
+			}
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 4; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    f0[ta], g0[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				f1[x] = fp4_spread(a[x].y);
+				g1[x] = fp4_spread(b[x].y);
+			}
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 4; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    f1[ta], g1[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				f0[x] = fp4_xor_spread(f0[x], f1[x]);
+				g0[x] = fp4_xor_spread(g0[x], g1[x]);
+			}
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 4; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    f0[ta], g0[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+		}
+		if(more) {
+			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < QS2; ++q) {
+				const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+				An[(2 * wp) * RS2 + row] = make_uint2(va[q].x, va[q].y);
+				An[(2 * wp + 1) * RS2 + row] = make_uint2(va[q].z, va[q].w);
+				Bn[(2 * wp) * RS2 + row] = make_uint2(vb[q].x, vb[q].y);
+				Bn[(2 * wp + 1) * RS2 + row] = make_uint2(vb[q].z, vb[q].w);
+			}
+		}
+		__syncthreads();
+	}
+	// epilogue: C/D of 32x32 (col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5));
+	// dist = (3 L - dot) / 4 over the slice's L = 32 Wl positions
+	const int L3 = 3 * 32 * Wl;
+#pragma unroll
+	for(int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const int l = 128 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			const long long L = (long long) I * TILE2 + l;
+			long long i = L;
+			if(BAND) {
+				const long long lb = L / SB;
+				i = (lb * world + rank) * SB + (L - lb * SB);
+			}
+			if(i >= n || (!BAND && (i < rowBegin || i >= rowEnd))) continue;
+			const long long base = BAND ? sh.off(i) : tri(i);
+#pragma unroll
+			for(int tb = 0; tb < 4; ++tb) {
+				const long long j = (long long) J * TILE2 + 128 * wc + 32 * tb + l32;
+				if(j < i) {
+					const unsigned d = (unsigned) ((L3 - (int) acc[ta][tb][r]) >> 2);
+					if(SPLIT) {
+						atomicAdd(&cnt[base + j - cbase], d);
+					} else {
+						const double v = nFactor * (double) d;
+						D[base + j] = Elem<ET>::put(v, 0.5, bs);
+					}
+				}
+			}
+		}
+	}
+}
+
 // split-K epilogue: D[f] = nFactor * count (fsacmpthrd.c:247-255)
 template <int ET>
 __global__ void k_snp_finish(const unsigned *__restrict__ cnt, long long cbase, long long f0, long long f1,
@@ -1138,6 +1328,106 @@ __global__ __launch_bounds__(256) void k_snp_pair_proxi(const uint4 *__restrict_
 // ------------------------------------------------------------------ host
 static inline long long cdivll(long long a, long long b) { return (a + b - 1) / b; }
 
+// the non-pair dist kernel: 2 = k_snp_mfma2 (256 x 256 tiles, default),
+// 1 = k_snp_mfma (128 x 128), 0 = the VALU tiles (CCG_DIST_MFMA)
+static int dist_kernel_choice() {
+	const char *mf = getenv("CCG_DIST_MFMA");
+	return mf ? atoi(mf) : 2;
+}
+
+// k_snp_mfma2 over the LT rows [rb, re) (world == 0) or over one rank's rows
+// of the band layout (world > 0), with split-K over word slices when the
+// tiles do not fill the chip (one block per CU) or a row exceeds the
+// f32-exact slice, counts finished by k_snp_finish
+template <int ET>
+static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D,
+                            long long rb, long long re, int rank, int world) {
+	typedef typename Elem<ET>::T T;
+	const long long n = a->n;
+	long long t_begin = 0, t_end = 0, f0 = 0, f1 = 0;
+	int npanels = 0;
+	long long *d_pfx = NULL;
+	if(world > 0) {
+		const long long nb = (n + SB - 1) / SB;
+		long long nloc = 0;   // owned rows below n
+		if(rank < nb) {
+			const long long owned = (nb - 1 - rank) / world + 1, last = (owned - 1) * world + rank;
+			nloc = (owned - 1) * SB + (n - last * SB < SB ? n - last * SB : SB);
+		}
+		npanels = (int) cdivll(nloc, TILE2);
+		if(npanels == 0) return CCG_OK;
+		std::vector<long long> pfx(npanels + 1, 0);
+		for(long long I = 0; I < npanels; ++I) {
+			const long long Lmax = (I + 1) * TILE2 - 1 < nloc - 1 ? (I + 1) * TILE2 - 1 : nloc - 1;
+			const long long lb = Lmax / SB, rmax = (lb * world + rank) * SB + (Lmax - lb * SB);
+			pfx[I + 1] = pfx[I] + cdivll(rmax, TILE2);
+		}
+		CCG_CHECK(hipMalloc(&d_pfx, (size_t) (npanels + 1) * sizeof(long long)));
+		CCG_CHECK(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
+		                         ctx->stream));
+		t_end = pfx[npanels];
+		f1 = ccg_shard_elems(n, rank, world);
+	} else {
+		const long long Ilo = rb / TILE2, Ihi = (re - 1) / TILE2;
+		t_begin = Ilo * (Ilo + 1) / 2;
+		t_end = (Ihi + 1) * (Ihi + 2) / 2;
+		f0 = tri(rb);
+		f1 = tri(re);
+	}
+	const long long tiles = t_end - t_begin;
+	hipDeviceProp_t prop;
+	CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+	const long long slots = prop.multiProcessorCount;   // one block per CU
+	const int chunks = Wp / KC2;
+	int S = 1;
+	if(tiles < 16 * slots) {
+		S = (int) cdivll(16 * slots, tiles);
+		if(S > chunks / 4) S = chunks / 4;
+		if(S < 1) S = 1;
+	}
+	int Wk = (int) cdivll(chunks, S) * KC2;
+	if(Wk > MFMA_KMAX) Wk = (MFMA_KMAX / KC2) * KC2;
+	S = (int) cdivll(Wp, Wk);
+	unsigned *cnt = NULL;
+	if(S > 1) {
+		CCG_CHECK(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)));
+		CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
+	}
+	const long long batch = 1 << 16;
+	for(long long t = t_begin * S; t < t_end * S; t += batch) {
+		const long long items = t_end * S - t < batch ? t_end * S - t : batch;
+		const uint2 *pl = (const uint2 *) planes;
+		if(world > 0) {
+			if(S > 1)
+				k_snp_mfma2<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,
+				    world);
+			else
+				k_snp_mfma2<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,
+				    world);
+		} else {
+			if(S > 1)
+				k_snp_mfma2<ET, true, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1);
+			else
+				k_snp_mfma2<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1);
+		}
+		CCG_CHECK(hipGetLastError());
+	}
+	if(S > 1) {
+		const long long g = cdivll(f1 - f0, 256);
+		k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, f0, f0, f1, nFactor,
+		                                                                                a->byteScale, (T *) D);
+		CCG_CHECK(hipGetLastError());
+	}
+	CCG_CHECK(hipStreamSynchronize(ctx->stream));
+	if(cnt) CCG_CHECK(hipFree(cnt));
+	if(d_pfx) CCG_CHECK(hipFree(d_pfx));
+	return CCG_OK;
+}
+
 template <int ET>
 static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D, void *N,
                       long long rb, long long re) {
@@ -1216,10 +1506,10 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 		}
 		return CCG_OK;
 	}
-	// MFMA form (k_snp_mfma, the default; CCG_DIST_MFMA=0 selects the VALU
-	// tiles): f32-exact while a slice holds < MFMA_KMAX words
-	const char *mf = getenv("CCG_DIST_MFMA");
-	const int use_mfma = mf ? atoi(mf) : 1;
+	// MFMA forms (k_snp_mfma2 the default, k_snp_mfma with CCG_DIST_MFMA=1,
+	// the VALU tiles with 0): f32-exact while a slice holds < MFMA_KMAX words
+	if(dist_kernel_choice() == 2) return snp_launch_mfma2<ET>(ctx, a, planes, Wp, nFactor, D, rb, re, 0, 0);
+	const int use_mfma = dist_kernel_choice();
 	int Sm = S, Wkm = Wk;
 	if(use_mfma && Wkm > MFMA_KMAX) {
 		Wkm = (MFMA_KMAX / kc) * kc;
@@ -1381,6 +1671,10 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 		CCG_CHECK(hipFree(d_pfx));
 		return CCG_OK;
 	}
+	if(dist_kernel_choice() == 2) {
+		CCG_CHECK(hipFree(d_pfx));
+		return snp_launch_mfma2<ET>(ctx, a, planes, Wp, nFactor, D, 0, n, rank, world);
+	}
 	if(mf ? atoi(mf) : 1) {
 		// the MFMA form with snp_launch's split-K over word slices when the
 		// rank's tiles do not fill the chip, or when a row exceeds the f32-exact
@@ -1528,7 +1822,7 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	const int W32 = (a->len + 31) / 32;
 	const int kc = a->pair ? KCP : KC;
 	const int Wp = (int) (cdivll(W32, kc) * kc);
-	const long long npad = cdivll(a->n, TILE) * TILE;
+	const long long npad = cdivll(a->n, TILE2) * TILE2;   // whole panels of either tile size
 	const size_t esz = a->pair ? sizeof(uint4) : sizeof(uint2);
 	void *planes = NULL;
 	int *d_inc = NULL;

@@ -180,7 +180,9 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
                                               (129, 700000, 8, (5, 129), False), (300, 1000, 8, None, True),
                                               (900, 30000, 4, None, True), (555, 4100, 2, (50, 400), True),
                                               (1100, 65, 8, None, True), (70, 6_000_000, 8, None, False),
-                                              (40, 5_800_000, 4, None, True)])
+                                              (40, 5_800_000, 4, None, True),
+                                              # enough 256 x 256 tiles that k_snp_mfma2 runs without split-K
+                                              (24000, 640, 4, None, False), (20000, 1000, 8, (3000, 17001), False)])
 def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
     """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma, k_snp_mfma_pair:
     tetrahedron +-1 vectors in MX-fp4, dist = (3 L - dot) / 4, in pair mode
@@ -200,7 +202,7 @@ def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
     if pair:   # per-taxon masks: ~1/8 of the positions excluded, differently per taxon
         inc &= (rng.integers(-2**31, 2**31, inc.shape, dtype=np.int64) | 0x77777777).astype(np.int32)
     out = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):   # VALU tiles, k_snp_mfma (128 x 128), k_snp_mfma2 (256 x 256, the default)
         monkeypatch.setenv("CCG_DIST_MFMA", mode)
         s_d = torch.from_numpy(seqs).cuda()
         i_d = torch.from_numpy(inc).cuda()
@@ -214,10 +216,11 @@ def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
         dev.snp_ltd_dev(s_d.data_ptr(), i_d.data_ptr(), n, L, W, D.data_ptr(), **kw)
         torch.cuda.synchronize()
         out[mode] = (D.cpu().numpy(), Nd.cpu().numpy() if pair else None)
-    assert (out["0"][0].view(np.uint8) == out["1"][0].view(np.uint8)).all()
-    if pair:
-        assert (out["0"][1].view(np.uint8) == out["1"][1].view(np.uint8)).all()
-    assert out["1"][0].any()
+    for mode in ("1", "2"):
+        assert (out["0"][0].view(np.uint8) == out[mode][0].view(np.uint8)).all(), mode
+        if pair:
+            assert (out["0"][1].view(np.uint8) == out[mode][1].view(np.uint8)).all(), mode
+    assert out["2"][0].any()
 
 
 @pytest.mark.parametrize("n,L,proxi,rate,et,norm", [(70, 3000, 10, 0.05, 8, 0), (65, 4097, 2, 0.3, 8, 1000),

@@ -1,5 +1,5 @@
-"""The MFMA form of the non-pair SNP distance (k_snp_mfma, CCG_DIST_MFMA=1)
-against the VALU tile kernel (k_snp_tile) on the same device-resident random
+"""The MFMA forms of the non-pair SNP distance (k_snp_mfma2, CCG_DIST_MFMA=2,
+the default; k_snp_mfma, 1) against the VALU tile kernel (k_snp_tile, 0) on the same device-resident random
 MSA (development aid; the engine reads CCG_DIST_MFMA once per process, so
 each mode runs in its own child process):
     python tools/check_dist_mfma.py [N] [L] [seed]
@@ -47,7 +47,7 @@ def main():
     seed = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):
         env = dict(os.environ, CCG_DIST_MFMA=mode)
         p = subprocess.run([sys.executable, "-c", CHILD.format(root=root, n=n, L=L, seed=seed)], env=env,
                            capture_output=True, text=True, timeout=600)
@@ -57,10 +57,11 @@ def main():
             sys.exit(1)
         _, t, rate, h, dmin, dmax = line[0].split()
         out[mode] = h
-        print(f"{'MFMA' if mode == '1' else 'VALU'}: N={n} L={L}: {float(t):.4f} s, {float(rate):.3e} taxa-pairs/s, "
+        print(f"{ {'0': 'VALU', '1': 'MFMA 128', '2': 'MFMA 256'}[mode]}: N={n} L={L}: {float(t):.4f} s, {float(rate):.3e} taxa-pairs/s, "
               f"{float(rate) * L:.3e} nt-comparisons/s, D in [{dmin}, {dmax}]", flush=True)
-    print("identical:", out["0"] == out["1"], flush=True)
-    sys.exit(0 if out["0"] == out["1"] else 2)
+    same = out["0"] == out["1"] == out["2"]
+    print("identical:", same, flush=True)
+    sys.exit(0 if same else 2)
 
 
 if __name__ == "__main__":
