@@ -15,17 +15,29 @@ from tools.synth import euclid  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 cfgs = sys.argv[2:] or [""]
 method = cg.CCG_TREE_NJ if os.environ.get("SWEEP_METHOD") == "nj" else cg.CCG_TREE_DNJ
-D = euclid(n)
 dev = cg.Device(0)
+if os.environ.get("SWEEP_DATA") == "c2":   # the bench headline's alignment at this n (configs[2] data)
+    import torch
+    from bench import make_headline_alignment
+    seqs, incs, W = make_headline_alignment(torch, n, 5_000_000)
+    Dd = torch.empty(n * (n - 1) // 2, dtype=torch.float64, device="cuda")
+    dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, 5_000_000, W, Dd.data_ptr())
+    D = Dd.cpu().numpy()
+    del seqs, incs, Dd
+    torch.cuda.empty_cache()
+else:
+    D = euclid(n)
+modes = (True,) if os.environ.get("SWEEP_EXACT_ONLY") else (False, True)
+reps = int(os.environ.get("SWEEP_REPS", "2"))
 ref = None
 for cfg in cfgs:
     env = dict(kv.split("=") for kv in cfg.split())
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     out = []
-    for exact in (False, True):
+    for exact in modes:
         best = 0.0
-        for _ in range(2):
+        for _ in range(reps):
             j, fn, fd, st = dev.tree(D, n, method=method, exact=exact)
             best = max(best, len(j) / (st[3] / 1e6))
         if exact:
