@@ -33,7 +33,7 @@ struct DenseRows {
 // waves of units run at small n).
 struct DnjGrid {
 	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
-	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0;
+	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = 0;
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
@@ -43,6 +43,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
@@ -809,6 +810,70 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 	TS(2, 2);
 	TS_SAMP(2);
 	TS_EXIT(2);
+}
+
+// The same rescans with one WAVE per unit (CCG_SCAN_WAVE=1): no block
+// reduce or barrier per unit, and a wave's next unit starts loading while
+// the current one reduces (the units of a wave are independent).  Lane l
+// takes the unit's columns c0 + l, c0 + l + 64, ...; UW loads of the row
+// (and of sD) in flight per lane.
+#define SCAN_UW 8
+template <int ET, bool GEN, class Rows, class Tail = NoTail>
+__global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                   int n, Rows rows, int seg, Tail tail = Tail()) {
+	__shared__ int erow[REPLAY_CAP];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int r0 = b.crow[tid];
+	const int done = ctl->done, T = ctl->T;
+	if(done) return;
+	tail.begin(b, n);
+	if(T == 0) return;
+	const int umax = dnj_umax(n, seg), nunits = T * umax;
+	if((int) blockIdx.x * (TB / 64) >= nunits) return;
+	const bool lds = T <= REPLAY_CAP;
+	if(lds) {
+		if(tid < T) erow[tid] = r0;
+		for(int e = TB + tid; e < T; e += TB) erow[e] = b.crow[e];
+	}
+	__syncthreads();
+	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	for(int u = gw; u < nunits; u += nw) {
+		const int e = u / umax, ua = e * umax;
+		const int r = lds ? erow[e] : b.crow[e];
+		const int c0 = (u - ua) * seg;
+		if(c0 >= r || !rows.owns(r)) continue;   // wave-uniform
+		const int c1 = c0 + seg < r ? c0 + seg : r;
+		const int Nr = GEN ? b.N[r] : n;
+		const double sDr = b.sD[r];
+		const typename Elem<ET>::T *row = D + rows.row(r);
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int base = c0; base < c1; base += 64 * SCAN_UW) {
+			typename Elem<ET>::T v[SCAN_UW];
+			double sk[SCAN_UW];
+			int nk[SCAN_UW];
+#pragma unroll
+			for(int m = 0; m < SCAN_UW; ++m) {
+				int c = base + 64 * m + lane;
+				c = c < c1 ? c : c1 - 1;
+				v[m] = row[c];
+				sk[m] = b.sD[c];
+				nk[m] = GEN ? b.N[c] : Nr;
+			}
+#pragma unroll
+			for(int m = 0; m < SCAN_UW; ++m) {
+				const int c = base + 64 * m + lane;
+				const double d = Elem<ET>::get(v[m], bs);
+				const double x = qcrit(Nr, nk[m], d, sDr, sk[m]);
+				const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+				q = take ? x : q;
+				idx = take ? c : idx;
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		if(lane == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, q, idx);
+	}
 }
 
 // ------------------------------------------------------------------ DNJ fold

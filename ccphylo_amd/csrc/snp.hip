@@ -241,12 +241,17 @@ typedef float v16f_t __attribute__((ext_vector_type(16)));
 #endif
 #define QS (TILE * KCM / 2 / 256)   // uint4 staged per thread per panel
 
+// (a & b) | c in one v_bitop3_b32 (truth table 0xEA in xor_or's convention)
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0xEA);
+}
+
 __device__ __forceinline__ v8i_t fp4_spread(uint32_t x) {
 	v8i_t v;
-	v[0] = (int) (((x << 3) & 0x88888888u) | 0x22222222u);
-	v[1] = (int) (((x << 2) & 0x88888888u) | 0x22222222u);
-	v[2] = (int) (((x << 1) & 0x88888888u) | 0x22222222u);
-	v[3] = (int) ((x & 0x88888888u) | 0x22222222u);
+	v[0] = (int) and_or(x << 3, 0x88888888u, 0x22222222u);
+	v[1] = (int) and_or(x << 2, 0x88888888u, 0x22222222u);
+	v[2] = (int) and_or(x << 1, 0x88888888u, 0x22222222u);
+	v[3] = (int) and_or(x, 0x88888888u, 0x22222222u);
 	v[4] = v[5] = v[6] = v[7] = 0;
 	return v;
 }
