@@ -817,8 +817,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__r
 // the current one reduces (the units of a wave are independent).  Lane l
 // takes the unit's columns c0 + l, c0 + l + 64, ...; UW loads of the row
 // (and of sD) in flight per lane.
-#define SCAN_UW 8
-template <int ET, bool GEN, class Rows, class Tail = NoTail>
+template <int ET, bool GEN, class Rows, class Tail = NoTail, int SCAN_UW = 8>
 __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	__shared__ int erow[REPLAY_CAP];

@@ -288,19 +288,82 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	}
 	__syncthreads();
 	if(s_stop) return;
-	if(wid == 0) {
+	{
 		TS(3, 2);
-		const int nS = s_nS;
+		const int nS = s_nS, total = nS + T;
 		const double m0 = s_m0;
-		int pi = s_pi, pj = s_pj;
-		bool had_bad;
-		// two calls so the LDS case keeps ds_* accesses (no flat addressing)
-		if(T <= REPLAY_CAP) replay_wave(nS + T, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad, n);
-		else replay_wave(nS + T, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, writer, b, pi, pj, &had_bad, n);
-		if(writer && lane == 0 && had_bad) ctl->serial_replays++;
-		if(lane == 0) {
-			s_pi = pi;
-			s_pj = pj;
+		const bool lds = T <= REPLAY_CAP;
+		const double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
+		// minQpair's replay.  Without "bad" entries (fresh < stale bound, rare)
+		// every entry contributes its fresh value to the running min, so the
+		// decisions are a prefix min over the entries in scan order: the whole
+		// block folds it (contiguous entries per thread, one block scan); the
+		// pair is the first entry reaching the overall minimum.  Only the
+		// writer block needs the per-entry accept decisions (its (Q, P) writes).
+		int bad = 0;
+		for(int e = tid; e < total; e += TB) bad |= !(x_f[e] >= x_b[e]);
+		if(__syncthreads_or(bad)) {
+			if(wid == 0) {
+				int pi = s_pi, pj = s_pj;
+				bool had_bad;
+				// two calls so the LDS case keeps ds_* accesses (no flat addressing)
+				if(lds) replay_wave(total, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad, n);
+				else replay_wave(total, m0, b.erow, b.ej, b.eb, b.ef, b.eacc, writer, b, pi, pj, &had_bad, n);
+				if(writer && lane == 0 && had_bad) ctl->serial_replays++;
+				if(lane == 0) {
+					s_pi = pi;
+					s_pj = pj;
+				}
+			}
+		} else {
+			__shared__ double s_wm[TB / 64];
+			__shared__ int s_we[TB / 64];
+			const int per = (total + TB - 1) / TB, e0 = tid * per, e1 = e0 + per < total ? e0 + per : total;
+			double tmin = DBL_MAX;
+			for(int e = e0; e < e1; ++e) tmin = x_f[e] < tmin ? x_f[e] : tmin;
+			const double inc = wave_incl_min(tmin);
+			if(lane == 63) s_wm[wid] = inc;
+			__syncthreads();
+			double carry = m0, cm = m0;
+#pragma unroll
+			for(int w = 0; w < TB / 64; ++w) {
+				if(w < wid) carry = s_wm[w] < carry ? s_wm[w] : carry;
+				cm = s_wm[w] < cm ? s_wm[w] : cm;
+			}
+			// the first entry reaching cm (only when it improves on m0)
+			int first = 0x7fffffff;
+			if(cm < m0) {
+				for(int e = e0; e < e1; ++e) {
+					if(x_f[e] == cm) {
+						first = e;
+						break;
+					}
+				}
+			}
+			first = wave_min_int(first);
+			if(lane == 0) s_we[wid] = first;
+			if(writer) {
+				// accept decisions of this thread's entries: b_e < the running min before e
+				double run = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);
+				run = run < carry ? run : carry;
+				const int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
+				for(int e = e0; e < e1; ++e) {
+					const double f = x_f[e];
+					if(x_b[e] < run) {
+						b.Q[x_row[e]] = f;
+						b.P[x_row[e]] = x_j[e];
+					}
+					run = f < run ? f : run;
+				}
+			}
+			__syncthreads();
+			if(tid == 0 && cm < m0) {
+				int fe = s_we[0];
+#pragma unroll
+				for(int w = 1; w < TB / 64; ++w) fe = s_we[w] < fe ? s_we[w] : fe;
+				s_pi = lds ? e_row[fe] : b.erow[fe];
+				s_pj = lds ? e_j[fe] : b.ej[fe];
+			}
 		}
 	}
 	__syncthreads();
@@ -1285,7 +1348,9 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
 		else k_dnj_plan<ET, GEN, DenseRows, false><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
 		kt.mark(CCG_K_FIND);
-		if(g_grid.scan_wave) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		if(g_grid.scan_wave == 2) k_dnj_scan_w<ET, GEN, DenseRows, NoTail, 16><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		else if(g_grid.scan_wave == 3) k_dnj_scan_w<ET, GEN, DenseRows, NoTail, 4><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		else if(g_grid.scan_wave) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
 		kt.mark(CCG_K_REST);
