@@ -33,7 +33,7 @@ struct DenseRows {
 // waves of units run at small n).
 struct DnjGrid {
 	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
-	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = 0;
+	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1;
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
@@ -44,6 +44,12 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
+	}
+	// rescans one unit per wave (k_dnj_scan_w) past 16384 taxa, where the
+	// units are long (measured at 50k: 88 -> 69 us per join); one unit per
+	// block below (10k: 9.4 against 9.8 us).  CCG_SCAN_WAVE=0/1 forces either.
+	int scan_mode(int n) const {
+		return scan_wave >= 0 ? scan_wave : n > 16384 ? 1 : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes

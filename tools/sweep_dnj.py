@@ -47,7 +47,9 @@ for cfg in cfgs:
         _, _, _, sp = dev.tree(D, n, method=method, exact=exact, profile=True)
         parts = [f"{nm} {sp[5 + 2 * c] / sp[4 + 2 * c] / 1e3:.1f}" for c, nm in enumerate(cg.native.KSTAT_NAMES)
                  if sp[4 + 2 * c] and nm != "init"]
-        out.append(f"{'exact' if exact else 'fast'} {best:8.0f} j/s [{', '.join(parts)}]")
+        nk = cg.native.NKSTAT
+        out.append(f"{'exact' if exact else 'fast'} {best:8.0f} j/s [{', '.join(parts)}] serial {sp[6 + 2 * nk]} "
+                   f"chain {sp[7 + 2 * nk]}")
     print(f"{cfg or 'default':40s} " + " | ".join(out) + f" joins {same}; rows {st[0]} cells {st[1]}", flush=True)
     for k, v in old.items():
         if v is None:
