@@ -27,13 +27,14 @@ struct DenseRows {
 #define REPLAY_CAP 2048  // rest entries staged in LDS
 #define JOIN_UPRE 2048   // rest-unit partials k_dnj_join prefetches into LDS
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
+#define PLAN_MAXB 256    // blocks of k_dnj_plan (one listing step of LT * FR rows each)
 
 // Grid of k_dnj_scan: min(ceil(n / scan_div), scan_max).  CCG_SCAN_DIV and
 // CCG_SCAN_MAX override it (tests shrink the grid so that several grid
 // waves of units run at small n).
 struct DnjGrid {
 	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
-	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1;
+	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
@@ -44,6 +45,15 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
+		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
+	}
+	// k_dnj_plan's grid: one listing step of (TBF - 64) FIND_RPT rows per block
+	// (CCG_PLAN_MULTI=0: one block walks every step, the round-2 form)
+	unsigned plan_blocks(int n) const {
+		if(!plan_multi) return 1;
+		const int step = (TBF - 64) * FIND_RPT;
+		const int g = (n - 1 + step - 1) / step;
+		return (unsigned) (g < 1 ? 1 : g > PLAN_MAXB ? PLAN_MAXB : g);
 	}
 	// rescans one unit per wave (k_dnj_scan_w) past 16384 taxa, where the
 	// units are long (measured at 50k: 88 -> 69 us per join); one unit per
@@ -288,6 +298,12 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 	const int top = n - 1;
+	// several blocks (large n): block b lists the rows of step b (LT FR rows
+	// from top - b LT FR down); every block runs the prologue itself, block 0
+	// persists it; entry positions follow from a decoupled look-back over the
+	// lower blocks' counts (ppub, tagged with n)
+	const int nblk = gridDim.x, bid = blockIdx.x, bstep = bid * (LT * FR), stride = nblk * (LT * FR);
+	__shared__ int s_off;
 	TS_ENTRY(1);
 	TS(1, 0);
 	const int lt = tid - 64;   // listing thread (waves 1..)
@@ -316,7 +332,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		for(int d = 0; d < qdelay; ++d) __builtin_amdgcn_s_sleep(32);
 #pragma unroll
 		for(int m = 0; m < FR; ++m) {
-			const int r = top - (m * LT + lt);
+			const int r = top - bstep - (m * LT + lt);
 			qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
 		}
 	} else {
@@ -496,17 +512,17 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			const int t0 = 2 * lane, t1 = 2 * lane + 1;
 			const int r0 = t0 < ntop ? sS[t0] : 0, r1 = t1 < ntop ? sS[t1] : 0;
 			const bool o0 = t0 < ntop && rows.owns(r0), o1 = t1 < ntop && rows.owns(r1);
-			if(t0 < ntop) {
+			if(t0 < ntop && bid == 0) {
 				b.crow[t0] = r0;
 				b.cbnd[t0] = sQS[t0];
 			}
-			if(t1 < ntop) {
+			if(t1 < ntop && bid == 0) {
 				b.crow[t1] = r1;
 				b.cbnd[t1] = sQS[t1];
 			}
 			const long long ctop = wave_sum_int((long long) (o0 ? r0 : 0) + (o1 ? r1 : 0));
 			
-			if(lane == 0) {
+			if(lane == 0 && bid == 0) {
 				if(!first) {   // persist the fold for the kernels after
 					b.Q[j] = Qj;
 					b.P[j] = Pj;
@@ -528,6 +544,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 					atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) ctop);
 					atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) ctop);
 				}
+			}
+			if(lane == 0) {
 				s_done = 0;
 				s_nS = nS;
 				s_ntop = ntop;
@@ -618,12 +636,12 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// ---- the rest of the entry list, after the top part: rows [1, smin) that
 	// are band rows of S or have Q < their bound, with positions and unit
 	// offsets from one prefix over (step, wave) counts
-	int T = ntop;
+	int T = ntop, listed = 0;
 	long long mycells = 0;
-	if(smin > 1) {
+	if(smin > 1 && top - bstep >= 1) {
 		double qn[FR];   // the next step's Q, loaded while this step runs
-		for(int base = top; base >= 1; base -= LT * FR) {
-			if(base != top && wid > 0) {
+		for(int base = top - bstep; base >= 1; base -= stride) {
+			if(base != top - bstep && wid > 0) {
 #pragma unroll
 				for(int m = 0; m < FR; ++m) qv[m] = qn[m];
 			}
@@ -687,10 +705,10 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// the next step's Q, issued after this step's compares (a wait for
 			// them must not hold up the compares) and in flight through the
 			// prefix and the writes
-			if(wid > 0 && base - LT * FR >= 1) {
+			if(wid > 0 && base - stride >= 1) {
 #pragma unroll
 				for(int m = 0; m < FR; ++m) {
-					const int r = base - LT * FR - (m * LT + lt);
+					const int r = base - stride - (m * LT + lt);
 					qn[m] = r >= 1 ? b.Q[r] : DBL_MAX;
 				}
 			}
@@ -715,10 +733,45 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 					pre += c[k];
 				}
 				if(lane == 0) s_cnt = tot;
+				if(nblk > 1) {
+					// publish this block's count, then the lower blocks' counts
+					// (dispatched before this block, they never wait on it)
+					if(lane == 0)
+						__hip_atomic_store(b.ppub + bid, ((unsigned long long) n << 32) | (unsigned) tot,
+						                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					int off = 0;
+					bool stuck = false;
+					for(int g0 = 0; g0 < bid; g0 += 64) {
+						const int g = g0 + lane;
+						unsigned long long u = 0;
+						bool ok = g >= bid;
+						for(int spin = 0;; ++spin) {
+							if(!ok) {
+								u = __hip_atomic_load(b.ppub + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+								ok = (int) (u >> 32) == n;
+							}
+							if(__all(ok)) break;
+							if(spin > (1 << 24)) {
+								stuck = true;
+								break;
+							}
+							__builtin_amdgcn_s_sleep(1);
+						}
+						off += wave_sum_int(g < bid && ok ? (int) (u & 0xffffffffu) : 0);
+					}
+					if(lane == 0) {
+						s_off = off;
+						if(stuck) {   // never expected: stop the loop and report it (tree_run_t)
+							ctl->final_n = -1;
+							ctl->done = 1;
+						}
+					}
+				}
 				TS(1, 13);
 				if(base == top) TS(1, 7);
 			}
 			__syncthreads();
+			if(nblk > 1 && base == top - bstep) T += s_off;
 #pragma unroll
 			for(int m = 0; m < FR; ++m) {
 				if(bm[m] == 0ull) continue;   // uniform (always for wave 0)
@@ -734,9 +787,27 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 			}
 			T += s_cnt;
+			listed += s_cnt;
 			if(base == top) TSW(1, 8, 64);
-			if(base - LT * FR < 1) break;
+			if(base - stride < 1) break;
 			__syncthreads();   // s_mw is reused by the next step
+		}
+	} else if(nblk > 1 && tid == 0) {
+		// nothing to list in this block: its count is 0, and the last block
+		// still needs the lower blocks' counts for the total
+		__hip_atomic_store(b.ppub + bid, (unsigned long long) n << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if(bid == nblk - 1) {
+			int off = 0;
+			for(int g = 0; g < bid; ++g) {
+				unsigned long long u = 0;
+				for(int spin = 0; spin <= (1 << 24); ++spin) {
+					u = __hip_atomic_load(b.ppub + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if((int) (u >> 32) == n) break;
+					__builtin_amdgcn_s_sleep(1);
+				}
+				off += (int) (u >> 32) == n ? (int) (u & 0xffffffffu) : 0;
+			}
+			T += off;
 		}
 	}
 	TS(1, 3);
@@ -746,8 +817,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) mycells);
 	}
 	if(tid == 0) {
-		ctl->T = T;
-		atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) T);   // no read: nothing waits
+		if(bid == nblk - 1) ctl->T = T;   // every entry up to the last block's
+		// the rows this block listed (block 0 also the top part of S)
+		atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) (listed + (bid == 0 ? ntop : 0)));   // no read: nothing waits
 	}
 	TS(1, 4);
 	TS_EXIT(1);

@@ -80,6 +80,7 @@ struct TreeBufs {
 	XsBlk *xblk;                // and each block's summary, crossing and tie records
 	XsCross *xcr;
 	XsTie *xti;
+	unsigned long long *ppub;   // k_dnj_plan with several blocks: each block's tagged entry count (look-back)
 	int maxu;
 };
 

@@ -1281,6 +1281,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
 	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
+	size_t o_pp = take(PLAN_MAXB * 8);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
 	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
@@ -1329,6 +1330,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.xblk = (XsBlk *) (m + o_xb);
 	b.xcr = (XsCross *) (m + o_xc);
 	b.xti = (XsTie *) (m + o_xt);
+	b.ppub = (unsigned long long *) (m + o_pp);
 	b.maxu = (int) maxu;
 	return CCG_OK;
 }
@@ -1345,8 +1347,9 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
 		// one-phase search: k_dnj_plan lists S and the rows below it under the
 		// partner-cell bound, k_dnj_scan rescans them all
-		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
-		else k_dnj_plan<ET, GEN, DenseRows, false><<<1, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
+		const unsigned gp = g_grid.plan_blocks(n);
+		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
+		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
 		kt.mark(CCG_K_FIND);
 		if(g_grid.scan_mode(n)) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
@@ -1543,6 +1546,11 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		}
 	}
 #endif
+	if(h.done && h.final_n < 0) {   // k_dnj_plan's look-back timed out (never expected)
+		hipFree(w.mem);
+		ccg_set_last_msg("k_dnj_plan: a block's look-back over the lower blocks timed out");
+		return CCG_EHIP;
+	}
 	*njoins = h.njoins;
 	*final_n = h.done ? h.final_n : n;
 	if(h.njoins) {
