@@ -953,6 +953,88 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 	}
 }
 
+// k_dnj_scan_w with 16-byte row loads (no missing entries): a lane reads
+// VEC = 16 / sizeof(element) consecutive cells per load (4 floats, 2 doubles),
+// so a float row streams at 1 KB per wave load instead of 256 B; the unit's
+// unaligned head and its tail (fewer than VEC cells each) are scalar.  sD is
+// gathered per cell.  UV vector loads in flight per lane (about 16 cells).
+template <int ET, class Rows, class Tail = NoTail>
+__global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                   int n, Rows rows, int seg, Tail tail = Tail()) {
+	typedef typename Elem<ET>::T T;
+	constexpr int VEC = 16 / (int) sizeof(T), UV = VEC >= 16 ? 1 : 16 / VEC;
+	__shared__ int erow[REPLAY_CAP];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int r0 = b.crow[tid];
+	const int done = ctl->done, Tn = ctl->T;
+	if(done) return;
+	tail.begin(b, n);
+	if(Tn == 0) return;
+	const int umax = dnj_umax(n, seg), nunits = Tn * umax;
+	if((int) blockIdx.x * (TB / 64) >= nunits) return;
+	const bool lds = Tn <= REPLAY_CAP;
+	if(lds) {
+		if(tid < Tn) erow[tid] = r0;
+		for(int e = TB + tid; e < Tn; e += TB) erow[e] = b.crow[e];
+	}
+	__syncthreads();
+	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	for(int u = gw; u < nunits; u += nw) {
+		const int e = u / umax, ua = e * umax;
+		const int r = lds ? erow[e] : b.crow[e];
+		const int c0 = (u - ua) * seg;
+		if(c0 >= r || !rows.owns(r)) continue;   // wave-uniform
+		const int c1 = c0 + seg < r ? c0 + seg : r;
+		const double sDr = b.sD[r];
+		const long long ro = rows.row(r);
+		const T *row = D + ro;
+		const int a = (int) ((VEC - (ro + c0) % VEC) % VEC);
+		const int ca = c0 + a < c1 ? c0 + a : c1;
+		const int nv = (c1 - ca) / VEC, ce = ca + nv * VEC;
+		double q = DBL_MAX;
+		int idx = 0;
+		auto cell = [&](int c) {
+			const double d = Elem<ET>::get(row[c], bs);
+			const double x = qcrit(n, n, d, sDr, b.sD[c]);
+			if(0 <= d && qarg_better(x, c, q, idx)) {
+				q = x;
+				idx = c;
+			}
+		};
+		if(lane < ca - c0) cell(c0 + lane);   // the unaligned head
+		if(lane < c1 - ce) cell(ce + lane);   // the tail
+		for(int v0 = 0; v0 < nv; v0 += 64 * UV) {
+			uint4 w[UV];
+			double sk[UV][VEC];
+#pragma unroll
+			for(int m = 0; m < UV; ++m) {
+				int k = v0 + 64 * m + lane;
+				k = k < nv ? k : nv - 1;
+				w[m] = *(const uint4 *) (row + ca + VEC * k);
+#pragma unroll
+				for(int t = 0; t < VEC; ++t) sk[m][t] = b.sD[ca + VEC * k + t];
+			}
+#pragma unroll
+			for(int m = 0; m < UV; ++m) {
+				const int k = v0 + 64 * m + lane;
+				const T *ev = (const T *) &w[m];
+#pragma unroll
+				for(int t = 0; t < VEC; ++t) {
+					const int c = ca + VEC * k + t;
+					const double d = Elem<ET>::get(ev[t], bs);
+					const double x = qcrit(n, n, d, sDr, sk[m][t]);
+					const bool take = k < nv && 0 <= d && qarg_better(x, c, q, idx);
+					q = take ? x : q;
+					idx = take ? c : idx;
+				}
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		if(lane == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, q, idx);
+	}
+}
+
 // ------------------------------------------------------------------ DNJ fold
 // Rows with many units (large n): each rest entry's unit partials folded once,
 // one wave per entry, into (rf, rj); k_dnj_join then reads one pair per entry

@@ -36,6 +36,8 @@ for k in prefixes:
     del loc
     torch.cuda.empty_cache()
     cls = {nt.KSTAT_NAMES[c]: round(st[5 + 2 * c] / 1e9, 3) for c in range(N) if st[4 + 2 * c]}
-    print(json.dumps({"n": n, "joins": len(j), "seconds": round(dt, 2), "exact": exact,
+    import hashlib
+    h = hashlib.sha256(j.tobytes()).hexdigest()[:12]
+    print(json.dumps({"n": n, "joins": len(j), "seconds": round(dt, 2), "exact": exact, "sha": h,
                       "rows": int(st[0]), "cells": int(st[1]), "serial_sums": int(st[6 + 2 * N]),
                       "chain_sums": int(st[7 + 2 * N]), "class_s": cls}), flush=True)
