@@ -884,7 +884,9 @@ def main():
     ap.add_argument("--shard-n", type=int, default=100_000)
     ap.add_argument("--shard-joins", type=int, default=64)
     ap.add_argument("--dnj-shard-n", type=int, default=200_000)
-    ap.add_argument("--dnj-shard-joins", type=int, default=0, help="0: the whole configs[3] tree")
+    ap.add_argument("--dnj-shard-joins", type=int, default=20_000,
+                    help="joins of the configs[3] tree to time (0: the whole tree; the rescans per join grow "
+                         "along this tree, DESIGN.md 4)")
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
     args = ap.parse_args()
@@ -1025,7 +1027,7 @@ def main():
         wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
         wd.daemon = True
         wd.start()
-        log("configs[3]: the whole DNJ tree of one 200k float matrix")
+        log(f"configs[3]: DNJ on one 200k float matrix ({args.dnj_shard_joins or 'all'} joins)")
         try:
             extras["dnj_sharded"] = dnj_shard_extra(dev, torch, rank=rank, world=world,
                                                     dist=dist if world > 1 else None, coll=coll,
