@@ -55,11 +55,14 @@ struct DnjGrid {
 		const int g = (n - 1 + step - 1) / step;
 		return (unsigned) (g < 1 ? 1 : g > PLAN_MAXB ? PLAN_MAXB : g);
 	}
-	// rescans one unit per wave (k_dnj_scan_w) past 16384 taxa, where the
-	// units are long (measured at 50k: 88 -> 69 us per join); one unit per
-	// block below (10k: 9.4 against 9.8 us).  CCG_SCAN_WAVE=0/1 forces either.
+	// rescans one unit per wave past 16384 taxa, where the units are long:
+	// 16-byte row loads (k_dnj_scan_v, mode 4; the GEN form k_dnj_scan_w,
+	// mode 1); one unit per block below (k_dnj_scan, mode 0).  Measured per
+	// join at 50k (headline data): 88.4 (block) -> 72.0 (wave) -> 66.7 us
+	// (wave, 16-byte loads); 10k: 9.4 (block) against 9.8 us (wave).
+	// CCG_SCAN_WAVE=0/1/4 forces a form.
 	int scan_mode(int n) const {
-		return scan_wave >= 0 ? scan_wave : n > 16384 ? 1 : 0;
+		return scan_wave >= 0 ? scan_wave : n > 16384 ? 4 : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
