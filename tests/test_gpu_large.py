@@ -224,3 +224,28 @@ def test_config4_pipeline_200k_world1_exact(dev, monkeypatch):
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "configs[4] pipeline 200k exact prefix")
+
+
+@pytest.mark.parametrize("env", ["", "CCG_SCAN_WAVE=1", "CCG_SCAN_WAVE=0 CCG_PLAN_MULTI=0"])
+def test_dnj_large_n_kernels_prefix(dev, monkeypatch, env):
+    """The large-n forms of the DNJ search (n > 16384): k_dnj_plan over
+    several blocks with the look-back for entry positions, the wave-per-unit
+    rescans with 16-byte row loads (default), the scalar wave form, and the
+    round-2 forms (one plan block, one unit per block): a 1500-join prefix of
+    a 33k Euclidean tree against the oracle (minQpair dnj.c:43-128)."""
+    import torch
+    import ccphylo_amd as cg
+    from oracle import pyoracle
+    from tools.synth import euclid_shard_dev
+    for kv in env.split():
+        k, v = kv.split("=")
+        monkeypatch.setenv(k, v)
+    n, k = 33_000, 1500
+    D = euclid_shard_dev(torch, n, 0, 1, seed=9)   # world 1: the packed LT
+    host = D.cpu().numpy()
+    got = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
+    del D
+    torch.cuda.empty_cache()
+    ref = pyoracle.tree(host, n, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
+    assert len(ref[0]) == k
+    _same_joins((got[0], 0, 0), (ref[0], 0, 0), f"dnj 33k prefix [{env}]")
