@@ -352,12 +352,14 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     words = (L + 31) // 32
     opw = OPS_PER_WORD_PAIR_PAIRMODE if pair else OPS_PER_WORD_PAIR
     ops = m * words * opw / world   # per GPU
-    mfma = os.environ.get("CCG_DIST_MFMA", "1") != "0"
+    mode_env = os.environ.get("CCG_DIST_MFMA", "2")
+    mfma = mode_env != "0"
     del seqs, incs, Dd, Nd
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "kernel": ("k_snp_mfma_pair" if pair else "k_snp_mfma") if mfma else ("k_snp_tile_pair" if pair else "k_snp_tile"),
+            "kernel": ("k_snp_mfma_pair" if pair else ("k_snp_mfma" if mode_env == "1" else "k_snp_mfma2")) if mfma
+            else ("k_snp_tile_pair" if pair else "k_snp_tile"),
             "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
             else valu_roofline(ops, dt, opw)}
 
@@ -717,9 +719,13 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
 
 
 HEADLINE_STATS = _latest("r03_kernel_stats_headline.csv")
-HSYM = {"dist": "k_snp_mfma", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
-        "dnj_requeue": "k_dnj_requeue", "exact_sum": "k_exact_sum", "dnj_select": "k_dnj_select",
-        "init": "k_init_rows"}
+HSYM = {"dist": ("k_snp_mfma2",), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan"),
+        "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join",), "dnj_requeue": ("k_dnj_requeue",),
+        "exact_sum": ("k_exact_sum",), "dnj_select": ("k_dnj_select",), "init": ("k_init_rows",)}
+
+
+def _base_symbol(name):
+    return re.match(r"(?:void )?([A-Za-z_]\w*)", name).group(1)
 
 
 def headline_profile_evidence(kernel):
@@ -727,22 +733,26 @@ def headline_profile_evidence(kernel):
     kernel, from the committed profiles of the same workload (if present)."""
     import csv
     out = {}
-    sym = HSYM.get(kernel, kernel)
-    try:
+    syms = HSYM.get(kernel, (kernel,))
+    try:   # launch-weighted over the class's kernel forms (e.g. the three scan forms)
+        calls = ns = 0
         with open(HEADLINE_STATS) as f:
             for r in csv.DictReader(f):
-                if r["Name"].replace("void ", "").startswith(sym + "<") or r["Name"] == sym:
-                    out["rocprof_mean_us"] = round(float(r["AverageNs"]) / 1e3, 3)
-                    out["rocprof_calls"] = int(r["Calls"])
-                    break
+                if _base_symbol(r["Name"]) in syms:
+                    calls += int(r["Calls"])
+                    ns += float(r["TotalDurationNs"])
+        if calls:
+            out["rocprof_mean_us"] = round(ns / calls / 1e3, 3)
+            out["rocprof_calls"] = calls
     except (OSError, KeyError, ValueError):
         pass
     try:
         with open(PMC_HEADLINE) as f:
             d = json.load(f)
-        k = d["kernels"].get(sym)
-        if k:
-            out["traffic"] = k["hbm_bytes_per_launch"]
+        ks = [d["kernels"][s] for s in syms if s in d["kernels"]]
+        launches = sum(k["launches"] for k in ks)
+        if launches:
+            out["traffic"] = round(sum(k["hbm_bytes_per_launch"] * k["launches"] for k in ks) / launches, 1)
             out["traffic_source"] = d.get("source")
     except (OSError, KeyError, ValueError):
         pass
@@ -757,7 +767,7 @@ def headline_roofline(n, L, elems, dist_kernel_ms, dist_launches, pst, world):
     engine's own rescanned cells for the scans), against 8 TB/s."""
     kernels = {}
     tf = FLOPS_PER_POSITION_PAIR * elems * float(L) / (dist_kernel_ms / 1e3) / 1e12
-    d = {"kernel": "k_snp_mfma" if world == 1 else "k_snp_mfma_band", "bound": "mfma", "achieved": round(tf, 1),
+    d = {"kernel": "k_snp_mfma2", "bound": "mfma", "achieved": round(tf, 1),
          "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4),
          "frac_of_measured_issue_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
          "step_ms": round(dist_kernel_ms, 2), "launches": dist_launches,
@@ -932,10 +942,10 @@ def main():
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0)
     dt = head["dt"]
-    # dist launches per call (snp_launch: batches of 16384 (tile, slice) items)
-    tiles = (-(-n // 128)) * (-(-n // 128) + 1) // 2
-    roof = headline_roofline(n, L, elems, head["dist_kernel_ms"], max(1, -(-tiles // 16384)) if world == 1 else 1,
-                             pst, world)
+    # dist launches per call (snp_launch_mfma2: 256 x 256 tiles in batches of
+    # 65536; no split-K at the headline's tile count)
+    tiles = (-(-n // 256)) * (-(-n // 256) + 1) // 2 // world
+    roof = headline_roofline(n, L, elems, head["dist_kernel_ms"], max(1, -(-tiles // 65536)), pst, world)
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
         "value": round(m * args.steps / dt, 1),

@@ -3,6 +3,11 @@ corrected as MI355X_MICROARCH.md's HBM section prescribes, written to a JSON
 summary that bench.py reads for roofline.traffic.
 
     python tools/pmc_summary.py gpurun_out/prof_r02 profiles/r02_pmc.json
+    python tools/pmc_summary.py --symbols SRC OUT "what was profiled"
+
+--symbols keys every kernel by its base symbol (template instantiations
+pooled, launch-weighted), reading SRC/pmc_fetch_h and SRC/pmc_write_h: the
+form bench.py's headline roofline reads (profiles/r03_pmc_headline.json).
 
 FETCH_SIZE/WRITE_SIZE are in KiB per dispatch.  FETCH_SIZE counts 64 B per
 128-B memory request on gfx950 (half the bytes of a coalesced streaming
@@ -32,7 +37,32 @@ def per_kernel(path):
     return d
 
 
+def by_symbol(src, out, what):
+    def pooled(path):
+        d = defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            m = re.match(r"(?:void )?(\w+)", r["Kernel_Name"])
+            d[m.group(1)].append(float(r["Counter_Value"]) * 1024.0)
+        return d
+    fetch = pooled(f"{src}/pmc_fetch_h/run_counter_collection.csv")
+    write = pooled(f"{src}/pmc_write_h/run_counter_collection.csv")
+    kernels = {}
+    for k, v in fetch.items():
+        f = 2.0 * statistics.mean(v)
+        w = statistics.mean(write.get(k, [0.0]))
+        kernels[k] = {"launches": len(v), "fetch_bytes_per_launch": round(f, 1),
+                      "write_bytes_per_launch": round(w, 1), "hbm_bytes_per_launch": round(f + w, 1)}
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of {what}; "
+                     f"FETCH_SIZE x2 per MI355X_MICROARCH.md (calibration in profiles/r02_pmc.json)",
+           "kernels": kernels}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--symbols":
+        return by_symbol(sys.argv[2], sys.argv[3], sys.argv[4])
     src, out = sys.argv[1], sys.argv[2]
     fetch = per_kernel(f"{src}/pmc_fetch/run_counter_collection.csv")
     write = per_kernel(f"{src}/pmc_write/run_counter_collection.csv")
