@@ -35,6 +35,7 @@ struct DenseRows {
 struct DnjGrid {
 	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
+	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	void load() {
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
@@ -46,12 +47,18 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
+		if(const char *e = getenv("CCG_PLAN_REGSEL")) plan_regsel = atoi(e);
+		if(const char *e = getenv("CCG_PLAN_FR")) plan_fr = atoi(e) < 1 ? 1 : atoi(e) > FIND_RPT ? FIND_RPT : atoi(e);
 	}
+	// k_dnj_plan's last argument: the Q-load delay (low 16 bits), bit 16 turns
+	// the register S selection off (on with CCG_PLAN_REGSEL=1)
+	// and bits 17-20 the rows per thread per listing step less one (CCG_PLAN_FR)
+	int plan_flags() const { return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17; }
 	// k_dnj_plan's grid: one listing step of (TBF - 64) FIND_RPT rows per block
 	// (CCG_PLAN_MULTI=0: one block walks every step, the round-2 form)
 	unsigned plan_blocks(int n) const {
 		if(!plan_multi) return 1;
-		const int step = (TBF - 64) * FIND_RPT;
+		const int step = (TBF - 64) * plan_fr;
 		const int g = (n - 1 + step - 1) / step;
 		return (unsigned) (g < 1 ? 1 : g > PLAN_MAXB ? PLAN_MAXB : g);
 	}
@@ -305,11 +312,19 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// from top - b LT FR down); every block runs the prologue itself, block 0
 	// persists it; entry positions follow from a decoupled look-back over the
 	// lower blocks' counts (ppub, tagged with n)
-	const int nblk = gridDim.x, bid = blockIdx.x, bstep = bid * (LT * FR), stride = nblk * (LT * FR);
+	// fr (<= FR): rows per thread per listing step, from the flags (small n:
+	// fewer rows per block, more blocks to pull Q in)
+	const int fr = ((qdelay >> 17) & 15) + 1;
+	const int nblk = gridDim.x, bid = blockIdx.x, bstep = bid * (LT * fr), stride = nblk * (LT * fr);
 	__shared__ int s_off;
 	TS_ENTRY(1);
 	TS(1, 0);
 	const int lt = tid - 64;   // listing thread (waves 1..)
+	// every row of the matrix sits in the listing's registers (one block, one
+	// step, no bands: n <= 15361): S is selected from them after the fold, by
+	// the whole block, instead of by wave 0 in dependent steps of loads
+	const bool regsel = !BANDS && nblk == 1 && top <= LT * fr && !((qdelay >> 16) & 1);   // (off by default)
+	qdelay &= 0xffff;
 	double qv[FR];
 	const int rt = top - lt;
 	bool have_rt = false;
@@ -320,23 +335,28 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		// top LT rows (speculative: S is not known yet), and Q of the listed
 		// rows in descending (m, lt) order, the bulk, held back by qdelay x 32 x
 		// 64 cycles so that wave 0's fold loads are not queued behind them
+		// (issue order: the partner index, then Q, then the cells that wait for
+		// the index; loads return in order, so Q issued behind the dependent
+		// cell loads would arrive a round trip later)
 		have_rt = rt >= 1 && rows.owns(rt);
 		if(have_rt) {
 			pr = b.P[rt];
-			pr = pr >= 0 && pr < rt ? pr : 0;
 			sdr = b.sD[rt];
-			dpr = Elem<ET>::get(D[rows.row(rt) + pr], bs);
-			sdp = b.sD[pr];
-			if(GEN) {
-				nr = b.N[rt];
-				np = b.N[pr];
-			}
+			if(GEN) nr = b.N[rt];
 		}
 		for(int d = 0; d < qdelay; ++d) __builtin_amdgcn_s_sleep(32);
 #pragma unroll
 		for(int m = 0; m < FR; ++m) {
 			const int r = top - bstep - (m * LT + lt);
-			qv[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+			const bool v = m < fr && r >= 1;
+			const double x = b.Q[v ? r : 1];
+			qv[m] = v ? x : DBL_MAX;
+		}
+		if(have_rt) {
+			pr = pr >= 0 && pr < rt ? pr : 0;
+			dpr = Elem<ET>::get(D[rows.row(rt) + pr], bs);
+			sdp = b.sD[pr];
+			if(GEN) np = b.N[pr];
 		}
 	} else {
 		// ---- prologue: fold, minPos, m0, S
@@ -415,7 +435,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 #pragma unroll
 		for(int m = 0; m < SEL_RPL; ++m) {
 			const int r = n - 1 - (m * 64 + lane);
-			topQ[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+			topQ[m] = r >= 1 && !regsel ? b.Q[r] : DBL_MAX;
 		}
 		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
 		const int Nm = first ? 0 : b.N[n];
@@ -464,7 +484,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// scan stops short, the rows below the examined ones are left to the
 			// listing under its bound, which never exceeds m0)
 			int cnt = 0, low = n;   // rows >= low examined
-			for(int base = n - 1, step = 0; base >= 1 && cnt < ktop && step < SEL_STEPS; base -= 64 * SEL_RPL, ++step) {
+			for(int base = n - 1, step = 0; !regsel && base >= 1 && cnt < ktop && step < SEL_STEPS;
+			    base -= 64 * SEL_RPL, ++step) {
 				if(step) {
 #pragma unroll
 					for(int m = 0; m < SEL_RPL; ++m) {   // all of the step's loads in flight at once
@@ -571,6 +592,78 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	__syncthreads();
 	TS(1, 1);
 	if(s_done) return;
+	// per (slot, wave) counts in s_mw -> exclusive prefix in scan order, the
+	// total in s_cnt (wave 0; the caller syncs before and after)
+	auto count_prefix = [&]() {
+		constexpr int NC = FR * LW, PER = (NC + 63) / 64;
+		int c[PER], sum = 0;
+#pragma unroll
+		for(int k = 0; k < PER; ++k) {
+			const int x = lane * PER + k;
+			c[k] = x < NC ? s_mw[x] : 0;
+			sum += c[k];
+		}
+		int tot;
+		int pre = wave_excl_scan(sum, &tot);
+#pragma unroll
+		for(int k = 0; k < PER; ++k) {
+			const int x = lane * PER + k;
+			if(x < NC) s_mw[x] = pre;
+			pre += c[k];
+		}
+		if(lane == 0) s_cnt = tot;
+		return tot;
+	};
+	if(regsel) {
+		// ---- S from the registers: the first ktop rows in descending order with
+		// Q < m0 (rows j and i with the fold's values), as wave 0's steps would
+		// find them, every row examined (so a short S leaves nothing to list)
+		const int jsub = s_jsub, isub = s_isub;
+		const double m0 = s_m0;
+		unsigned long long bs_[FR];
+#pragma unroll
+		for(int m = 0; m < FR; ++m) {
+			bs_[m] = 0ull;
+			if(wid > 0) {
+				const int r = top - (m * LT + lt);
+				qv[m] = r == jsub ? s_Qj : r == isub ? s_Qi : qv[m];
+				bs_[m] = __ballot(r >= 1 && qv[m] < m0);
+				if(lane == 0) s_mw[m * LW + wid - 1] = __popcll(bs_[m]);
+			}
+		}
+		__syncthreads();
+		if(wid == 0) count_prefix();
+		__syncthreads();
+		const int tot = s_cnt, nt = tot < ktop ? tot : ktop;
+		long long ctop = 0;
+#pragma unroll
+		for(int m = 0; m < FR; ++m) {
+			if(bs_[m] == 0ull) continue;   // uniform (always for wave 0)
+			const int r = top - (m * LT + lt);
+			const int pos = s_mw[m * LW + wid - 1] + (int) __builtin_amdgcn_mbcnt_hi(
+			                    (unsigned) (bs_[m] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned) bs_[m], 0));
+			if(((bs_[m] >> lane) & 1ull) && pos < ktop) {
+				sS[pos] = r;
+				sQS[pos] = qv[m];
+				b.crow[pos] = r;
+				b.cbnd[pos] = qv[m];
+				ctop += rows.owns(r) ? r : 0;
+			}
+		}
+		ctop = wave_sum_int(ctop);
+		if(lane == 0 && ctop) {
+			atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) ctop);
+			atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) ctop);
+		}
+		__syncthreads();
+		if(tid == 0) {
+			const int sm = nt == ktop ? sS[ktop - 1] : 1;
+			s_nS = s_ntop = nt;
+			s_smin = sm;
+			ctl->smin = sm;
+		}
+		__syncthreads();
+	}
 	const int nS = s_nS, ntop = s_ntop, smin = s_smin, isub = s_isub, jsub = s_jsub;
 	const double m0 = s_m0;
 	// ---- the Q criterion at the partner cell of the top rows, with the fold's
@@ -673,7 +766,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			unsigned long long bm[FR];
 #pragma unroll
 			for(int m = 0; m < FR; ++m) bm[m] = 0ull;
-			const int mlim = (base - 1) / LT + 1 < FR ? (base - 1) / LT + 1 : FR;   // slots holding rows >= 1
+			const int mlim = (base - 1) / LT + 1 < fr ? (base - 1) / LT + 1 : fr;   // slots holding rows >= 1
 #pragma unroll
 			for(int m = 0; m < FR; ++m) {
 				if(m >= mlim) continue;   // uniform; no break: the loop stays unrolled (registers, not scratch)
@@ -712,30 +805,14 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 #pragma unroll
 				for(int m = 0; m < FR; ++m) {
 					const int r = base - stride - (m * LT + lt);
-					qn[m] = r >= 1 ? b.Q[r] : DBL_MAX;
+					qn[m] = m < fr && r >= 1 ? b.Q[r] : DBL_MAX;
 				}
 			}
 			TSW(1, 12, 64);
 			if(base == top) TSW(1, 6, 64);
 			__syncthreads();
 			if(wid == 0) {
-				constexpr int NC = FR * LW, PER = (NC + 63) / 64;
-				int c[PER], sum = 0;
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					c[k] = x < NC ? s_mw[x] : 0;
-					sum += c[k];
-				}
-				int tot;
-				int pre = wave_excl_scan(sum, &tot);
-#pragma unroll
-				for(int k = 0; k < PER; ++k) {
-					const int x = lane * PER + k;
-					if(x < NC) s_mw[x] = pre;
-					pre += c[k];
-				}
-				if(lane == 0) s_cnt = tot;
+				const int tot = count_prefix();
 				if(nblk > 1) {
 					// publish this block's count, then the lower blocks' counts
 					// (dispatched before this block, they never wait on it)

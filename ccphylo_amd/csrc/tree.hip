@@ -150,6 +150,25 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	const bool writer = blockIdx.x == 0;
 	TS_ENTRY(3);
 	TS(3, 0);
+	// updateD's operands for the plan's candidate pair (pos_i, pos_j), loaded
+	// now: when the replay keeps that pair (no rescanned row improves on m0)
+	// the update needs no dependent load after it; sD / N of k in any case
+	const int k = blockIdx.x * TB + tid;
+	int ci = ctl->pos_i, cj = ctl->pos_j;
+	ci = ci < 0 || ci >= n ? 0 : ci;
+	cj = cj < 0 || cj >= ci ? 0 : cj;
+	typename Elem<ET>::T pik = 0, pkj = 0;
+	double sDk = 0;
+	int Nk = 0;
+	if(!general && k < n) {
+		sDk = b.sD[k];
+		Nk = b.N[k];
+		if(k != ci && k != cj) {
+			pik = D[k < ci ? tri(ci) + k : tri(k) + ci];
+			pkj = D[k < cj ? tri(cj) + k : tri(k) + cj];
+		}
+	}
+	const typename Elem<ET>::T pij = D[tri(ci) + cj];
 	// every thread prefetches rest-unit partials (their count is not known yet);
 	// with k_dnj_fold (prefold) the entries' folded pairs instead
 	if(prefold) {
@@ -377,15 +396,12 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		return;
 	}
 	// ---- join: limbLength (nj.c:42) and updateD (nj.c:836)
-	const int k = blockIdx.x * TB + tid;
-	const double Dij = Elem<ET>::get(D[tri(i) + j], bs);
-	double Dik = 0, Dkj = 0, sDk = 0;
-	int Nk = 0;
+	const bool hit = i == ci && j == cj;   // uniform
+	const double Dij = Elem<ET>::get(hit ? pij : D[tri(i) + j], bs);
+	double Dik = 0, Dkj = 0;
 	if(!general && k < n && k != i && k != j) {
-		Dik = Elem<ET>::get(D[k < i ? tri(i) + k : tri(k) + i], bs);
-		Dkj = Elem<ET>::get(D[k < j ? tri(j) + k : tri(k) + j], bs);
-		sDk = b.sD[k];
-		Nk = b.N[k];
+		Dik = Elem<ET>::get(hit ? pik : D[k < i ? tri(i) + k : tri(k) + i], bs);
+		Dkj = Elem<ET>::get(hit ? pkj : D[k < j ? tri(j) + k : tri(k) + j], bs);
 	}
 	if(writer && tid == 0) {
 		double Li, Lj;
@@ -571,6 +587,13 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	if(k < nn) vm = D[tri(nn) + k];   // row nn, moved to i
 	const int Nm0 = b.N[nn];
 	const double sDm0 = b.sD[nn];
+	// column j of the joined pair, read by every thread (not through wave 0's
+	// LDS copy), so these loads overlap wave 0's row sum; row i's writes below
+	// never touch column j
+	int jq = ctl->j;
+	jq = jq < 0 || jq >= n ? 0 : jq;
+	typename Elem<ET>::T vj = 0;
+	if(k < n && k != jq) vj = k < jq ? D[tri(jq) + k] : D[tri(k) + jq];
 	if(wid == 0) {
 		const int done = ctl->done;
 		const bool exact = exact_arg != 0;   // a launch argument: the row sum's loads wait for no ctl load
@@ -620,7 +643,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	int rj = 0, pk = -1, r2j = 0, p2k = -1, fp = 0;
 	if(k < n) {
 		if(k < j) {
-			double d = Elem<ET>::get(D[tri(j) + k], bs);
+			double d = Elem<ET>::get(vj, bs);   // j == jq (ctl->j, read twice)
 			if(0 <= d) {
 				rq = qcrit(Nj, Nk, d, sdj, sDk);
 				rj = k;
@@ -630,7 +653,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			double qk = qk0;
 			int pkk = pkk0;
 			bool upd = false;
-			double d = Elem<ET>::get(D[tri(k) + j], bs);
+			double d = Elem<ET>::get(vj, bs);
 			if(0 <= d) {
 				double q = qcrit(Nj, Nk, d, sdj, sDk);
 				if(q <= qk) {
@@ -1348,8 +1371,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		// one-phase search: k_dnj_plan lists S and the rows below it under the
 		// partner-cell bound, k_dnj_scan rescans them all
 		const unsigned gp = g_grid.plan_blocks(n);
-		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_qdelay);
-		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_qdelay);
+		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
+		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 		kt.mark(CCG_K_FIND);
 		if(g_grid.scan_mode(n) == 4 && !GEN) k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else if(g_grid.scan_mode(n) == 4) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);

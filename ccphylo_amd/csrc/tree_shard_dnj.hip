@@ -651,8 +651,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			// one-phase search (k_dnj_plan): each rank lists the S rows and the
 			// rows below S it owns, under the bound of its own S rows' partner
 			// cells (a subset of S: looser, still exact after the replay)
-			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_qdelay);
-			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_qdelay);
+			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
+			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
 			if(grid.scan_mode(n) == 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
 			else if(grid.scan_mode(n)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
