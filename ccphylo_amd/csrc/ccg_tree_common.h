@@ -39,6 +39,7 @@ struct TreeCtl {
 	long long rows, cells, cells_top, cells_rest;
 	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
 	int rtotal;          // sharded DNJ: replay entries whose accept flags k_shd_join applies
+	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
 };
 
 struct XsBlk;
@@ -387,7 +388,8 @@ __device__ unsigned long long g_samp[256 * 64 * 3];
 // non-finite c, or more crossings / ties than the lists hold returns false
 // and the caller runs the serial chain.  Validated against the serial sum on
 // 3000 random, dyadic tie-heavy and wide-range inputs (tools/sim_exact_sum.py).
-#define XS_CAP 128                // crossings / ties listed per sum
+#define XS_CAP 128                // crossings / ties listed per sum (xs_walk_blocks: crossings)
+#define XS_CAP_T 512              // xs_walk_blocks: ties listed per sum (one per run and join block)
 #define XS_HEAD 64                // elements summed serially first
 
 struct XsCross {
@@ -723,7 +725,17 @@ static __device__ bool exact_sum_w(const double *__restrict__ c, int n, double *
 //   block: joins the rows' records (prefixes over the blocks, checks) and
 //   walks the crossings (xs_walk_blocks), exactly as exact_sum_w's wave 0 does.
 // Any failed check falls back to the serial chain, in the consumer.
-#define XB_CAP 8                  // crossing / tie records per join block
+#define XB_CAP 8                  // crossing records per join block
+#define XB_CAP_T (XB_CAP + 1)     // tie records per join block: one per run (a run's later ties are resolved in place)
+// why the parallel form declined (TreeCtl::xs_why counts, CCG_XS_WHY=1 prints them)
+#define XS_WHY_VALUE 1    // a negative / non-finite contribution, a subnormal or infinite prefix
+#define XS_WHY_NC 2       // more than XB_CAP crossings in one join block
+#define XS_WHY_NT 4       // more than XB_CAP ties in one join block
+#define XS_WHY_STUCK 8    // the look-back for the block's prefix timed out
+#define XS_WHY_EX0 16     // a block's assumed start binade was not the walk's
+#define XS_WHY_CAP 32     // more than XS_CAP crossings / ties in the row
+#define XS_WHY_WALK 64    // the walk's own checks (binade, < 2^53)
+#define XS_NWHY 7
 #define XS_TAG_BITS 20
 
 struct XsBlk {
@@ -754,7 +766,7 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 	const double A = wave_sum_fixed(x[0] + x[1] + x[2] + x[3]);
 	if(lane == 0) __hip_atomic_store(b.xagg + blk, xs_granule(A, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	const int k0 = TB * blk + XW_EL * lane;
-	bool bad = false;
+	bool bad = false, stuck = false;   // (reasons for the consumer's diagnostics: XS_WHY_*)
 #pragma unroll
 	for(int e = 0; e < XW_EL; ++e) {
 		bad |= !(x[e] >= 0.0 && x[e] <= DBL_MAX);
@@ -789,7 +801,7 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 				}
 				if(__all(ok)) break;
 				if(spin > (1 << 22)) {   // bounded: a stuck predecessor costs the serial chain, never a hang
-					bad = true;
+					stuck = true;
 					break;
 				}
 				__builtin_amdgcn_s_sleep(2);
@@ -838,8 +850,15 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 			acc = wave_sum_fixed(run);   // integers below 2^53: exact in any order
 		} else {
 			XsCross *xc = b.xcr + (size_t) blk * XB_CAP;
-			XsTie *xt = b.xti + (size_t) blk * XB_CAP;
+			XsTie *xt = b.xti + (size_t) blk * XB_CAP_T;
 			int from = 0;
+			// a run's first tie in this block is a record (its rounding depends on
+			// the parity of the sum before the block); after any tie the sum is
+			// even (round half to even), so each later tie of the run rounds up
+			// iff the increments since the previous tie plus floor(c/u) are odd,
+			// known here: its true increment goes into the run sum directly
+			bool tied = false;
+			double acc_t = 0;
 			for(unsigned long long f = fm; f; f &= f - 1) {
 				const int L = __ffsll((long long) f) - 1;
 				acc += wave_sum_fixed(lane >= from && lane < L ? run : 0.0);
@@ -861,9 +880,10 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 						}
 						++nc;
 						acc = 0;
-					} else {
-						if((tmL >> e) & 1u) {
-							if(nt < XB_CAP && lane == 0) {
+						tied = false;
+					} else if((tmL >> e) & 1u) {
+						if(!tied) {
+							if(nt < XB_CAP_T && lane == 0) {
 								XsTie r;
 								r.k = k;
 								r.pi = (xs_par(acc) + xs_par(fe) + 1) & 1;
@@ -872,7 +892,14 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 								xt[nt] = r;
 							}
 							++nt;
+							tied = true;
+							acc += fe;
+						} else {
+							const bool up = xs_par(acc - acc_t + (fe - 1.0)) != 0;
+							acc += up ? fe : fe - 1.0;
 						}
+						acc_t = acc;
+					} else {
 						acc += fe;
 					}
 				}
@@ -881,8 +908,9 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 			acc += wave_sum_fixed(lane >= from ? run : 0.0);
 		}
 	}
-	bad |= ep_c == 0x7FF || nc > XB_CAP || nt > XB_CAP;
-	bad = __any(bad);
+	bad |= ep_c == 0x7FF;
+	const int why = (__any(bad) ? XS_WHY_VALUE : 0) | (__any(stuck) ? XS_WHY_STUCK : 0) |
+	                (nc > XB_CAP ? XS_WHY_NC : 0) | (nt > XB_CAP_T ? XS_WHY_NT : 0);   // nc, nt: uniform
 	if(lane == 0) {
 		XsBlk s;
 		s.tail = acc;
@@ -892,7 +920,7 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 		s.tp = xs_par(acc);
 		s.ex0 = ex0;
 		s.eh = eH;
-		s.bad = bad;
+		s.bad = why;
 		s.pad0 = s.pad1 = 0;
 		b.xblk[blk] = s;
 	}
@@ -916,23 +944,23 @@ __device__ __forceinline__ void xs_prefetch(const TreeBufs &b, int G, XsPre &p) 
 		p.blk = b.xblk[g];
 #pragma unroll
 		for(int c = 0; c < XS_PRE_C; ++c) p.cr[c] = b.xcr[(size_t) g * XB_CAP + c];
-		p.ti = b.xti[(size_t) g * XB_CAP];
+		p.ti = b.xti[(size_t) g * XB_CAP_T];
 	}
 }
 
-__device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPre *pre, int n) {
+__device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPre *pre, int n, int *why_out) {
 	(void) n;   // trace stamps only
 	__shared__ XsCross lc[XS_CAP];
 	__shared__ int lcR[XS_CAP], lcT[XS_CAP];   // the crossing's block: Rw, global index of its first tie
-	__shared__ XsTie lt[XS_CAP];
-	__shared__ int ltR[XS_CAP];                // the tie's block: Rw
+	__shared__ XsTie lt[XS_CAP_T];
+	__shared__ int ltR[XS_CAP_T];              // the tie's block: Rw
 	__shared__ double lseg[XS_CAP + 1];
 	const int lane = threadIdx.x & 63;
 	for(int q = lane; q <= XS_CAP; q += 64) lseg[q] = 0.0;
 	const double SH = b.xblk[0].head;
 	const int eH = b.xblk[0].eh;
 	int cob = 0, tob = 0, Rwb = 0;
-	bool bad = false;
+	int why = 0;
 	wave_sync();
 	for(int g0 = 0; g0 < G; g0 += 64) {
 		const int g = g0 + lane;
@@ -943,7 +971,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 			s.tail = 0;
 			s.nc = s.nt = s.tp = s.ex0 = s.bad = 0;
 		}
-		bad |= s.bad || s.nc > XB_CAP || s.nt > XB_CAP;
+		why |= s.bad | (s.nc > XB_CAP ? XS_WHY_NC : 0) | (s.nt > XB_CAP_T ? XS_WHY_NT : 0);
 		int tc, tt, tr;
 		const int co = cob + wave_excl_scan(s.nc, &tc);
 		const int to = tob + wave_excl_scan(s.nt, &tt);
@@ -955,9 +983,9 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 				lcT[co + c] = to;
 			}
 		}
-		for(int t = 0; t < s.nt && t < XB_CAP; ++t) {
-			if(to + t < XS_CAP) {
-				lt[to + t] = pre && g0 == 0 && t == 0 ? pre->ti : b.xti[(size_t) g * XB_CAP + t];
+		for(int t = 0; t < s.nt && t < XB_CAP_T; ++t) {
+			if(to + t < XS_CAP_T) {
+				lt[to + t] = pre && g0 == 0 && t == 0 ? pre->ti : b.xti[(size_t) g * XB_CAP_T + t];
 				ltR[to + t] = Rw;
 			}
 		}
@@ -966,17 +994,20 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 			// the block's first run must have assumed its segment's binade; its
 			// last run's sum goes to its segment (integer-valued: exact in any order)
 			const int want = co == 0 ? eH : co - 1 < XS_CAP ? lc[co - 1].x : -1;
-			bad |= s.ex0 != want;
+			why |= s.ex0 != want ? XS_WHY_EX0 : 0;
 			if(co + s.nc <= XS_CAP) atomicAdd(&lseg[co + s.nc], s.tail);
-			else bad = true;
+			else why |= XS_WHY_CAP;
 		}
 		cob += tc;
 		tob += tt;
 		Rwb += tr;
 	}
 	const int nx = cob, ntot = tob;
-	bad = __any(bad) || nx > XS_CAP - 1 || ntot > XS_CAP;
-	if(bad) return false;
+	why |= nx > XS_CAP - 1 || ntot > XS_CAP_T ? XS_WHY_CAP : 0;
+#pragma unroll
+	for(int q = 0; q < XS_NWHY; ++q) why |= __any((why >> q) & 1) ? 1 << q : 0;
+	*why_out = why;
+	if(why) return false;
 	wave_sync();
 	TS(4, 7);
 	// ---- per segment: its increment for an even / odd start (ties rounded to even)
@@ -1053,6 +1084,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 	}
 #endif
 	*out = S;
+	if(!ok) *why_out = XS_WHY_WALK;
 	return ok;
 }
 
@@ -1070,8 +1102,15 @@ __device__ void row_sum_j_wave(const TreeBufs &b, int n, bool exact, bool genera
 	*chain = false;
 	if(*need) {
 		double r;
-		if(xs_walk_blocks(b, G, &r, exact ? &pre : nullptr, n)) *sd = r;
-		else *chain = true;
+		int why = 0;
+		if(xs_walk_blocks(b, G, &r, exact ? &pre : nullptr, n, &why)) {
+			*sd = r;
+		} else {
+			*chain = true;
+			if(blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+				for(int q = 0; q < XS_NWHY; ++q)
+					if((why >> q) & 1) atomicAdd(&b.ctl->xs_why[q], 1);
+		}
 	}
 }
 

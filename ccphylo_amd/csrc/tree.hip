@@ -1303,7 +1303,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_bq = take(nb * 8), o_br = take(nb * 4), o_sp = take((DNJ_B + 1) * 4), o_cs = take(ncand * 4);
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
-	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
+	size_t o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
 	size_t o_pp = take(PLAN_MAXB * 8);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
@@ -1496,6 +1496,10 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	CCG_CHECK(hipStreamSynchronize(st));
 	float ms = 0;
 	CCG_CHECK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+	if(getenv("CCG_XS_WHY"))   // diagnostics: why exact row sums fell back to the serial chain
+		fprintf(stderr, "xs_why: value %d nc %d nt %d stuck %d ex0 %d cap %d walk %d (chain sums %d of %d)\n",
+		        h.xs_why[0], h.xs_why[1], h.xs_why[2], h.xs_why[3], h.xs_why[4], h.xs_why[5], h.xs_why[6],
+		        h.chain_sums, h.serial_sums);
 #ifdef CCG_TRACE
 	{
 		static unsigned long long tr[256 * NKT * 16];

@@ -483,7 +483,7 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	size_t o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
 	// exact row sums over the join blocks (xs_join_row / xs_walk_blocks)
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xcr = take(nb * XB_CAP * sizeof(XsCross));
-	size_t o_xt = take(nb * XB_CAP * sizeof(XsTie));
+	size_t o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
 	size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll_in->world));
 	char *m;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
