@@ -17,6 +17,12 @@ static double cref, ccur[NK], stages[NK], maxst[NK], its;
 #define NH 4
 static const int HA[NH] = {32, 16, 16, 8}, HB[NH] = {-64, -64, -112, -120};   /* -k: minima of k equal row blocks */
 static double chyb[NH];
+/* H1 (16 top + 64 band rows) with, in addition, the bound from every row
+ * above r's 256-row block: V_k = max(q at k's partner cell, Q_k) (a cell of
+ * row k bounds its fresh minimum), block minima of V (the requeue could
+ * publish them); VB[1]: the same with every row above r (the idea's limit) */
+static double cvb[2];
+static const int32_t *g_P;
 static int cmpq_desc_rows;   /* unused */
 static const double *g_Q;
 static int by_q(const void *a, const void *b) {
@@ -34,6 +40,7 @@ static double fresh_of(const Ltd *D, int r, const double *sD, const int32_t *N, 
 }
 
 static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, const double *Q, int cand) {
+	const int32_t *P = g_P;
 	double m0 = DBL_MAX;
 	if(cand && m0 != Q[cand]) m0 = Q[cand];
 	double *memo = malloc(n * sizeof(double));
@@ -122,6 +129,65 @@ static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, co
 		free(inS);
 		free(cand);
 	}
+	/* H1 + V block minima / every row above */
+	{
+		double *V = malloc(n * sizeof(double)), *bmin = malloc(((n >> 8) + 2) * sizeof(double));
+		for(int k = 0; k < n; ++k) {
+			V[k] = DBL_MAX;
+			if(k >= 1 && P[k] >= 0 && P[k] < k) {
+				const double d = at(D, k, P[k]);
+				if(d >= 0) {
+					const double q = qval(N[k], N[P[k]], d, sD[k], sD[P[k]]);
+					V[k] = q > Q[k] ? q : Q[k];
+				}
+			}
+		}
+		const int nb = (n >> 8) + 1;
+		for(int g = 0; g <= nb; ++g) bmin[g] = DBL_MAX;
+		for(int k = 0; k < n; ++k) if(V[k] < bmin[k >> 8]) bmin[k >> 8] = V[k];
+		for(int g = nb - 1; g >= 0; --g) if(bmin[g + 1] < bmin[g]) bmin[g] = bmin[g + 1];   /* suffix min: blocks >= g */
+		int *cand = malloc(n * sizeof(int)), nc = 0;
+		for(int r = n - 1; r >= 1; --r) if(Q[r] < m0) cand[nc++] = r;
+		char *inS = calloc(n, 1);
+		for(int mode = 0; mode < 2; ++mode) {
+			memset(inS, 0, n);
+			double cells = 0;
+			int A = 16 < nc ? 16 : nc;
+			for(int k = 0; k < A; ++k) inS[cand[k]] = 1;
+			if(nc - A > 0) {
+				const int lowest = A ? cand[A - 1] : n, g = (lowest + 63) / 64;
+				for(int b0 = 0; b0 < lowest; b0 += g) {
+					int best = -1;
+					for(int r = b0; r < b0 + g && r < lowest; ++r)
+						if(r >= 1 && Q[r] < m0 && (best < 0 || Q[r] < Q[best])) best = r;
+					if(best >= 0) inS[best] = 1;
+				}
+			}
+			double bound = m0, vrun = DBL_MAX;
+			int prev = n;
+			for(int k = 0; k < nc; ++k) {
+				int r = cand[k];
+				if(mode == 1) for(int x = prev - 1; x > r; --x) if(V[x] < vrun) vrun = V[x];   /* every row above r */
+				prev = r;
+				double bb = bound;
+				const double vb = mode == 0 ? bmin[(r >> 8) + 1] : vrun;
+				if(vb < bb) bb = vb;
+				if(inS[r]) {
+					double f = fresh_of(D, r, sD, N, memo, have);
+					double v = f > Q[r] ? f : Q[r];
+					cells += r;
+					if(v < bound) bound = v;
+				} else if(Q[r] < bb) {
+					cells += r;
+				}
+			}
+			cvb[mode] += cells;
+		}
+		free(inS);
+		free(cand);
+		free(V);
+		free(bmin);
+	}
 	its += 1;
 	free(memo);
 	free(have);
@@ -130,6 +196,7 @@ static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, co
 int main(int argc, char **argv) {
 	int n = argc > 1 ? atoi(argv[1]) : 2000;
 	int every = argc > 2 ? atoi(argv[2]) : 1;
+	const int maxj = argc > 3 ? atoi(argv[3]) : 1 << 30;   /* stop (and print) after this many joins */
 	double *Dm = malloc((size_t) n * (n - 1) / 2 * sizeof(double));
 	srand(1);
 	double *pts = malloc((size_t) n * 8 * sizeof(double));
@@ -143,6 +210,7 @@ int main(int argc, char **argv) {
 	Ltd D = {8, 1.0, Dm};
 	double *sD = malloc(n * sizeof(double)), *Q = malloc(n * sizeof(double));
 	int32_t *N = malloc(n * sizeof(int32_t)), *P = malloc(n * sizeof(int32_t));
+	g_P = P;
 	init_sums(&D, n, sD, N);
 	init_hnj(&D, n, sD, N, Q, P);
 	int j = min_q_row(Q, n);
@@ -161,13 +229,15 @@ int main(int argc, char **argv) {
 		int mj = dnj_pop_arrange(&D, &n, sD, N, Q, P, i);
 		j = mj == n ? mi : mi == n ? mj : min_pos(Q, mi, mj);
 		++joins;
-		if(joins % (n0 / 8) == 0) {
+		if(joins % (n0 / 8) == 0 || joins == maxj) {
 			printf("  after %d joins: ref cells/join %.0f", joins, cref / its);
 			for(int k = 0; k < NK; ++k) printf(" | %d,%d,%d x%.2f st %.2f (max %.0f)", Seqs[k][0], Seqs[k][1], Seqs[k][2], ccur[k] / cref, stages[k] / its, maxst[k]);
 			for(int h = 0; h < NH; ++h) printf(" | H%d+%d x%.2f", HA[h], HB[h], chyb[h] / cref);
+			printf(" | H16+64+Vblk x%.2f | H16+64+Vall x%.2f", cvb[0] / cref, cvb[1] / cref);
 			printf("\n");
 			fflush(stdout);
 		}
+		if(joins == maxj) break;
 	}
 	return 0;
 }
