@@ -278,15 +278,35 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			const bool lds = T <= REPLAY_CAP;
 			int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
 			double *x_b = lds ? e_b : b.eb, *x_f = lds ? e_f : b.ef;
-			for(int e = 256 + tid; e < T; e += TB) {
+			// prefolded (large n, many entries): 8 entries per thread per step, all
+			// of their loads in flight together
+			for(int e0 = 256 + tid; prefold && e0 < T; e0 += 8 * TB) {
+				int r[8], idx[8], sl[8];
+				double bnd[8], q[8];
+#pragma unroll
+				for(int m = 0; m < 8; ++m) {
+					const int e = e0 + m * TB < T ? e0 + m * TB : e0;
+					r[m] = b.crow[e];
+					bnd[m] = b.cbnd[e];
+					q[m] = e < JOIN_UPRE ? lq[e] : b.rf[e];
+					idx[m] = e < JOIN_UPRE ? lj[e] : b.rj[e];
+					sl[m] = s_merged ? b.cslot[e] : s_nS + e;
+				}
+#pragma unroll
+				for(int m = 0; m < 8; ++m) {
+					if(e0 + m * TB >= T) continue;
+					x_row[sl[m]] = r[m];
+					x_j[sl[m]] = idx[m];
+					x_b[sl[m]] = bnd[m];
+					x_f[sl[m]] = q[m];
+				}
+			}
+			for(int e = 256 + tid; !prefold && e < T; e += TB) {
 				const int r = b.crow[e];
 				const double bnd = b.cbnd[e];
 				double q = DBL_MAX;
 				int idx = 0;
-				if(prefold) {
-					q = e < JOIN_UPRE ? lq[e] : b.rf[e];
-					idx = e < JOIN_UPRE ? lj[e] : b.rj[e];
-				} else if(e * dnj_umax(n, seg) + dcdiv(r, seg) <= JOIN_UPRE) {
+				if(e * dnj_umax(n, seg) + dcdiv(r, seg) <= JOIN_UPRE) {
 					const int ua = e * dnj_umax(n, seg), ub = ua + dcdiv(r, seg);
 					for(int u = ua; u < ub; ++u) {
 						if(qarg_better(lq[u], lj[u], q, idx)) {
@@ -319,8 +339,51 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		// block folds it (contiguous entries per thread, one block scan); the
 		// pair is the first entry reaching the overall minimum.  Only the
 		// writer block needs the per-entry accept decisions (its (Q, P) writes).
+		// each thread's contiguous chunk [e0, e1): in registers up to RP entries
+		// (one round trip when the entries are in HBM), else in steps of 8
+		constexpr int RP = 16;
+		const int per = (total + TB - 1) / TB, e0 = tid * per, e1 = e0 + per < total ? e0 + per : total;
+		const bool inreg = per >= 2 && per <= RP;   // uniform (one entry per thread: the plain loops)
+		double rf[RP], rb[RP];
 		int bad = 0;
-		for(int e = tid; e < total; e += TB) bad |= !(x_f[e] >= x_b[e]);
+		double tmin = DBL_MAX;
+		if(inreg) {
+#pragma unroll
+			for(int m = 0; m < RP; ++m) {
+				rf[m] = DBL_MAX;
+				rb[m] = 0;
+				if(m < per) {   // uniform
+					const int e = e0 + m < e1 ? e0 + m : 0;
+					rf[m] = x_f[e];
+					rb[m] = x_b[e];
+				}
+			}
+#pragma unroll
+			for(int m = 0; m < RP; ++m) {
+				if(e0 + m >= e1) continue;
+				bad |= !(rf[m] >= rb[m]);
+				tmin = rf[m] < tmin ? rf[m] : tmin;
+			}
+		} else {
+			for(int e = e0; e < e1; e += 8) {
+				double f8[8], b8[8];
+#pragma unroll
+				for(int m = 0; m < 8; ++m) {
+					f8[m] = DBL_MAX;
+					b8[m] = 0;
+					if(e + m < e1) {
+						f8[m] = x_f[e + m];
+						b8[m] = x_b[e + m];
+					}
+				}
+#pragma unroll
+				for(int m = 0; m < 8; ++m) {
+					if(e + m >= e1) continue;
+					bad |= !(f8[m] >= b8[m]);
+					tmin = f8[m] < tmin ? f8[m] : tmin;
+				}
+			}
+		}
 		if(__syncthreads_or(bad)) {
 			if(wid == 0) {
 				int pi = s_pi, pj = s_pj;
@@ -337,9 +400,6 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 		} else {
 			__shared__ double s_wm[TB / 64];
 			__shared__ int s_we[TB / 64];
-			const int per = (total + TB - 1) / TB, e0 = tid * per, e1 = e0 + per < total ? e0 + per : total;
-			double tmin = DBL_MAX;
-			for(int e = e0; e < e1; ++e) tmin = x_f[e] < tmin ? x_f[e] : tmin;
 			const double inc = wave_incl_min(tmin);
 			if(lane == 63) s_wm[wid] = inc;
 			__syncthreads();
@@ -352,10 +412,16 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 			// the first entry reaching cm (only when it improves on m0)
 			int first = 0x7fffffff;
 			if(cm < m0) {
-				for(int e = e0; e < e1; ++e) {
-					if(x_f[e] == cm) {
-						first = e;
-						break;
+				if(inreg) {
+#pragma unroll
+					for(int m = RP - 1; m >= 0; --m)
+						if(e0 + m < e1 && rf[m] == cm) first = e0 + m;
+				} else {
+					for(int e = e0; e < e1; ++e) {
+						if(x_f[e] == cm) {
+							first = e;
+							break;
+						}
 					}
 				}
 			}
@@ -366,13 +432,35 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				double run = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);
 				run = run < carry ? run : carry;
 				const int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
-				for(int e = e0; e < e1; ++e) {
-					const double f = x_f[e];
-					if(x_b[e] < run) {
-						b.Q[x_row[e]] = f;
-						b.P[x_row[e]] = x_j[e];
+				if(inreg) {
+					int rr[RP], rj[RP];
+#pragma unroll
+					for(int m = 0; m < RP; ++m) {
+						rr[m] = rj[m] = 0;
+						if(m < per) {   // uniform
+							const int e = e0 + m < e1 ? e0 + m : 0;
+							rr[m] = x_row[e];
+							rj[m] = x_j[e];
+						}
 					}
-					run = f < run ? f : run;
+#pragma unroll
+					for(int m = 0; m < RP; ++m) {
+						if(e0 + m >= e1) continue;
+						if(rb[m] < run) {
+							b.Q[rr[m]] = rf[m];
+							b.P[rr[m]] = rj[m];
+						}
+						run = rf[m] < run ? rf[m] : run;
+					}
+				} else {
+					for(int e = e0; e < e1; ++e) {
+						const double f = x_f[e];
+						if(x_b[e] < run) {
+							b.Q[x_row[e]] = f;
+							b.P[x_row[e]] = x_j[e];
+						}
+						run = f < run ? f : run;
+					}
 				}
 			}
 			__syncthreads();

@@ -15,12 +15,14 @@
 //      its own S rows and its own rows below S with Q under the bound; any
 //      other row is provably skipped by dnj.c:88;
 //   2. k_dnj_scan rescans the listed units; its tail (RecTail) folds each
-//      row's units into a record indexed by row -- a bitmap of the listed
-//      rows, f64 fresh q, i32 j -- and copies row n-1 (the pop moves it to
-//      slot i, dnj.c:817 / matrix.c:518) behind the records; the other ranks
-//      hold zeros in every byte they do not own;
-//      -> allreduce-sum of records + row n-1: a gather, exact (the 8 rows of
-//      a bitmap byte are one band: one owner, no carries);
+//      row's units into a record of the rank's own rows, indexed by the
+//      row's position among them -- one bit byte per owned band, f64 fresh
+//      q, i32 j -- and the owner of row n-1 (the pop moves it to slot i,
+//      dnj.c:817 / matrix.c:518) copies it out;
+//      -> allgather of the ranks' record slots (each rank sends only its own
+//      rows' records: half the ring bytes of the round-2 allreduce-as-gather
+//      over dense row-indexed arrays) and a broadcast of row n-1 from its
+//      owner;
 //   3. k_shd_pick: every block replays minQpair's accept/reject decisions
 //      over the listed rows in descending order (replay_wave); rows that the
 //      serial scan would skip have bound >= running min, so the replay
@@ -42,14 +44,29 @@
 #include "ccg_shard.h"
 
 // ------------------------------------------------------------------ records
-// [bitmap of rows (u64 words)][f64 fresh q][i32 fresh j], laid out for size n
+// Per join, one rank's slot: [a bit byte per owned band (row r of band g is
+// bit r % 8 of byte g / world)][f64 fresh q][i32 fresh j] of its owned rows
+// by position (g / world) * 8 + r % 8, sized for the rank that owns the most
+// bands at size n; the allgather lays the slots side by side, rank order.
+static_assert(SB == 8, "one bit byte per shard band");
+struct RecSlot {
+	size_t f_off, j_off, bytes;
+};
+static __host__ __device__ inline RecSlot rec_slot(int n, int world) {
+	const int nb = (n + SB - 1) / SB, omb = (nb + world - 1) / world;
+	RecSlot s;
+	s.f_off = ((size_t) omb + 15) & ~(size_t) 15;
+	s.j_off = s.f_off + (size_t) omb * SB * 8;
+	s.bytes = (s.j_off + (size_t) omb * SB * 4 + 15) & ~(size_t) 15;
+	return s;
+}
+// a row's owner and position among the owner's rows
+static __host__ __device__ inline int rec_owner(int r, int world) { return (r / SB) % world; }
+static __host__ __device__ inline int rec_pos(int r, int world) { return (r / SB) / world * SB + r % SB; }
+
+// initHNJ's gather (once): [bitmap of rows (u64 words)][f64 q][i32 j], dense
 static __host__ __device__ inline size_t rec_bits_bytes(int n) { return (size_t) ((n + 63) / 64) * 8; }
 static __host__ __device__ inline size_t rec_bytes(int n) { return rec_bits_bytes(n) + (size_t) n * 12; }
-// row n-1 behind the records (16-byte aligned), n-1 elements of es bytes
-static __host__ __device__ inline size_t rec_xm_off(int n) { return (rec_bytes(n) + 15) & ~(size_t) 15; }
-static __host__ __device__ inline size_t rec_all_bytes(int n, int es) {
-	return rec_xm_off(n) + (((size_t) (n - 1) * es + 15) & ~(size_t) 15);
-}
 
 struct RecView {
 	unsigned *bits;
@@ -77,13 +94,13 @@ template <int ET>
 struct RecTail {
 	const typename Elem<ET>::T *D;
 	Shard sh;
-	void *R;
+	void *R;                          // this rank's record slot
+	typename Elem<ET>::T *xm;         // row n-1 (its owner fills it; broadcast after)
 	unsigned *cnt;   // n0 zeros
 	__device__ void begin(const TreeBufs &, int n) const {
-		typename Elem<ET>::T *xm = (typename Elem<ET>::T *) ((char *) R + rec_xm_off(n));
-		const bool own = sh.owns(n - 1);
-		const typename Elem<ET>::T *row = D + (own ? sh.off(n - 1) : 0);
-		for(int k = blockIdx.x * TB + threadIdx.x; k < n - 1; k += gridDim.x * TB) xm[k] = own ? row[k] : 0;
+		if(!sh.owns(n - 1)) return;
+		const typename Elem<ET>::T *row = D + sh.off(n - 1);
+		for(int k = blockIdx.x * TB + threadIdx.x; k < n - 1; k += gridDim.x * TB) xm[k] = row[k];
 	}
 	__device__ void unit(const TreeBufs &b, int n, int u, int ua, int ub, int r, double q, int j) const {
 		if(ub - ua > 1) {
@@ -104,10 +121,11 @@ struct RecTail {
 			}
 			__hip_atomic_store(cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
-		const RecView v = rec_view(R, n);
-		v.f[r] = q;
-		v.j[r] = j;
-		atomicOr(&v.bits[r >> 5], 1u << (r & 31));
+		const RecSlot s = rec_slot(n, sh.world);
+		const int o = rec_pos(r, sh.world), ob = o / SB;
+		((double *) ((char *) R + s.f_off))[o] = q;
+		((int *) ((char *) R + s.j_off))[o] = j;
+		atomicOr((unsigned *) R + (ob >> 2), 1u << ((ob & 3) * 8 + (r & 7)));
 	}
 };
 
@@ -145,7 +163,25 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 	__shared__ int s_i, s_j;
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x;
-	const RecView v = rec_view(R, n);
+	// the gathered slots (R: world x rs.bytes)
+	const int W = sh.world;
+	const RecSlot rs = rec_slot(n, W);
+	const int nbands = (n + SB - 1) / SB;
+	auto rbits = [&](int w) -> unsigned {   // rows 32w .. 32w + 31: bands 4w .. 4w + 3
+		unsigned x = 0;
+#pragma unroll
+		for(int t = 0; t < 4; ++t) {
+			const int g = 4 * w + t;
+			if(g < nbands) x |= (unsigned) ((const unsigned char *) R)[(size_t) (g % W) * rs.bytes + g / W] << (8 * t);
+		}
+		return x;
+	};
+	auto rf = [&](int r) {
+		return ((const double *) ((const char *) R + (size_t) rec_owner(r, W) * rs.bytes + rs.f_off))[rec_pos(r, W)];
+	};
+	auto rj = [&](int r) {
+		return ((const int *) ((const char *) R + (size_t) rec_owner(r, W) * rs.bytes + rs.j_off))[rec_pos(r, W)];
+	};
 	// rows [1, n) with their bit set; thread t owns a contiguous run of
 	// bitmap words, the highest runs first (the first word and the replay's
 	// inputs are loaded before the stop test: one round trip fewer)
@@ -157,7 +193,7 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 		return x;
 	};
 	const int wfirst = nw - 1 - tid * per;
-	const unsigned x0 = wfirst >= 0 ? v.bits[wfirst] : 0u;
+	const unsigned x0 = wfirst >= 0 ? rbits(wfirst) : 0u;
 	const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
 	const double m0 = ctl->m0;
 	if(ctl->done) return;
@@ -165,7 +201,7 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 	int cnt = 0;
 	for(int q = 0; q < per; ++q) {
 		const int w = nw - 1 - (tid * per + q);
-		if(w >= 0) cnt += __popc(word(w, q == 0 ? x0 : v.bits[w]));
+		if(w >= 0) cnt += __popc(word(w, q == 0 ? x0 : rbits(w)));
 	}
 	int total;
 	int pos = block_excl_scan(cnt, s_scan, &total);
@@ -176,7 +212,7 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 	for(int q = 0; q < per; ++q) {
 		const int w = nw - 1 - (tid * per + q);
 		if(w < 0) break;
-		unsigned x = word(w, q == 0 ? x0 : v.bits[w]);
+		unsigned x = word(w, q == 0 ? x0 : rbits(w));
 		while(x) {
 			const int bit = 31 - __clz((int) x);
 			x &= ~(1u << bit);
@@ -189,8 +225,8 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 	for(int e = tid; e < total; e += PICK_T) {
 		const int r = x_row[e];
 		x_b[e] = b.Q[r];
-		x_f[e] = v.f[r];
-		x_j[e] = v.j[r];
+		x_f[e] = rf(r);
+		x_j[e] = rj(r);
 	}
 	__syncthreads();
 	PTS(3);
@@ -457,15 +493,9 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 			}
 		}
 	}
-	// records of the next join (size n - 1): bitmap words, q and j
-	if(k < n) {
-		const RecView v = rec_view(R, nn);
-		if((k & 63) == 0) ((unsigned long long *) v.bits)[k >> 6] = 0;
-		if(k < nn) {
-			v.f[k] = 0;
-			v.j[k] = 0;
-		}
-	}
+	// this rank's record slot for the next join: its bit bytes (q and j are
+	// read only where a bit is set)
+	if((size_t) k * 4 < rec_slot(n, sh.world).f_off) ((unsigned *) R)[k] = 0;
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
 	// fold); only when the next S has a band part
@@ -570,7 +600,9 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		sz += (bytes + 255) & ~(size_t) 255;
 		return off;
 	};
-	const size_t o_R = take(rec_all_bytes(n0, ET)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	const RecSlot rs0 = rec_slot(n0, coll->world);
+	const size_t o_R = take(rec_bytes(n0)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
+	const size_t o_Sl = take(rs0.bytes), o_G = take((size_t) coll->world * rs0.bytes);
 	const size_t o_Xj = take((size_t) n0 * ET + 8), o_pf = take((size_t) n0), o_pa = take((size_t) PICK_MAXB * n0), o_pc = take((size_t) n0 * 4);
 	const size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll->world));
 	char *m = NULL;
@@ -581,7 +613,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	size_t hcap = sh_init_host_bytes(n0, coll->world);
 	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
-	if(rec_all_bytes(n0, ET) > hcap) hcap = rec_all_bytes(n0, ET);
+	if(rec_bytes(n0) > hcap) hcap = rec_bytes(n0);
+	if((size_t) coll->world * rs0.bytes > hcap) hcap = (size_t) coll->world * rs0.bytes;
 	if(coll->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
 		hipFree(m);
 		hipFree(w.mem);
@@ -591,7 +624,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	CollRun cr = {coll, st, h, &kt};
 	DnjGrid grid;
 	grid.load();
-	void *R = m + o_R;
+	void *R = m + o_R, *Sl = m + o_Sl, *G = m + o_G;   // initHNJ's gather; this rank's record slot; the gathered slots
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm), *Xj = (T *) (m + o_Xj);
 	ShInitStat istat = {0, 0};
 	unsigned char *pflag = (unsigned char *) (m + o_pf), *pacc = (unsigned char *) (m + o_pa);
@@ -645,7 +678,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
 			const unsigned gn = cdiv(n, TB), gp = cdiv(n, PICK_T) < PICK_MAXB ? cdiv(n, PICK_T) : PICK_MAXB;
-			T *Xmr = (T *) ((char *) R + rec_xm_off(n));   // row n-1, gathered with the records
+			T *Xmr = Xm;   // row n-1, broadcast by its owner
 			const unsigned gc = grid.scan(n);
 			const int seg = grid.seg(n);
 			// one-phase search (k_dnj_plan): each rank lists the S rows and the
@@ -654,18 +687,19 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
-			if(grid.scan_mode(n) == 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
-			else if(grid.scan_mode(n)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
-			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, R, pcnt});
+			if(grid.scan_mode(n) == 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			else if(grid.scan_mode(n)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
 			kt.mark(CCG_K_REST);
-			SD_TRY(cr.allreduce(R, rec_all_bytes(n, ET)));
-			k_shd_pick<ET><<<gp, PICK_T, 0, st>>>(D, b, n, sh, R, X, pacc, pflag, n0, dbg);
+			SD_TRY(cr.allgather(Sl, G, rec_slot(n, sh.world).bytes));
+			SD_TRY(cr.bcast(Xm, Xm, (size_t) (n - 1) * ET, rec_owner(n - 1, sh.world)));
+			k_shd_pick<ET><<<gp, PICK_T, 0, st>>>(D, b, n, sh, G, X, pacc, pflag, n0, dbg);
 			kt.mark(CCG_K_UPDATE);
 			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
 			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj, pflag);
 			kt.mark(CCG_K_UPDATE);
-			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
-			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, R);
+			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, Sl);
+			else k_shd_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, Sl);
 			kt.mark(CCG_K_REQUEUE);
 			SD_HIP(hipGetLastError());
 			launches += 5;
