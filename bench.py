@@ -137,6 +137,8 @@ def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan):
         return s * cells_select + 8.0 * sn
     if kernel == "dnj_scan":        # one GPU: every rescanned D cell (S and the rows below it) + the sD vector once
         return s * (cells_select + cells_scan) + 8.0 * sn
+    if kernel == "dnj_scan_ref":    # the cells the reference's minQpair rule rescans (cells_scan)
+        return s * cells_scan + 8.0 * sn
     if kernel == "dnj_find":        # k_dnj_plan: Q of every row; P, the partner cell, sD of row and partner
         return 8.0 * sn + (20.0 + s) * float(sum(min(k - 1, 960) for k in sizes))   # for the top rows
     if kernel == "nj_argmin":       # every LT cell + sD
@@ -186,6 +188,21 @@ def rocprof_mean_us(kernel):
     return None
 
 
+def refrule_scan(stats, n, s, launches, sec_per_launch):
+    """The scan's rate by SURVEY 8(d)'s unit: the cells the reference's own
+    minQpair rule rescans (the engine counts them from its replay decisions,
+    stats[11 + 2 NKSTAT]) instead of the engine's speculative cells."""
+    K = len(KNAMES)
+    if len(stats) < 12 + 2 * K or not stats[11 + 2 * K]:
+        return {}
+    ab = algorithmic_bytes_total("dnj_scan_ref", n, s, 0, stats[11 + 2 * K]) / launches
+    return {"reference_rule_rows": int(stats[10 + 2 * K]), "reference_rule_cells": int(stats[11 + 2 * K]),
+            "engine_cells": int(stats[4 + 2 * K] + stats[5 + 2 * K]),
+            "engine_over_reference_cells": round((stats[4 + 2 * K] + stats[5 + 2 * K]) / stats[11 + 2 * K], 3),
+            "algorithmic_bytes_per_launch_reference_rule": round(ab, 1),
+            "frac_reference_rule": round(ab / sec_per_launch / 1e9 / HBM_PEAK_GBS, 5)}
+
+
 def roofline(stats, n, s):
     """Dominant kernel (largest total device time) of a profiled run."""
     per = {}
@@ -211,6 +228,8 @@ def roofline(stats, n, s):
         if rp:
             kernels[k]["rocprof_mean_us"] = rp
             kernels[k]["frac_rocprof_duration"] = round(ab / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
+        if k == "dnj_scan":
+            kernels[k].update(refrule_scan(stats, n, s, c, ev))
     traffic, src = pmc_traffic(name)
     out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -558,7 +577,9 @@ def refrule_cells(dev, torch, seqs, incs, n, L, W, prefix, threads):
     D = torch.empty(m, dtype=torch.float64, device="cuda")
     dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
     host = D.cpu().numpy()
-    j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=prefix)
+    j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, max_joins=prefix,
+                                 profile=True)
+    K = len(KNAMES)
     del D
     torch.cuda.empty_cache()
     t0 = time.perf_counter()
@@ -570,6 +591,7 @@ def refrule_cells(dev, torch, seqs, incs, n, L, W, prefix, threads):
     return {"joins": prefix, "engine_rows": int(st[0]), "engine_cells": int(st[1]),
             "reference_rule_rows": int(rst[0]), "reference_rule_cells": int(rst[1]),
             "engine_over_reference_cells": round(int(st[1]) / max(int(rst[1]), 1), 3),
+            "engine_counter_equals_oracle": (int(st[10 + 2 * K]), int(st[11 + 2 * K])) == (int(rst[0]), int(rst[1])),
             "joins_identical_to_oracle": same, "oracle_s": round(dt, 1)}
 
 
@@ -789,6 +811,8 @@ def headline_roofline(n, L, elems, dist_kernel_ms, dist_launches, pst, world):
                  "frac": round(gbs / HBM_PEAK_GBS, 5), "step_ms": round(ns / 1e6, 2), "launches": cnt,
                  "avg_launch_us": round(ns / cnt / 1e3, 3), "algorithmic_bytes_per_launch": round(ab / cnt, 1)}
             k.update(headline_profile_evidence(name))
+            if name == "dnj_scan":
+                k.update(refrule_scan(pst, n, 8, cnt, ns / cnt / 1e9))
             kernels[name] = k
         if pst[4 + 2 * 8]:
             kernels["coll"] = {"step_ms": round(pst[5 + 2 * 8] / 1e6, 2), "launches": pst[4 + 2 * 8],
@@ -859,6 +883,8 @@ def config1_extras(dev, torch, td, n=10_000, steps=3, cpu=True, threads=16):
     out["dnj_exact"]["reference_rule"] = {
         "rows_rescanned": int(rst[0]), "cells_rescanned": int(rst[1]),
         "engine_over_reference_cells": round(out["dnj_exact"]["cells_rescanned"] / max(int(rst[1]), 1), 3),
+        "engine_counter_equals_oracle": (int(pst[10 + 2 * len(KNAMES)]), int(pst[11 + 2 * len(KNAMES)])) ==
+                                        (int(rst[0]), int(rst[1])),
         "joins_identical_to_oracle": bool(len(rj) == len(j) and (rj == j).all())}
     if cpu:
         out["dnj_exact"]["cpu_baseline"] = cpu_baseline(D, n, td)
@@ -973,6 +999,11 @@ def main():
                   "included_positions": head["included_positions"]},
         "roofline": roof,
     }
+    if pst is not None and pst[11 + 2 * len(KNAMES)]:   # the whole tree, counted in the profiled step
+        result["split"]["reference_rule_rows"] = int(pst[10 + 2 * len(KNAMES)])
+        result["split"]["reference_rule_cells"] = int(pst[11 + 2 * len(KNAMES)])
+        result["split"]["engine_over_reference_cells"] = round(head["cells_rescanned"] /
+                                                               int(pst[11 + 2 * len(KNAMES)]), 3)
     log(f"headline: {result['value']:.4g} taxa-pairs/s, {result['ms_per_step']} ms per step")
     if rank == 0 and world == 1 and not args.no_cpu:
         log("headline cpu_baseline (reference dist + tree on 256 taxa)")

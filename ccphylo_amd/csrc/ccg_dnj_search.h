@@ -36,7 +36,9 @@ struct DnjGrid {
 	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
+	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
 	void load() {
+		if(const char *e = getenv("CCG_JOIN_PF")) join_pf = atoi(e);
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
 		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
@@ -1116,20 +1118,45 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 }
 
 // ------------------------------------------------------------------ DNJ fold
-// Rows with many units (large n): each rest entry's unit partials folded once,
-// one wave per entry, into (rf, rj); k_dnj_join then reads one pair per entry
-// instead of folding every entry's units in each of its blocks.
+// Rows with many units (large n): each entry's unit partials folded once into
+// (rf, rj), one lane per entry and one wave per 64-entry chunk (scan order),
+// and per chunk the summary k_dnj_join_pf replays from: the minimum fresh
+// value, the row and partner of the first entry reaching it, and whether any
+// entry is "bad" (fresh below its stale bound: minQpair's running min is then
+// not a prefix min).
 template <int UNUSED = 0>
 __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
 	const TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
 	const int T = ctl->T, lane = threadIdx.x & 63, umax = dnj_umax(n, seg);
+	const int nc = (T + 63) >> 6;
 	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
-	for(int e = w0; e < T; e += nw) {
-		const int ua = e * umax, ub = ua + dcdiv(b.crow[e], seg);
+	for(int c = w0; c < nc; c += nw) {
+		const int e = (c << 6) + lane;
+		const bool valid = e < T;
+		const int r = valid ? b.crow[e] : 0;
+		const double bnd = valid ? b.cbnd[e] : 0.0;
+		const int ua = e * umax, ub = ua + (valid ? dcdiv(r, seg) : 0);
 		double q = DBL_MAX;
 		int idx = 0;
-		for(int u = ua + lane; u < ub; u += 64) {
+		int u = ua;
+		for(; u + 4 <= ub; u += 4) {   // 4 units' loads in flight
+			double oq[4];
+			int oi[4];
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				oq[m] = b.cq[u + m];
+				oi[m] = b.cj[u + m];
+			}
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				if(qarg_better(oq[m], oi[m], q, idx)) {
+					q = oq[m];
+					idx = oi[m];
+				}
+			}
+		}
+		for(; u < ub; ++u) {
 			const double oq = b.cq[u];
 			const int oi = b.cj[u];
 			if(qarg_better(oq, oi, q, idx)) {
@@ -1137,10 +1164,20 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
 				idx = oi;
 			}
 		}
-		qarg_wave_reduce(q, idx);
-		if(lane == 0) {
+		if(valid) {
 			b.rf[e] = q;
 			b.rj[e] = idx;
+		}
+		const double mq = readlane_d(wave_incl_min(valid ? q : DBL_MAX), 63);
+		const unsigned long long hm = __ballot(valid && q == mq);
+		const unsigned long long bm = __ballot(valid && !(q >= bnd));
+		const int first = hm ? __ffsll((long long) hm) - 1 : 0;
+		const int fr = __shfl(r, first), fj = __shfl(idx, first);
+		if(lane == 0) {
+			b.chg[c] = mq;
+			b.chr[c] = fr;
+			b.chj[c] = fj;
+			b.chb[c] = bm != 0ull;
 		}
 	}
 }
@@ -1217,6 +1254,7 @@ __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_r
 	// final pass: decisions, writes and the pair (the first contributor that
 	// reaches the final minimum, if it is below m0)
 	double cm = m0;
+	long long nacc = 0, cacc = 0;   // minQpair's own rescans (ctl->ref_rows / ref_cells)
 	for(int g0 = 0; g0 < total; g0 += 256) {
 		double fv[4], bv[4];
 		int rv[4], jv[4], av[4];
@@ -1241,6 +1279,10 @@ __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_r
 			double pre = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, x);
 			pre = pre < cm ? pre : cm;
 			const bool accepted = good ? bb < pre : contrib;
+			if(accepted) {
+				++nacc;
+				cacc += rv[k];
+			}
 			if(writer && acc_out) {
 				if(valid) acc_out[c0 + lane] = accepted;   // applied later (k_shd_join)
 			} else if(writer && accepted) {
@@ -1252,6 +1294,14 @@ __device__ __forceinline__ void replay_wave(int total, double m0, const int *e_r
 		}
 	}
 	TS(3, 7);
+	if(writer) {
+		nacc = wave_sum_int(nacc);
+		cacc = wave_sum_int(cacc);
+		if(lane == 0 && nacc) {
+			atomicAdd((unsigned long long *) &b.ctl->ref_rows, (unsigned long long) nacc);
+			atomicAdd((unsigned long long *) &b.ctl->ref_cells, (unsigned long long) cacc);
+		}
+	}
 	if(total && cm < m0) {
 		int first_e = 0x7fffffff;
 		for(int e0 = lane; e0 < total; e0 += 256) {

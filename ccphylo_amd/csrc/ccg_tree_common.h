@@ -37,6 +37,7 @@ struct TreeCtl {
 	int xnj;             // k_exact_sum: count and row sum of the new row j
 	double xsum;
 	long long rows, cells, cells_top, cells_rest;
+	long long ref_rows, ref_cells;  // rows / cells minQpair's own rule rescans (dnj.c:78: Q[r] < running min)
 	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
 	int rtotal;          // sharded DNJ: replay entries whose accept flags k_shd_join applies
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
@@ -82,6 +83,9 @@ struct TreeBufs {
 	XsCross *xcr;
 	XsTie *xti;
 	unsigned long long *ppub;   // k_dnj_plan with several blocks: each block's tagged entry count (look-back)
+	unsigned long long *jpub;   // k_dnj_join_pf, replay path: the pair block 0 chose, tagged with n (n, i, j: 21 bits each)
+	double *chg;                // k_dnj_fold: per 64-entry chunk, the minimum fresh value,
+	int *chr, *chj, *chb;       // the row and partner of its first entry reaching it, and whether any entry is "bad"
 	int maxu;
 };
 

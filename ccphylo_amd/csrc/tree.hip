@@ -132,9 +132,58 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
 }
 
 
+// limbLength (nj.c:42), the join record and updateD (nj.c:836) of the pair
+// (i, j); (ci, cj) is the plan's candidate pair, whose operands the caller
+// loaded at entry (pij, pik, pkj)
+template <int ET>
+__device__ __forceinline__ void join_tail(typename Elem<ET>::T *__restrict__ D, double bs, const TreeBufs &b, int n,
+                                          int general, int i, int j, int ci, int cj, typename Elem<ET>::T pij,
+                                          typename Elem<ET>::T pik, typename Elem<ET>::T pkj, double sDk, int Nk,
+                                          int neg, int nj, int exact) {
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, k = blockIdx.x * TB + tid;
+	const bool writer = blockIdx.x == 0;
+	if(i == 0 && j == 0) {
+		if(writer && tid == 0) {
+			ctl->done = 1;
+			ctl->final_n = n;
+		}
+		return;
+	}
+	// ---- join: limbLength (nj.c:42) and updateD (nj.c:836)
+	const bool hit = i == ci && j == cj;   // uniform
+	const double Dij = Elem<ET>::get(hit ? pij : D[tri(i) + j], bs);
+	double Dik = 0, Dkj = 0;
+	if(!general && k < n && k != i && k != j) {
+		Dik = Elem<ET>::get(hit ? pik : D[k < i ? tri(i) + k : tri(k) + i], bs);
+		Dkj = Elem<ET>::get(hit ? pkj : D[k < j ? tri(j) + k : tri(k) + j], bs);
+	}
+	if(writer && tid == 0) {
+		double Li, Lj;
+		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, neg);
+		ctl->i = i;
+		ctl->j = j;
+		ctl->Li = Li;
+		ctl->Lj = Lj;
+		ctl->Dij = Dij;
+		ccg_join J;
+		J.i = i;
+		J.j = j;
+		J.Li = Li;
+		J.Lj = Lj;
+		b.joins[nj] = J;
+		ctl->njoins = nj + 1;
+	}
+	TS(3, 4);
+	if(general) return;
+	update_body<ET>(D, bs, b, n, i, j, Dij, exact, k, Dik, Dkj, sDk, Nk, blockIdx.x);
+	TS(3, 5);
+}
+
 // ------------------------------------------------------------------ DNJ join
 // Wave 0: fresh mins of the rest entries (fold of their units), minQpair's
 // replay; then limbLength, the join record and updateD with the whole grid.
+// (n <= prefold_n; larger matrices use k_dnj_join_pf below.)
 template <int ET, bool GEN>
 __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
                                                  int general, int prefold, int seg) {
@@ -432,6 +481,7 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 				double run = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);
 				run = run < carry ? run : carry;
 				const int *x_row = lds ? e_row : b.erow, *x_j = lds ? e_j : b.ej;
+				long long nacc = 0, cacc = 0;   // minQpair's own rescans (ctl->ref_rows / ref_cells)
 				if(inreg) {
 					int rr[RP], rj[RP];
 #pragma unroll
@@ -449,6 +499,8 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 						if(rb[m] < run) {
 							b.Q[rr[m]] = rf[m];
 							b.P[rr[m]] = rj[m];
+							++nacc;
+							cacc += rr[m];
 						}
 						run = rf[m] < run ? rf[m] : run;
 					}
@@ -458,9 +510,17 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 						if(x_b[e] < run) {
 							b.Q[x_row[e]] = f;
 							b.P[x_row[e]] = x_j[e];
+							++nacc;
+							cacc += x_row[e];
 						}
 						run = f < run ? f : run;
 					}
+				}
+				nacc = wave_sum_int(nacc);
+				cacc = wave_sum_int(cacc);
+				if(lane == 0 && nacc) {
+					atomicAdd((unsigned long long *) &ctl->ref_rows, (unsigned long long) nacc);
+					atomicAdd((unsigned long long *) &ctl->ref_cells, (unsigned long long) cacc);
 				}
 			}
 			__syncthreads();
@@ -475,42 +535,179 @@ __global__ __launch_bounds__(TB) void k_dnj_join(typename Elem<ET>::T *__restric
 	}
 	__syncthreads();
 	TS(3, 3);
-	const int i = s_pi, j = s_pj;
-	if(i == 0 && j == 0) {
-		if(writer && tid == 0) {
-			ctl->done = 1;
-			ctl->final_n = n;
+	join_tail<ET>(D, bs, b, n, general, s_pi, s_pj, ci, cj, pij, pik, pkj, sDk, Nk, s_neg, s_nj, s_exact);
+	TS_EXIT(3);
+}
+
+// ------------------------------------------------------------------ DNJ join, large n
+// With k_dnj_fold (n > prefold_n) the entries' fresh values and the 64-entry
+// chunk summaries are in HBM, in scan order.  Without a "bad" entry minQpair's
+// running min is a prefix min (replay_wave's comment), so every block finds
+// the pair from the chunk summaries alone: the overall minimum cm and, when it
+// improves on m0, the first chunk reaching it.  Each wave then applies its own
+// chunk's accept decisions (an entry is accepted iff its stale bound is below
+// the running min before it: the owner's prefix over the chunks before, then
+// the chunk's own prefix).  Nothing is copied, and no block reads every entry
+// (at n = 200k late in configs[3] a join lists ~28k rows).  With a bad entry
+// (or force_replay) block 0 runs replay_wave over the entries in HBM and
+// publishes the pair (tagged with n); the other blocks wait for it (block 0 is
+// dispatched first and waits on no other block).
+template <int ET, bool GEN>
+__global__ __launch_bounds__(TB) void k_dnj_join_pf(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                                    int general, int force_replay) {
+	__shared__ double s_wm[TB / 64], s_tpre[TB];
+	__shared__ int s_wi[TB / 64], s_pi, s_pj;
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const bool writer = blockIdx.x == 0;
+	TS_ENTRY(3);
+	TS(3, 0);
+	const int k = blockIdx.x * TB + tid;
+	const int pos_i = ctl->pos_i, pos_j = ctl->pos_j;
+	int ci = pos_i, cj = pos_j;
+	ci = ci < 0 || ci >= n ? 0 : ci;
+	cj = cj < 0 || cj >= ci ? 0 : cj;
+	typename Elem<ET>::T pik = 0, pkj = 0;
+	double sDk = 0;
+	int Nk = 0;
+	if(!general && k < n) {
+		sDk = b.sD[k];
+		Nk = b.N[k];
+		if(k != ci && k != cj) {
+			pik = D[k < ci ? tri(ci) + k : tri(k) + ci];
+			pkj = D[k < cj ? tri(cj) + k : tri(k) + cj];
 		}
-		return;
 	}
-	// ---- join: limbLength (nj.c:42) and updateD (nj.c:836)
-	const bool hit = i == ci && j == cj;   // uniform
-	const double Dij = Elem<ET>::get(hit ? pij : D[tri(i) + j], bs);
-	double Dik = 0, Dkj = 0;
-	if(!general && k < n && k != i && k != j) {
-		Dik = Elem<ET>::get(hit ? pik : D[k < i ? tri(i) + k : tri(k) + i], bs);
-		Dkj = Elem<ET>::get(hit ? pkj : D[k < j ? tri(j) + k : tri(k) + j], bs);
+	const typename Elem<ET>::T pij = D[tri(ci) + cj];
+	const int done = ctl->done, T = ctl->T, nj = ctl->njoins, neg = ctl->neg, exact = ctl->exact;
+	const double m0 = ctl->m0;
+	if(done) return;
+	const int nc = (T + 63) >> 6;
+	// this wave's chunk of the accept pass: its loads go out now
+	const int cw = (int) blockIdx.x * (TB / 64) + wid, ea = (cw << 6) + lane;
+	const bool va = ea < T;
+	double af = DBL_MAX, ab = 0;
+	int ar = 0, aj = 0;
+	if(va) {
+		af = b.rf[ea];
+		ab = b.cbnd[ea];
+		ar = b.crow[ea];
+		aj = b.rj[ea];
 	}
-	if(writer && tid == 0) {
-		double Li, Lj;
-		limb_length(&Li, &Lj, b.sD[i], b.sD[j], b.N[i], b.N[j], Dij, s_neg);
-		ctl->i = i;
-		ctl->j = j;
-		ctl->Li = Li;
-		ctl->Lj = Lj;
-		ctl->Dij = Dij;
-		ccg_join J;
-		J.i = i;
-		J.j = j;
-		J.Li = Li;
-		J.Lj = Lj;
-		b.joins[s_nj] = J;
-		ctl->njoins = s_nj + 1;
+	// every chunk's minimum and bad flag: thread t holds chunks [t per, (t + 1) per)
+	const int per = (nc + TB - 1) / TB, c0 = tid * per, c1 = c0 + per < nc ? c0 + per : nc;
+	double tmin = DBL_MAX;
+	int bad = force_replay && T > 0;
+	for(int c = c0; c < c1; c += 8) {
+		double g[8];
+		int f[8];
+#pragma unroll
+		for(int m = 0; m < 8; ++m) {
+			const int cc = c + m < c1 ? c + m : c0;
+			g[m] = b.chg[cc];
+			f[m] = b.chb[cc];
+		}
+#pragma unroll
+		for(int m = 0; m < 8; ++m) {
+			if(c + m >= c1) continue;
+			tmin = g[m] < tmin ? g[m] : tmin;
+			bad |= f[m];
+		}
 	}
-	TS(3, 4);
-	if(general) return;
-	update_body<ET>(D, bs, b, n, i, j, Dij, s_exact, k, Dik, Dkj, sDk, Nk, blockIdx.x);
-	TS(3, 5);
+	TS(3, 1);
+	if(__syncthreads_or(bad)) {
+		// minQpair's serial replay (rare): block 0, entries in HBM
+		if(writer) {
+			if(wid == 0) {
+				int pi = pos_i, pj = pos_j;
+				bool had_bad;
+				replay_wave(T, m0, b.crow, b.rj, b.cbnd, b.rf, b.eacc, true, b, pi, pj, &had_bad, n);
+				if(lane == 0) {
+					s_pi = pi;
+					s_pj = pj;
+					if(had_bad) ctl->serial_replays++;
+					__hip_atomic_store(b.jpub, ((unsigned long long) n << 42) | ((unsigned long long) pi << 21) |
+					                           (unsigned) pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
+			}
+		} else if(tid == 0) {
+			unsigned long long u = 0;
+			bool ok = false;
+			for(int spin = 0; spin <= (1 << 24) && !ok; ++spin) {
+				u = __hip_atomic_load(b.jpub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				ok = (int) (u >> 42) == n;
+				if(!ok) __builtin_amdgcn_s_sleep(1);
+			}
+			s_pi = ok ? (int) ((u >> 21) & 0x1fffff) : 0;
+			s_pj = ok ? (int) (u & 0x1fffff) : 0;
+			if(!ok) {   // never expected: stop the loop and report it (tree_run_t)
+				ctl->final_n = -1;
+				ctl->done = 1;
+			}
+		}
+		__syncthreads();
+		TS(3, 3);
+		join_tail<ET>(D, bs, b, n, general, s_pi, s_pj, ci, cj, pij, pik, pkj, sDk, Nk, neg, nj, exact);
+		TS_EXIT(3);
+		return;   // replay_wave applied the accept decisions
+	}
+	// the running min is a prefix min: block scan over the slices
+	const double inc = wave_incl_min(tmin);
+	if(lane == 63) s_wm[wid] = inc;
+	__syncthreads();
+	double carry = m0, cm = m0;
+#pragma unroll
+	for(int w = 0; w < TB / 64; ++w) {
+		if(w < wid) carry = s_wm[w] < carry ? s_wm[w] : carry;
+		cm = s_wm[w] < cm ? s_wm[w] : cm;
+	}
+	double ex = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);   // before this thread's slice
+	s_tpre[tid] = ex < carry ? ex : carry;
+	// the pair: the first entry reaching cm, when it improves on m0
+	int first = 0x7fffffff;
+	if(cm < m0 && tmin == cm) {
+		for(int c = c0; c < c1; ++c) {
+			if(b.chg[c] == cm) {
+				first = c;
+				break;
+			}
+		}
+	}
+	first = wave_min_int(first);
+	if(lane == 0) s_wi[wid] = first;
+	__syncthreads();
+	int i = pos_i, j = pos_j;
+	if(cm < m0) {
+		int fc = s_wi[0];
+#pragma unroll
+		for(int w = 1; w < TB / 64; ++w) fc = s_wi[w] < fc ? s_wi[w] : fc;
+		i = b.chr[fc];
+		j = b.chj[fc];
+	}
+	TS(3, 3);
+	join_tail<ET>(D, bs, b, n, general, i, j, ci, cj, pij, pik, pkj, sDk, Nk, neg, nj, exact);
+	// accept decisions of this wave's chunk
+	if(cw < nc) {   // uniform per wave
+		const int t = cw / per, cs = t * per;
+		double pc = s_tpre[t];
+		for(int x0 = cs; x0 < cw; x0 += 64) {   // the owner's chunks before cw
+			const double g = x0 + lane < cw ? b.chg[x0 + lane] : DBL_MAX;
+			pc = g < pc ? g : pc;
+		}
+		pc = readlane_d(wave_incl_min(pc), 63);
+		double run = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, wave_incl_min(af));
+		run = run < pc ? run : pc;
+		const bool acc = va && ab < run;
+		if(acc) {
+			b.Q[ar] = af;
+			b.P[ar] = aj;
+		}
+		const long long nacc = __popcll(__ballot(acc)), cacc = wave_sum_int((long long) (acc ? ar : 0));
+		if(lane == 0 && nacc) {
+			atomicAdd((unsigned long long *) &ctl->ref_rows, (unsigned long long) nacc);
+			atomicAdd((unsigned long long *) &ctl->ref_cells, (unsigned long long) cacc);
+		}
+	}
 	TS_EXIT(3);
 }
 
@@ -1392,7 +1589,9 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
 	size_t o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
-	size_t o_pp = take(PLAN_MAXB * 8);
+	size_t o_pp = take(PLAN_MAXB * 8), o_jp = take(8);
+	const size_t nch = ncand / 64 + 2;   // k_dnj_fold's chunk summaries
+	size_t o_hg = take(nch * 8), o_hr = take(nch * 4), o_hj = take(nch * 4), o_hb = take(nch * 4);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
 	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
@@ -1442,6 +1641,11 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.xcr = (XsCross *) (m + o_xc);
 	b.xti = (XsTie *) (m + o_xt);
 	b.ppub = (unsigned long long *) (m + o_pp);
+	b.jpub = (unsigned long long *) (m + o_jp);
+	b.chg = (double *) (m + o_hg);
+	b.chr = (int *) (m + o_hr);
+	b.chj = (int *) (m + o_hj);
+	b.chb = (int *) (m + o_hb);
 	b.maxu = (int) maxu;
 	return CCG_OK;
 }
@@ -1468,7 +1672,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
 		kt.mark(CCG_K_REST);
-		k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold, seg);
+		if(prefold && g_grid.join_pf) k_dnj_join_pf<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, g_grid.join_pf == 2);
+		else k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold, seg);
 		if(GEN) k_update_general<ET><<<1, 1024, 0, st>>>(D, bs, b, n);
 		kt.mark(CCG_K_UPDATE);
 		if(xs) {
@@ -1665,7 +1870,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 #endif
 	if(h.done && h.final_n < 0) {   // k_dnj_plan's look-back timed out (never expected)
 		hipFree(w.mem);
-		ccg_set_last_msg("k_dnj_plan: a block's look-back over the lower blocks timed out");
+		ccg_set_last_msg("k_dnj_plan / k_dnj_join: a block's wait on a lower block timed out");
 		return CCG_EHIP;
 	}
 	*njoins = h.njoins;
@@ -1694,6 +1899,10 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest;
 			stats[6 + 2 * CCG_NKSTAT] = h.serial_sums;
 			stats[7 + 2 * CCG_NKSTAT] = h.chain_sums;
+			stats[8 + 2 * CCG_NKSTAT] = 0;
+			stats[9 + 2 * CCG_NKSTAT] = 0;
+			stats[10 + 2 * CCG_NKSTAT] = h.ref_rows;
+			stats[11 + 2 * CCG_NKSTAT] = h.ref_cells;
 		}
 	}
 	CCG_CHECK(hipStreamSynchronize(st));

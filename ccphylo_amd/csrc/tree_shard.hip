@@ -630,6 +630,8 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			stats[7 + 2 * CCG_NKSTAT] = 0;
 			stats[8 + 2 * CCG_NKSTAT] = istat.coll_bytes;
 			stats[9 + 2 * CCG_NKSTAT] = istat.hard;
+			stats[10 + 2 * CCG_NKSTAT] = 0;
+			stats[11 + 2 * CCG_NKSTAT] = 0;
 		}
 	}
 out:

@@ -764,6 +764,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			stats[7 + 2 * CCG_NKSTAT] = hc.chain_sums;
 			stats[8 + 2 * CCG_NKSTAT] = istat.coll_bytes;
 			stats[9 + 2 * CCG_NKSTAT] = istat.hard;
+			stats[10 + 2 * CCG_NKSTAT] = hc.ref_rows;
+			stats[11 + 2 * CCG_NKSTAT] = hc.ref_cells;
 		}
 	}
 out:

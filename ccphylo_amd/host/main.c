@@ -259,7 +259,7 @@ static int main_tree(int argc, char **argv) {
 			ccg_tree_args ta = {n, et, bs, m, flag, !fast, 0, 0};
 			int nj = 0, fn = 0;
 			double fd = 0;
-			int64_t st[10 + 2 * CCG_NKSTAT];
+			int64_t st[12 + 2 * CCG_NKSTAT];
 			memset(st, 0, sizeof(st));
 			int rc;
 			if(gpus) {

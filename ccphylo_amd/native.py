@@ -326,7 +326,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (10 + 2 * NKSTAT))()
+        st = (C.c_int64 * (12 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         rc = fn_(self.h, C.byref(a), C.c_void_p(dptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd), st)
         self._check(rc, "ccg_tree")
@@ -353,7 +353,7 @@ class Device:
         nj = C.c_int(0)
         fn = C.c_int(0)
         fd = C.c_double(0)
-        st = (C.c_int64 * (10 + 2 * NKSTAT))()
+        st = (C.c_int64 * (12 + 2 * NKSTAT))()
         a = TreeArgs(n, etype, byte_scale, method, flags, int(exact), int(profile), int(max_joins))
         cp = C.byref(coll.c) if coll is not None else None
         rc = fn_(self.h, C.byref(a), cp, C.c_void_p(ptr), joins.ctypes.data, C.byref(nj), C.byref(fn), C.byref(fd),

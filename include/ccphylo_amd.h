@@ -166,7 +166,7 @@ typedef struct {
 	                          prefix of a large tree); 0: run to n = 2 */
 } ccg_tree_args;
 
-/* stats layout (ccg_tree / ccg_tree_dev / ccg_tree_shard*, 10 + 2*CCG_NKSTAT
+/* stats layout (ccg_tree / ccg_tree_dev / ccg_tree_shard*, 12 + 2*CCG_NKSTAT
  * entries when profile = 1, else 4): [0] rows rescanned, [1] cells
  * rescanned, [2] kernel launches, [3] device time (us); then for kernel class
  * c: [4+2c] launches, [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT]
@@ -176,7 +176,10 @@ typedef struct {
  * declined); sharded engines only: [8+2*CCG_NKSTAT] bytes this rank put into
  * the initSummaD collectives, [9+2*CCG_NKSTAT] columns whose column part
  * went through the serial gather (the rest are exact sums of per-rank
- * statistics).  Classes: */
+ * statistics); DNJ: [10+2*CCG_NKSTAT] rows and [11+2*CCG_NKSTAT] cells that
+ * the reference's own minQpair rule rescans (dnj.c:78, a row whose stored Q is
+ * below the running min), counted from the replay's accept decisions: the
+ * SURVEY 8(d) unit beside the engine's speculative [0] / [1].  Classes: */
 #define CCG_K_INIT     0   /* initSummaD / initHNJ / first candidate */
 #define CCG_K_TOP      1   /* sharded DNJ k_dnj_select: requeue fold, top rows S, their rescans */
 #define CCG_K_REST     2   /* DNJ k_dnj_scan: rescans of the listed rows (one GPU: S and the rows below it) */

@@ -305,15 +305,17 @@ def _clade_ltd(n, seed, L=3000, clades=16):
     return L - same[i, j]
 
 
-@pytest.mark.parametrize("kind,n,env", [("euc", 1500, "8,8,3,0"), ("euc", 2500, "64,16,2,0"),
-                                        ("clade", 1500, "8,8,4,0"), ("clade", 2500, "32,4,1,0"),
-                                        ("clade", 3000, "1024,2048,8,0")])
+@pytest.mark.parametrize("kind,n,env", [("euc", 1500, "1,8,3,0"), ("euc", 2500, "2,16,2,0"),
+                                        ("clade", 1500, "2,8,4,0"), ("clade", 2500, "1,4,1,0"),
+                                        ("clade", 3000, "0,2048,8,0"), ("euc", 3000, "1,2048,1,0")])
 def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
     """The large-n settings of the DNJ search at small n: rescan units of
     several SEG (CCG_SEG_MUL), each rest row's units folded once by k_dnj_fold
     (CCG_PREFOLD_N=0) and scan grids far smaller than the units
-    (CCG_SCAN_MAX: many grid waves).  Joins bit-identical to the serial
-    reference (exact row sums), single GPU and sharded."""
+    (CCG_SCAN_MAX: many grid waves), with the chunk-summary join kernel
+    k_dnj_join_pf (CCG_JOIN_PF=1), its block-0 replay path forced (2) or the
+    per-block replay (0).  Joins bit-identical to the serial reference (exact
+    row sums), single GPU and sharded."""
     from oracle import pyoracle
     if kind == "euc":
         rng = np.random.default_rng(n)
@@ -322,7 +324,8 @@ def test_dnj_large_n_modes(dev, monkeypatch, kind, n, env):
         D = np.sqrt(((pts[i] - pts[j]) ** 2).sum(1))
     else:
         D = _clade_ltd(n, n)
-    _, scan, segm, pf = env.split(",")
+    jpf, scan, segm, pf = env.split(",")
+    monkeypatch.setenv("CCG_JOIN_PF", jpf)
     monkeypatch.setenv("CCG_SCAN_MAX", scan)
     monkeypatch.setenv("CCG_SEG_MUL", segm)
     monkeypatch.setenv("CCG_PREFOLD_N", pf)
@@ -479,3 +482,27 @@ def test_nj_fast_sums_types(dev, et):
     assert fast[1] == exact[1] and (fast[0]["i"] == exact[0]["i"]).all() and (fast[0]["j"] == exact[0]["j"]).all()
     for f in ("Li", "Lj"):
         np.testing.assert_allclose(fast[0][f], exact[0][f], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind,n,band", [("euc", 1500, False), ("clade", 2000, False), ("snp", 1200, False),
+                                         ("euc", 2000, True), ("clade", 2500, True)])
+def test_dnj_reference_rule_counters(dev, monkeypatch, kind, n, band):
+    """stats[10/11 + 2 NKSTAT]: the rows and cells the reference's minQpair
+    rescans (dnj.c:78), counted from the engine's replay decisions, equal the
+    oracle's serial count (SURVEY 8(d)'s DNJ unit); single GPU and sharded
+    kernels, with the small-n and the band choice of S."""
+    from oracle import pyoracle
+    from ccphylo_amd import native
+    K = native.NKSTAT
+    D = _euclid(n, n) if kind == "euc" else _clade_ltd(n, n) if kind == "clade" else _snp(n, n)
+    if band:
+        monkeypatch.setenv("CCG_S_SPLIT_N", "1000")
+    ref, rfn, rfd, rst = pyoracle.tree(D, n, method=1, stats=True)
+    got, fn, fd, st = dev.tree(D, n, method=1, exact=True, profile=True)
+    assert len(got) == len(ref) and (got == ref).all()
+    assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1]))
+    assert st[1] >= st[11 + 2 * K]   # the engine rescans a superset
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")
+    sh = dev.tree_shard(D, n, None, method=1, exact=True, profile=True)
+    assert (sh[0] == got).all()
+    assert (sh[3][10 + 2 * K], sh[3][11 + 2 * K]) == (int(rst[0]), int(rst[1]))

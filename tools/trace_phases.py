@@ -41,6 +41,15 @@ elif "--clade" in sys.argv:   # config-3-like clade data (tools/config3.py) thro
     dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dd.data_ptr())
     D = Dd.cpu().numpy()
     del seqs, Dd
+elif "--c3" in sys.argv:   # configs[3]'s float Euclidean matrix on the device, a join prefix (--joins J)
+    import torch
+    from tools.synth import euclid_shard_dev
+    J = int(sys.argv[sys.argv.index("--joins") + 1]) if "--joins" in sys.argv else 26000
+    loc = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)
+    torch.cuda.synchronize()
+    joins, fn, fd, st = dev.tree_dev(loc.data_ptr(), n, etype=4, method=method, exact=True, max_joins=J)
+    print(f"c3 prefix: {len(joins)} joins, device {st[3] / 1e3:.1f} ms", flush=True)
+    sys.exit(0)
 else:
     D = euclid(n)
 for exact in ((True,) if "--exact" in sys.argv else (False, True)):
