@@ -68,10 +68,11 @@ struct DnjGrid {
 	// 16-byte row loads (k_dnj_scan_v, mode 4; the GEN form k_dnj_scan_w,
 	// mode 1); one unit per block below (k_dnj_scan, mode 0).  Measured per
 	// join at 50k (headline data): 88.4 (block) -> 72.0 (wave) -> 66.7 us
-	// (wave, 16-byte loads); 10k: 9.4 (block) against 9.8 us (wave).
-	// CCG_SCAN_WAVE=0/1/4 forces a form.
+	// (wave, 16-byte loads) -> 65.2 us (+ nontemporal row loads and 16-byte
+	// sD loads where aligned, mode 9; 8433 -> 8920 joins/s); 10k: 9.4 (block)
+	// against 9.8 us (wave).  CCG_SCAN_WAVE=0/1/4..11 forces a form.
 	int scan_mode(int n) const {
-		return scan_wave >= 0 ? scan_wave : n > 16384 ? 4 : 0;
+		return scan_wave >= 0 ? scan_wave : n > 16384 ? 9 : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
@@ -372,24 +373,36 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		__builtin_amdgcn_s_setprio(3);   // wave 0's loads first: the fold is the critical path
 		if(!first) {
 			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
-			for(int w = lane; w < G; w += 64) {
-				double oq[4], ocq;
-				int oi[4], ocp;
+			// FU requeue blocks per lane per round trip: every load of a step is
+			// issued before the first compare (the winner is unique under
+			// qarg_better's total order, so the fold order is free)
+			constexpr int FU = 4;
+			for(int w0 = lane; w0 < G; w0 += 64 * FU) {
+				double oq[FU][4], ocq[FU];
+				int oi[FU][4], ocp[FU];
 #pragma unroll
-				for(int t = 0; t < 4; ++t) {   // every load issued before the first compare
-					oq[t] = b.qpart[4 * w + t];
-					oi[t] = b.ipart[4 * w + t];
+				for(int u = 0; u < FU; ++u) {
+					const int w = w0 + 64 * u < G ? w0 + 64 * u : w0;
+#pragma unroll
+					for(int t = 0; t < 4; ++t) {
+						oq[u][t] = b.qpart[4 * w + t];
+						oi[u][t] = b.ipart[4 * w + t];
+					}
+					ocq[u] = b.cfq[w];
+					ocp[u] = b.cfp[w];
 				}
-				ocq = b.cfq[w];
-				ocp = b.cfp[w];
 #pragma unroll
-				for(int t = 0; t < 4; ++t) {
-					if(qarg_better(oq[t], oi[t], q[t], ix[t])) {
-						q[t] = oq[t];
-						ix[t] = oi[t];
-						if(t == 1) {
-							cq1 = ocq;
-							cp1 = ocp;
+				for(int u = 0; u < FU; ++u) {
+					if(w0 + 64 * u >= G) continue;
+#pragma unroll
+					for(int t = 0; t < 4; ++t) {
+						if(qarg_better(oq[u][t], oi[u][t], q[t], ix[t])) {
+							q[t] = oq[u][t];
+							ix[t] = oi[u][t];
+							if(t == 1) {
+								cq1 = ocq[u];
+								cp1 = ocp[u];
+							}
 						}
 					}
 				}
@@ -1040,11 +1053,18 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // so a float row streams at 1 KB per wave load instead of 256 B; the unit's
 // unaligned head and its tail (fewer than VEC cells each) are scalar.  sD is
 // gathered per cell.  UV vector loads in flight per lane (about 16 cells).
-template <int ET, class Rows, class Tail = NoTail>
+// MODE (measurement variants, CCG_SCAN_WAVE = 4 + MODE): bit 0 streams the
+// row with nontemporal loads (read once; sD keeps the caches), bit 1
+// software-pipelines the unit: the next UV loads are issued before the
+// current ones are compared (half UV, two register sets), bit 2 loads sD
+// 16 bytes at a time where the unit's aligned start is even (sD + ca 16-byte
+// aligned; uniform per unit).
+template <int ET, class Rows, class Tail = NoTail, int MODE = 0>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
-	constexpr int VEC = 16 / (int) sizeof(T), UV = VEC >= 16 ? 1 : 16 / VEC;
+	constexpr bool NTL = MODE & 1, PIPE = (MODE & 2) != 0, SDV = (MODE & 4) != 0;
+	constexpr int VEC = 16 / (int) sizeof(T), UV0 = VEC >= 16 ? 1 : 16 / VEC, UV = PIPE && UV0 > 1 ? UV0 / 2 : UV0;
 	__shared__ int erow[REPLAY_CAP];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
@@ -1086,30 +1106,65 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		};
 		if(lane < ca - c0) cell(c0 + lane);   // the unaligned head
 		if(lane < c1 - ce) cell(ce + lane);   // the tail
-		for(int v0 = 0; v0 < nv; v0 += 64 * UV) {
-			uint4 w[UV];
-			double sk[UV][VEC];
+		uint4 w[2][UV];
+		double sk[2][UV][VEC];
+		const bool sda = SDV && (ca & 1) == 0;   // uniform
+		auto load = [&](int buf, int v0) {
 #pragma unroll
 			for(int m = 0; m < UV; ++m) {
 				int k = v0 + 64 * m + lane;
 				k = k < nv ? k : nv - 1;
-				w[m] = *(const uint4 *) (row + ca + VEC * k);
+				const uint4 *src = (const uint4 *) (row + ca + VEC * k);
+				if(NTL) {
+					typedef unsigned u4v __attribute__((ext_vector_type(4)));
+					const u4v x = __builtin_nontemporal_load((const u4v *) src);
+					w[buf][m] = make_uint4(x.x, x.y, x.z, x.w);
+				} else {
+					w[buf][m] = *src;
+				}
+				if(sda) {
 #pragma unroll
-				for(int t = 0; t < VEC; ++t) sk[m][t] = b.sD[ca + VEC * k + t];
+					for(int t = 0; t < VEC; t += 2) {
+						const double2 x = *(const double2 *) (b.sD + ca + VEC * k + t);
+						sk[buf][m][t] = x.x;
+						sk[buf][m][t + 1] = x.y;
+					}
+				} else {
+#pragma unroll
+					for(int t = 0; t < VEC; ++t) sk[buf][m][t] = b.sD[ca + VEC * k + t];
+				}
 			}
+		};
+		auto compare = [&](int buf, int v0) {
 #pragma unroll
 			for(int m = 0; m < UV; ++m) {
 				const int k = v0 + 64 * m + lane;
-				const T *ev = (const T *) &w[m];
+				const T *ev = (const T *) &w[buf][m];
 #pragma unroll
 				for(int t = 0; t < VEC; ++t) {
 					const int c = ca + VEC * k + t;
 					const double d = Elem<ET>::get(ev[t], bs);
-					const double x = qcrit(n, n, d, sDr, sk[m][t]);
+					const double x = qcrit(n, n, d, sDr, sk[buf][m][t]);
 					const bool take = k < nv && 0 <= d && qarg_better(x, c, q, idx);
 					q = take ? x : q;
 					idx = take ? c : idx;
 				}
+			}
+		};
+		if(PIPE) {
+			if(nv > 0) load(0, 0);
+			int v0 = 0;
+			for(; v0 + 64 * UV < nv; v0 += 128 * UV) {
+				load(1, v0 + 64 * UV);
+				compare(0, v0);
+				if(v0 + 128 * UV < nv) load(0, v0 + 128 * UV);
+				compare(1, v0 + 64 * UV);
+			}
+			if(v0 < nv) compare(0, v0);
+		} else {
+			for(int v0 = 0; v0 < nv; v0 += 64 * UV) {
+				load(0, v0);
+				compare(0, v0);
 			}
 		}
 		qarg_wave_reduce(q, idx);

@@ -1666,8 +1666,15 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
 		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 		kt.mark(CCG_K_FIND);
-		if(g_grid.scan_mode(n) == 4 && !GEN) k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		else if(g_grid.scan_mode(n) == 4) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		const int sm = g_grid.scan_mode(n);
+		if(sm >= 4 && !GEN) {
+			switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+				SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7)
+#undef SV_
+				default: k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+			}
+		} else if(sm >= 4) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else if(g_grid.scan_mode(n)) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
@@ -1714,6 +1721,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 	return (GEN ? 4 : 3) + xs;
 }
 
+static bool g_progress = false;
+
 template <int ET>
 static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins,
                       int *final_n, double *final_d, int64_t *stats) {
@@ -1725,6 +1734,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	TreeWork w;
 	g_grid = DnjGrid();
 	g_grid.load();
+	g_progress = getenv("CCG_PROGRESS") != nullptr;
 	int rc = ccg_tree_alloc(&w, n0, st);
 	if(rc) return rc;
 	TreeBufs b = w.b;
@@ -1776,6 +1786,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			since_check = 0;
 			CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 			CCG_CHECK(hipStreamSynchronize(st));
+			if(g_progress && (n0 - n) % (16 * 1024) == 0)   // long trees (CCG_PROGRESS=1): a line per 16384 joins
+				fprintf(stderr, "ccg_tree: %d joins, n = %d, rows %lld cells %lld (reference rule %lld / %lld)\n", n0 - n,
+				        n, h.rows, h.cells, h.ref_rows, h.ref_cells);
 			if(h.done) {
 				stopped = true;
 				break;

@@ -139,7 +139,7 @@ def test_config2_dist_and_dnj_prefix(dev):
     import torch
     import ccphylo_amd as cg
     from oracle import pyoracle
-    n, L, k = 50_000, 5_000_000, 60
+    n, L, k = 50_000, 5_000_000, 1000
     seqs, incs, D = _clade_snp_ltd(dev, torch, n, L, clades=512)
     lib = pyoracle.lib()
     hinc = incs.cpu().numpy().view(np.uint32).copy()
@@ -180,6 +180,32 @@ def test_config3_sharded_dnj_prefix(dev, monkeypatch):
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "sharded dnj 200k float exact prefix")
+
+
+def test_config3_single_vs_sharded_prefix(dev, monkeypatch):
+    """configs[3]'s matrix past the point where a join lists ~10k rows (the
+    first 12k joins): the single engine (k_dnj_fold chunk summaries and
+    k_dnj_join_pf) against the row-sharded kernels at world 1 (k_shd_pick's
+    replay_wave), two independent forms of minQpair's replay: identical joins
+    and identical reference-rule rescan counts."""
+    import torch
+    import ccphylo_amd as cg
+    from tools.synth import euclid_shard_dev
+    K = cg.native.NKSTAT
+    n, k = 200_000, 12_000
+    out = []
+    for force in ("0", "1"):
+        monkeypatch.setenv("CCG_SHARD_FORCE", force)
+        loc = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)
+        out.append(dev.tree_shard_dev(loc.data_ptr(), n, None, etype=4, method=cg.CCG_TREE_DNJ, exact=True,
+                                      max_joins=k, profile=True))
+        del loc
+        torch.cuda.empty_cache()
+    (a, _, _, sa), (b, _, _, sb) = out
+    assert len(a) == k and len(b) == k
+    _same_joins((a, 0, 0), (b, 0, 0), "configs[3] single engine vs sharded kernels")
+    assert (sa[10 + 2 * K], sa[11 + 2 * K]) == (sb[10 + 2 * K], sb[11 + 2 * K])
+    assert sa[10 + 2 * K] > 10 * k   # long listings: the large-T join path ran
 
 
 def test_config4_pipeline_200k_world1_exact(dev, monkeypatch):

@@ -4,6 +4,7 @@ reference's own minQpair rule rescans (dnj.c:78), counted by the engine from
 its replay decisions (stats[10/11 + 2 NKSTAT]).  One JSON line per prefix.
 
 usage: python tools/c3_refrule.py [n] [prefix,prefix,...] [float|double]
+(prefix 0: the whole tree; CCG_PROGRESS=1 prints a line per 16384 joins)
 """
 import json
 import os
@@ -17,7 +18,19 @@ from ccphylo_amd import native as nt  # noqa: E402
 from tools.synth import euclid_shard_dev  # noqa: E402
 
 
+def heartbeat(every=40.0):
+    import threading
+
+    def beat():
+        t0 = time.perf_counter()
+        while True:
+            time.sleep(every)
+            print(f"... {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    heartbeat()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000
     prefixes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [10_000, 30_000]
     dt_ = torch.float32 if (len(sys.argv) < 4 or sys.argv[3] == "float") else torch.float64
