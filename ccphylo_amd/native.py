@@ -262,6 +262,13 @@ class Device:
             raise CcgError(f"ccg_init({device}) failed: {self.lib.ccg_strerror(rc).decode()}")
         self.h = h
 
+    @staticmethod
+    def count() -> int:
+        """Visible GPUs (ccg_device_count)."""
+        c = C.c_int(0)
+        rc = engine_lib().ccg_device_count(C.byref(c))
+        return c.value if rc == 0 else 0
+
     def close(self):
         if self.h:
             self.lib.ccg_destroy(self.h)

@@ -233,3 +233,26 @@ def test_cli_dist_tree_world8_20k(tmp_path, method):
              "host"])
         outs[g] = out.read_bytes()
     assert outs[8] == outs[1] and len(outs[1]) > 20000
+
+
+def _devices():
+    import ccphylo_amd as cg
+    return cg.Device.count()
+
+
+@pytest.mark.parametrize("method", ["dnj", "nj"])
+def test_cli_tree_rccl_multi_gpu(tmp_path, method):
+    """RCCL with one rank per GPU (the configuration of the driver's 8-GPU
+    node): `tree --gpus G --transport rccl` for G = 2 and every visible GPU,
+    against the one-GPU CLI.  Skipped on a one-GPU box, where several ranks
+    cannot share a device over RCCL (the host transport covers those worlds)."""
+    ndev = _devices()
+    if ndev < 2:
+        pytest.skip(f"{ndev} GPU(s) visible: RCCL with world > 1 needs one GPU per rank")
+    from tools.synth import euclid
+    n = 3000
+    path = tmp_path / "m.phy"
+    _write_phylip(path, euclid(n, seed=6), n)
+    one = cli(["tree", "-i", str(path), "-m", method])
+    for g in sorted({2, ndev}):
+        assert cli(["tree", "-i", str(path), "-m", method, "--gpus", str(g), "--transport", "rccl"]) == one, g
