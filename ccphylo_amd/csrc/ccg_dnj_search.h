@@ -70,9 +70,11 @@ struct DnjGrid {
 	// join at 50k (headline data): 88.4 (block) -> 72.0 (wave) -> 66.7 us
 	// (wave, 16-byte loads) -> 65.2 us (+ nontemporal row loads and 16-byte
 	// sD loads where aligned, mode 9; 8433 -> 8920 joins/s); 10k: 9.4 (block)
-	// against 9.8 us (wave).  CCG_SCAN_WAVE=0/1/4..11 forces a form.
-	int scan_mode(int n) const {
-		return scan_wave >= 0 ? scan_wave : n > 16384 ? 9 : 0;
+	// against 9.8 us (wave).  Float rows keep mode 4: configs[3]'s first 30k
+	// joins rescan in 41.7 s with it against 46.0 (mode 9), 46.8 (11), 47.0
+	// (13), 47.5 s (15).  CCG_SCAN_WAVE=0/1/4..19 forces a form.
+	int scan_mode(int n, int et = 8) const {
+		return scan_wave >= 0 ? scan_wave : n > 16384 ? (et == 8 ? 9 : 4) : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
@@ -1058,13 +1060,14 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // software-pipelines the unit: the next UV loads are issued before the
 // current ones are compared (half UV, two register sets), bit 2 loads sD
 // 16 bytes at a time where the unit's aligned start is even (sD + ca 16-byte
-// aligned; uniform per unit).
+// aligned; uniform per unit), bit 3 doubles the loads in flight per lane.
 template <int ET, class Rows, class Tail = NoTail, int MODE = 0>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
 	constexpr bool NTL = MODE & 1, PIPE = (MODE & 2) != 0, SDV = (MODE & 4) != 0;
-	constexpr int VEC = 16 / (int) sizeof(T), UV0 = VEC >= 16 ? 1 : 16 / VEC, UV = PIPE && UV0 > 1 ? UV0 / 2 : UV0;
+	constexpr int VEC = 16 / (int) sizeof(T), UV0 = (VEC >= 16 ? 1 : 16 / VEC) * (MODE & 8 ? 2 : 1);
+	constexpr int UV = PIPE && UV0 > 1 ? UV0 / 2 : UV0;
 	__shared__ int erow[REPLAY_CAP];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;

@@ -1666,16 +1666,16 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
 		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 		kt.mark(CCG_K_FIND);
-		const int sm = g_grid.scan_mode(n);
+		const int sm = g_grid.scan_mode(n, ET);
 		if(sm >= 4 && !GEN) {
 			switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
-				SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7)
+				SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7) SV_(13) SV_(15)
 #undef SV_
 				default: k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 			}
 		} else if(sm >= 4) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		else if(g_grid.scan_mode(n)) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		else if(sm) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
 		kt.mark(CCG_K_REST);

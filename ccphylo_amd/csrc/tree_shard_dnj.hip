@@ -687,9 +687,9 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
-			if(grid.scan_mode(n) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
-			else if(grid.scan_mode(n) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
-			else if(grid.scan_mode(n)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			if(grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			else if(grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			else if(grid.scan_mode(n, ET)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
 			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
 			kt.mark(CCG_K_REST);
 			SD_TRY(cr.allgather(Sl, G, rec_slot(n, sh.world).bytes));
