@@ -26,12 +26,18 @@ sources) running the same pipeline (`dist -t <nproc>` then `tree`) on the
 first taxa of the same alignment, whose distances and Newick are compared
 with the GPU's.
 
+SURVEY 8(d) prices the DNJ rescans by the cells the REFERENCE's minQpair
+rule rescans: the engine counts them from its replay decisions (stats[10/11
++ 2 NKSTAT]); `split.reference_rule_cells` is the whole headline tree's, and
+the scan kernels report `frac_reference_rule` beside the engine-cell `frac`.
+
 extras: configs[1] (N = 10k Phylip matrix: DNJ exact and fast, NJ, HNJ, with
-the reference's DNJ and NJ on the host), the reference-rule rescanned cells
- against the engine's at configs[1] and on a configs[2] prefix,
-dist alone at 8192 x 1 Mbp (non-pair and pair mode), KMA `cos`, configs[3]
-(one 200k float matrix, the whole exact DNJ tree: the single-GPU engine at
-N = 1, sharded over RCCL at N > 1) and the sharded NJ.
+the reference's DNJ and NJ on the host), the oracle's serial count of the
+reference-rule cells at configs[1] and on a configs[2] prefix (checks the
+engine's counters), dist alone at 8192 x 1 Mbp (non-pair and pair mode), KMA
+`cos`, configs[3] (one 200k float matrix, exact DNJ, a 20k-join prefix by
+default -- the whole tree is profiles/r03_config3_whole_tree.json: the
+single-GPU engine at N = 1, sharded over RCCL at N > 1) and the sharded NJ.
 """
 import argparse
 import json
@@ -48,7 +54,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-# dist roofline: 32-bit integer VALU issue.  A 32-position word pair costs 3
+# VALU dist kernel (k_snp_tile, CCG_DIST_MFMA=0; the MFMA kernels below are
+# the default): 32-bit integer VALU issue.  A 32-position word pair costs 3
 # instructions (v_xor, v_bitop3, v_bcnt with accumulate).  Nominal peak
 # (MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz =
 # 7.86e13 instruction-lanes/s (`peak`, `frac`).  Measured on gfx950
@@ -82,6 +89,7 @@ def _latest(*names):
 PMC_SUMMARY = _latest("r03_pmc.json", "r02_pmc.json")
 PMC_HEADLINE = _latest("r03_pmc_headline.json")
 SHARD_LEG_TIMEOUT_S = 600
+HEADLINE_TIMEOUT_S = 1200
 
 
 _LEG = ["start"]
@@ -964,9 +972,24 @@ def main():
     m = n * (n - 1) // 2
     elems = m if world == 1 else nt.shard_elems(n, rank, world)
     log(f"headline: configs[2] pipeline {n} x {L}, world {world}, {args.warmup} warmup + {args.steps} steps")
+    hwd = None
+    if world > 1:   # a collective that never completes ends the run with a line saying so, not a hang
+        import threading
+
+        def _headline_timeout():
+            if rank == 0:
+                print(json.dumps({"metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
+                                  "value": None, "n_gpus": world, "error": f"sharded headline did not finish in "
+                                  f"{HEADLINE_TIMEOUT_S} s (transport {transport})"}), flush=True)
+            os._exit(3)
+        hwd = threading.Timer(HEADLINE_TIMEOUT_S, _headline_timeout)
+        hwd.daemon = True
+        hwd.start()
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0)
+    if hwd is not None:
+        hwd.cancel()
     dt = head["dt"]
     # dist launches per call (snp_launch_mfma2: 256 x 256 tiles in batches of
     # 65536; no split-K at the headline's tile count)
