@@ -919,7 +919,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=50_000, help="headline taxa (configs[2])")
+    ap.add_argument("--n", "--taxa", dest="n", type=int, default=50_000,
+                    help="headline taxa (configs[2]; --taxa under torchrun, whose own options take --n)")
     ap.add_argument("--L", type=int, default=5_000_000, help="headline alignment length (configs[2])")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
