@@ -750,7 +750,7 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
 
 HEADLINE_STATS = _latest("r03_kernel_stats_headline.csv")
 HSYM = {"dist": ("k_snp_mfma2",), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan"),
-        "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join",), "dnj_requeue": ("k_dnj_requeue",),
+        "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join_pf", "k_dnj_join"), "dnj_requeue": ("k_dnj_requeue",),
         "exact_sum": ("k_exact_sum",), "dnj_select": ("k_dnj_select",), "init": ("k_init_rows",)}
 
 

@@ -24,14 +24,20 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def matrix(n, kind, seed=11):
+def matrix(n, kind, seed=11, threads=16):
+    from concurrent.futures import ThreadPoolExecutor
     rng = np.random.default_rng(seed)
     pts = rng.random((n, 8))
     D = np.empty(n * (n - 1) // 2)
-    for i in range(1, n):
-        o = i * (i - 1) // 2
-        d = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
-        D[o:o + i] = np.rint(d * 5000.0) if kind == "int" else np.round(d * 1e9) / 1e9
+
+    def rows(r0, r1):   # row by row, the same arithmetic in any thread
+        for i in range(max(r0, 1), r1):
+            o = i * (i - 1) // 2
+            d = np.sqrt(((pts[:i] - pts[i]) ** 2).sum(1))
+            D[o:o + i] = np.rint(d * 5000.0) if kind == "int" else np.round(d * 1e9) / 1e9
+    step = 512
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda r: rows(r, min(n, r + step)), range(0, n, step)))
     return D
 
 
