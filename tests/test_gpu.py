@@ -506,3 +506,19 @@ def test_dnj_reference_rule_counters(dev, monkeypatch, kind, n, band):
     sh = dev.tree_shard(D, n, None, method=1, exact=True, profile=True)
     assert (sh[0] == got).all()
     assert (sh[3][10 + 2 * K], sh[3][11 + 2 * K]) == (int(rst[0]), int(rst[1]))
+
+
+@pytest.mark.parametrize("n,jpf", [(900, "1"), (1400, "2"), (1400, "0")])
+def test_dnj_missing_large_n_join(dev, monkeypatch, n, jpf):
+    """Missing entries (updateD's general body, k_update_general) through the
+    large-n join forms at small n: k_dnj_fold's chunk summaries with
+    k_dnj_join_pf (1), its block-0 replay path (2), the per-block replay (0);
+    joins bit-identical to the serial reference."""
+    from oracle import pyoracle
+    monkeypatch.setenv("CCG_PREFOLD_N", "0")
+    monkeypatch.setenv("CCG_JOIN_PF", jpf)
+    D = _missing_ltd(n, n)
+    got, fn, fd, _ = dev.tree(D, n, method=1, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=1)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
