@@ -1175,6 +1175,95 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	}
 }
 
+// Row groups (measurement form, CCG_SCAN_WAVE = 20 / 21): one wave rescans
+// the same seg-cell column range of G consecutive entries, so each sD load
+// serves G rows (sD bytes per cell / G) and the wave holds G row streams in
+// flight; rows are read one cell per lane (4- or 8-byte loads, coalesced per
+// row), each row's (q, j) reduced and stored as its own unit partial, so the
+// fold and the join read the layout of k_dnj_scan_v.  UC columns per lane per
+// step.
+template <int ET, int G, int UC>
+__global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                   int n, int seg) {
+	typedef typename Elem<ET>::T T;
+	__shared__ int erow[REPLAY_CAP];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int r0 = b.crow[tid];
+	const int done = ctl->done, Tn = ctl->T;
+	if(done) return;
+	if(Tn == 0) return;
+	const int umax = dnj_umax(n, seg), ngroups = (Tn + G - 1) / G, nunits = ngroups * umax;
+	if((int) blockIdx.x * (TB / 64) >= nunits) return;
+	const bool lds = Tn <= REPLAY_CAP;
+	if(lds) {
+		if(tid < Tn) erow[tid] = r0;
+		for(int e = TB + tid; e < Tn; e += TB) erow[e] = b.crow[e];
+	}
+	__syncthreads();
+	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	for(int u = gw; u < nunits; u += nw) {
+		const int g = u / umax, s = u - g * umax, c0 = s * seg;
+		int r[G], c1[G];
+		bool act[G];
+		int cmax = c0;
+#pragma unroll
+		for(int k = 0; k < G; ++k) {
+			const int e = g * G + k;
+			r[k] = e < Tn ? (lds ? erow[e] : b.crow[e]) : 0;
+			act[k] = e < Tn && c0 < r[k];
+			c1[k] = act[k] ? (c0 + seg < r[k] ? c0 + seg : r[k]) : c0;
+			cmax = c1[k] > cmax ? c1[k] : cmax;
+		}
+		if(cmax == c0) continue;   // wave-uniform
+		double sDr[G], q[G];
+		int idx[G];
+		const T *row[G];
+#pragma unroll
+		for(int k = 0; k < G; ++k) {
+			sDr[k] = act[k] ? b.sD[r[k]] : 0.0;
+			row[k] = D + tri(act[k] ? r[k] : 1);
+			q[k] = DBL_MAX;
+			idx[k] = 0;
+		}
+		for(int base = c0; base < cmax; base += 64 * UC) {
+			double sk[UC];
+			T v[G][UC];
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				sk[m] = b.sD[c < cmax ? c : cmax - 1];
+#pragma unroll
+				for(int k = 0; k < G; ++k) v[k][m] = row[k][c < c1[k] ? c : (act[k] ? c1[k] - 1 : 0)];
+			}
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+#pragma unroll
+				for(int k = 0; k < G; ++k) {
+					const double d = Elem<ET>::get(v[k][m], bs);
+					const double x = qcrit(n, n, d, sDr[k], sk[m]);
+					const bool take = c < c1[k] && 0 <= d && qarg_better(x, c, q[k], idx[k]);
+					q[k] = take ? x : q[k];
+					idx[k] = take ? c : idx[k];
+				}
+			}
+		}
+#pragma unroll
+		for(int k = 0; k < G; ++k) {
+			if(!act[k]) continue;   // wave-uniform
+			double qq = q[k];
+			int ii = idx[k];
+			qarg_wave_reduce(qq, ii);
+			if(lane == 0) {
+				const int e = g * G + k;
+				b.cq[e * umax + s] = qq;
+				b.cj[e * umax + s] = ii;
+			}
+		}
+	}
+}
+
 // ------------------------------------------------------------------ DNJ fold
 // Rows with many units (large n): each entry's unit partials folded once into
 // (rf, rj), one lane per entry and one wave per 64-entry chunk (scan order),

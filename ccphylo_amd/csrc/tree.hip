@@ -1667,7 +1667,9 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 		kt.mark(CCG_K_FIND);
 		const int sm = g_grid.scan_mode(n, ET);
-		if(sm >= 4 && !GEN) {
+		if(sm == 20 && !GEN) k_dnj_scan_g<ET, 4, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+		else if(sm == 21 && !GEN) k_dnj_scan_g<ET, 8, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+		else if(sm >= 4 && !GEN) {
 			switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
 				SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7) SV_(13) SV_(15)

@@ -522,3 +522,22 @@ def test_dnj_missing_large_n_join(dev, monkeypatch, n, jpf):
     ref, rfn, rfd = pyoracle.tree(D, n, method=1)
     assert (fn, fd) == (rfn, rfd)
     assert len(got) == len(ref) and (got == ref).all()
+
+
+@pytest.mark.parametrize("mode", ["20", "21"])
+@pytest.mark.parametrize("kind,n,et", [("euc", 2500, 8), ("clade", 3000, 8), ("euc", 2000, 4)])
+def test_dnj_scan_row_groups(dev, monkeypatch, mode, kind, n, et):
+    """The row-group rescan (k_dnj_scan_g: G rows per wave sharing the sD
+    loads of a column range) at small n with the large-n fold and join:
+    joins bit-identical to the serial reference."""
+    from oracle import pyoracle
+    monkeypatch.setenv("CCG_SCAN_WAVE", mode)
+    monkeypatch.setenv("CCG_PREFOLD_N", "0")
+    monkeypatch.setenv("CCG_SEG_MUL", "1")
+    D = _euclid(n, n) if kind == "euc" else _clade_ltd(n, n)
+    if et == 4:
+        D = D.astype(np.float32)
+    got, fn, fd, _ = dev.tree(D, n, etype=et, method=1, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, etype=et, method=1)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
