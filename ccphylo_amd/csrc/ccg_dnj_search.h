@@ -70,11 +70,15 @@ struct DnjGrid {
 	// join at 50k (headline data): 88.4 (block) -> 72.0 (wave) -> 66.7 us
 	// (wave, 16-byte loads) -> 65.2 us (+ nontemporal row loads and 16-byte
 	// sD loads where aligned, mode 9; 8433 -> 8920 joins/s); 10k: 9.4 (block)
-	// against 9.8 us (wave).  Float rows keep mode 4: configs[3]'s first 30k
-	// joins rescan in 41.7 s with it against 46.0 (mode 9), 46.8 (11), 47.0
-	// (13), 47.5 s (15).  CCG_SCAN_WAVE=0/1/4..19 forces a form.
+	// against 9.8 us (wave).  Float rows take the row-group form (mode 20,
+	// k_dnj_scan_g, 4 rows per wave sharing the sD loads): configs[3]'s first
+	// 30k joins rescan in 34.0 s against 47.0 s with mode 4 on the same box
+	// (mode 4 41.7-47.0 s over boxes; 9: 46.0, 11: 46.8, 13: 47.0, 15: 47.5);
+	// double rows gain nothing from it at 50k (67.3 against 68.0 us per join).
+	// In the sharded engine (no row groups) modes >= 4 run k_dnj_scan_v.
+	// CCG_SCAN_WAVE=0/1/4..19/20/21 forces a form.
 	int scan_mode(int n, int et = 8) const {
-		return scan_wave >= 0 ? scan_wave : n > 16384 ? (et == 8 ? 9 : 4) : 0;
+		return scan_wave >= 0 ? scan_wave : n > 16384 ? (et == 8 ? 9 : 20) : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
