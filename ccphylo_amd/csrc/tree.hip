@@ -1669,6 +1669,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int sm = g_grid.scan_mode(n, ET);
 		if(sm == 20 && !GEN) k_dnj_scan_g<ET, 4, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 		else if(sm == 21 && !GEN) k_dnj_scan_g<ET, 8, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+		else if(sm == 22 && !GEN) k_dnj_scan_g<ET, 4, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+		else if(sm == 23 && !GEN) k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 		else if(sm >= 4 && !GEN) {
 			switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
