@@ -74,7 +74,8 @@ struct DnjGrid {
 	// k_dnj_scan_g, 4 rows per wave sharing the sD loads): configs[3]'s first
 	// 30k joins rescan in 34.0 s against 47.0 s with mode 4 on the same box
 	// (mode 4 41.7-47.0 s over boxes; 9: 46.0, 11: 46.8, 13: 47.0, 15: 47.5);
-	// double rows gain nothing from it at 50k (67.3 against 68.0 us per join).
+	// double rows gain nothing from it at 50k (joins/s: G4/UC8 8472, G4/UC4
+	// 8453, G2/UC8 8656 against 8901 for mode 9; modes 20, 22, 23).
 	// In the sharded engine (no row groups) modes >= 4 run k_dnj_scan_v.
 	// CCG_SCAN_WAVE=0/1/4..19/20/21 forces a form.
 	int scan_mode(int n, int et = 8) const {
