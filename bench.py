@@ -132,6 +132,14 @@ def host_cpus():
     return ncpu, quota
 
 
+def effective_cores():
+    """The CPUs a CPU baseline can actually use: the affinity set, capped by
+    the cgroup quota (the GPU box lists every host CPU but grants 16)."""
+    import math
+    ncpu, quota = host_cpus()
+    return max(1, min(ncpu, math.ceil(quota))) if quota else ncpu
+
+
 from tools.synth import euclid as euclid_ltd  # noqa: E402
 
 
@@ -265,7 +273,7 @@ def cpu_baseline(D, n, tmpdir, threads=None, method="dnj"):
     host pthreads (`-t`); the faster is the baseline.  Falls back to the
     oracle's C restatement in-process."""
     if threads is None:
-        threads = sorted({1, host_cpus()[0]})
+        threads = sorted({1, effective_cores()})
     ref = os.path.join(ROOT, "oracle", "_ref", "ccphylo")
     if os.path.exists(ref):
         from ccphylo_amd import native
@@ -317,7 +325,7 @@ def cpu_baseline_dist(tmpdir, sizes=(1024, 2048), L=20_000, threads=None):
     if not os.path.exists(ref):
         return None
     ncpu, quota = host_cpus()
-    threads = threads or ncpu
+    threads = threads or effective_cores()
     rng = np.random.default_rng(11)
     lut = np.frombuffer(b"ACGT", dtype=np.uint8)
     walls = {}
@@ -458,13 +466,14 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
     if not os.path.exists(ref):
         return {"error": "reference binary absent (oracle/_ref not built)"}
     ncpu, quota = host_cpus()
+    cores = effective_cores()
     masked = [w for w in range((L + 31) // 32) if incs_host[w] == 0]
     fa = os.path.join(tmpdir, "head.fsa")
     phy = os.path.join(tmpdir, "head.phy")
     nwk = os.path.join(tmpdir, "head.nwk")
     packed_rows_to_fasta(fa, seqs_host[:m], L, masked)
     t0 = time.perf_counter()
-    subprocess.run([ref, "dist", "-i", fa, "-t", str(ncpu), "-o", phy], capture_output=True, timeout=900, check=True)
+    subprocess.run([ref, "dist", "-i", fa, "-t", str(cores), "-o", phy], capture_output=True, timeout=900, check=True)
     t1 = time.perf_counter()
     # -x 3: the reference's formNode (nwck.c:52-53, :75) reserves 32 bytes for
     # "(" + two ":%.*f" lengths + ",)"; at the default 9 digits a length of
@@ -484,14 +493,16 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
     os.unlink(phy)
     os.unlink(nwk)
     pairs = m * (m - 1) / 2
-    return {"value": round(pairs / (t2 - t0), 2), "unit": "taxa-pairs/s (dist + DNJ tree, end to end)",
-            "cores": ncpu, "host_cpus": ncpu, "cgroup_cpu_quota": quota, "kind": "reference",
+    return {"value": round(pairs / (t2 - t0), 2),
+            "unit": "taxa-pairs/s (dist + DNJ tree, end to end, FASTA parse included; a sample rate)",
+            "cores": cores, "host_cpus": ncpu, "cgroup_cpu_quota": quota, "kind": "reference",
             "dist_s": round(t1 - t0, 3), "tree_s": round(t2 - t1, 3),
             "dist_nt_comparisons_per_s": round(pairs * L / (t1 - t0), 1),
             "parity_mismatched_cells": mism, "parity_newick_identical": same_tree,
-            "sample": f"reference ccphylo 0.8.5 `dist -t {ncpu}` + `tree -x 3` (DNJ) on the first {m} taxa of the same "
-                      f"{L / 1e6:g} Mbp alignment (FASTA, parse included); the GPU's LT cells and Newick for the same "
-                      f"taxa are compared with the reference's"}
+            "sample": f"SAMPLE RATE: reference ccphylo 0.8.5 `dist -t {cores}` + `tree -x 3` (DNJ) on the first {m} "
+                      f"of the {L / 1e6:g} Mbp headline alignment's taxa (a {m * L / 4e9:.2f} GB FASTA written and "
+                      f"parsed inside the time); the GPU's LT cells and Newick for the same taxa are compared with "
+                      f"the reference's"}
 
 
 def make_headline_alignment(torch, n, L):
@@ -914,6 +925,25 @@ def config1_extras(dev, torch, td, n=10_000, steps=3, cpu=True, threads=16):
     return out
 
 
+def spawn_ranks(world):
+    """One child process per rank (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT as torch.distributed.run sets them), each running
+    this script with the same arguments.  Returns the largest exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:   # a free port for the rendezvous store
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return (max(bad, key=abs) if bad else 0) & 0xFF
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -935,6 +965,16 @@ def main():
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N rank
+        # processes here, before this process touches any GPU, and exit with
+        # the worst of their codes (rank 0 prints the line)
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (the launcher's world must match)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -8,7 +8,7 @@ int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int 
 int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out,
                            bool host_in);
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
-                  double *final_d, int64_t *stats);
+                  double *final_d, int64_t *stats, const ccg_dnj_state *sin, ccg_dnj_state *sout);
 int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel);
 
 static char g_last_error[512];
@@ -157,7 +157,21 @@ int ccg_tree_dev(ccg_ctx *c, const ccg_tree_args *a, void *D, ccg_join *joins, i
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
 	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
-	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats);
+	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats, NULL, NULL);
+}
+
+int ccg_tree_dev_state(ccg_ctx *c, const ccg_tree_args *a, void *D, const ccg_dnj_state *in, ccg_dnj_state *out,
+                       ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats) {
+	if(!c || !a || !D || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
+	if(a->n < 3 || a->method != CCG_TREE_DNJ) return CCG_EINVAL;
+	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
+	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
+	if(in && (in->n != a->n || !in->sD || !in->Q || !in->N || !in->P || in->cand < 0 || in->cand >= in->n))
+		return CCG_EINVAL;
+	if(out && (!out->sD || !out->Q || !out->N || !out->P)) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	CCG_CHECK(hipDeviceSynchronize());
+	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats, in, out);
 }
 
 int ccg_tree(ccg_ctx *c, const ccg_tree_args *a, const void *D, ccg_join *joins, int *njoins, int *final_n,

@@ -78,6 +78,10 @@ struct DnjGrid {
 	// 8453, G2/UC8 8656 against 8901 for mode 9; modes 20, 22, 23).
 	// In the sharded engine (no row groups) modes >= 4 run k_dnj_scan_v.
 	// CCG_SCAN_WAVE=0/1/4..19/20/21 forces a form.
+	// past 16384 taxa: double rows (the headline) stream with the 16-byte
+	// nontemporal wave scan (9); narrower rows (float -p, u16 -s, u8 -b) in row
+	// groups (20), where the 8-byte sD load per cell outweighs the row bytes
+	// and one sD load serves 4 rows
 	int scan_mode(int n, int et = 8) const {
 		return scan_wave >= 0 ? scan_wave : n > 16384 ? (et == 8 ? 9 : 20) : 0;
 	}
@@ -1180,7 +1184,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	}
 }
 
-// Row groups (measurement form, CCG_SCAN_WAVE = 20 / 21): one wave rescans
+// Row groups (the default rescan past 16384 taxa for every element type but
+// double, scan_mode 20; 21-23 are other (G, UC) forms for measurement,
+// CCG_SCAN_WAVE): one wave rescans
 // the same seg-cell column range of G consecutive entries, so each sD load
 // serves G rows (sD bytes per cell / G) and the wave holds G row streams in
 // flight; rows are read one cell per lane (4- or 8-byte loads, coalesced per

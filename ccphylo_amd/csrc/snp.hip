@@ -14,9 +14,15 @@
 // (v_xor, v_bitop3, v_bcnt with accumulate).
 // Pair mode keeps each taxon's mask m beside its planes:
 //   d += popc(((hi_a ^ hi_b) | (lo_a ^ lo_b)) & m_a & m_b), n += popc(m_a & m_b).
-// This is VALU-integer-bound (no dense contraction, MFMA not used): 128x128
-// pair tiles, 8x8 pairs per thread in registers, KC-word chunks of both row
-// panels staged through LDS.
+// Two kernel families compute it:
+//   - the default, k_snp_mfma2 (non-pair) / k_snp_mfma_pair: the count as an
+//     exact MX-fp4 dot product on the matrix cores (each code a +-1
+//     tetrahedron vector, dist = (3 L - dot) / 4), 256x256 pair tiles,
+//     MFMA-bound;
+//   - k_snp_tile / k_snp_tile_pair (CCG_DIST_MFMA=0): the popcount form
+//     above, VALU-integer-bound, 128x128 pair tiles, 8x8 pairs per thread in
+//     registers.
+// Both stage KC-word chunks of the two row panels through LDS.
 #include <vector>
 #include "ccg_internal.h"
 #include "ccg_shard_layout.h"
@@ -1368,8 +1374,11 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 			pfx[I + 1] = pfx[I] + cdivll(rmax, TILE2);
 		}
 		CCG_CHECK(hipMalloc(&d_pfx, (size_t) (npanels + 1) * sizeof(long long)));
-		CCG_CHECK(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
-		                         ctx->stream));
+		if(hipMemcpyAsync(d_pfx, pfx.data(), (size_t) (npanels + 1) * sizeof(long long), hipMemcpyHostToDevice,
+		                  ctx->stream) != hipSuccess) {
+			hipFree(d_pfx);
+			return CCG_EHIP;
+		}
 		t_end = pfx[npanels];
 		f1 = ccg_shard_elems(n, rank, world);
 	} else {
@@ -1381,7 +1390,10 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	}
 	const long long tiles = t_end - t_begin;
 	hipDeviceProp_t prop;
-	CCG_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+	if(hipGetDeviceProperties(&prop, ctx->device) != hipSuccess) {
+		hipFree(d_pfx);
+		return CCG_EHIP;
+	}
 	const long long slots = prop.multiProcessorCount;   // one block per CU
 	const int chunks = Wp / KC2;
 	int S = 1;
@@ -1393,12 +1405,19 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	int Wk = (int) cdivll(chunks, S) * KC2;
 	if(Wk > MFMA_KMAX) Wk = (MFMA_KMAX / KC2) * KC2;
 	S = (int) cdivll(Wp, Wk);
-	unsigned *cnt = NULL;
-	if(S > 1) {
-		CCG_CHECK(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)));
-		CCG_CHECK(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
-	}
 	const long long batch = 1 << 16;
+	unsigned *cnt = NULL;
+	int rc = CCG_OK;
+	// every failure below leaves through `out`, which frees d_pfx and cnt
+#define MF2_TRY(x) do { if((x) != hipSuccess) { rc = CCG_EHIP; goto out; } } while(0)
+	if(S > 1) {
+		if(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)) != hipSuccess) {
+			cnt = NULL;
+			rc = CCG_ENOMEM;
+			goto out;
+		}
+		MF2_TRY(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
+	}
 	for(long long t = t_begin * S; t < t_end * S; t += batch) {
 		const long long items = t_end * S - t < batch ? t_end * S - t : batch;
 		const uint2 *pl = (const uint2 *) planes;
@@ -1419,18 +1438,21 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 				k_snp_mfma2<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
 				    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1);
 		}
-		CCG_CHECK(hipGetLastError());
+		MF2_TRY(hipGetLastError());
 	}
 	if(S > 1) {
 		const long long g = cdivll(f1 - f0, 256);
 		k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, f0, f0, f1, nFactor,
 		                                                                                a->byteScale, (T *) D);
-		CCG_CHECK(hipGetLastError());
+		MF2_TRY(hipGetLastError());
 	}
-	CCG_CHECK(hipStreamSynchronize(ctx->stream));
-	if(cnt) CCG_CHECK(hipFree(cnt));
-	if(d_pfx) CCG_CHECK(hipFree(d_pfx));
-	return CCG_OK;
+	MF2_TRY(hipStreamSynchronize(ctx->stream));
+out:
+#undef MF2_TRY
+	if(rc != CCG_OK) hipStreamSynchronize(ctx->stream);   // no launch may still read cnt / d_pfx
+	if(cnt && hipFree(cnt) != hipSuccess && rc == CCG_OK) rc = CCG_EHIP;
+	if(d_pfx && hipFree(d_pfx) != hipSuccess && rc == CCG_OK) rc = CCG_EHIP;
+	return rc;
 }
 
 template <int ET>
@@ -1779,7 +1801,12 @@ static int snp_planes(ccg_ctx *ctx, const ccg_snp_args *a, int W32, int Wp, void
 			*mask = NULL;
 			return CCG_ENOMEM;
 		}
-		CCG_CHECK(hipMemcpyAsync(*mask, a->incs, (size_t) a->stride * 4, hipMemcpyHostToDevice, ctx->stream));
+		if(hipMemcpyAsync(*mask, a->incs, (size_t) a->stride * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+			hipFree(stage);
+			hipFree(*mask);
+			*mask = NULL;
+			return CCG_EHIP;
+		}
 	}
 	uint64_t *sseq = (uint64_t *) stage;
 	uint32_t *sinc = (uint32_t *) ((char *) stage + (size_t) R * a->stride * 8);
@@ -1900,7 +1927,7 @@ extern "C" int ccg_last_dist_ms(ccg_ctx *ctx, double *ms) {
 // the matrix type).  The fused `dist --tree` stores the same values in place:
 // K = round-half-even(d * 10^p) exactly (d * 10^p = hi + lo without error),
 // then K / 10^p is one correctly rounded division of exact operands, which is
-// strtod's result for the printed decimal.  Cells whose product reaches 2^52
+// strtod's result for the printed decimal.  Cells whose product reaches 2^53
 // (more digits than a double carries) set *bad; the caller refuses them.
 template <typename T>
 __global__ void k_round_decimal(T *__restrict__ D, long long elems, double P, int *__restrict__ bad) {
@@ -1909,14 +1936,27 @@ __global__ void k_round_decimal(T *__restrict__ D, long long elems, double P, in
 		const double x = (double) D[e];
 		if(x == trunc(x)) continue;   // "%d" or the integer's exact digits
 		const double hi = x * P, lo = fma(x, P, -hi);
-		if(!(fabs(hi) < 4503599627370496.0)) {
+		const double ah = fabs(hi);
+		if(!(ah < 9007199254740992.0)) {   // K itself may not be a double past 2^53
 			atomicOr(bad, 1);
 			continue;
 		}
-		double K = rint(hi);   // half-even on hi; the exact tie needs lo == 0
-		const double d = hi - K;
-		if(d == 0.5 && lo > 0) K += 1.0;
-		else if(d == -0.5 && lo < 0) K -= 1.0;
+		double K;
+		if(ah < 4503599627370496.0) {
+			K = rint(hi);   // half-even on hi; the exact tie needs lo == 0
+			const double d = hi - K;
+			if(d == 0.5 && lo > 0) K += 1.0;
+			else if(d == -0.5 && lo < 0) K -= 1.0;
+		} else {
+			// 2^52 <= |hi| < 2^53: hi is an integer and |lo| <= 1/2 (half an
+			// ulp), so x P rounds to hi unless lo is an exact tie, which goes
+			// to the even neighbour (|K| <= 2^53 stays exact)
+			K = hi;
+			if(lo == 0.5 || lo == -0.5) {
+				const double other = hi + (lo > 0 ? 1.0 : -1.0);
+				K = fmod(hi, 2.0) == 0.0 ? hi : other;
+			}
+		}
 		D[e] = (T) (K / P);
 	}
 }

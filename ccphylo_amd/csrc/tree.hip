@@ -1650,6 +1650,16 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	return CCG_OK;
 }
 
+// DNJ: k_dnj_plan of the join at matrix size n (first: the run's first join,
+// whose candidate k_dnj_prep or a resumed state left in ctl)
+template <int ET, bool GEN>
+static void enqueue_plan(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first) {
+	const int seg = g_grid.seg(n);
+	const unsigned gp = g_grid.plan_blocks(n);
+	if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
+	else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
+}
+
 // One join's kernels for a matrix of n taxa; returns the launch count.
 template <int ET, bool GEN>
 static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first,
@@ -1662,9 +1672,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int seg = g_grid.seg(n), prefold = g_grid.prefold(n);
 		// one-phase search: k_dnj_plan lists S and the rows below it under the
 		// partner-cell bound, k_dnj_scan rescans them all
-		const unsigned gp = g_grid.plan_blocks(n);
-		if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
-		else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
+		enqueue_plan<ET, GEN>(st, D, bs, b, n, first);
 		kt.mark(CCG_K_FIND);
 		const int sm = g_grid.scan_mode(n, ET);
 		if(sm == 20 && !GEN) k_dnj_scan_g<ET, 4, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
@@ -1729,7 +1737,8 @@ static bool g_progress = false;
 
 template <int ET>
 static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins,
-                      int *final_n, double *final_d, int64_t *stats) {
+                      int *final_n, double *final_d, int64_t *stats, const ccg_dnj_state *sin,
+                      ccg_dnj_state *sout) {
 	typedef typename Elem<ET>::T T;
 	T *D = (T *) Dd;
 	const int n0 = a->n;
@@ -1748,6 +1757,11 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	init.exact = a->exact != 0;
 	init.method = a->method;
 	init.hj = init.hi = -1;
+	if(sin) {   // a resumed DNJ state: its candidate takes k_dnj_prep's place
+		init.cand = sin->cand;
+		init.cand_q = sin->Q[sin->cand];
+		init.cand_p = sin->P[sin->cand];
+	}
 	CCG_CHECK(hipMemcpyAsync(b.ctl, &init, sizeof(init), hipMemcpyHostToDevice, st));
 	long long launches = 0;
 	static thread_local KTimer kt;   // one per host thread (the CLI runs one rank per thread)
@@ -1756,7 +1770,16 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	k_init_rows<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
 	k_init_cols<ET><<<cdiv(n0, TB), TB, 0, st>>>(D, n0, bs, b.sD, b.N, b.ctl);
 	launches += 2;
-	if(a->method == CCG_TREE_DNJ) {
+	bool resumed_counts = false;   // a resumed state whose N differs from the matrix size somewhere
+	if(sin) {
+		// initSummaD above only detected missing entries (ctl->has_missing);
+		// the state's own vectors replace its sums
+		CCG_CHECK(hipMemcpyAsync(b.sD, sin->sD, (size_t) n0 * 8, hipMemcpyHostToDevice, st));
+		CCG_CHECK(hipMemcpyAsync(b.Q, sin->Q, (size_t) n0 * 8, hipMemcpyHostToDevice, st));
+		CCG_CHECK(hipMemcpyAsync(b.N, sin->N, (size_t) n0 * 4, hipMemcpyHostToDevice, st));
+		CCG_CHECK(hipMemcpyAsync(b.P, sin->P, (size_t) n0 * 4, hipMemcpyHostToDevice, st));
+		for(int k = 0; k < n0 && !resumed_counts; ++k) resumed_counts = sin->N[k] != n0;
+	} else if(a->method == CCG_TREE_DNJ) {
 		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(DenseRows(), D, n0, bs, b.sD, b.N, b.Q, b.P);
 		k_dnj_prep<><<<1, TB, 0, st>>>(b, n0);
 		launches += 2;
@@ -1769,7 +1792,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	TreeCtl h;
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 	CCG_CHECK(hipStreamSynchronize(st));
-	const bool general = h.has_missing != 0;
+	// GEN = false assumes N[k] == n for every row (no missing entries ever)
+	const bool general = h.has_missing != 0 || resumed_counts;
 #ifdef CCG_TRACE
 	const char *tn = getenv("CCG_TRACE_N");
 	int trace_hi = tn ? atoi(tn) : n0 / 2;
@@ -1902,6 +1926,29 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		CCG_CHECK(hipStreamSynchronize(st));
 		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
 	}
+	if(sout) {   // the loop state after the last join, as the next minQpair reads it
+		sout->n = h.done ? 0 : n;
+		sout->cand = 0;
+		if(!h.done) {
+			if(n != n0) {
+				// the next join's plan prologue folds the last requeue's partials
+				// into Q/P of rows j and i (and moves row n's sD/N to i) and
+				// picks the candidate (minPos, dnj.c:1026-1032); nothing after
+				// it in this run reads what else it lists
+				if(general) enqueue_plan<ET, true>(st, D, bs, b, n, 0);
+				else enqueue_plan<ET, false>(st, D, bs, b, n, 0);
+				CCG_CHECK(hipGetLastError());
+			}
+			TreeCtl h2;   // h keeps the run's counters (the extra plan adds its S cells)
+			CCG_CHECK(hipMemcpyAsync(&h2, b.ctl, sizeof(h2), hipMemcpyDeviceToHost, st));
+			CCG_CHECK(hipMemcpyAsync(sout->sD, b.sD, (size_t) n * 8, hipMemcpyDeviceToHost, st));
+			CCG_CHECK(hipMemcpyAsync(sout->Q, b.Q, (size_t) n * 8, hipMemcpyDeviceToHost, st));
+			CCG_CHECK(hipMemcpyAsync(sout->N, b.N, (size_t) n * 4, hipMemcpyDeviceToHost, st));
+			CCG_CHECK(hipMemcpyAsync(sout->P, b.P, (size_t) n * 4, hipMemcpyDeviceToHost, st));
+			CCG_CHECK(hipStreamSynchronize(st));
+			sout->cand = h2.cand;
+		}
+	}
 	if(stats) {
 		stats[0] = h.rows;
 		stats[1] = h.cells;
@@ -1989,12 +2036,12 @@ int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out,
 }
 
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
-                  double *final_d, int64_t *stats) {
+                  double *final_d, int64_t *stats, const ccg_dnj_state *sin, ccg_dnj_state *sout) {
 	switch(a->etype) {
-		case 8: return tree_run_t<8>(ctx, a, Dd, joins, njoins, final_n, final_d, stats);
-		case 4: return tree_run_t<4>(ctx, a, Dd, joins, njoins, final_n, final_d, stats);
-		case 2: return tree_run_t<2>(ctx, a, Dd, joins, njoins, final_n, final_d, stats);
-		case 1: return tree_run_t<1>(ctx, a, Dd, joins, njoins, final_n, final_d, stats);
+		case 8: return tree_run_t<8>(ctx, a, Dd, joins, njoins, final_n, final_d, stats, sin, sout);
+		case 4: return tree_run_t<4>(ctx, a, Dd, joins, njoins, final_n, final_d, stats, sin, sout);
+		case 2: return tree_run_t<2>(ctx, a, Dd, joins, njoins, final_n, final_d, stats, sin, sout);
+		case 1: return tree_run_t<1>(ctx, a, Dd, joins, njoins, final_n, final_d, stats, sin, sout);
 		default: return CCG_EINVAL;
 	}
 }

@@ -22,6 +22,7 @@
 // continued serially from column chunks gathered the same way.  The joins are
 // therefore bit-identical to ccg_tree's for every world size.
 #include <dlfcn.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <rccl/rccl.h>
@@ -380,9 +381,23 @@ static int rccl_load() {
 	return CCG_OK;
 }
 
+// A rank's communicator.  ccg_rccl_abort may run on another thread (the
+// multi-GPU CLI aborts every rank's communicator when one rank fails): `mu`
+// serialises it against this rank's own collective calls, and once `aborted`
+// is set the calls fail without touching the (freed) communicator; the
+// owner's ccg_rccl_close then only frees this struct.
 struct RcclUser {
 	ncclComm_t comm;
+	pthread_mutex_t mu;
+	int aborted;
 };
+
+static int rccl_gone(RcclUser *u, const char *what) {
+	char m[160];
+	snprintf(m, sizeof(m), "%s: the communicator was aborted (a peer rank failed)", what);
+	ccg_set_last_msg(m);
+	return 1;
+}
 
 // widest element that tiles the byte range (the sum is a gather either way)
 static void rccl_type(const void *p, size_t bytes, ncclDataType_t *t, size_t *count) {
@@ -403,7 +418,14 @@ static int rccl_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 	ncclDataType_t t;
 	size_t cnt;
 	rccl_type(buf, bytes, &t, &cnt);
-	ncclResult_t r = g_rccl.all_reduce(buf, buf, cnt, t, ncclSum, ((RcclUser *) user)->comm, (hipStream_t) stream);
+	RcclUser *u = (RcclUser *) user;
+	pthread_mutex_lock(&u->mu);
+	if(u->aborted) {
+		pthread_mutex_unlock(&u->mu);
+		return rccl_gone(u, "ncclAllReduce");
+	}
+	ncclResult_t r = g_rccl.all_reduce(buf, buf, cnt, t, ncclSum, u->comm, (hipStream_t) stream);
+	pthread_mutex_unlock(&u->mu);
 	if(r != ncclSuccess) {
 		char m[160];
 		snprintf(m, sizeof(m), "ncclAllReduce: %s", g_rccl.err(r));
@@ -413,8 +435,14 @@ static int rccl_allreduce(void *user, void *buf, size_t bytes, void *stream) {
 }
 
 static int rccl_bcast(void *user, const void *send, void *recv, size_t bytes, int root, void *stream) {
-	ncclResult_t r = g_rccl.bcast(send ? send : recv, recv, bytes, ncclUint8, root, ((RcclUser *) user)->comm,
-	                              (hipStream_t) stream);
+	RcclUser *u = (RcclUser *) user;
+	pthread_mutex_lock(&u->mu);
+	if(u->aborted) {
+		pthread_mutex_unlock(&u->mu);
+		return rccl_gone(u, "ncclBroadcast");
+	}
+	ncclResult_t r = g_rccl.bcast(send ? send : recv, recv, bytes, ncclUint8, root, u->comm, (hipStream_t) stream);
+	pthread_mutex_unlock(&u->mu);
 	if(r != ncclSuccess) {
 		char m[160];
 		snprintf(m, sizeof(m), "ncclBroadcast: %s", g_rccl.err(r));
@@ -428,7 +456,14 @@ static int rccl_allgather(void *user, const void *send, void *recv, size_t bytes
 	size_t cnt;
 	// the widest element tiling both buffers and the slot size
 	rccl_type((const void *) ((uintptr_t) send | (uintptr_t) recv), bytes, &t, &cnt);
-	ncclResult_t r = g_rccl.all_gather(send, recv, cnt, t, ((RcclUser *) user)->comm, (hipStream_t) stream);
+	RcclUser *u = (RcclUser *) user;
+	pthread_mutex_lock(&u->mu);
+	if(u->aborted) {
+		pthread_mutex_unlock(&u->mu);
+		return rccl_gone(u, "ncclAllGather");
+	}
+	ncclResult_t r = g_rccl.all_gather(send, recv, cnt, t, u->comm, (hipStream_t) stream);
+	pthread_mutex_unlock(&u->mu);
 	if(r != ncclSuccess) {
 		char m[160];
 		snprintf(m, sizeof(m), "ncclAllGather: %s", g_rccl.err(r));
@@ -651,7 +686,7 @@ int ccg_tree_shard_dnj_impl(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *
 
 // tree.hip: the single-GPU engine
 int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *joins, int *njoins, int *final_n,
-                  double *final_d, int64_t *stats);
+                  double *final_d, int64_t *stats, const ccg_dnj_state *sin, ccg_dnj_state *sout);
 
 // world 1 holds the whole matrix in the band layout, which is the packed LT
 // the single-GPU engine consumes: with nothing to exchange it runs that engine
@@ -702,6 +737,7 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 	CCG_CHECK(hipSetDevice(ctx->device));
 	RcclUser *u = (RcclUser *) calloc(1, sizeof(RcclUser));
 	if(!u) return CCG_ENOMEM;
+	pthread_mutex_init(&u->mu, NULL);
 	ncclUniqueId uid;
 	memcpy(&uid, id, sizeof(uid));
 	ncclResult_t r = g_rccl.init_rank(&u->comm, world, uid, rank);
@@ -709,6 +745,7 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 		char m[160];
 		snprintf(m, sizeof(m), "ncclCommInitRank: %s", g_rccl.err(r));
 		ccg_set_last_msg(m);
+		pthread_mutex_destroy(&u->mu);
 		free(u);
 		return CCG_EHIP;
 	}
@@ -726,13 +763,26 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 int ccg_rccl_abort(ccg_coll *c) {
 	if(!c || !c->user) return CCG_EINVAL;
 	if(!g_rccl.abort_comm) return CCG_EUNSUP;
-	return g_rccl.abort_comm(((RcclUser *) c->user)->comm) == ncclSuccess ? CCG_OK : CCG_EHIP;
+	RcclUser *u = (RcclUser *) c->user;
+	pthread_mutex_lock(&u->mu);   // waits for an enqueue in progress on the owner's thread
+	int rc = CCG_OK;
+	if(!u->aborted) {
+		u->aborted = 1;
+		rc = g_rccl.abort_comm(u->comm) == ncclSuccess ? CCG_OK : CCG_EHIP;
+		u->comm = NULL;
+	}
+	pthread_mutex_unlock(&u->mu);
+	return rc;
 }
 
+// the owner's call: destroys the communicator (or, after an abort, only
+// frees what is left of it)
 int ccg_rccl_close(ccg_coll *c) {
 	if(!c || !c->user) return CCG_EINVAL;
 	RcclUser *u = (RcclUser *) c->user;
-	ncclResult_t r = g_rccl.destroy(u->comm);
+	ncclResult_t r = ncclSuccess;
+	if(!u->aborted) r = g_rccl.destroy(u->comm);
+	pthread_mutex_destroy(&u->mu);
 	free(u);
 	c->user = NULL;
 	return r == ncclSuccess ? CCG_OK : CCG_EHIP;
@@ -760,7 +810,7 @@ int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll,
 		if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 		CCG_CHECK(hipSetDevice(c->device));
 		CCG_CHECK(hipDeviceSynchronize());
-		return ccg_tree_impl(c, a, Dloc, joins, njoins, final_n, final_d, stats);
+		return ccg_tree_impl(c, a, Dloc, joins, njoins, final_n, final_d, stats, NULL, NULL);
 	}
 	int rc = shard_check(c, a, coll);
 	if(rc) return rc;

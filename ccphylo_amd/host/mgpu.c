@@ -46,7 +46,6 @@ typedef struct {
 	int acc_fail;         /* rank 0 could not grow acc: every rank fails the call */
 	int first_fail;       /* the rank that aborted the group first (its error is the one reported) */
 	ccg_coll **rccl;      /* each rank's open RCCL communicator (NULL once closed or aborted) */
-	int *rccl_aborted;
 } tgroup;
 
 typedef struct {
@@ -86,7 +85,6 @@ static void tg_abort(tgroup *g, int rank) {
 		if(g->rccl[r]) {
 			ccg_rccl_abort(g->rccl[r]);
 			g->rccl[r] = NULL;
-			g->rccl_aborted[r] = 1;
 		}
 	}
 	pthread_mutex_unlock(&g->mu);
@@ -99,13 +97,12 @@ static void tg_rccl_set(tgroup *g, int rank, ccg_coll *c) {
 	pthread_mutex_unlock(&g->mu);
 }
 
-/* 1 when the rank still owns its communicator (and now closes it itself) */
-static int tg_rccl_take(tgroup *g, int rank) {
+/* the rank leaves the registry before closing its communicator itself
+ * (ccg_rccl_close destroys it, or frees what an abort left of it) */
+static void tg_rccl_take(tgroup *g, int rank) {
 	pthread_mutex_lock(&g->mu);
-	const int own = g->rccl[rank] != NULL && !g->rccl_aborted[rank];
 	g->rccl[rank] = NULL;
 	pthread_mutex_unlock(&g->mu);
-	return own;
 }
 
 /* every rank states whether its setup succeeded; 1 when all did (the same
@@ -295,7 +292,10 @@ static void *rank_main(void *p) {
 	/* the others leave their next (or current) collective */
 	if(rc) tg_abort(j->tg, j->rank);
 out:
-	if(have_coll && tg_rccl_take(j->tg, j->rank)) ccg_rccl_close(&coll);
+	if(have_coll) {
+		tg_rccl_take(j->tg, j->rank);   /* no tg_abort reaches it after this */
+		ccg_rccl_close(&coll);
+	}
 	if(dloc) ccg_free(ctx, dloc);
 	if(ctx) ccg_destroy(ctx);
 	return NULL;
@@ -319,7 +319,6 @@ static int run_ranks(const ccq_mgpu *c, const void *D, const ccg_tree_args *ta, 
 	tg.world = G;
 	tg.bufs = calloc((size_t) G, sizeof(void *));
 	tg.rccl = calloc((size_t) G, sizeof(ccg_coll *));
-	tg.rccl_aborted = calloc((size_t) G, sizeof(int));
 	pthread_mutex_init(&tg.mu, NULL);
 	pthread_cond_init(&tg.cv, NULL);
 	rank_job *jobs = calloc((size_t) G, sizeof(rank_job));
@@ -395,7 +394,6 @@ out:
 	pthread_cond_destroy(&tg.cv);
 	free(tg.bufs);
 	free(tg.rccl);
-	free(tg.rccl_aborted);
 	free(tg.acc);
 	return rc;
 }

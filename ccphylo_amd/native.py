@@ -92,6 +92,12 @@ BROADCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
+class DnjState(C.Structure):
+    """ccg_dnj_state: a DNJ loop state between two joins (host arrays)."""
+    _fields_ = [("n", C.c_int), ("cand", C.c_int), ("sD", C.c_void_p), ("Q", C.c_void_p), ("N", C.c_void_p),
+                ("P", C.c_void_p)]
+
+
 class Coll(C.Structure):
     _fields_ = [("user", C.c_void_p), ("rank", C.c_int), ("world", C.c_int), ("host_staged", C.c_int),
                 ("allreduce_sum_u8", ALLREDUCE_FN), ("broadcast", BROADCAST_FN), ("allgather", ALLGATHER_FN)]
@@ -107,7 +113,7 @@ ENGINE_SYMBOLS = [
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
-    "ccg_round_decimal_dev", "ccg_last_dist_ms",
+    "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -158,6 +164,9 @@ def engine_lib():
         lib.ccg_tree.argtypes = [C.c_void_p, C.POINTER(TreeArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int),
                                  C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         lib.ccg_tree_dev.argtypes = lib.ccg_tree.argtypes
+        lib.ccg_tree_dev_state.argtypes = [C.c_void_p, C.POINTER(TreeArgs), C.c_void_p, C.POINTER(DnjState),
+                                           C.POINTER(DnjState), C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         lib.ccg_malloc.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_size_t]
         lib.ccg_free.argtypes = [C.c_void_p, C.c_void_p]
         lib.ccg_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
@@ -327,6 +336,38 @@ class Device:
         """Same on a device LT (ccg_tree_dev); the buffer is consumed."""
         return self._tree(self.lib.ccg_tree_dev, dptr, n, etype, byte_scale, method, flags, exact, profile,
                           max_joins)
+
+    def tree_dev_state(self, dptr, n, etype=8, byte_scale=1.0, flags=0, exact=True, profile=False, max_joins=0,
+                       state=None, want_state=True):
+        """DNJ on a device LT with a checkpoint (ccg_tree_dev_state): `state`
+        (a dict n, cand, sD, Q, N, P, e.g. a previous call's) resumes the loop
+        instead of initialising it; with want_state the state after the last
+        join comes back.  Returns (joins, final_n, final_d, stats, state)."""
+        sin = None
+        if state is not None:
+            arrs = [np.ascontiguousarray(state[k], dtype=t) for k, t in
+                    (("sD", np.float64), ("Q", np.float64), ("N", np.int32), ("P", np.int32))]
+            assert int(state["n"]) == n and all(len(x) >= n for x in arrs)
+            sin = DnjState(n, int(state["cand"]), *[x.ctypes.data for x in arrs])
+        out, sout = None, None
+        if want_state:
+            out = {"sD": np.zeros(n), "Q": np.zeros(n), "N": np.zeros(n, dtype=np.int32),
+                   "P": np.zeros(n, dtype=np.int32)}
+            sout = DnjState(0, 0, out["sD"].ctypes.data, out["Q"].ctypes.data, out["N"].ctypes.data,
+                            out["P"].ctypes.data)
+        joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)
+        nj, fn, fd = C.c_int(0), C.c_int(0), C.c_double(0)
+        st = (C.c_int64 * (12 + 2 * NKSTAT))()
+        a = TreeArgs(n, etype, byte_scale, CCG_TREE_DNJ, flags, int(exact), int(profile), int(max_joins))
+        rc = self.lib.ccg_tree_dev_state(self.h, C.byref(a), C.c_void_p(dptr), C.byref(sin) if sin else None,
+                                         C.byref(sout) if sout else None, joins.ctypes.data, C.byref(nj),
+                                         C.byref(fn), C.byref(fd), st)
+        self._check(rc, "ccg_tree_dev_state")
+        if out is not None:
+            m = sout.n
+            out = {k: v[:m] for k, v in out.items()}
+            out["n"], out["cand"] = m, sout.cand
+        return joins[:nj.value], fn.value, fd.value, list(st), out
 
     def _tree(self, fn_, dptr, n, etype, byte_scale, method, flags, exact, profile, max_joins=0):
         joins = np.zeros(max(n, 1), dtype=JOIN_DTYPE)

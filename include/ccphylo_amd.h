@@ -207,6 +207,26 @@ int ccg_tree(ccg_ctx *ctx, const ccg_tree_args *a, const void *D,
 int ccg_tree_dev(ccg_ctx *ctx, const ccg_tree_args *a, void *D_dev,
                  ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
 
+/* A DNJ loop state between two joins (dnj.c:985-1052): what the next
+ * minQpair (dnj.c:43) reads.  Host arrays of at least n entries. */
+typedef struct {
+	int n;                 /* matrix size (D holds its n(n-1)/2 cells) */
+	int cand;              /* minQpair's candidate row (minPos, dnj.c:1026-1032) */
+	double *sD, *Q;        /* row sums (initSummaD / updateD) and stale row minima */
+	int32_t *N, *P;        /* taxa counts and the rows' partners */
+} ccg_dnj_state;
+
+/* ccg_tree_dev with CCG_TREE_DNJ, checkpointed: `in` (may be NULL) starts the
+ * loop from that state instead of initSummaD / initHNJ (D_dev holds its LT,
+ * a->n == in->n); `out` (may be NULL) receives the state at exit, after
+ * a->max_joins joins, D_dev then holding its LT.  A run from `in` makes the
+ * joins the uninterrupted run makes after the same state (bit-identical; the
+ * reference has no checkpoint, so this is its loop split in two).  The single
+ * GPU engine only (no sharding); out->n = 0 if the loop stopped (pos == 0). */
+int ccg_tree_dev_state(ccg_ctx *ctx, const ccg_tree_args *a, void *D_dev, const ccg_dnj_state *in,
+                       ccg_dnj_state *out, ccg_join *joins, int *njoins, int *final_n, double *final_d,
+                       int64_t *stats);
+
 /* ------------------------------------------------------------------ */
 /* sharded tree: one LT matrix split over `world` ranks  */
 /* ------------------------------------------------------------------ */

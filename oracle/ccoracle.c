@@ -272,93 +272,149 @@ static void st_raw(int et, double bs, void *M, int64_t f, double v_scaled_plus_r
 /* fsacmpthrd.c:108-259 cmpFsaThrd and :261-480 cmpairFsaThrd, for the MSA
  * driver (cdist.c:196) where every loaded taxon is included, so LT cell
  * (pi, pj) holds pair (pi, pj). */
+typedef struct {
+	int n, len, pair, etype;
+	const uint64_t *seqs;
+	const uint32_t *incs;
+	unsigned norm, minLength, proxi;
+	double nFactor, byteScale;
+	void *D, *N;
+	int64_t W;
+	int r0, stride;   /* rows r0, r0 + stride, ... (threads) */
+	const uint64_t *spread;   /* non-pair: spread32 of each mask word, computed once */
+} SnpArg;
+
+/* orc_fsacmp with the mask words already spread (the same sum) */
+static inline uint32_t fsacmp_spread(const uint64_t *a, const uint64_t *b, const uint64_t *sp, int W32) {
+	uint32_t d = 0;
+	for(int w = 0; w < W32; ++w) {
+		uint64_t x = a[w] ^ b[w];
+		d += __builtin_popcountll((x | (x >> 1)) & 0x5555555555555555ull & sp[w]);
+	}
+	return d;
+}
+
+/* one LT row i: cells (i, 0..i-1) */
+static void snp_row(const SnpArg *a, int64_t i, uint32_t *pm) {
+	const int64_t W = a->W;
+	const uint64_t *seqs = a->seqs;
+	const uint32_t *incs = a->incs;
+	const int etype = a->etype;
+	const double byteScale = a->byteScale;
+	void *D = a->D, *N = a->N;
+	for(int64_t j = 0; j < i; ++j) {
+		const int64_t f = tri(i) + j;
+		if(!a->pair) {
+			uint64_t dist = fsacmp_spread(seqs + i * W, seqs + j * W, a->spread, (a->len + 31) / 32);
+			double v = a->nFactor * dist;
+			if(etype == 8) {
+				((double *) D)[f] = v;
+			} else if(etype == 4) {
+				((float *) D)[f] = v;
+			} else {
+				st_raw(etype, byteScale, D, f, v * byteScale + 0.5);
+			}
+			continue;
+		}
+		memset(pm, 0, (W + 4 + a->proxi / 32) * sizeof(uint32_t));
+		orc_mask_proxi(pm, incs + i * W, incs + j * W, seqs + i * W, seqs + j * W, a->len, a->proxi);
+		uint64_t dn = orc_fsacmpair(seqs + i * W, seqs + j * W, pm, a->len);
+		uint32_t inc = (uint32_t) dn;
+		uint64_t dist = dn >> 32;
+		const unsigned norm = a->norm;
+		if(etype == 8) {
+			double *Dp = D;
+			if(a->minLength <= inc) {
+				if(norm) {
+					Dp[f] = (double) (dist * norm);
+					Dp[f] /= inc;
+				} else {
+					Dp[f] = (double) dist;
+				}
+			} else {
+				Dp[f] = -1.0;
+			}
+			if(N) ((double *) N)[f] = inc;
+		} else if(etype == 4) {
+			float *Dp = D;
+			if(a->minLength <= inc) {
+				if(norm) {
+					Dp[f] = (float) (dist * norm);
+					Dp[f] /= (float) inc;
+				} else {
+					Dp[f] = (float) dist;
+				}
+			} else {
+				Dp[f] = -1.0f;
+			}
+			if(N) ((float *) N)[f] = (float) inc;
+		} else {
+			double v;
+			if(a->minLength <= inc) {
+				if(norm) {
+					v = ((double) (dist * norm) * byteScale + 0.5) / inc;
+				} else {
+					v = (double) dist * byteScale + 0.5;
+				}
+			} else {
+				v = -1.0 * byteScale + 0;
+			}
+			st_raw(etype, byteScale, D, f, v);
+			if(N) st_raw(etype, byteScale, N, f, inc * byteScale + 0.5);
+		}
+	}
+}
+
+static void *snp_worker(void *p) {
+	SnpArg *a = p;
+	uint32_t *pm = a->pair ? malloc((a->W + 4 + a->proxi / 32) * sizeof(uint32_t)) : NULL;
+	for(int64_t i = 1 + a->r0; i < a->n; i += a->stride) snp_row(a, i, pm);
+	free(pm);
+	return NULL;
+}
+
+int orc_snp_ltd_ex(int n, int len, const uint64_t *seqs, const uint32_t *incs, int pair,
+                   unsigned norm, unsigned minLength, double minCov, unsigned proxi,
+                   int etype, double byteScale, void *D, void *N, int threads) {
+	SnpArg a = {n, len, pair, etype, seqs, incs, norm, minLength, proxi, 1.0, byteScale, D, N,
+	            len / 32 + 1 /* stride used by the reference (cdist.c:290) */, 0, 1, NULL};
+	int inc_total = 0;
+	uint64_t *spread = NULL;
+	if(!pair) {
+		spread = malloc(((len + 31) / 32 + 1) * sizeof(uint64_t));
+		for(int w = 0; w < (len + 31) / 32; ++w) spread[w] = spread32(incs[w]);
+		a.spread = spread;
+		inc_total = orc_npos(incs, len);
+		if(norm) {
+			a.nFactor = norm;
+			a.nFactor /= inc_total;
+		}
+	} else if(minLength < minCov * len) {
+		a.minLength = minCov * len;
+	}
+	if(threads > 256) threads = 256;
+	if(threads <= 1 || n < 256) {
+		snp_worker(&a);
+		free(spread);
+		return inc_total;
+	}
+	pthread_t th[256];
+	SnpArg args[256];
+	for(int t = 0; t < threads; ++t) {
+		args[t] = a;
+		args[t].r0 = t;
+		args[t].stride = threads;
+		pthread_create(&th[t], NULL, snp_worker, &args[t]);
+	}
+	for(int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+	free(spread);
+	return inc_total;
+}
+
 int orc_snp_ltd(int n, int len, const uint64_t *seqs, const uint32_t *incs, int pair,
                 unsigned norm, unsigned minLength, double minCov, unsigned proxi,
                 int etype, double byteScale, void *D, void *N) {
-	int64_t W = len / 32 + 1;    /* stride used by the reference (cdist.c:290) */
-	int inc_total = 0;
-	if(!pair) {
-		double nFactor;
-		inc_total = orc_npos(incs, len);
-		if(norm) {
-			nFactor = norm;
-			nFactor /= inc_total;
-		} else {
-			nFactor = 1.0;
-		}
-		for(int64_t i = 1; i < n; ++i) {
-			for(int64_t j = 0; j < i; ++j) {
-				uint64_t dist = orc_fsacmp(seqs + i * W, seqs + j * W, incs, len);
-				int64_t f = tri(i) + j;
-				double v = nFactor * dist;
-				if(etype == 8) {
-					((double *) D)[f] = v;
-				} else if(etype == 4) {
-					((float *) D)[f] = v;
-				} else {
-					st_raw(etype, byteScale, D, f, v * byteScale + 0.5);
-				}
-			}
-		}
-		return inc_total;
-	}
-	/* pair mode */
-	if(minLength < minCov * len) {
-		minLength = minCov * len;
-	}
-	uint32_t *pm = malloc((W + 4 + proxi / 32) * sizeof(uint32_t));
-	for(int64_t i = 1; i < n; ++i) {
-		for(int64_t j = 0; j < i; ++j) {
-			memset(pm, 0, (W + 4 + proxi / 32) * sizeof(uint32_t));
-			orc_mask_proxi(pm, incs + i * W, incs + j * W, seqs + i * W, seqs + j * W, len, proxi);
-			uint64_t dn = orc_fsacmpair(seqs + i * W, seqs + j * W, pm, len);
-			uint32_t inc = (uint32_t) dn;
-			uint64_t dist = dn >> 32;
-			int64_t f = tri(i) + j;
-			if(etype == 8) {
-				double *Dp = D;
-				if(minLength <= inc) {
-					if(norm) {
-						Dp[f] = (double) (dist * norm);
-						Dp[f] /= inc;
-					} else {
-						Dp[f] = (double) dist;
-					}
-				} else {
-					Dp[f] = -1.0;
-				}
-				if(N) ((double *) N)[f] = inc;
-			} else if(etype == 4) {
-				float *Dp = D;
-				if(minLength <= inc) {
-					if(norm) {
-						Dp[f] = (float) (dist * norm);
-						Dp[f] /= (float) inc;
-					} else {
-						Dp[f] = (float) dist;
-					}
-				} else {
-					Dp[f] = -1.0f;
-				}
-				if(N) ((float *) N)[f] = (float) inc;
-			} else {
-				double v;
-				if(minLength <= inc) {
-					if(norm) {
-						v = ((double) (dist * norm) * byteScale + 0.5) / inc;
-					} else {
-						v = (double) dist * byteScale + 0.5;
-					}
-				} else {
-					v = -1.0 * byteScale + 0;
-				}
-				st_raw(etype, byteScale, D, f, v);
-				if(N) st_raw(etype, byteScale, N, f, inc * byteScale + 0.5);
-			}
-		}
-	}
-	free(pm);
-	return inc_total;
+	return orc_snp_ltd_ex(n, len, seqs, incs, pair, norm, minLength, minCov, proxi, etype, byteScale, D, N, 1);
 }
 
 /* ------------------------------------------------------------------ */
@@ -757,6 +813,95 @@ static uint64_t min_q_pair(const Ltd *D, int n, const double *sD, const int32_t 
 	return pos;
 }
 
+/* min_q_pair with `threads` pthreads (test infrastructure for large n, where
+ * one join rescans ~1e9 cells).  The serial loop's decisions are replayed in
+ * its own order: rows are collected in descending order while Q[r] < min (the
+ * running min only decreases, so a row with Q[r] >= min at collection time is
+ * skipped by the serial loop too), their fresh row minima are computed in
+ * parallel into scratch (row_min is a function of row r alone), then the batch
+ * is walked in order with dnj.c:78's test against the now-current min: an
+ * accepted row stores P/Q and may lower min, a rejected one keeps its stale
+ * Q/P and its fresh value is discarded.  So Q, P, the returned pos and the
+ * reference-rule counters equal min_q_pair's bit for bit (pinned by
+ * tests/test_oracle_golden.py::test_oracle_parallel_min_q_pair). */
+typedef struct {
+	const Ltd *D;
+	const double *sD;
+	const int32_t *N;
+	const int *rows;
+	double *fq;
+	int *fj;
+	int cnt;
+	int next;     /* atomic row cursor */
+} RescanArg;
+
+static void *rescan_worker(void *p) {
+	RescanArg *a = p;
+	for(;;) {
+		int k = __atomic_fetch_add(&a->next, 1, __ATOMIC_RELAXED);
+		if(k >= a->cnt) break;
+		a->fq[k] = row_min(a->D, a->rows[k], a->sD, a->N, &a->fj[k], 0);
+	}
+	return NULL;
+}
+
+#define RESCAN_BATCH_ROWS 8192
+/* below this many cells a batch is rescanned on the calling thread
+ * (ORC_PAR_CELLS overrides it: the tests force the threaded path at small n) */
+static int64_t rescan_par_cells(void) {
+	const char *e = getenv("ORC_PAR_CELLS");
+	return e ? atoll(e) : (1 << 22);
+}
+
+static uint64_t min_q_pair_par(const Ltd *D, int n, const double *sD, const int32_t *N, double *Q, int32_t *P,
+                               int cand, int64_t *stats, int threads, int *rows, double *fq, int *fj) {
+	double min = DBL_MAX;
+	uint64_t pos = 0;
+	if(cand && min != Q[cand]) {
+		min = Q[cand];
+		pos = ((uint64_t) cand << 32) | (uint32_t) P[cand];
+	}
+	int lim = 64;   /* batches grow, so an early steep drop of min wastes little */
+	const int64_t par_cells = rescan_par_cells();
+	for(int i = n - 1; i > 0;) {
+		int cnt = 0, r = i;
+		int64_t cells = 0;
+		for(; r > 0 && cnt < lim; --r) {
+			if(Q[r] < min) {
+				rows[cnt++] = r;
+				cells += r;
+			}
+		}
+		if(cells >= par_cells && threads > 1) {
+			RescanArg a = {D, sD, N, rows, fq, fj, cnt, 0};
+			pthread_t th[256];
+			int nt = threads > 256 ? 256 : threads;
+			for(int t = 0; t < nt; ++t) pthread_create(&th[t], NULL, rescan_worker, &a);
+			for(int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
+		} else {
+			for(int k = 0; k < cnt; ++k) fq[k] = row_min(D, rows[k], sD, N, &fj[k], 0);
+		}
+		for(int k = 0; k < cnt; ++k) {
+			const int row = rows[k];
+			if(Q[row] < min) {
+				if(stats) {
+					++stats[0];
+					stats[1] += row;
+				}
+				P[row] = fj[k];
+				Q[row] = fq[k];
+				if(fq[k] < min) {
+					min = fq[k];
+					pos = ((uint64_t) row << 32) | (uint32_t) fj[k];
+				}
+			}
+		}
+		i = r;
+		if(lim < RESCAN_BATCH_ROWS) lim *= 2;
+	}
+	return pos;
+}
+
 /* dnj.c:607-710 updateDNJ (after updateD): returns p */
 static int update_dnj_q(const Ltd *D, int n, const double *sD, const int32_t *N, double *Q, int32_t *P,
                         int i, int j) {
@@ -922,6 +1067,48 @@ static void hnj_pop_arrange(Ltd *D, int *n, double *sD, int32_t *N, double *Q, i
 	}
 }
 
+/* dnj.c:1020-1052, the DNJ loop from candidate row j: minQpair, limbLength,
+ * updateD, updateDNJ, DNJ_popArrange, minPos.  *np is the matrix size (updated);
+ * returns the joins made.  next_cand (may be NULL) receives the candidate the
+ * loop would start its next minQpair from (the state a resume continues). */
+static int dnj_loop(Ltd *D, int *np, double *sD, int32_t *N, double *Q, int32_t *P, int j, int neg,
+                    orc_join *joins, int lim, int64_t *stats, int threads, int *next_cand) {
+	int n = *np, nj = 0;
+	int *rows = NULL, *fj = NULL;
+	double *fq = NULL;
+	if(threads > 1) {
+		rows = malloc(RESCAN_BATCH_ROWS * sizeof(int));
+		fj = malloc(RESCAN_BATCH_ROWS * sizeof(int));
+		fq = malloc(RESCAN_BATCH_ROWS * sizeof(double));
+	}
+	uint64_t pos;
+	while(n != 2 && nj < lim &&
+	      (pos = threads > 1 ? min_q_pair_par(D, n, sD, N, Q, P, j, stats, threads, rows, fq, fj)
+	                         : min_q_pair(D, n, sD, N, Q, P, j, stats))) {
+		j = (int) (pos & 0xFFFFFFFFu);
+		int i = (int) (pos >> 32);
+		double Li, Lj;
+		limb_length(&Li, &Lj, i, j, sD, N, ld(D, tri(i) + j), neg);
+		joins[nj].i = i; joins[nj].j = j; joins[nj].Li = Li; joins[nj].Lj = Lj; ++nj;
+		update_d(D, n, sD, N, i, j, Li, Lj);
+		int mi = update_dnj_q(D, n, sD, N, Q, P, i, j);
+		int mj = dnj_pop_arrange(D, &n, sD, N, Q, P, i);
+		if(mj == n) {
+			j = mi;
+		} else if(mi == n) {
+			j = mj;
+		} else {
+			j = min_pos(Q, mi, mj);
+		}
+	}
+	free(rows);
+	free(fj);
+	free(fq);
+	*np = n;
+	if(next_cand) *next_cand = j;
+	return nj;
+}
+
 int orc_tree(int n, int etype, double byteScale, void *Dbase, int method, int flags,
              orc_join *joins, int *final_n, double *final_d, int64_t *stats) {
 	return orc_tree_ex(n, etype, byteScale, Dbase, method, flags, joins, final_n, final_d, stats, 0, 1);
@@ -975,25 +1162,7 @@ int orc_tree_ex(int n, int etype, double byteScale, void *Dbase, int method, int
 	} else {
 		/* dnj.c:985-1052 */
 		init_hnj_par(&D, n, sD, N, Q, P, threads);
-		int j = min_q_row(Q, n);
-		uint64_t pos;
-		while(n != 2 && nj < lim && (pos = min_q_pair(&D, n, sD, N, Q, P, j, stats))) {
-			j = (int) (pos & 0xFFFFFFFFu);
-			int i = (int) (pos >> 32);
-			double Li, Lj;
-			limb_length(&Li, &Lj, i, j, sD, N, ld(&D, tri(i) + j), neg);
-			joins[nj].i = i; joins[nj].j = j; joins[nj].Li = Li; joins[nj].Lj = Lj; ++nj;
-			update_d(&D, n, sD, N, i, j, Li, Lj);
-			int mi = update_dnj_q(&D, n, sD, N, Q, P, i, j);
-			int mj = dnj_pop_arrange(&D, &n, sD, N, Q, P, i);
-			if(mj == n) {
-				j = mi;
-			} else if(mi == n) {
-				j = mj;
-			} else {
-				j = min_pos(Q, mi, mj);
-			}
-		}
+		nj = dnj_loop(&D, &n, sD, N, Q, P, min_q_row(Q, n), neg, joins, lim, stats, threads, NULL);
 	}
 	*final_n = n;
 	*final_d = n == 2 ? ld(&D, 0) : -1.0;
@@ -1001,5 +1170,27 @@ int orc_tree_ex(int n, int etype, double byteScale, void *Dbase, int method, int
 	free(Q);
 	free(N);
 	free(P);
+	return nj;
+}
+
+int orc_dnj_init(int n, int etype, double byteScale, const void *Dbase, double *sD, double *Q, int32_t *N, int32_t *P,
+                 int threads) {
+	Ltd D = {etype, byteScale, (void *) Dbase};
+	init_sums_par(&D, n, sD, N, threads);
+	init_hnj_par(&D, n, sD, N, Q, P, threads);
+	return min_q_row(Q, n);
+}
+
+int orc_dnj_resume(int n, int etype, double byteScale, void *Dbase, double *sD, double *Q, int32_t *N, int32_t *P,
+                   int cand, int flags, orc_join *joins, int *final_n, double *final_d, int64_t *stats,
+                   int max_joins, int threads, int *next_cand) {
+	Ltd D = {etype, byteScale, Dbase};
+	if(stats) {
+		stats[0] = stats[1] = 0;
+	}
+	int nj = dnj_loop(&D, &n, sD, N, Q, P, cand, (flags & 2) != 0, joins, max_joins > 0 ? max_joins : INT_MAX, stats,
+	                  threads, next_cand);
+	*final_n = n;
+	*final_d = n == 2 ? ld(&D, 0) : -1.0;
 	return nj;
 }

@@ -58,9 +58,31 @@ int orc_tree(int n, int etype, double byteScale, void *D, int method, int flags,
 
 /* orc_tree with a join limit (max_joins > 0: the first max_joins joins of the
  * same run) and `threads` pthreads for the O(n^2) initSummaD / initHNJ passes
- * (same per-row operation order, so bit-identical to threads = 1). */
+ * (same per-row operation order) and DNJ's minQpair rescans (same decisions,
+ * see min_q_pair_par), so bit-identical to threads = 1. */
 int orc_tree_ex(int n, int etype, double byteScale, void *D, int method, int flags,
                 orc_join *joins, int *final_n, double *final_d, int64_t *stats, int max_joins, int threads);
+
+/* Resume the DNJ loop (dnj.c:1020-1052) from a saved state: D holds the LT of
+ * the current n rows, sD/Q/N/P the per-row vectors after the last join (as
+ * the next minQpair reads them) and cand the candidate row minPos chose
+ * (dnj.c:1026-1032).  The arrays are updated in place; *next_cand (may be
+ * NULL) receives the candidate for a further resume.  threads > 1 rescans
+ * minQpair's rows with pthreads (same decisions, see min_q_pair_par). */
+int orc_dnj_resume(int n, int etype, double byteScale, void *D, double *sD, double *Q, int32_t *N, int32_t *P,
+                   int cand, int flags, orc_join *joins, int *final_n, double *final_d, int64_t *stats,
+                   int max_joins, int threads, int *next_cand);
+
+/* The state orc_dnj_resume starts a whole DNJ run from: initSummaD
+ * (nj.c:111), initHNJ (hclust.c:56) and the first candidate (minQ,
+ * hclust.c:353, as dnj.c:1015).  Returns the candidate row. */
+int orc_dnj_init(int n, int etype, double byteScale, const void *D, double *sD, double *Q, int32_t *N, int32_t *P,
+                 int threads);
+
+/* orc_snp_ltd with `threads` pthreads over the LT rows (same cells). */
+int orc_snp_ltd_ex(int n, int len, const uint64_t *seqs, const uint32_t *incs, int pair,
+                   unsigned norm, unsigned minLength, double minCov, unsigned proxi,
+                   int etype, double byteScale, void *D, void *N, int threads);
 
 /* B1/B2: distances between KMA count matrices (*.mat[.gz]) of template
  * `tmpl` (ltdmatrixthrd.c:376 ltdMatrixThrd, matcmp.c:448 cmpMats, metrics

@@ -36,6 +36,12 @@ def lib():
                                   C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_void_p, C.c_int, C.c_int]
         L.orc_snp_ltd.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_uint, C.c_double,
                                   C.c_uint, C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+        L.orc_snp_ltd_ex.argtypes = L.orc_snp_ltd.argtypes + [C.c_int]
+        L.orc_dnj_init.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_int]
+        L.orc_dnj_resume.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int),
+                                     C.POINTER(C.c_double), C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int)]
         L.orc_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.orc_init_inc.argtypes = [C.c_void_p, C.c_int]
         L.orc_inc_update.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint, C.c_int]
@@ -56,8 +62,8 @@ def lib():
 def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False, max_joins=0, threads=1, copy=True):
     """Serial NJ (method 0) / DNJ (method 1) / HNJ (method 2) exactly as the reference.
     max_joins > 0 stops after that many joins (a prefix of the same run);
-    threads > 1 runs the O(n^2) initSummaD / initHNJ passes on pthreads (same
-    per-row order, bit-identical).  copy=False destroys D in place (it must
+    threads > 1 runs the O(n^2) initSummaD / initHNJ passes and DNJ's
+    minQpair rescans on pthreads (same order / decisions, bit-identical).  copy=False destroys D in place (it must
     then be a writable contiguous array of the element type: large n).
     Returns (joins, final_n, final_d[, stats])."""
     if copy:
@@ -75,8 +81,48 @@ def tree(D, n, etype=8, byte_scale=1.0, method=1, flags=0, stats=False, max_join
     return res + (st,) if stats else res
 
 
+class DnjState:
+    """A DNJ loop state (dnj.c:985-1052 between two joins): the LT of the
+    current n rows, the per-row vectors minQpair reads and its candidate row."""
+
+    def __init__(self, D, n, sD, Q, N, P, cand, etype=8, byte_scale=1.0):
+        self.D, self.n, self.sD, self.Q, self.N, self.P = D, int(n), sD, Q, N, P
+        self.cand, self.etype, self.byte_scale = int(cand), etype, byte_scale
+
+
+def dnj_init(D, n, etype=8, byte_scale=1.0, threads=1):
+    """initSummaD + initHNJ + the first candidate: the state a whole DNJ run
+    starts from.  D is taken over (the state's matrix is D itself)."""
+    D = np.ascontiguousarray(D, dtype=ETYPES[etype])
+    sD, Q = np.zeros(n), np.zeros(n)
+    N, P = np.zeros(n, dtype=np.int32), np.zeros(n, dtype=np.int32)
+    cand = lib().orc_dnj_init(n, etype, byte_scale, D.ctypes.data, sD.ctypes.data, Q.ctypes.data, N.ctypes.data,
+                              P.ctypes.data, threads)
+    return DnjState(D, n, sD, Q, N, P, cand, etype, byte_scale)
+
+
+def dnj_resume(state, max_joins=0, flags=0, threads=1, stats=False):
+    """Continues the DNJ loop from `state` (updated in place) for max_joins
+    joins (0: to the end).  Returns (joins, final_n, final_d[, stats])."""
+    s = state
+    for a, dt in ((s.sD, np.float64), (s.Q, np.float64), (s.N, np.int32), (s.P, np.int32)):
+        assert a.dtype == dt and a.flags.c_contiguous and a.flags.writeable and len(a) >= s.n
+    assert s.D.dtype == ETYPES[s.etype] and s.D.flags.c_contiguous and s.D.flags.writeable
+    assert s.D.size >= s.n * (s.n - 1) // 2
+    cap = min(s.n, max_joins) if max_joins > 0 else s.n
+    joins = np.zeros(max(cap, 1), dtype=JOIN_DTYPE)
+    fn, fd, nc = C.c_int(0), C.c_double(0), C.c_int(0)
+    st = np.zeros(2, dtype=np.int64)
+    nj = lib().orc_dnj_resume(s.n, s.etype, s.byte_scale, s.D.ctypes.data, s.sD.ctypes.data, s.Q.ctypes.data,
+                              s.N.ctypes.data, s.P.ctypes.data, s.cand, flags, joins.ctypes.data, C.byref(fn),
+                              C.byref(fd), st.ctypes.data, max_joins, threads, C.byref(nc))
+    s.n, s.cand = fn.value, nc.value
+    res = (joins[:nj], fn.value, fd.value)
+    return res + (st,) if stats else res
+
+
 def snp_ltd(seqs, incs, n, length, pair=False, norm=0, min_length=1, min_cov=0.0, proxi=0, etype=8,
-            byte_scale=1.0, want_n=False):
+            byte_scale=1.0, want_n=False, threads=1):
     seqs = np.ascontiguousarray(seqs, dtype=np.uint64)
     incs = np.ascontiguousarray(incs, dtype=np.uint32)
     W = length // 32 + 1
@@ -84,8 +130,9 @@ def snp_ltd(seqs, incs, n, length, pair=False, norm=0, min_length=1, min_cov=0.0
     m = n * (n - 1) // 2
     D = np.zeros(max(m, 1), dtype=ETYPES[etype])
     N = np.zeros(max(m, 1), dtype=ETYPES[etype]) if want_n else None
-    inc = lib().orc_snp_ltd(n, length, seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length, min_cov,
-                            proxi, etype, byte_scale, D.ctypes.data, N.ctypes.data if N is not None else None)
+    inc = lib().orc_snp_ltd_ex(n, length, seqs.ctypes.data, incs.ctypes.data, int(pair), norm, min_length, min_cov,
+                               proxi, etype, byte_scale, D.ctypes.data, N.ctypes.data if N is not None else None,
+                               threads)
     return D[:m], (N[:m] if N is not None else None), inc
 
 

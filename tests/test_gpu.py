@@ -525,19 +525,91 @@ def test_dnj_missing_large_n_join(dev, monkeypatch, n, jpf):
 
 
 @pytest.mark.parametrize("mode", ["20", "21"])
-@pytest.mark.parametrize("kind,n,et", [("euc", 2500, 8), ("clade", 3000, 8), ("euc", 2000, 4)])
+@pytest.mark.parametrize("kind,n,et", [("euc", 2500, 8), ("clade", 3000, 8), ("euc", 2000, 4), ("clade", 2500, 2),
+                                       ("clade", 2000, 1)])
 def test_dnj_scan_row_groups(dev, monkeypatch, mode, kind, n, et):
     """The row-group rescan (k_dnj_scan_g: G rows per wave sharing the sD
-    loads of a column range) at small n with the large-n fold and join:
-    joins bit-identical to the serial reference."""
+    loads of a column range; the default past 16384 taxa for float, u16 and
+    u8 rows) at small n with the large-n fold and join: joins bit-identical
+    to the serial reference."""
     from oracle import pyoracle
     monkeypatch.setenv("CCG_SCAN_WAVE", mode)
     monkeypatch.setenv("CCG_PREFOLD_N", "0")
     monkeypatch.setenv("CCG_SEG_MUL", "1")
     D = _euclid(n, n) if kind == "euc" else _clade_ltd(n, n)
+    bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 0.1}[et]
     if et == 4:
         D = D.astype(np.float32)
-    got, fn, fd, _ = dev.tree(D, n, etype=et, method=1, exact=True)
-    ref, rfn, rfd = pyoracle.tree(D, n, etype=et, method=1)
+    elif et in (2, 1):   # dtouc(d, 0.5) stores (bytescale.c)
+        D = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
+    got, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True)
+    ref, rfn, rfd = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1)
     assert (fn, fd) == (rfn, rfd)
     assert len(got) == len(ref) and (got == ref).all()
+
+
+def _state_equal(g, r, n):
+    """An engine checkpoint (ccg_dnj_state + its device LT) against the
+    oracle's DnjState after the same joins: every vector bit for bit."""
+    assert g["n"] == r.n == n
+    assert g["cand"] == r.cand
+    assert (g["sD"] == r.sD[:n]).all() and (g["Q"] == r.Q[:n]).all()
+    assert (g["N"] == r.N[:n]).all() and (g["P"] == r.P[:n]).all()
+
+
+@pytest.mark.parametrize("kind,n,et,cuts", [("clade", 2500, 8, (300, 1100)), ("euc", 2000, 4, (1, 700)),
+                                            ("miss", 1500, 8, (200, 900)), ("snp", 1800, 8, (1, 1000))])
+def test_dnj_checkpoint_vs_oracle(dev, kind, n, et, cuts):
+    """ccg_tree_dev_state: the engine's DNJ loop state after k joins (D, sD, Q,
+    N, P and minPos's candidate, dnj.c:985-1052) equals the oracle's after the
+    same k joins bit for bit; the run resumed from it (and the oracle resumed
+    from the engine's state) continue with the uninterrupted run's joins."""
+    import torch
+    from oracle import pyoracle
+    D = {"euc": lambda: _euclid(n, n), "snp": lambda: _snp(n, n), "clade": lambda: _clade_ltd(n, n),
+         "miss": lambda: _missing_ltd(n, n)}[kind]()
+    D = D.astype(np.float32) if et == 4 else D
+    whole, wfn, wfd = pyoracle.tree(D, n, etype=et, method=1)
+    ost = pyoracle.dnj_init(D.copy(), n, etype=et)
+    Dd = torch.from_numpy(np.ascontiguousarray(D)).cuda()
+    torch.cuda.synchronize()
+    state, done, m = None, [], n
+    for k in list(cuts) + [0]:
+        got, fn, fd, _, st = dev.tree_dev_state(Dd.data_ptr(), m, etype=et, max_joins=k, state=state)
+        ref, rfn, rfd = pyoracle.dnj_resume(ost, max_joins=k)
+        assert len(got) == len(ref) and (got == ref).all(), (kind, k)
+        done.append(got)
+        if k:
+            _state_equal(st, ost, m - k)
+            mm = m - k
+            cells = Dd[:mm * (mm - 1) // 2].cpu().numpy()
+            assert (cells == ost.D[:mm * (mm - 1) // 2]).all()
+            # the oracle continues 150 joins from the ENGINE's state
+            gst = pyoracle.DnjState(cells.copy(), mm, st["sD"].copy(), st["Q"].copy(), st["N"].copy(),
+                                    st["P"].copy(), st["cand"], etype=et)
+            ref2 = pyoracle.dnj_resume(gst, max_joins=150)[0]
+            assert (ref2 == whole[sum(len(x) for x in done):][:150]).all()
+            m, state = mm, st
+        else:
+            assert (fn, fd) == (wfn, wfd) and (rfn, rfd) == (wfn, wfd)
+    assert (np.concatenate(done) == whole).all()
+
+
+def test_dnj_checkpoint_large_n(dev):
+    """The checkpoint at n > 16384 (band rows of S, k_dnj_fold, k_dnj_join_pf):
+    20k Euclidean doubles, state after 400 joins against the oracle's, then
+    400 more joins from it on both sides."""
+    import torch
+    from oracle import pyoracle
+    n, k = 20_000, 400
+    D = _euclid(n, 3)
+    Dd = torch.from_numpy(D).cuda()
+    torch.cuda.synchronize()
+    got, _, _, _, st = dev.tree_dev_state(Dd.data_ptr(), n, max_joins=k)
+    ost = pyoracle.dnj_init(D, n, threads=8)
+    ref = pyoracle.dnj_resume(ost, max_joins=k, threads=8)[0]
+    assert (got == ref).all()
+    _state_equal(st, ost, n - k)
+    got2 = dev.tree_dev_state(Dd.data_ptr(), n - k, max_joins=k, state=st, want_state=False)[0]
+    ref2 = pyoracle.dnj_resume(ost, max_joins=k, threads=8)[0]
+    assert (got2 == ref2).all()

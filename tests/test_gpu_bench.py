@@ -1,0 +1,43 @@
+"""bench.py's multi-GPU launch: `python bench.py --gpus N`
+without a launcher starts N rank processes itself, before any GPU call, and
+the sharded headline gives the one-GPU joins.  On a one-GPU box the ranks
+share the device over the host-staged gloo transport (a rehearsal of the
+8-GPU run, not a timing)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--n", "3000", "--L", "20000", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-extras"]
+
+
+def _bench(args, env=None, timeout=300):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def test_bench_world_mismatch_refused():
+    """--gpus N under a launcher whose WORLD_SIZE differs: exit non-zero
+    before any GPU work (no GPU needed)."""
+    p = _bench(["--gpus", "2"] + SMALL, env={"WORLD_SIZE": "3", "RANK": "0"}, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=3" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_spawned_same_joins():
+    one = _bench(["--gpus", "1"] + SMALL)
+    assert one.returncode == 0, one.stderr[-3000:]
+    two = _bench(["--gpus", "2", "--shard-transport", "gloo"] + SMALL)
+    assert two.returncode == 0, two.stderr[-3000:]
+    l1 = json.loads(one.stdout.strip().splitlines()[-1])
+    l2 = json.loads(two.stdout.strip().splitlines()[-1])
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    assert l2["split"]["joins_sha256"] == l1["split"]["joins_sha256"]
+    assert l2["split"]["joins"] == l1["split"]["joins"] == 2998

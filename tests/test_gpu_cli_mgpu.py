@@ -168,13 +168,15 @@ def test_round_decimal_dev():
     import ccphylo_amd as cg
     rng = np.random.default_rng(5)
     x = np.concatenate([rng.random(20000) * 10.0 ** rng.integers(-6, 6, 20000), np.arange(50.0),
-                        np.array([0.5e-9, 1.5e-9, 2.5e-9, 0.1, 0.7, 123456.7890123455, 1e-12, 4.4e5])])
+                        np.array([0.5e-9, 1.5e-9, 2.5e-9, 0.1, 0.7, 123456.7890123455, 1e-12, 4.4e5]),
+                        # |x 10^p| in [2^52, 2^53) at p = 9: the integral-hi branch
+                        4.6e6 + rng.random(4000) * 4.3e6, -(4.6e6 + rng.random(500) * 4.3e6)])
     dev = cg.Device(0)
     try:
         for p in (9, 4, 0, 12):
             for dt, et in ((np.float64, 8), (np.float32, 4)):
                 h = x.astype(dt)
-                h = h[(h == np.trunc(h)) | (np.abs(h.astype(np.float64)) * 10.0 ** p < 2.0 ** 51)]
+                h = h[(h == np.trunc(h)) | (np.abs(h.astype(np.float64)) * 10.0 ** p < 2.0 ** 53 * 0.999)]
                 t = torch.from_numpy(h.copy()).cuda()
                 rc = dev.lib.ccg_round_decimal_dev(dev.h, C_void(t.data_ptr()), C_i64(len(h)), et, p)
                 assert rc == 0, (p, et)

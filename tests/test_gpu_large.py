@@ -162,24 +162,31 @@ def test_config2_dist_and_dnj_prefix(dev):
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "dnj configs[2] exact prefix")
 
 
-def test_config3_sharded_dnj_prefix(dev, monkeypatch):
-    """configs[3]: N = 200k Euclidean (seed 4), float (`-p`, 80 GB), through
-    the row-sharded kernels at world 1 (band layout = the packed LT), exact
-    DNJ, the first 500 joins against the oracle's prefix."""
-    monkeypatch.setenv("CCG_SHARD_FORCE", "1")
+def test_config3_dnj_prefix(dev, monkeypatch):
+    """configs[3]: N = 200k Euclidean (seed 4), float (`-p`, 80 GB), exact DNJ
+    against the oracle's serial minQpair (threaded rescans, same decisions):
+    the single engine's default float path (row-group rescans k_dnj_scan_g,
+    k_dnj_fold, k_dnj_join_pf) over the first 2000 joins, and the row-sharded
+    kernels at world 1 (band layout = the packed LT) over the first 500."""
     import torch
     import ccphylo_amd as cg
     from oracle import pyoracle
     from tools.synth import euclid_shard_dev
-    n, k = 200_000, 500
-    loc = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)
-    host = loc.cpu().numpy()
-    got = dev.tree_shard_dev(loc.data_ptr(), n, None, etype=4, method=cg.CCG_TREE_DNJ, exact=True, max_joins=k)
-    del loc
-    torch.cuda.empty_cache()
+    n, k, ks = 200_000, 2000, 500
+    got = {}
+    for force, kk in (("0", k), ("1", ks)):
+        monkeypatch.setenv("CCG_SHARD_FORCE", force)
+        loc = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)
+        if force == "0":
+            host = loc.cpu().numpy()
+        got[force] = dev.tree_shard_dev(loc.data_ptr(), n, None, etype=4, method=cg.CCG_TREE_DNJ, exact=True,
+                                        max_joins=kk)
+        del loc
+        torch.cuda.empty_cache()
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
-    _same_joins((got[0], 0, 0), (ref[0], 0, 0), "sharded dnj 200k float exact prefix")
+    _same_joins((got["0"][0], 0, 0), (ref[0], 0, 0), "single engine dnj 200k float exact prefix")
+    _same_joins((got["1"][0], 0, 0), (ref[0][:ks], 0, 0), "sharded dnj 200k float exact prefix")
 
 
 def test_config3_single_vs_sharded_prefix(dev, monkeypatch):

@@ -348,3 +348,55 @@ def test_dist_shard_layout_pair(dev, monkeypatch, n, L, et, proxi, world, mfma):
     finally:
         dev.free(ps)
         dev.free(pi)
+
+
+class _DeviceSelfColl:
+    """A world-1 ccg_coll with host_staged = 0 whose callbacks move DEVICE
+    buffers with hipMemcpyAsync on the engine's stream, as RCCL's enqueue
+    does: the non-staged CollRun paths (the allgather or its allreduce
+    emulation, the broadcast of row n-1) without RCCL."""
+
+    def __init__(self, native_allgather=True):
+        import ctypes as C
+        import importlib.util
+        from ccphylo_amd import native
+        spec = importlib.util.find_spec("torch")
+        hip = C.CDLL(os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so"))
+        hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        self.calls = {"allreduce": 0, "broadcast": 0, "allgather": 0}
+
+        def copy(dst, src, nbytes, stream):
+            if nbytes and dst != src:
+                return int(hip.hipMemcpyAsync(dst, src, nbytes, 3, stream) != 0)   # device to device
+            return 0
+
+        def allreduce(user, buf, nbytes, stream):   # one rank: the sum is the buffer
+            self.calls["allreduce"] += 1
+            return 0
+
+        def broadcast(user, send, recv, nbytes, root, stream):
+            self.calls["broadcast"] += 1
+            return copy(recv, send, nbytes, stream) if send else 0
+
+        def allgather(user, send, recv, nbytes, stream):
+            self.calls["allgather"] += 1
+            return copy(recv, send, nbytes, stream)
+
+        self._fns = (native.ALLREDUCE_FN(allreduce), native.BROADCAST_FN(broadcast),
+                     native.ALLGATHER_FN(allgather) if native_allgather else native.ALLGATHER_FN())
+        self.c = native.Coll(None, 0, 1, 0, *self._fns)
+
+
+@pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
+@pytest.mark.parametrize("native_allgather", [True, False])
+def test_shard_device_transport_world1(dev, method, native_allgather):
+    """The sharded kernels over a device-side transport (host_staged = 0) give
+    the single engine's joins (exact row sums)."""
+    n = 1500
+    D = _snp(n, 41) if method else _euclid(n, 41)
+    want = dev.tree(D, n, method=method, exact=True)[:3]
+    coll = _DeviceSelfColl(native_allgather)
+    got = dev.tree_shard(D, n, coll, method=method, exact=True)[:3]
+    assert (got[1], got[2]) == (want[1], want[2])
+    assert len(got[0]) == len(want[0]) and (got[0] == want[0]).all()
+    assert coll.calls["allgather" if native_allgather else "allreduce"] > 0

@@ -80,3 +80,71 @@ def test_oracle_threaded_init_and_prefix(method, et):
     pre = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=method, threads=3, max_joins=40)
     assert (full[0] == par[0]).all() and full[1:] == par[1:]
     assert len(pre[0]) == 40 and (pre[0] == full[0][:40]).all()
+
+
+def _snp_clade_ltd(n, L, clades, seed=5):
+    """An integer SNP-count LT with many exact ties (clade-structured random
+    packed alignment through the oracle's fsacmp)."""
+    import numpy as np
+    from oracle import pyoracle
+    from tools.synth import clade_packed
+    seqs, incs = clade_packed(n, L, clades, seed)
+    D, _, _ = pyoracle.snp_ltd(seqs, incs, n, L)
+    return D
+
+
+@pytest.mark.parametrize("kind", ["euc", "snp"])
+def test_oracle_parallel_min_q_pair(monkeypatch, kind):
+    """min_q_pair_par (threaded speculative rescans + the serial loop's own
+    accept order, the large-n checker) equals min_q_pair (dnj.c:43-128) bit
+    for bit: joins, lengths, final pair and the reference-rule counters."""
+    import numpy as np
+    from oracle import pyoracle
+    from tools.synth import euclid
+    monkeypatch.setenv("ORC_PAR_CELLS", "0")   # every batch through the threads
+    n = 1200
+    D = euclid(n, 7) if kind == "euc" else _snp_clade_ltd(n, 600, 24)
+    ser = pyoracle.tree(D, n, method=1, stats=True)
+    par = pyoracle.tree(D, n, method=1, stats=True, threads=4)
+    assert (ser[0] == par[0]).all() and ser[1:3] == par[1:3]
+    assert (ser[3] == par[3]).all()
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_oracle_dnj_resume_chain(monkeypatch, threads):
+    """orc_dnj_init + orc_dnj_resume in three legs (state carried between
+    them: D, sD, Q, N, P and minPos's candidate) give the one-run tree."""
+    import numpy as np
+    from oracle import pyoracle
+    monkeypatch.setenv("ORC_PAR_CELLS", "0")
+    n = 900
+    D = _snp_clade_ltd(n, 800, 16, seed=8)
+    whole = pyoracle.tree(D, n, method=1, stats=True)
+    st = pyoracle.dnj_init(D.copy(), n, threads=threads)
+    parts, cells = [], np.zeros(2, dtype=np.int64)
+    for k in (150, 400, 0):
+        j, fn, fd, s = pyoracle.dnj_resume(st, max_joins=k, threads=threads, stats=True)
+        parts.append(j)
+        cells += s
+    got = np.concatenate(parts)
+    assert (got == whole[0]).all() and (fn, fd) == whole[1:3]
+    assert (cells == whole[3]).all()
+
+
+def test_oracle_threaded_snp_ltd():
+    """orc_snp_ltd_ex over row-interleaved pthreads = the serial fill, both
+    modes (pair mode with -P)."""
+    import numpy as np
+    from oracle import pyoracle
+    from tools.synth import clade_packed
+    n, L = 300, 700
+    seqs, incs = clade_packed(n, L, 8, 3)
+    a = pyoracle.snp_ltd(seqs, incs, n, L)[0]
+    b = pyoracle.snp_ltd(seqs, incs, n, L, threads=4)[0]
+    assert (a == b).all()
+    W = L // 32 + 1
+    pinc = np.tile(incs, (n, 1))
+    pinc[::7, 3] = 0
+    a = pyoracle.snp_ltd(seqs, pinc, n, L, pair=True, proxi=5, want_n=True)
+    b = pyoracle.snp_ltd(seqs, pinc, n, L, pair=True, proxi=5, want_n=True, threads=3)
+    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()

@@ -41,3 +41,36 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
         pos += vals.numel()
     assert pos == sum(sizes)
     return out
+
+
+def clade_packed(n, L, clades, seed=3, every=10, flips=8):
+    """A clade-structured packed alignment in the reference's layout, numpy
+    only (the same bytes on the GPU box and in the build container): `clades`
+    random root sequences, taxon t = root t % clades with each bit set to 1
+    with p = 2^-flips xor-ed in (~0.8% of the 2-bit codes flipped at 8), as
+    tools/config3.make_packed.  Returns (seqs n x W u64, W = L // 32 + 1
+    words per taxon as cdist.c:290 allocates, positions past L zero;
+    incs W u32: every `every`-th word excluded (the "N columns"), the tail
+    past L cleared as initIncPos does, fsacmp.c:164)."""
+    W = L // 32 + 1
+    rng = np.random.default_rng(seed)
+    roots = rng.integers(0, 2 ** 64, (clades, W), dtype=np.uint64, endpoint=False)
+    seqs = np.empty((n, W), dtype=np.uint64)
+    step = 4096
+    for t0 in range(0, n, step):
+        t1 = min(n, t0 + step)
+        m = rng.integers(0, 2 ** 64, (t1 - t0, W), dtype=np.uint64, endpoint=False)
+        for _ in range(flips - 1):
+            m &= rng.integers(0, 2 ** 64, (t1 - t0, W), dtype=np.uint64, endpoint=False)
+        seqs[t0:t1] = roots[np.arange(t0, t1) % clades] ^ m
+    W32 = (L + 31) // 32
+    seqs[:, W32:] = 0
+    if L % 32:
+        seqs[:, W32 - 1] &= np.uint64(((1 << (2 * (L % 32))) - 1) << (64 - 2 * (L % 32)))
+    incs = np.full(W, 0xFFFFFFFF, dtype=np.uint32)
+    if every:
+        incs[::every] = 0
+    incs[W32:] = 0
+    if L % 32:
+        incs[W32 - 1] &= np.uint32((0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF)
+    return seqs, incs
