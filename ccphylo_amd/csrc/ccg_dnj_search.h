@@ -37,8 +37,10 @@ struct DnjGrid {
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
+	int scan_fold = 1; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=0)
 	void load() {
 		if(const char *e = getenv("CCG_JOIN_PF")) join_pf = atoi(e);
+		if(const char *e = getenv("CCG_SCAN_FOLD")) scan_fold = atoi(e);
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
 		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
@@ -948,6 +950,97 @@ struct NoTail {
 		b.cj[u] = j;
 	}
 };
+// k_dnj_fold's work done by the scan itself (no kernel boundary, no extra
+// pass over the partials): a unit's wave stores its partial and counts itself
+// in per entry; the entry's last unit folds the entry (rf, rj), counts the
+// entry in per 64-entry chunk, and the chunk's last entry writes the chunk
+// summary k_dnj_join_pf replays from.  Partials are stored write-through and
+// drained (s_waitcnt) before the relaxed count, read back with agent-scope
+// loads (the pattern of the sharded engine's RecTail); each last arriver
+// resets its counter, so they are zero between joins.
+struct FoldTail {
+	__device__ __forceinline__ void begin(const TreeBufs &, int) const {}
+};
+
+template <class Tail>
+__device__ __forceinline__ void tail_unit(const Tail &t, const TreeBufs &b, int n, int u, int ua, int ub, int r,
+                                          double q, int j, int e, int T) {
+	(void) e;
+	(void) T;
+	if((threadIdx.x & 63) == 0) t.unit(b, n, u, ua, ub, r, q, j);
+}
+
+// all lanes of the wave, with the wave's (q, j) of unit u of entry e
+__device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, int n, int u, int ua, int ub, int r,
+                                          double q, int j, int e, int T) {
+	(void) n;
+	(void) r;
+	const int lane = threadIdx.x & 63;
+	int chunk_done = 0;
+	if(lane == 0) {
+		bool last = true;
+		if(ub - ua > 1) {
+			__hip_atomic_store(b.cq + u, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(b.cj + u, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			const unsigned seen = __hip_atomic_fetch_add(b.ecnt + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			last = (int) seen == ub - ua - 1;
+			if(last) {
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+				for(int x0 = ua; x0 < ub; x0 += 4) {   // 4 partials' loads in flight
+					double oq[4];
+					int oi[4];
+#pragma unroll
+					for(int m = 0; m < 4; ++m) {
+						const int x = x0 + m < ub ? x0 + m : ub - 1;
+						oq[m] = __hip_atomic_load(b.cq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						oi[m] = __hip_atomic_load(b.cj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					}
+#pragma unroll
+					for(int m = 0; m < 4; ++m) {
+						if(x0 + m < ub && qarg_better(oq[m], oi[m], q, j)) {
+							q = oq[m];
+							j = oi[m];
+						}
+					}
+				}
+				__hip_atomic_store(b.ecnt + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+		}
+		if(last) {
+			__hip_atomic_store(b.rf + e, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(b.rj + e, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			const int c = e >> 6, ce = T - (c << 6) < 64 ? T - (c << 6) : 64;
+			const unsigned seen = __hip_atomic_fetch_add(b.ccnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if((int) seen == ce - 1) {
+				chunk_done = 1;
+				__hip_atomic_store(b.ccnt + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+		}
+	}
+	if(!__shfl(chunk_done, 0)) return;
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	// the chunk summary, as k_dnj_fold leaves it
+	const int c = e >> 6, e2 = (c << 6) + lane;
+	const bool valid = e2 < T;
+	const int rr = valid ? b.crow[e2] : 0;
+	const double bnd = valid ? b.cbnd[e2] : 0.0;
+	const double f = valid ? __hip_atomic_load(b.rf + e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : DBL_MAX;
+	const int fj = valid ? __hip_atomic_load(b.rj + e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+	const double mq = readlane_d(wave_incl_min(f), 63);
+	const unsigned long long hm = __ballot(valid && f == mq);
+	const unsigned long long bm = __ballot(valid && !(f >= bnd));
+	const int first = hm ? __ffsll((long long) hm) - 1 : 0;
+	const int fr = __shfl(rr, first), fjj = __shfl(fj, first);
+	if(lane == 0) {
+		b.chg[c] = mq;
+		b.chr[c] = fr;
+		b.chj[c] = fjj;
+		b.chb[c] = bm != 0ull;
+	}
+}
+
 template <int ET, bool GEN, class Rows, class Tail = NoTail>
 __global__ __launch_bounds__(TB) void k_dnj_scan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                  int n, Rows rows, int seg, Tail tail = Tail()) {
@@ -1055,7 +1148,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		if(lane == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, q, idx);
+		tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, T);
 	}
 }
 
@@ -1180,7 +1273,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		if(lane == 0) tail.unit(b, n, u, ua, ua + dcdiv(r, seg), r, q, idx);
+		tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn);
 	}
 }
 
@@ -1193,7 +1286,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 // row), each row's (q, j) reduced and stored as its own unit partial, so the
 // fold and the join read the layout of k_dnj_scan_v.  UC columns per lane per
 // step.
-template <int ET, int G, int UC>
+template <int ET, int G, int UC, bool FOLD = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int seg) {
 	typedef typename Elem<ET>::T T;
@@ -1266,8 +1359,10 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 			double qq = q[k];
 			int ii = idx[k];
 			qarg_wave_reduce(qq, ii);
-			if(lane == 0) {
-				const int e = g * G + k;
+			const int e = g * G + k;
+			if(FOLD) {
+				tail_unit(FoldTail(), b, n, e * umax + s, e * umax, e * umax + dcdiv(r[k], seg), r[k], qq, ii, e, Tn);
+			} else if(lane == 0) {
 				b.cq[e * umax + s] = qq;
 				b.cj[e * umax + s] = ii;
 			}

@@ -86,6 +86,8 @@ struct TreeBufs {
 	unsigned long long *jpub;   // k_dnj_join_pf, replay path: the pair block 0 chose, tagged with n (n, i, j: 21 bits each)
 	double *chg;                // k_dnj_fold: per 64-entry chunk, the minimum fresh value,
 	int *chr, *chj, *chb;       // the row and partner of its first entry reaching it, and whether any entry is "bad"
+	unsigned *ecnt, *ccnt;      // the scan's fold at its last arrivals: units arrived per entry / entries per
+	                            // 64-entry chunk (zero between joins: each last arriver resets its counter)
 	int maxu;
 };
 

@@ -23,6 +23,7 @@
 //     above, VALU-integer-bound, 128x128 pair tiles, 8x8 pairs per thread in
 //     registers.
 // Both stage KC-word chunks of the two row panels through LDS.
+#include <cstring>
 #include <vector>
 #include "ccg_internal.h"
 #include "ccg_shard_layout.h"
@@ -49,9 +50,13 @@ __device__ __forceinline__ uint32_t compress_even(uint64_t x) {
 	return (uint32_t) x;
 }
 
-// qseq2nibble word (position p at bits 63-2p..62-2p) -> (hi, lo) planes
+// qseq2nibble word (position p at bits 63-2p..62-2p) -> (hi, lo) planes.
+// Non-pair mode may compact the words: plane word w holds alignment word
+// widx[w] (the words the global mask does not exclude entirely, in order), so
+// W32 is then their count; widx = NULL keeps every word.
 __global__ void k_planes(const uint64_t *__restrict__ seqs, const uint32_t *__restrict__ incs, int n, int stride,
-                         int W32, int Wp, int pair, uint2 *__restrict__ out2, uint4 *__restrict__ out4) {
+                         int W32, int Wp, int pair, uint2 *__restrict__ out2, uint4 *__restrict__ out4,
+                         const int *__restrict__ widx) {
 	// grid-stride: n * Wp exceeds 2^32 work-items at config sizes (50k x 5M)
 	const long long total = (long long) n * Wp;
 	for(long long e = (long long) blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -59,10 +64,11 @@ __global__ void k_planes(const uint64_t *__restrict__ seqs, const uint32_t *__re
 		const int t = (int) (e / Wp), w = (int) (e % Wp);
 		uint32_t hi = 0, lo = 0, m = 0;
 		if(w < W32) {
-			uint64_t x = seqs[(size_t) t * stride + w];
+			const int ws = widx ? widx[w] : w;
+			uint64_t x = seqs[(size_t) t * stride + ws];
 			hi = compress_even(x >> 1);
 			lo = compress_even(x);
-			m = pair ? incs[(size_t) t * stride + w] : incs[w];
+			m = pair ? incs[(size_t) t * stride + ws] : incs[ws];
 		}
 		if(pair) {
 			out4[e] = make_uint4(hi, lo, m, 0);
@@ -1780,12 +1786,12 @@ int ccg_snp_shard_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, int rank, int wo
 // copy of the packed MSA would add another 25 GB).  *mask = the device copy of
 // the non-pair include mask (k_popsum reads it), or NULL.
 static int snp_planes(ccg_ctx *ctx, const ccg_snp_args *a, int W32, int Wp, void *planes, bool host_in,
-                      uint32_t **mask) {
+                      uint32_t **mask, const int *widx) {
 	*mask = NULL;
 	if(!host_in) {
 		const long long total = (long long) a->n * Wp, pg = cdivll(total, 256);
 		k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(
-		    a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair, (uint2 *) planes, (uint4 *) planes);
+		    a->seqs, a->incs, a->n, a->stride, W32, Wp, a->pair, (uint2 *) planes, (uint4 *) planes, widx);
 		CCG_CHECK(hipGetLastError());
 		return CCG_OK;
 	}
@@ -1824,7 +1830,7 @@ static int snp_planes(ccg_ctx *ctx, const ccg_snp_args *a, int W32, int Wp, void
 		const long long pg = cdivll(rows * Wp, 256);
 		k_planes<<<(unsigned) (pg < 262144 ? pg : 262144), 256, 0, ctx->stream>>>(
 		    sseq, a->pair ? sinc : *mask, (int) rows, a->stride, W32, Wp, a->pair, (uint2 *) planes + t0 * Wp,
-		    (uint4 *) planes + t0 * Wp);
+		    (uint4 *) planes + t0 * Wp, widx);
 		if(hipGetLastError() != hipSuccess) rc = CCG_EHIP;
 	}
 	hipStreamSynchronize(ctx->stream);
@@ -1853,18 +1859,58 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	}
 	const int W32 = (a->len + 31) / 32;
 	const int kc = a->pair ? KCP : KC;
-	const int Wp = (int) (cdivll(W32, kc) * kc);
+	// Non-pair mode: a word the global mask excludes entirely contributes to
+	// no pair (fsacmp.c:552 counts included positions only), so the planes
+	// keep only the other words (partial words stay masked); the pair kernels
+	// then stream and multiply ~10% fewer words on the headline's alignment.
+	// Pair mode's masks are per taxon and stay whole.
+	std::vector<int> keep;
+	int Wc = W32;
+	if(!a->pair) {
+		std::vector<uint32_t> hm((size_t) W32);
+		if(host_in) std::memcpy(hm.data(), a->incs, (size_t) W32 * 4);
+		else {
+			CCG_CHECK(hipMemcpyAsync(hm.data(), a->incs, (size_t) W32 * 4, hipMemcpyDeviceToHost, ctx->stream));
+			CCG_CHECK(hipStreamSynchronize(ctx->stream));
+		}
+		for(int w = 0; w < W32; ++w)
+			if(hm[w]) keep.push_back(w);
+		Wc = (int) keep.size();
+		if(Wc == W32 || getenv("CCG_DIST_NOCOMPACT")) {
+			keep.clear();
+			Wc = W32;
+		}
+		if(Wc == 0) Wc = 1;   // nothing included: one all-zero word (every count 0)
+	}
+	const int Wp = (int) (cdivll(Wc, kc) * kc);
 	const long long npad = cdivll(a->n, TILE2) * TILE2;   // whole panels of either tile size
 	const size_t esz = a->pair ? sizeof(uint4) : sizeof(uint2);
 	void *planes = NULL;
-	int *d_inc = NULL;
+	int *d_inc = NULL, *d_widx = NULL;
 	CCG_CHECK(hipMalloc(&planes, (size_t) npad * Wp * esz));
-	CCG_CHECK(hipMalloc(&d_inc, sizeof(int)));
-	CCG_CHECK(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream));
-	uint32_t *mask = NULL;
-	if(int prc = snp_planes(ctx, a, W32, Wp, planes, host_in, &mask)) {
+	if(hipMalloc(&d_inc, sizeof(int)) != hipSuccess ||
+	   (!keep.empty() && hipMalloc(&d_widx, keep.size() * sizeof(int)) != hipSuccess)) {
 		hipFree(planes);
 		hipFree(d_inc);
+		return CCG_ENOMEM;
+	}
+	uint32_t *mask = NULL;
+	int prc = CCG_OK;
+	if(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream) != hipSuccess ||
+	   (d_widx && hipMemcpyAsync(d_widx, keep.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice,
+	                             ctx->stream) != hipSuccess))
+		prc = CCG_EHIP;
+	if(!prc) {
+		// the compacted word list, or every word (a mask with no included word: one zero word)
+		const int *widx = d_widx;
+		const int Wsrc = d_widx ? Wc : (a->pair || Wc == W32 ? W32 : 0);
+		prc = snp_planes(ctx, a, Wsrc, Wp, planes, host_in, &mask, widx);
+	}
+	if(prc) {
+		hipStreamSynchronize(ctx->stream);
+		hipFree(planes);
+		hipFree(d_inc);
+		hipFree(d_widx);
 		hipFree(mask);
 		return prc;
 	}
@@ -1875,6 +1921,7 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 		CCG_CHECK(hipStreamSynchronize(ctx->stream));
 	}
 	if(mask) CCG_CHECK(hipFree(mask));
+	if(d_widx) CCG_CHECK(hipFree(d_widx));
 	double nFactor = 1.0;
 	if(!a->pair && a->norm) {
 		nFactor = a->norm;

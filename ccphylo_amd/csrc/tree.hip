@@ -1592,6 +1592,7 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	size_t o_pp = take(PLAN_MAXB * 8), o_jp = take(8);
 	const size_t nch = ncand / 64 + 2;   // k_dnj_fold's chunk summaries
 	size_t o_hg = take(nch * 8), o_hr = take(nch * 4), o_hj = take(nch * 4), o_hb = take(nch * 4);
+	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
 	char *m;
 	CCG_CHECK(hipMalloc((void **) &m, sz));
 	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
@@ -1646,6 +1647,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.chr = (int *) (m + o_hr);
 	b.chj = (int *) (m + o_hj);
 	b.chb = (int *) (m + o_hb);
+	b.ecnt = (unsigned *) (m + o_ec);
+	b.ccnt = (unsigned *) (m + o_cc);
 	b.maxu = (int) maxu;
 	return CCG_OK;
 }
@@ -1675,21 +1678,42 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		enqueue_plan<ET, GEN>(st, D, bs, b, n, first);
 		kt.mark(CCG_K_FIND);
 		const int sm = g_grid.scan_mode(n, ET);
-		if(sm == 20 && !GEN) k_dnj_scan_g<ET, 4, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
-		else if(sm == 21 && !GEN) k_dnj_scan_g<ET, 8, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
-		else if(sm == 22 && !GEN) k_dnj_scan_g<ET, 4, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
-		else if(sm == 23 && !GEN) k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
-		else if(sm >= 4 && !GEN) {
-			switch(sm) {
-#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
-				SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7) SV_(13) SV_(15)
-#undef SV_
-				default: k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		// the wave-per-unit scans fold the entries at their last arrivals
+		// (FoldTail) instead of a k_dnj_fold pass
+		const bool tfold = prefold && g_grid.scan_fold && sm >= 1;
+		if(sm >= 20 && sm <= 23 && !GEN) {
+			if(tfold) {
+				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 21) k_dnj_scan_g<ET, 8, 4, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 22) k_dnj_scan_g<ET, 4, 4, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else k_dnj_scan_g<ET, 2, 8, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+			} else {
+				if(sm == 20) k_dnj_scan_g<ET, 4, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 21) k_dnj_scan_g<ET, 8, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 22) k_dnj_scan_g<ET, 4, 4><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 			}
-		} else if(sm >= 4) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		else if(sm) k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		if(prefold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
+		} else if(sm >= 4 && !GEN) {
+			if(tfold) {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, FoldTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(5)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows, FoldTail><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			} else {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(2) SV_(3) SV_(4) SV_(5) SV_(6) SV_(7) SV_(13) SV_(15)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			}
+		} else if(sm >= 1) {
+			if(tfold) k_dnj_scan_w<ET, GEN, DenseRows, FoldTail><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+			else k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		} else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		if(prefold && !tfold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
 		kt.mark(CCG_K_REST);
 		if(prefold && g_grid.join_pf) k_dnj_join_pf<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, g_grid.join_pf == 2);
 		else k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold, seg);
@@ -1702,7 +1726,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		kt.mark(CCG_K_REQUEUE);
-		return (GEN ? 5 : 4) + prefold + xs;
+		return (GEN ? 5 : 4) + (prefold && !tfold) + xs;
 	}
 	if(method == CCG_TREE_HNJ) {
 		k_hnj_argmin<><<<gn, TB, 0, st>>>(b, n);

@@ -613,3 +613,67 @@ def test_dnj_checkpoint_large_n(dev):
     got2 = dev.tree_dev_state(Dd.data_ptr(), n - k, max_joins=k, state=st, want_state=False)[0]
     ref2 = pyoracle.dnj_resume(ost, max_joins=k, threads=8)[0]
     assert (got2 == ref2).all()
+
+
+@pytest.mark.parametrize("n,L,et,excl,norm", [(300, 5000, 8, 10, 0), (777, 4097, 4, 3, 0), (2100, 3200, 8, 7, 1000),
+                                              (129, 64, 2, 1, 0), (500, 100, 1, 100, 0), (257, 9000, 8, 0, 0)])
+def test_dist_compacted_words(dev, monkeypatch, n, L, et, excl, norm):
+    """Non-pair dist keeps only the words the global mask does not exclude
+    entirely in its bit planes (fsacmp.c:552 counts included positions only):
+    the matrix equals the uncompacted planes' (CCG_DIST_NOCOMPACT=1) and the
+    oracle's bit for bit; every `excl`-th word excluded, partial words kept
+    masked, all words excluded (excl = 1), none (0); the device-, host- and
+    shard-input paths."""
+    from oracle import pyoracle
+    from tools.synth import clade_packed
+    seqs, incs = clade_packed(n, L, 8, seed=n, every=excl)
+    incs[1::5] &= np.uint32(0x0FF0F00F)   # partial words
+    bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 0.05}[et]
+    want = pyoracle.snp_ltd(seqs, incs, n, L, norm=norm, etype=et, byte_scale=bs)[0]
+    got = dev.snp_ltd(seqs, incs, n, L, norm=norm, etype=et, byte_scale=bs)[0]
+    monkeypatch.setenv("CCG_DIST_NOCOMPACT", "1")
+    whole = dev.snp_ltd(seqs, incs, n, L, norm=norm, etype=et, byte_scale=bs)[0]
+    monkeypatch.delenv("CCG_DIST_NOCOMPACT")
+    assert (got.view(np.uint8) == want.view(np.uint8)).all()
+    assert (whole.view(np.uint8) == want.view(np.uint8)).all()
+    if et in (8, 4):   # the band shard from host memory (ccg_snp_ltd_shard), world 3
+        import torch
+        from ccphylo_amd import native as nt
+        for rank in range(3):
+            elems = nt.shard_elems(n, rank, 3)
+            Dl = torch.zeros(max(elems, 1), dtype=torch.float64 if et == 8 else torch.float32, device="cuda")
+            dev.snp_ltd_shard(seqs, incs, n, L, Dl.data_ptr(), rank, 3, etype=et, norm=norm)
+            loc = Dl.cpu().numpy()
+            for r in range(1, n):
+                if nt.shard_owner(r, 3) == rank:
+                    o = nt.shard_row_offset(r, rank, 3)
+                    assert (loc[o:o + r] == want[r * (r - 1) // 2:r * (r - 1) // 2 + r]).all(), (rank, r)
+
+
+@pytest.mark.parametrize("kind,n,et,mode", [("euc", 2500, 8, "9"), ("clade", 3000, 8, "4"), ("euc", 2000, 4, "20"),
+                                            ("clade", 2200, 8, "1"), ("miss", 1400, 8, "1"), ("snp", 1800, 2, "20")])
+def test_dnj_scan_tail_fold(dev, monkeypatch, kind, n, et, mode):
+    """The fold of each entry's unit partials and the 64-entry chunk
+    summaries at the scan's last arrivals (FoldTail, the default past 16384
+    taxa) instead of a k_dnj_fold pass, at small n through CCG_PREFOLD_N=0
+    and small rescan units (many units per row, many arrivals per entry):
+    wave scans with 16-byte loads (9, 4), row groups (20), the GEN wave scan
+    with missing entries (1); joins bit-identical to the serial reference and
+    to CCG_SCAN_FOLD=0 (k_dnj_fold)."""
+    from oracle import pyoracle
+    monkeypatch.setenv("CCG_SCAN_WAVE", mode)
+    monkeypatch.setenv("CCG_PREFOLD_N", "0")
+    monkeypatch.setenv("CCG_SEG_MUL", "1")
+    D = {"euc": lambda: _euclid(n, n + 1), "snp": lambda: _snp(n, n), "clade": lambda: _clade_ltd(n, n + 2),
+         "miss": lambda: _missing_ltd(n, n)}[kind]()
+    bs = {8: 1.0, 4: 1.0, 2: 4.0}[et]
+    if et == 4:
+        D = D.astype(np.float32)
+    elif et == 2:
+        D = np.clip(D * bs + 0.5, 0, 65535).astype(np.uint16)
+    ref, rfn, rfd = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1)
+    for fold in ("1", "0"):
+        monkeypatch.setenv("CCG_SCAN_FOLD", fold)
+        got, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True)
+        assert (fn, fd) == (rfn, rfd), fold
+        assert len(got) == len(ref) and (got == ref).all(), fold
