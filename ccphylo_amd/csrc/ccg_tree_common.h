@@ -98,6 +98,7 @@ struct TreeWork {
 	void *mem;
 };
 int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st);
+size_t ccg_tree_bytes(int n);   // what ccg_tree_alloc allocates
 
 // ------------------------------------------------------------------ helpers
 __host__ __device__ static inline unsigned cdiv(long long a, long long b) { return (unsigned) ((a + b - 1) / b); }

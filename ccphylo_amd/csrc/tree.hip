@@ -1545,7 +1545,9 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 }
 
 // ------------------------------------------------------------------ host
-int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
+// The device layout of one tree run (one allocation), sized for n taxa:
+// returns its bytes, and with m != NULL points b's arrays into it.
+static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
 	const size_t maxu = cdiv(n, SEG) + 1;
 	// every row below S may qualify: room for n entries and their units
@@ -1556,8 +1558,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	DnjGrid g;
 	g.load();
 	int umax = dnj_umax(n, g.seg(n));
-	for(int m = 2; m <= 9; ++m) {
-		const int k = 16384 * m - 1;
+	for(int mm = 2; mm <= 9; ++mm) {
+		const int k = 16384 * mm - 1;
 		if(k <= n && dnj_umax(k, g.seg(k)) > umax) umax = dnj_umax(k, g.seg(k));
 	}
 	size_t cunits = ncand * (size_t) umax;
@@ -1593,11 +1595,8 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	const size_t nch = ncand / 64 + 2;   // k_dnj_fold's chunk summaries
 	size_t o_hg = take(nch * 8), o_hr = take(nch * 4), o_hj = take(nch * 4), o_hb = take(nch * 4);
 	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
-	char *m;
-	CCG_CHECK(hipMalloc((void **) &m, sz));
-	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
-	w->mem = m;
-	TreeBufs &b = w->b;
+	if(!m) return sz;
+	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
 	b.Q = (double *) (m + o_Q);
 	b.contrib = (double *) (m + o_c);
@@ -1650,6 +1649,18 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	b.ecnt = (unsigned *) (m + o_ec);
 	b.ccnt = (unsigned *) (m + o_cc);
 	b.maxu = (int) maxu;
+	return sz;
+}
+
+size_t ccg_tree_bytes(int n) { return tree_layout(NULL, n, NULL); }
+
+int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
+	const size_t sz = tree_layout(NULL, n, NULL);
+	char *m;
+	CCG_CHECK(hipMalloc((void **) &m, sz));
+	CCG_CHECK(hipMemsetAsync(m, 0, sz, st));
+	w->mem = m;
+	tree_layout(&w->b, n, m);
 	return CCG_OK;
 }
 

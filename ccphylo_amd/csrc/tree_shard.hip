@@ -484,6 +484,45 @@ static int sh_nlb(int n, const Shard &sh) {
 	return nb > sh.rank ? (nb - sh.rank + sh.world - 1) / sh.world : 0;
 }
 
+// the sharded NJ's device state (one allocation): the TreeBufs subset its
+// loop uses, the argmin records with row n-1 behind them, lines i / j, the
+// exact row sums' records and the init gathers
+struct ShnLayout {
+	size_t o_sD, o_c, o_N, o_ws, o_wa, o_wc, o_we, o_qp, o_fp, o_j, o_ctl, o_F, o_rec, o_X, o_Xm;
+	size_t o_xa, o_xb, o_xcr, o_xt, o_rp, o_is, rec_b, sz = 0;
+	ShnLayout(int n0, int world, int es) {
+		auto take = [&](size_t bytes) {
+			size_t off = sz;
+			sz += (bytes + 255) & ~(size_t) 255;
+			return off;
+		};
+		const size_t nb = (size_t) cdiv(n0, TB) + 1;
+		const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
+		o_sD = take(((size_t) n0 + 1) * 8);
+		o_c = take(((size_t) n0 + 1) * 8);
+		o_N = take(((size_t) n0 + 1) * 4);
+		o_ws = take(nb * 8);
+		o_wa = take(nb * 8);
+		o_wc = take(nb * 4);
+		o_we = take(nb * 4);
+		o_qp = take(SH_GRID * 8);
+		o_fp = take(SH_GRID * 8);
+		o_j = take((size_t) n0 * sizeof(ccg_join));
+		o_ctl = take(sizeof(TreeCtl));
+		rec_b = ((size_t) world * sizeof(ShRec) + 15) & ~(size_t) 15;
+		o_F = take((size_t) (nseg0 + 2) * 8);
+		o_rec = take(rec_b + (size_t) n0 * es + 16);
+		o_X = take((size_t) 2 * n0 * es);
+		o_Xm = take((size_t) n0 * es + 8);
+		o_xa = take(nb * 8);
+		o_xb = take(nb * sizeof(XsBlk));
+		o_xcr = take(nb * XB_CAP * sizeof(XsCross));
+		o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
+		o_rp = take(sh_rp_bytes(n0));
+		o_is = take(sh_init_scratch_bytes(n0, world));
+	}
+};
+
 template <int ET>
 static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll_in, void *Dd,
                             ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats) {
@@ -499,27 +538,13 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	}
 	const Shard sh = {coll_in->rank, coll_in->world};
 	// device state: the single-GPU TreeBufs subset this loop uses
-	const size_t nb = (size_t) cdiv(n0, TB) + 1;
 	const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
-	const size_t rp_bytes = sh_rp_bytes(n0);
-	size_t sz = 0;
-	auto take = [&](size_t bytes) {
-		size_t off = sz;
-		sz += (bytes + 255) & ~(size_t) 255;
-		return off;
-	};
-	size_t o_sD = take((n0 + 1) * 8), o_c = take((n0 + 1) * 8), o_N = take((n0 + 1) * 4);
-	size_t o_ws = take(nb * 8), o_wa = take(nb * 8), o_wc = take(nb * 4), o_we = take(nb * 4);
-	size_t o_qp = take(SH_GRID * 8), o_fp = take(SH_GRID * 8);
-	size_t o_j = take((size_t) n0 * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
-	// the argmin records, then row n-1 (16-byte aligned), gathered by one allreduce
-	const size_t rec_b = ((size_t) coll_in->world * sizeof(ShRec) + 15) & ~(size_t) 15;
-	size_t o_F = take((size_t) (nseg0 + 2) * 8), o_rec = take(rec_b + (size_t) n0 * ET + 16);
-	size_t o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
-	// exact row sums over the join blocks (xs_join_row / xs_walk_blocks)
-	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xcr = take(nb * XB_CAP * sizeof(XsCross));
-	size_t o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
-	size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll_in->world));
+	const ShnLayout L(n0, coll_in->world, ET);
+	const size_t rec_b = L.rec_b, sz = L.sz;
+	const size_t o_sD = L.o_sD, o_c = L.o_c, o_N = L.o_N, o_ws = L.o_ws, o_wa = L.o_wa, o_wc = L.o_wc, o_we = L.o_we;
+	const size_t o_qp = L.o_qp, o_fp = L.o_fp, o_j = L.o_j, o_ctl = L.o_ctl, o_F = L.o_F, o_rec = L.o_rec;
+	const size_t o_X = L.o_X, o_Xm = L.o_Xm, o_xa = L.o_xa, o_xb = L.o_xb, o_xcr = L.o_xcr, o_xt = L.o_xt;
+	const size_t o_rp = L.o_rp, o_is = L.o_is;
 	char *m;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) return CCG_ENOMEM;
 	size_t hcap = sh_init_host_bytes(n0, coll_in->world);
@@ -681,6 +706,7 @@ out:
 }
 
 // tree_shard_dnj.hip
+size_t ccg_shard_dnj_bytes(int n, int world, int es);
 int ccg_tree_shard_dnj_impl(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll, void *Dloc, ccg_join *joins,
                             int *njoins, int *final_n, double *final_d, int64_t *stats);
 
@@ -757,6 +783,22 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 	out->allreduce_sum_u8 = rccl_allreduce;
 	out->broadcast = rccl_bcast;
 	out->allgather = rccl_allgather;
+	return CCG_OK;
+}
+
+int ccg_tree_shard_bytes(int64_t n, int etype, int method, int world, int64_t *device_bytes, int64_t *gather_bytes) {
+	if(!device_bytes || n < 3 || n > INT32_MAX - 512 || world < 1) return CCG_EINVAL;
+	if(etype != 8 && etype != 4 && etype != 2 && etype != 1) return CCG_EINVAL;
+	if(method != CCG_TREE_NJ && method != CCG_TREE_DNJ) return CCG_EINVAL;
+	const int n0 = (int) n;
+	*device_bytes = (int64_t) (method == CCG_TREE_DNJ ? ccg_shard_dnj_bytes(n0, world, etype)
+	                                                  : ShnLayout(n0, world, etype).sz);
+	// sh_init_chunk's bound on the hard-column gather buffer (a quarter of the
+	// free memory, at most 16 GB, at least 256 columns)
+	if(gather_bytes) {
+		int64_t g = (int64_t) 16 << 30, mn = (int64_t) 256 * n0 * etype;
+		*gather_bytes = g > mn ? g : mn;
+	}
 	return CCG_OK;
 }
 

@@ -579,6 +579,34 @@ static int shd_init_hnj(const typename Elem<ET>::T *D, int n0, double bs, const 
 }
 
 // ------------------------------------------------------------------ host driver
+// the sharded DNJ's buffers beyond ccg_tree_alloc's (one allocation): the
+// records, lines i / j, row n-1, the new line j, the replay's scratch and the
+// init gathers
+struct ShdLayout {
+	size_t o_R, o_X, o_Xm, o_Sl, o_G, o_Xj, o_pf, o_pa, o_pc, o_rp, o_is, sz = 0;
+	ShdLayout(int n0, int world, int es) {
+		auto take = [&](size_t bytes) {
+			size_t off = sz;
+			sz += (bytes + 255) & ~(size_t) 255;
+			return off;
+		};
+		const RecSlot rs0 = rec_slot(n0, world);
+		o_R = take(rec_bytes(n0));
+		o_X = take((size_t) 2 * n0 * es);
+		o_Xm = take((size_t) n0 * es + 8);
+		o_Sl = take(rs0.bytes);
+		o_G = take((size_t) world * rs0.bytes);
+		o_Xj = take((size_t) n0 * es + 8);
+		o_pf = take((size_t) n0);
+		o_pa = take((size_t) PICK_MAXB * n0);
+		o_pc = take((size_t) n0 * 4);
+		o_rp = take(sh_rp_bytes(n0));
+		o_is = take(sh_init_scratch_bytes(n0, world));
+	}
+};
+
+size_t ccg_shard_dnj_bytes(int n, int world, int es) { return ccg_tree_bytes(n) + ShdLayout(n, world, es).sz; }
+
 template <int ET>
 static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, void *Dd,
                                 ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats) {
@@ -592,19 +620,10 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	TreeWork w;
 	if((rc = ccg_tree_alloc(&w, n0, st))) return rc;
 	TreeBufs b = w.b;
-	// shard buffers: records, lines i/j, row n-1, new line j, init gathers
-	const size_t rp_bytes = sh_rp_bytes(n0);
-	size_t sz = 0;
-	auto take = [&](size_t bytes) {
-		size_t off = sz;
-		sz += (bytes + 255) & ~(size_t) 255;
-		return off;
-	};
+	const ShdLayout L(n0, coll->world, ET);
 	const RecSlot rs0 = rec_slot(n0, coll->world);
-	const size_t o_R = take(rec_bytes(n0)), o_X = take((size_t) 2 * n0 * ET), o_Xm = take((size_t) n0 * ET + 8);
-	const size_t o_Sl = take(rs0.bytes), o_G = take((size_t) coll->world * rs0.bytes);
-	const size_t o_Xj = take((size_t) n0 * ET + 8), o_pf = take((size_t) n0), o_pa = take((size_t) PICK_MAXB * n0), o_pc = take((size_t) n0 * 4);
-	const size_t o_rp = take(rp_bytes), o_is = take(sh_init_scratch_bytes(n0, coll->world));
+	const size_t o_R = L.o_R, o_X = L.o_X, o_Xm = L.o_Xm, o_Sl = L.o_Sl, o_G = L.o_G, o_Xj = L.o_Xj, o_pf = L.o_pf;
+	const size_t o_pa = L.o_pa, o_pc = L.o_pc, o_rp = L.o_rp, o_is = L.o_is, sz = L.sz;
 	char *m = NULL;
 	unsigned char *h = NULL;
 	if(hipMalloc((void **) &m, sz) != hipSuccess) {

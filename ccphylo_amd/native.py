@@ -113,7 +113,7 @@ ENGINE_SYMBOLS = [
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
-    "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state",
+    "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state", "ccg_tree_shard_bytes",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -185,6 +185,8 @@ def engine_lib():
                                        C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int64)]
         lib.ccg_tree_shard_dev.argtypes = lib.ccg_tree_shard.argtypes
+        lib.ccg_tree_shard_bytes.argtypes = [C.c_int64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                             C.POINTER(C.c_int64)]
         lib.ccg_kma_ltd.argtypes = [C.c_void_p, C.POINTER(KmaArgs), C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
         lib.ccg_kma_ltd_dev.argtypes = lib.ccg_kma_ltd.argtypes
         lib.ccg_selftest_row_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_double),
@@ -514,6 +516,16 @@ class Device:
 
 
 # ---------------------------------------------------------------- sharding
+def tree_shard_bytes(n, etype=4, method=CCG_TREE_DNJ, world=8):
+    """(device bytes ccg_tree_shard_dev allocates beside the shard, bound on
+    the init's hard-column gather buffer) -- ccg_tree_shard_bytes (no GPU)."""
+    d, g = C.c_int64(0), C.c_int64(0)
+    rc = engine_lib().ccg_tree_shard_bytes(int(n), etype, method, world, C.byref(d), C.byref(g))
+    if rc:
+        raise CcgError(f"ccg_tree_shard_bytes: {rc}")
+    return d.value, g.value
+
+
 def shard_owner(row, world):
     """Rank owning LT row `row`: bands of SHARD_BAND rows dealt round-robin."""
     return (row // SHARD_BAND) % world

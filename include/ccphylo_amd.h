@@ -290,6 +290,15 @@ int ccg_tree_shard_dev(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *col
 int ccg_tree_shard(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll *coll, const void *D,
                    ccg_join *joins, int *njoins, int *final_n, double *final_d, int64_t *stats);
 
+/* Device bytes ccg_tree_shard_dev allocates beside the rank's shard for a run
+ * of n taxa over `world` ranks (the replicated per-taxon vectors, the per-join
+ * buffers, the initSummaD exchange), for planning a large run's memory
+ * (configs[4]: n = 1e6, a 250 GB float shard per rank).  *gather_bytes (may
+ * be NULL) bounds the extra buffer the exact initSummaD allocates, during the
+ * init only, when some column sums need the serial gather (non-integral cells,
+ * DESIGN.md 6; integer SNP counts need none). */
+int ccg_tree_shard_bytes(int64_t n, int etype, int method, int world, int64_t *device_bytes, int64_t *gather_bytes);
+
 /* dist straight into one rank's shard ("dist writes the
  * shards that DNJ consumes in place"): ccg_snp_ltd_dev semantics
  * (a->row_begin = a->row_end = 0), but only the rank's owned rows are

@@ -282,3 +282,94 @@ def test_dnj_large_n_kernels_prefix(dev, monkeypatch, env):
     ref = pyoracle.tree(host, n, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), f"dnj 33k prefix [{env}]")
+
+
+@pytest.fixture(scope="module")
+def msa_1e6():
+    """configs[4]'s alignment: n = 1e6 taxa x L = 100 kbp, tree-like (512
+    clades), packed in HOST memory (25 GB; every rank holds it and streams it
+    into its bit planes), every 10th word excluded."""
+    import torch
+    from tools.config5_rank import make_packed_host
+    n, L = 1_000_000, 100_000
+    W = L // 32 + 1
+    seqs = make_packed_host(torch, n, W)
+    incs = np.full(W, 0xFFFFFFFF, dtype=np.uint32)
+    incs[::10] = 0
+    incs[(L + 31) // 32:] = 0
+    if L % 32:
+        incs[(L + 31) // 32 - 1] &= (0xFFFFFFFF << (32 - L % 32)) & 0xFFFFFFFF
+    yield n, L, seqs, incs
+    del seqs
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_config4_rank_1e6(dev, msa_1e6, rank):
+    """configs[4] (n = 1e6, world 8) for one rank on one MI355X: the rank's
+    dist straight into its 250 GB float band shard (ccg_snp_ltd_shard, the
+    alignment streamed from host memory into compacted bit planes), sampled
+    cells against the oracle's fsacmp (fsacmp.c:552), the dist's HBM peak
+    within 280 GB; then, with the planes freed, the rank's whole tree-phase
+    state (ccg_tree_shard_bytes: every buffer ccg_tree_shard_dev allocates
+    beside the shard for DNJ at this n) allocated next to the shard.  The
+    cross-rank exchange of the tree needs the 8-GPU node."""
+    import json
+    import torch
+    from ccphylo_amd import native as nt
+    from oracle import pyoracle
+    n, L, seqs, incs = msa_1e6
+    world = 8
+    torch.cuda.empty_cache()
+    free0, total = torch.cuda.mem_get_info()
+    elems = nt.shard_elems(n, rank, world)
+    Dloc = dev.malloc(elems * 4)
+    tree_b = None
+    try:
+        t0 = __import__("time").perf_counter()
+        inc = dev.snp_ltd_shard(seqs, incs, n, L, Dloc, rank, world, etype=4)
+        dist_s = __import__("time").perf_counter() - t0
+        assert inc == int(np.unpackbits(incs.view(np.uint8)).sum())
+        # the planes the dist held beside the shard: kept words (compacted) x 2 bits, rows padded to 256
+        Wc = int((incs[:(L + 31) // 32] != 0).sum())
+        planes = -(-n // 256) * 256 * (-(-Wc // 16) * 16) * 8
+        peak = elems * 4 + planes + (256 << 20)
+        assert peak <= 280e9, peak
+        lib = pyoracle.lib()
+        rng = np.random.default_rng(rank + 1)
+        host = np.empty(1, dtype=np.float32)
+        rows = [r for r in (n - 1, n // 2 + 3, 8 * world * 3 + rank * 8 + 5, 8 * rank + 1)
+                if r >= 1 and nt.shard_owner(r, world) == rank]
+        rows += [int(b) * 8 + int(rng.integers(0, 8)) for b in rng.integers(0, n // 8, 64) if b % world == rank][:8]
+        checked = 0
+        for i in rows:
+            if i >= n or i < 1:
+                continue
+            for j in sorted({0, i // 2, i - 1, int(rng.integers(0, i))}):
+                want = lib.orc_fsacmp(seqs[i].ctypes.data, seqs[j].ctypes.data, incs.ctypes.data, L)
+                dev.d2h(host, Dloc + 4 * (nt.shard_row_offset(i, rank, world) + j))
+                assert float(host[0]) == float(want), (rank, i, j)
+                checked += 1
+        assert checked >= 20
+        # the tree phase: its whole device state beside the shard
+        tree_b, gather_b = nt.tree_shard_bytes(n, 4, 1, world)
+        free1, _ = torch.cuda.mem_get_info()
+        Tb = dev.malloc(tree_b)
+        free2, _ = torch.cuda.mem_get_info()
+        dev.free(Tb)
+        rec = {"n": n, "L": L, "world": world, "rank": rank, "dist_s": round(dist_s, 3), "rank_cells": elems,
+               "rank_taxa_pairs_per_s": round(elems / dist_s, 1), "shard_GB": round(elems * 4 / 1e9, 2),
+               "kept_words": Wc, "planes_GB": round(planes / 1e9, 2), "dist_peak_GB": round(peak / 1e9, 2),
+               "tree_phase_state_GB": round(tree_b / 1e9, 3),
+               "tree_phase_total_GB": round((elems * 4 + tree_b) / 1e9, 2),
+               "init_gather_bound_GB": round(gather_b / 1e9, 2),
+               "hbm_total_GB": round(total / 1e9, 2), "hbm_free_before_GB": round(free0 / 1e9, 2),
+               "hbm_free_after_shard_GB": round(free1 / 1e9, 2),
+               "hbm_free_with_tree_state_GB": round(free2 / 1e9, 2), "checked_cells": checked}
+        print(json.dumps(rec))
+        if os.environ.get("CCG_CONFIG4_OUT"):
+            with open(os.environ["CCG_CONFIG4_OUT"], "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        # the tree phase leaves the init's gather room too (used only by hard columns)
+        assert free2 > 1e9
+    finally:
+        dev.free(Dloc)

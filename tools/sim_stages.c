@@ -21,7 +21,7 @@ static double chyb[NH];
  * above r's 256-row block: V_k = max(q at k's partner cell, Q_k) (a cell of
  * row k bounds its fresh minimum), block minima of V (the requeue could
  * publish them); VB[1]: the same with every row above r (the idea's limit) */
-static double cvb[2];
+static double cvb[4];
 static const int32_t *g_P;
 static int cmpq_desc_rows;   /* unused */
 static const double *g_Q;
@@ -149,7 +149,7 @@ static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, co
 		int *cand = malloc(n * sizeof(int)), nc = 0;
 		for(int r = n - 1; r >= 1; --r) if(Q[r] < m0) cand[nc++] = r;
 		char *inS = calloc(n, 1);
-		for(int mode = 0; mode < 2; ++mode) {
+		for(int mode = 0; mode < 4; ++mode) {   /* 2: S by partner cells, no V (the engine); 3: + Vblk */
 			memset(inS, 0, n);
 			double cells = 0;
 			int A = 16 < nc ? 16 : nc;
@@ -170,11 +170,11 @@ static void sim_iter(const Ltd *D, int n, const double *sD, const int32_t *N, co
 				if(mode == 1) for(int x = prev - 1; x > r; --x) if(V[x] < vrun) vrun = V[x];   /* every row above r */
 				prev = r;
 				double bb = bound;
-				const double vb = mode == 0 ? bmin[(r >> 8) + 1] : vrun;
+				const double vb = mode == 0 || mode == 3 ? bmin[(r >> 8) + 1] : mode == 1 ? vrun : DBL_MAX;
 				if(vb < bb) bb = vb;
 				if(inS[r]) {
 					double f = fresh_of(D, r, sD, N, memo, have);
-					double v = f > Q[r] ? f : Q[r];
+					double v = mode >= 2 ? V[r] : f > Q[r] ? f : Q[r];
 					cells += r;
 					if(v < bound) bound = v;
 				} else if(Q[r] < bb) {
@@ -198,6 +198,12 @@ int main(int argc, char **argv) {
 	int every = argc > 2 ? atoi(argv[2]) : 1;
 	const int maxj = argc > 3 ? atoi(argv[3]) : 1 << 30;   /* stop (and print) after this many joins */
 	double *Dm = malloc((size_t) n * (n - 1) / 2 * sizeof(double));
+	if(argc > 4) {   /* a matrix from a file: n(n-1)/2 raw doubles (e.g. clade SNP counts) */
+		FILE *f = fopen(argv[4], "rb");
+		if(!f || fread(Dm, sizeof(double), (size_t) n * (n - 1) / 2, f) != (size_t) n * (n - 1) / 2) return 1;
+		fclose(f);
+		goto loaded;
+	}
 	srand(1);
 	double *pts = malloc((size_t) n * 8 * sizeof(double));
 	for(int k = 0; k < n * 8; ++k) pts[k] = rand() / (RAND_MAX + 1.0);
@@ -207,6 +213,7 @@ int main(int argc, char **argv) {
 			for(int d = 0; d < 8; ++d) s += (pts[i * 8 + d] - pts[j * 8 + d]) * (pts[i * 8 + d] - pts[j * 8 + d]);
 			Dm[tri(i) + j] = round(sqrt(s) * 1e9) / 1e9;
 		}
+loaded:;
 	Ltd D = {8, 1.0, Dm};
 	double *sD = malloc(n * sizeof(double)), *Q = malloc(n * sizeof(double));
 	int32_t *N = malloc(n * sizeof(int32_t)), *P = malloc(n * sizeof(int32_t));
@@ -233,7 +240,8 @@ int main(int argc, char **argv) {
 			printf("  after %d joins: ref cells/join %.0f", joins, cref / its);
 			for(int k = 0; k < NK; ++k) printf(" | %d,%d,%d x%.2f st %.2f (max %.0f)", Seqs[k][0], Seqs[k][1], Seqs[k][2], ccur[k] / cref, stages[k] / its, maxst[k]);
 			for(int h = 0; h < NH; ++h) printf(" | H%d+%d x%.2f", HA[h], HB[h], chyb[h] / cref);
-			printf(" | H16+64+Vblk x%.2f | H16+64+Vall x%.2f", cvb[0] / cref, cvb[1] / cref);
+			printf(" | H16+64+Vblk x%.2f | H16+64+Vall x%.2f | H16+64 partner x%.2f | partner+Vblk x%.2f", cvb[0] / cref,
+			       cvb[1] / cref, cvb[2] / cref, cvb[3] / cref);
 			printf("\n");
 			fflush(stdout);
 		}
