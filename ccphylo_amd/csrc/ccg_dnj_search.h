@@ -38,9 +38,12 @@ struct DnjGrid {
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
 	int scan_fold = 1; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=0)
+	int scan_prune = 1; // band mode: the scan rescans S first and prunes the other entries under its exact
+	                    // fresh minima (CCG_SCAN_PRUNE=0: off)
 	void load() {
 		if(const char *e = getenv("CCG_JOIN_PF")) join_pf = atoi(e);
 		if(const char *e = getenv("CCG_SCAN_FOLD")) scan_fold = atoi(e);
+		if(const char *e = getenv("CCG_SCAN_PRUNE")) scan_prune = atoi(e);
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
 		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
@@ -57,7 +60,9 @@ struct DnjGrid {
 	// k_dnj_plan's last argument: the Q-load delay (low 16 bits), bit 16 turns
 	// the register S selection off (on with CCG_PLAN_REGSEL=1)
 	// and bits 17-20 the rows per thread per listing step less one (CCG_PLAN_FR)
-	int plan_flags() const { return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17; }
+	int plan_flags(bool prune = false) const {
+		return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17 | (prune ? 1 << 21 : 0);
+	}
 	// k_dnj_plan's grid: one listing step of (TBF - 64) FIND_RPT rows per block
 	// (CCG_PLAN_MULTI=0: one block walks every step, the round-2 form)
 	unsigned plan_blocks(int n) const {
@@ -340,6 +345,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// step, no bands: n <= 15361): S is selected from them after the fold, by
 	// the whole block, instead of by wave 0 in dependent steps of loads
 	const bool regsel = !BANDS && nblk == 1 && top <= LT * fr && !((qdelay >> 16) & 1);   // (off by default)
+	// S for the scan's pruning (band mode): its rows, Q and unit prefix persisted,
+	// every entry flagged (eS) and each S row's entry index recorded
+	const bool prune = BANDS && ((qdelay >> 21) & 1);
 	qdelay &= 0xffff;
 	double qv[FR];
 	const int rt = top - lt;
@@ -592,10 +600,39 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				ctl->nS = 0;     // k_dnj_join: every entry is in the list
 				ctl->ntop = 0;
 				ctl->smin = smin;
+				ctl->pS = prune ? nS : 0;
 				if(ctop) {
 					atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) ctop);
 					atomicAdd((unsigned long long *) &ctl->cells_top, (unsigned long long) ctop);
 				}
+			}
+			if(prune && bid == 0) {
+				// S in scan order (top rows, then band rows: descending), the
+				// top part's entries are the list's head; its rescan units
+				// prefixed for the scan's S phase
+				const int ta = lane, tb = lane + 64;
+				const int ua = ta < nS ? (int) dcdiv(sS[ta], seg) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], seg) : 0;
+				int tota, totb;
+				const int pa = wave_excl_scan(ua, &tota), pb = wave_excl_scan(ub, &totb);
+				if(ta < nS) {
+					b.pS_row[ta] = sS[ta];
+					b.pS_q[ta] = sQS[ta];
+					b.pS_uo[ta] = pa;
+					if(ta < ntop) {
+						b.pS_ent[ta] = ta;
+						b.eS[ta] = 1;
+					}
+				}
+				if(tb < nS) {
+					b.pS_row[tb] = sS[tb];
+					b.pS_q[tb] = sQS[tb];
+					b.pS_uo[tb] = tota + pb;
+					if(tb < ntop) {
+						b.pS_ent[tb] = tb;
+						b.eS[tb] = 1;
+					}
+				}
+				if(lane == 0) b.pS_uo[nS] = tota + totb;
 			}
 			if(lane == 0) {
 				s_done = 0;
@@ -792,6 +829,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			if(base == top) TS(1, 5);
 			if(base == top - LT * FR) TS(1, 9);
 			unsigned long long bm[FR];
+			unsigned sbm = 0;   // bit m: this lane's slot-m row is a band row of S
 #pragma unroll
 			for(int m = 0; m < FR; ++m) bm[m] = 0ull;
 			const int mlim = (base - 1) / LT + 1 < fr ? (base - 1) / LT + 1 : fr;   // slots holding rows >= 1
@@ -818,6 +856,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 				bool f = false;
 				if(r >= 1 && r < smin && rows.owns(r)) f = srow || qv[m] < bnd;
+				sbm |= (f && srow ? 1u : 0u) << m;
 				bm[m] = __ballot(f);
 				if(lane == 0 && wid > 0) s_mw[m * LW + wid - 1] = __popcll(bm[m]);
 			}
@@ -892,6 +931,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 					                                                __builtin_amdgcn_mbcnt_lo((unsigned) bm[m], 0));
 					b.crow[pos] = r;
 					b.cbnd[pos] = qv[m];
+					if(prune) {
+						const bool isS = (sbm >> m) & 1u;
+						b.eS[pos] = isS;
+						if(isS) b.pS_ent[s_above(r)] = pos;
+					}
 				}
 			}
 			T += s_cnt;
@@ -964,19 +1008,94 @@ struct FoldTail {
 
 template <class Tail>
 __device__ __forceinline__ void tail_unit(const Tail &t, const TreeBufs &b, int n, int u, int ua, int ub, int r,
-                                          double q, int j, int e, int T) {
+                                          double q, int j, int e, int T, bool sent = false) {
 	(void) e;
 	(void) T;
+	(void) sent;
 	if((threadIdx.x & 63) == 0) t.unit(b, n, u, ua, ub, r, q, j);
 }
 
-// all lanes of the wave, with the wave's (q, j) of unit u of entry e
+// the scan's S phase is complete (every S entry folded): the bound table, by
+// one wave.  Row pS_row[t] leaves minQpair's running min at most
+// max(fresh, Q) whether or not the reference rescans it (a rescanned row
+// lowers it to <= fresh, a skipped one had it <= Q), so below S row t the
+// running min is at most pS_bnd[t] = min(m0, min over S rows t' <= t of
+// max(fresh_t', Q_t')); published with sready = n
+__device__ __forceinline__ void s_table(const TreeBufs &b, int n) {
+	const int lane = threadIdx.x & 63, nS = b.ctl->pS;
+	const double m0 = b.ctl->m0;
+	double v[2];
+#pragma unroll
+	for(int h = 0; h < 2; ++h) {
+		const int t = lane + 64 * h;
+		v[h] = DBL_MAX;
+		if(t < nS) {
+			const double f = __hip_atomic_load(b.rf + b.pS_ent[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			const double qt = b.pS_q[t];
+			v[h] = f > qt ? f : qt;
+		}
+	}
+	double x0 = wave_incl_min(v[0]);
+	x0 = x0 < m0 ? x0 : m0;
+	const double c = readlane_d(x0, 63);
+	double x1 = wave_incl_min(v[1]);
+	x1 = x1 < c ? x1 : c;
+	if(lane < nS) __hip_atomic_store(b.pS_bnd + lane, x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if(lane + 64 < nS) __hip_atomic_store(b.pS_bnd + lane + 64, x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if(lane == 0) {
+		__hip_atomic_store(&b.ctl->scnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_store(&b.ctl->sready, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+// The S bound table in a wave's registers (lanes t and t + 64), and the
+// bound below row r: the entry at the number of S rows above r
+struct SBound {
+	int ra, rb;
+	double ba, bb, m0;
+	int nS;
+	bool ok;
+	// waits (bounded) for the S phase of this join; false: no pruning
+	__device__ __forceinline__ bool load(const TreeBufs &b, int n) {
+		const int lane = threadIdx.x & 63;
+		nS = b.ctl->pS;
+		m0 = b.ctl->m0;
+		ok = false;
+		if(nS <= 0) return false;
+		if(lane == 0) {
+			for(int spin = 0; spin < (1 << 18); ++spin) {
+				if(__hip_atomic_load(&b.ctl->sready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) n) {
+					ok = true;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(2);
+			}
+		}
+		ok = __shfl(ok, 0);
+		if(!ok) return false;   // never expected: the units then run unpruned (still exact)
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		ra = lane < nS ? b.pS_row[lane] : -1;
+		rb = lane + 64 < nS ? b.pS_row[lane + 64] : -1;
+		ba = lane < nS ? __hip_atomic_load(b.pS_bnd + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : m0;
+		bb = lane + 64 < nS ? __hip_atomic_load(b.pS_bnd + lane + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : m0;
+		return true;
+	}
+	__device__ __forceinline__ double at(int r) const {
+		const int t = __popcll(__ballot(ra > r)) + __popcll(__ballot(rb > r));
+		const double xa = __shfl(ba, t - 1 < 63 ? (t - 1 < 0 ? 0 : t - 1) : 63);
+		const double xb = __shfl(bb, t - 65 < 0 ? 0 : t - 65);
+		return t == 0 ? m0 : t <= 64 ? xa : xb;
+	}
+};
+
+// all lanes of the wave, with the wave's (q, j) of unit u of entry e; sent:
+// entry e is an S row of the scan's S phase
 __device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, int n, int u, int ua, int ub, int r,
-                                          double q, int j, int e, int T) {
-	(void) n;
+                                          double q, int j, int e, int T, bool sent = false) {
 	(void) r;
 	const int lane = threadIdx.x & 63;
-	int chunk_done = 0;
+	int chunk_done = 0, s_done = 0;
 	if(lane == 0) {
 		bool last = true;
 		if(ub - ua > 1) {
@@ -1017,7 +1136,16 @@ __device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, i
 				chunk_done = 1;
 				__hip_atomic_store(b.ccnt + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
+			if(sent) {
+				const unsigned sseen = __hip_atomic_fetch_add(&b.ctl->scnt, 1u, __ATOMIC_RELAXED,
+				                                              __HIP_MEMORY_SCOPE_AGENT);
+				s_done = (int) sseen == b.ctl->pS - 1;
+			}
 		}
+	}
+	if(__shfl(s_done, 0)) {
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		s_table(b, n);
 	}
 	if(!__shfl(chunk_done, 0)) return;
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1163,7 +1291,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // current ones are compared (half UV, two register sets), bit 2 loads sD
 // 16 bytes at a time where the unit's aligned start is even (sD + ca 16-byte
 // aligned; uniform per unit), bit 3 doubles the loads in flight per lane.
-template <int ET, class Rows, class Tail = NoTail, int MODE = 0>
+template <int ET, class Rows, class Tail = NoTail, int MODE = 0, bool PRUNE = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
@@ -1187,12 +1315,28 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	}
 	__syncthreads();
 	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
-	for(int u = gw; u < nunits; u += nw) {
-		const int e = u / umax, ua = e * umax;
-		const int r = lds ? erow[e] : b.crow[e];
-		const int c0 = (u - ua) * seg;
-		if(c0 >= r || !rows.owns(r)) continue;   // wave-uniform
+	// PRUNE (band mode): the S entries' units first (the lowest waves), their
+	// exact fresh minima then bound every other entry (SBound), and an entry
+	// whose stale Q is not below the bound at its row is one minQpair skips
+	// (dnj.c:78): its units load nothing and leave DBL_MAX, which the replay
+	// neither accepts nor lets into the running min
+	const int nSp = PRUNE ? ctl->pS : 0;
+	__shared__ int s_uo[DNJ_B + 1];
+	int su = 0;
+	if(PRUNE && nSp) {
+		for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
+		__syncthreads();
+		su = s_uo[nSp];
+	}
+	long long pruned = 0;
+	auto unit = [&](int u, int e, int r, int c0, bool skip, bool sent) {
+		const int ua = e * umax;
 		const int c1 = c0 + seg < r ? c0 + seg : r;
+		if(skip) {
+			pruned += c1 - c0;
+			tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, DBL_MAX, 0, e, Tn, sent);
+			return;
+		}
 		const double sDr = b.sD[r];
 		const long long ro = rows.row(r);
 		const T *row = D + ro;
@@ -1273,8 +1417,37 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn);
+		tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn, sent);
+	};
+	for(int v = gw; v < su; v += nw) {   // the S phase
+		int lo = 0, hi = nSp;   // the S row t with s_uo[t] <= v < s_uo[t + 1]
+		while(hi - lo > 1) {
+			const int mid = (lo + hi) >> 1;
+			if(s_uo[mid] <= v) lo = mid; else hi = mid;
+		}
+		const int e = b.pS_ent[lo];
+		unit(e * umax + v - s_uo[lo], e, b.pS_row[lo], (v - s_uo[lo]) * seg, false, true);
 	}
+	SBound sb;
+	bool have_sb = false;
+	for(int u = gw; u < nunits; u += nw) {
+		const int e = u / umax, ua = e * umax;
+		const int r = lds ? erow[e] : b.crow[e];
+		const int c0 = (u - ua) * seg;
+		if(c0 >= r || !rows.owns(r)) continue;   // wave-uniform
+		bool skip = false;
+		if(PRUNE && nSp) {
+			if(b.eS[e]) continue;   // ran in the S phase
+			if(!have_sb) {
+				sb.load(b, n);
+				have_sb = true;
+			}
+			skip = sb.ok && !(b.cbnd[e] < sb.at(r));
+		}
+		unit(u, e, r, c0, skip, false);
+	}
+	if(PRUNE && pruned && lane == 0)   // (uniform: every lane counted the same units)
+		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
 }
 
 // Row groups (the default rescan past 16384 taxa for every element type but
@@ -1286,11 +1459,12 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 // row), each row's (q, j) reduced and stored as its own unit partial, so the
 // fold and the join read the layout of k_dnj_scan_v.  UC columns per lane per
 // step.
-template <int ET, int G, int UC, bool FOLD = false>
+template <int ET, int G, int UC, bool FOLD = false, bool PRUNE = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int seg) {
 	typedef typename Elem<ET>::T T;
 	__shared__ int erow[REPLAY_CAP];
+	__shared__ int s_uo[DNJ_B + 1];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int r0 = b.crow[tid];
@@ -1304,20 +1478,99 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 		if(tid < Tn) erow[tid] = r0;
 		for(int e = TB + tid; e < Tn; e += TB) erow[e] = b.crow[e];
 	}
+	// PRUNE (band mode, with FOLD): the S entries' units first, one row per
+	// wave, then the groups, whose entries below the S bound table's value at
+	// their row (k_dnj_scan_v) load nothing and leave DBL_MAX
+	const int nSp = PRUNE ? ctl->pS : 0;
+	int su = 0;
+	if(PRUNE && nSp)
+		for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
 	__syncthreads();
+	if(PRUNE && nSp) su = s_uo[nSp];
 	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	long long pruned = 0;
+	for(int v = gw; v < su; v += nw) {   // the S phase (PRUNE only)
+		int lo = 0, hi = nSp;
+		while(hi - lo > 1) {
+			const int mid = (lo + hi) >> 1;
+			if(s_uo[mid] <= v) lo = mid; else hi = mid;
+		}
+		const int e = b.pS_ent[lo], r = b.pS_row[lo], s = v - s_uo[lo], c0 = s * seg;
+		const int c1 = c0 + seg < r ? c0 + seg : r;
+		const double sDr = b.sD[r];
+		const T *row = D + tri(r);
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int base = c0; base < c1; base += 64 * UC) {
+			double sk[UC];
+			T vv[UC];
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const int cc = c < c1 ? c : c1 - 1;
+				sk[m] = b.sD[cc];
+				vv[m] = row[cc];
+			}
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const double d = Elem<ET>::get(vv[m], bs);
+				const double x = qcrit(n, n, d, sDr, sk[m]);
+				const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+				q = take ? x : q;
+				idx = take ? c : idx;
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		tail_unit(FoldTail(), b, n, e * umax + s, e * umax, e * umax + dcdiv(r, seg), r, q, idx, e, Tn, true);
+	}
+	SBound sb;
+	bool have_sb = false;
 	for(int u = gw; u < nunits; u += nw) {
 		const int g = u / umax, s = u - g * umax, c0 = s * seg;
 		int r[G], c1[G];
-		bool act[G];
+		bool act[G], skip[G];
 		int cmax = c0;
 #pragma unroll
 		for(int k = 0; k < G; ++k) {
 			const int e = g * G + k;
 			r[k] = e < Tn ? (lds ? erow[e] : b.crow[e]) : 0;
 			act[k] = e < Tn && c0 < r[k];
+			skip[k] = false;
+			if(PRUNE && nSp && act[k] && b.eS[e]) act[k] = false;   // ran in the S phase: no arrival here
+		}
+		if(PRUNE && nSp) {
+			bool any = false;
+#pragma unroll
+			for(int k = 0; k < G; ++k) any = any || act[k];
+			if(any && !have_sb) {   // uniform
+				sb.load(b, n);
+				have_sb = true;
+			}
+			if(any && sb.ok) {
+#pragma unroll
+				for(int k = 0; k < G; ++k) {
+					if(act[k] && !(b.cbnd[g * G + k] < sb.at(r[k]))) {   // uniform
+						skip[k] = true;
+						act[k] = false;
+					}
+				}
+			}
+		}
+#pragma unroll
+		for(int k = 0; k < G; ++k) {
 			c1[k] = act[k] ? (c0 + seg < r[k] ? c0 + seg : r[k]) : c0;
 			cmax = c1[k] > cmax ? c1[k] : cmax;
+		}
+		if(PRUNE) {
+#pragma unroll
+			for(int k = 0; k < G; ++k) {
+				if(!skip[k]) continue;   // uniform
+				const int e = g * G + k;
+				pruned += (c0 + seg < r[k] ? c0 + seg : r[k]) - c0;
+				tail_unit(FoldTail(), b, n, e * umax + s, e * umax, e * umax + dcdiv(r[k], seg), r[k], DBL_MAX, 0, e,
+				          Tn);
+			}
 		}
 		if(cmax == c0) continue;   // wave-uniform
 		double sDr[G], q[G];
@@ -1368,6 +1621,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 			}
 		}
 	}
+	if(PRUNE && pruned && lane == 0)
+		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
 }
 
 // ------------------------------------------------------------------ DNJ fold

@@ -40,6 +40,10 @@ struct TreeCtl {
 	long long ref_rows, ref_cells;  // rows / cells minQpair's own rule rescans (dnj.c:78: Q[r] < running min)
 	int hj, hi, hjb, hib;  // HNJ: rows j / i of the last join whose minima are still in partials (-1: none)
 	int rtotal;          // sharded DNJ: replay entries whose accept flags k_shd_join applies
+	int pS;              // S rows whose exact fresh minima prune the scan (0: no pruning this join)
+	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
+	unsigned sready;     // = n once the scan's S bound table is written (tagged: no reset)
+	long long cells_pruned;  // listed cells the scan skipped under the S bound table
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
 };
 
@@ -88,6 +92,9 @@ struct TreeBufs {
 	int *chr, *chj, *chb;       // the row and partner of its first entry reaching it, and whether any entry is "bad"
 	unsigned *ecnt, *ccnt;      // the scan's fold at its last arrivals: units arrived per entry / entries per
 	                            // 64-entry chunk (zero between joins: each last arriver resets its counter)
+	int *pS_row, *pS_ent, *pS_uo;   // S for the scan's pruning: rows (descending), entry index, unit prefix
+	double *pS_q, *pS_bnd;          // their Q (stale bounds), and the bound table the scan builds
+	unsigned char *eS;              // per entry: 1 for an S row
 	int maxu;
 };
 

@@ -1595,6 +1595,8 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	const size_t nch = ncand / 64 + 2;   // k_dnj_fold's chunk summaries
 	size_t o_hg = take(nch * 8), o_hr = take(nch * 4), o_hj = take(nch * 4), o_hb = take(nch * 4);
 	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
+	size_t o_pr = take(DNJ_B * 4), o_pe = take(DNJ_B * 4), o_pu = take((DNJ_B + 1) * 4), o_pq = take(DNJ_B * 8);
+	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent);
 	if(!m) return sz;
 	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
@@ -1648,6 +1650,12 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.chb = (int *) (m + o_hb);
 	b.ecnt = (unsigned *) (m + o_ec);
 	b.ccnt = (unsigned *) (m + o_cc);
+	b.pS_row = (int *) (m + o_pr);
+	b.pS_ent = (int *) (m + o_pe);
+	b.pS_uo = (int *) (m + o_pu);
+	b.pS_q = (double *) (m + o_pq);
+	b.pS_bnd = (double *) (m + o_pb);
+	b.eS = (unsigned char *) (m + o_eS);
 	b.maxu = (int) maxu;
 	return sz;
 }
@@ -1666,11 +1674,21 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 
 // DNJ: k_dnj_plan of the join at matrix size n (first: the run's first join,
 // whose candidate k_dnj_prep or a resumed state left in ctl)
+// the scan rescans S first and prunes the other entries under S's exact
+// fresh minima: band mode, the wave scans with the fold at their last
+// arrivals, no missing entries
+static bool dnj_prune(int n, int et, bool gen) {
+	const int sm = g_grid.scan_mode(n, et);
+	return g_grid.scan_prune && !gen && g_grid.bands(n) && g_grid.prefold(n) && g_grid.scan_fold &&
+	       ((sm >= 4 && sm < 20) || (sm >= 20 && sm <= 23));
+}
+
 template <int ET, bool GEN>
 static void enqueue_plan(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first) {
 	const int seg = g_grid.seg(n);
 	const unsigned gp = g_grid.plan_blocks(n);
-	if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags());
+	const bool prune = dnj_prune(n, ET, GEN);
+	if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags(prune));
 	else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 }
 
@@ -1692,8 +1710,14 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		// the wave-per-unit scans fold the entries at their last arrivals
 		// (FoldTail) instead of a k_dnj_fold pass
 		const bool tfold = prefold && g_grid.scan_fold && sm >= 1;
+		const bool prune = dnj_prune(n, ET, GEN);
 		if(sm >= 20 && sm <= 23 && !GEN) {
-			if(tfold) {
+			if(prune) {
+				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 21) k_dnj_scan_g<ET, 8, 4, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 22) k_dnj_scan_g<ET, 4, 4, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+				else k_dnj_scan_g<ET, 2, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
+			} else if(tfold) {
 				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 				else if(sm == 21) k_dnj_scan_g<ET, 8, 4, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 				else if(sm == 22) k_dnj_scan_g<ET, 4, 4, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
@@ -1705,7 +1729,14 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 				else k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 			}
 		} else if(sm >= 4 && !GEN) {
-			if(tfold) {
+			if(prune) {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, FoldTail, M, true><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(5)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows, FoldTail, 0, true><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			} else if(tfold) {
 				switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, FoldTail, M><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
 					SV_(1) SV_(5)
@@ -1986,7 +2017,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	}
 	if(stats) {
 		stats[0] = h.rows;
-		stats[1] = h.cells;
+		stats[1] = h.cells - h.cells_pruned;   // cells the scans loaded (listed, less the S-pruned ones)
 		stats[2] = launches;
 		stats[3] = (int64_t) (ms * 1000.0);
 		if(a->profile) {
@@ -1995,7 +2026,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 				stats[5 + 2 * c] = kt.ns[c];
 			}
 			stats[4 + 2 * CCG_NKSTAT] = h.cells_top;
-			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest;
+			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest - h.cells_pruned;
 			stats[6 + 2 * CCG_NKSTAT] = h.serial_sums;
 			stats[7 + 2 * CCG_NKSTAT] = h.chain_sums;
 			stats[8 + 2 * CCG_NKSTAT] = 0;

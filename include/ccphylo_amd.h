@@ -167,8 +167,8 @@ typedef struct {
 } ccg_tree_args;
 
 /* stats layout (ccg_tree / ccg_tree_dev / ccg_tree_shard*, 12 + 2*CCG_NKSTAT
- * entries when profile = 1, else 4): [0] rows rescanned, [1] cells
- * rescanned, [2] kernel launches, [3] device time (us); then for kernel class
+ * entries when profile = 1, else 4): [0] rows listed for rescans, [1] cells
+ * rescanned (loaded; the single engine's scan may prune listed rows), [2] kernel launches, [3] device time (us); then for kernel class
  * c: [4+2c] launches, [5+2c] summed duration in ns; then [4+2*CCG_NKSTAT]
  * cells rescanned by CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST;
  * [6+2*CCG_NKSTAT] exact row sums that needed the serial order,

@@ -677,3 +677,41 @@ def test_dnj_scan_tail_fold(dev, monkeypatch, kind, n, et, mode):
         got, fn, fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True)
         assert (fn, fd) == (rfn, rfd), fold
         assert len(got) == len(ref) and (got == ref).all(), fold
+
+
+@pytest.mark.parametrize("kind,n,et,mode,bands", [("clade", 3000, 8, "9", 64), ("euc", 2500, 8, "9", 64),
+                                                  ("clade", 2600, 4, "20", 64), ("euc", 2200, 4, "20", 32),
+                                                  ("snp", 2000, 2, "20", 64), ("clade", 2400, 8, "4", 120),
+                                                  ("clade", 2000, 1, "21", 64)])
+def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
+    """Band mode's in-scan pruning: the scan rescans S (top + band rows) first,
+    builds the bound table from their exact fresh minima (max(fresh, Q),
+    prefix-min from m0), and an entry whose stale Q is not below it at its row
+    (so minQpair skips it, dnj.c:78) loads nothing.  At small n through
+    CCG_S_SPLIT_N / CCG_PREFOLD_N: joins and the reference-rule counters equal
+    the serial oracle's, CCG_SCAN_PRUNE=0 gives the same joins, and the
+    pruned run loads no more cells."""
+    from oracle import pyoracle
+    from ccphylo_amd import native
+    K = native.NKSTAT
+    monkeypatch.setenv("CCG_SCAN_WAVE", mode)
+    monkeypatch.setenv("CCG_PREFOLD_N", "0")
+    monkeypatch.setenv("CCG_SEG_MUL", "1")
+    monkeypatch.setenv("CCG_S_SPLIT_N", "100")
+    monkeypatch.setenv("CCG_S_BANDS", str(bands))
+    D = {"euc": lambda: _euclid(n, n + 3), "snp": lambda: _snp(n, n + 1), "clade": lambda: _clade_ltd(n, n + 4)}[kind]()
+    bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 0.1}[et]
+    if et == 4:
+        D = D.astype(np.float32)
+    elif et in (2, 1):
+        D = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
+    ref, rfn, rfd, rst = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1, stats=True)
+    cells = {}
+    for prune in ("1", "0"):
+        monkeypatch.setenv("CCG_SCAN_PRUNE", prune)
+        got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
+        assert (fn, fd) == (rfn, rfd), prune
+        assert len(got) == len(ref) and (got == ref).all(), prune
+        assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), prune
+        cells[prune] = st[1]
+    assert int(rst[1]) <= cells["1"] <= cells["0"]
