@@ -608,10 +608,10 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			}
 			if(prune && bid == 0) {
 				// S in scan order (top rows, then band rows: descending), the
-				// top part's entries are the list's head; its rescan units
-				// prefixed for the scan's S phase
+				// top part's entries are the list's head; its SEG-cell rescan
+				// units prefixed for the scan's S phase
 				const int ta = lane, tb = lane + 64;
-				const int ua = ta < nS ? (int) dcdiv(sS[ta], seg) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], seg) : 0;
+				const int ua = ta < nS ? (int) dcdiv(sS[ta], SEG) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], SEG) : 0;
 				int tota, totb;
 				const int pa = wave_excl_scan(ua, &tota), pb = wave_excl_scan(ub, &totb);
 				if(ta < nS) {
@@ -1089,18 +1089,18 @@ struct SBound {
 	}
 };
 
-// all lanes of the wave, with the wave's (q, j) of unit u of entry e; sent:
-// entry e is an S row of the scan's S phase
-__device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, int n, int u, int ua, int ub, int r,
-                                          double q, int j, int e, int T, bool sent = false) {
-	(void) r;
+// all lanes of the wave, with the wave's (q, j) of unit u of entry e, whose
+// partials are pq / pj [ua, ub); sent: entry e is an S row of the scan's S
+// phase (its partials then live in uq / uj, indexed by the S unit)
+__device__ __forceinline__ void fold_arrive(const TreeBufs &b, int n, double *pq, int *pj, int u, int ua, int ub,
+                                            double q, int j, int e, int T, bool sent) {
 	const int lane = threadIdx.x & 63;
 	int chunk_done = 0, s_done = 0;
 	if(lane == 0) {
 		bool last = true;
 		if(ub - ua > 1) {
-			__hip_atomic_store(b.cq + u, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			__hip_atomic_store(b.cj + u, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(pq + u, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(pj + u, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 			const unsigned seen = __hip_atomic_fetch_add(b.ecnt + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			last = (int) seen == ub - ua - 1;
@@ -1112,8 +1112,8 @@ __device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, i
 #pragma unroll
 					for(int m = 0; m < 4; ++m) {
 						const int x = x0 + m < ub ? x0 + m : ub - 1;
-						oq[m] = __hip_atomic_load(b.cq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-						oi[m] = __hip_atomic_load(b.cj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						oq[m] = __hip_atomic_load(pq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						oi[m] = __hip_atomic_load(pj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					}
 #pragma unroll
 					for(int m = 0; m < 4; ++m) {
@@ -1167,6 +1167,12 @@ __device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, i
 		b.chj[c] = fjj;
 		b.chb[c] = bm != 0ull;
 	}
+}
+
+__device__ __forceinline__ void tail_unit(const FoldTail &, const TreeBufs &b, int n, int u, int ua, int ub, int r,
+                                          double q, int j, int e, int T, bool sent = false) {
+	(void) r;
+	fold_arrive(b, n, b.cq, b.cj, u, ua, ub, q, j, e, T, sent);
 }
 
 template <int ET, bool GEN, class Rows, class Tail = NoTail>
@@ -1307,7 +1313,10 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	tail.begin(b, n);
 	if(Tn == 0) return;
 	const int umax = dnj_umax(n, seg), nunits = Tn * umax;
-	if((int) blockIdx.x * (TB / 64) >= nunits) return;
+	const int nSp = PRUNE ? ctl->pS : 0;
+	// (the S phase's SEG-cell units may outnumber the entries' units)
+	const int su0 = PRUNE && nSp ? b.pS_uo[nSp] : 0;
+	if((int) blockIdx.x * (TB / 64) >= (nunits > su0 ? nunits : su0)) return;
 	const bool lds = Tn <= REPLAY_CAP;
 	if(lds) {
 		if(tid < Tn) erow[tid] = r0;
@@ -1320,7 +1329,6 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	// whose stale Q is not below the bound at its row is one minQpair skips
 	// (dnj.c:78): its units load nothing and leave DBL_MAX, which the replay
 	// neither accepts nor lets into the running min
-	const int nSp = PRUNE ? ctl->pS : 0;
 	__shared__ int s_uo[DNJ_B + 1];
 	int su = 0;
 	if(PRUNE && nSp) {
@@ -1329,12 +1337,13 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		su = s_uo[nSp];
 	}
 	long long pruned = 0;
-	auto unit = [&](int u, int e, int r, int c0, bool skip, bool sent) {
+	// one unit: columns [c0, c1) of entry e's row r; S-phase units (sent) are
+	// SEG cells with their partials in uq / uj at the S unit index
+	auto unit = [&](int u, int e, int r, int c0, int c1, bool skip, bool sent, int sua, int sub) {
 		const int ua = e * umax;
-		const int c1 = c0 + seg < r ? c0 + seg : r;
 		if(skip) {
 			pruned += c1 - c0;
-			tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, DBL_MAX, 0, e, Tn, sent);
+			tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, DBL_MAX, 0, e, Tn);
 			return;
 		}
 		const double sDr = b.sD[r];
@@ -1417,16 +1426,17 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn, sent);
+		if(PRUNE && sent) fold_arrive(b, n, b.uq, b.uj, u, sua, sub, q, idx, e, Tn, true);
+		else tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn);
 	};
-	for(int v = gw; v < su; v += nw) {   // the S phase
+	for(int v = gw; v < su; v += nw) {   // the S phase: SEG-cell units (short, so the phase is)
 		int lo = 0, hi = nSp;   // the S row t with s_uo[t] <= v < s_uo[t + 1]
 		while(hi - lo > 1) {
 			const int mid = (lo + hi) >> 1;
 			if(s_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int e = b.pS_ent[lo];
-		unit(e * umax + v - s_uo[lo], e, b.pS_row[lo], (v - s_uo[lo]) * seg, false, true);
+		const int r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;
+		unit(v, b.pS_ent[lo], r, c0, c0 + SEG < r ? c0 + SEG : r, false, true, s_uo[lo], s_uo[lo + 1]);
 	}
 	SBound sb;
 	bool have_sb = false;
@@ -1444,7 +1454,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 			skip = sb.ok && !(b.cbnd[e] < sb.at(r));
 		}
-		unit(u, e, r, c0, skip, false);
+		unit(u, e, r, c0, c0 + seg < r ? c0 + seg : r, skip, false, 0, 0);
 	}
 	if(PRUNE && pruned && lane == 0)   // (uniform: every lane counted the same units)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
@@ -1472,7 +1482,10 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 	if(done) return;
 	if(Tn == 0) return;
 	const int umax = dnj_umax(n, seg), ngroups = (Tn + G - 1) / G, nunits = ngroups * umax;
-	if((int) blockIdx.x * (TB / 64) >= nunits) return;
+	const int nSp = PRUNE ? ctl->pS : 0;
+	// (the S phase may hold more units than the groups: S rows one per wave)
+	const int su0 = PRUNE && nSp ? b.pS_uo[nSp] : 0;
+	if((int) blockIdx.x * (TB / 64) >= (nunits > su0 ? nunits : su0)) return;
 	const bool lds = Tn <= REPLAY_CAP;
 	if(lds) {
 		if(tid < Tn) erow[tid] = r0;
@@ -1481,7 +1494,6 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 	// PRUNE (band mode, with FOLD): the S entries' units first, one row per
 	// wave, then the groups, whose entries below the S bound table's value at
 	// their row (k_dnj_scan_v) load nothing and leave DBL_MAX
-	const int nSp = PRUNE ? ctl->pS : 0;
 	int su = 0;
 	if(PRUNE && nSp)
 		for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
@@ -1495,8 +1507,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 			const int mid = (lo + hi) >> 1;
 			if(s_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int e = b.pS_ent[lo], r = b.pS_row[lo], s = v - s_uo[lo], c0 = s * seg;
-		const int c1 = c0 + seg < r ? c0 + seg : r;
+		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;   // SEG-cell S units
+		const int c1 = c0 + SEG < r ? c0 + SEG : r;
 		const double sDr = b.sD[r];
 		const T *row = D + tri(r);
 		double q = DBL_MAX;
@@ -1522,7 +1534,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		tail_unit(FoldTail(), b, n, e * umax + s, e * umax, e * umax + dcdiv(r, seg), r, q, idx, e, Tn, true);
+		fold_arrive(b, n, b.uq, b.uj, v, s_uo[lo], s_uo[lo + 1], q, idx, e, Tn, true);
 	}
 	SBound sb;
 	bool have_sb = false;
