@@ -17,7 +17,8 @@ struct DenseRows {
 
 #define DNJ_B 128        // capacity of S, the candidate rows rescanned speculatively
 #define DNJ_BANDS 64     // S: the top rows with Q < m0, then the min-Q row of each
-                         // of at most this many bands below them (DnjGrid::top/bands)
+                         // of this many bands below them (DnjGrid::top/bands)
+#define DNJ_BANDS_MAX 128  // CCG_S_BANDS up to this (two bands per lane of k_dnj_plan's wave 0)
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
 #define SEL_STEPS 8      // steps of the S scan at most (then the listing takes over)
@@ -111,7 +112,7 @@ struct DnjGrid {
 	}
 	int bands(int n) const {
 		int b = s_bands >= 0 ? s_bands : n > s_split_n ? DNJ_BANDS : 0;
-		b = b > DNJ_BANDS ? DNJ_BANDS : b;
+		b = b > DNJ_BANDS_MAX ? DNJ_BANDS_MAX : b;
 		return top(n) + b > DNJ_B ? DNJ_B - top(n) : b;
 	}
 	unsigned scan(int n) const {
@@ -430,13 +431,16 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			}
 		}
 		// band candidates: lane l holds the min-Q row of the requeue blocks
-		// [l G / kbands, (l + 1) G / kbands) with its partner, and loads that
-		// partner's cell right away
-		double bcq = DBL_MAX, bd = -1.0, bsr = 0.0, bsp = 0.0;
-		int bcr = 0, bcp = 0, bnr = n, bnp = n;
-		if(BANDS && !first && lane < kbands) {
+		// [k G / kbands, (k + 1) G / kbands) of bands k = l and l + 64 (h = 0, 1)
+		// with its partner, and loads that partner's cell right away
+		double bcq[2] = {DBL_MAX, DBL_MAX}, bd[2] = {-1.0, -1.0}, bsr[2] = {0.0, 0.0}, bsp[2] = {0.0, 0.0};
+		int bcr[2] = {0, 0}, bcp[2] = {0, 0}, bnr[2] = {n, n}, bnp[2] = {n, n};
+#pragma unroll
+		for(int h = 0; h < 2; ++h) {
+			const int k = lane + 64 * h;
+			if(!(BANDS && !first && k < kbands)) continue;
 			const int G = (int) cdiv(n + 1, TB);
-			const int ga = lane * G / kbands, gz = (lane + 1) * G / kbands;
+			const int ga = k * G / kbands, gz = (k + 1) * G / kbands;
 			for(int g0 = ga; g0 < gz; g0 += 4) {
 				double oq[4];
 				int orr[4], op[4];
@@ -449,21 +453,21 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				}
 #pragma unroll
 				for(int m = 0; m < 4; ++m) {
-					if(g0 + m < gz && qarg_better(oq[m], orr[m], bcq, bcr)) {
-						bcq = oq[m];
-						bcr = orr[m];
-						bcp = op[m];
+					if(g0 + m < gz && qarg_better(oq[m], orr[m], bcq[h], bcr[h])) {
+						bcq[h] = oq[m];
+						bcr[h] = orr[m];
+						bcp[h] = op[m];
 					}
 				}
 			}
-			if(bcr >= 1 && rows.owns(bcr)) {
-				bcp = bcp >= 0 && bcp < bcr ? bcp : 0;
-				bd = Elem<ET>::get(D[rows.row(bcr) + bcp], bs);
-				bsr = b.sD[bcr];
-				bsp = b.sD[bcp];
+			if(bcr[h] >= 1 && rows.owns(bcr[h])) {
+				bcp[h] = bcp[h] >= 0 && bcp[h] < bcr[h] ? bcp[h] : 0;
+				bd[h] = Elem<ET>::get(D[rows.row(bcr[h]) + bcp[h]], bs);
+				bsr[h] = b.sD[bcr[h]];
+				bsp[h] = b.sD[bcp[h]];
 				if(GEN) {
-					bnr = b.N[bcr];
-					bnp = b.N[bcp];
+					bnr[h] = b.N[bcr[h]];
+					bnp[h] = b.N[bcp[h]];
 				}
 			}
 		}
@@ -554,17 +558,24 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// part, with the Q criterion at its partner cell (rows j and i of the
 			// previous join are never band candidates)
 			if(BANDS && smin > 1 && kbands) {
-				const bool f = bcr >= 1 && bcr < smin && bcq < m0;
-				const unsigned long long bm = __ballot(f);
-				const int pos = ntop + __popcll(lane == 63 ? 0ull : bm >> (lane + 1));
-				if(f) {
-					const bool pm = bcp == isub;
-					sS[pos] = bcr;
-					sQS[pos] = bcq;
-					sQP[pos] = 0 <= bd ? qcrit(GEN ? bnr : n, GEN ? (pm ? Nm : bnp) : n, bd, bsr, pm ? sDm : bsp)
-					                   : DBL_MAX;
+				// descending rows: bands 127..64 (h = 1), then 63..0
+				int base_pos = ntop;
+#pragma unroll
+				for(int h = 1; h >= 0; --h) {
+					const bool f = bcr[h] >= 1 && bcr[h] < smin && bcq[h] < m0;
+					const unsigned long long bm = __ballot(f);
+					const int pos = base_pos + __popcll(lane == 63 ? 0ull : bm >> (lane + 1));
+					if(f) {
+						const bool pm = bcp[h] == isub;
+						sS[pos] = bcr[h];
+						sQS[pos] = bcq[h];
+						sQP[pos] = 0 <= bd[h] ? qcrit(GEN ? bnr[h] : n, GEN ? (pm ? Nm : bnp[h]) : n, bd[h], bsr[h],
+						                              pm ? sDm : bsp[h])
+						                      : DBL_MAX;
+					}
+					base_pos += __popcll(bm);
 				}
-				nS = ntop + __popcll(bm);
+				nS = base_pos;
 			}
 			wave_sync();
 			
