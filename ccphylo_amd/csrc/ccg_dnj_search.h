@@ -41,10 +41,13 @@ struct DnjGrid {
 	int scan_fold = 1; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=0)
 	int scan_prune = 1; // band mode: the scan rescans S first and prunes the other entries under its exact
 	                    // fresh minima (CCG_SCAN_PRUNE=0: off)
+	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
+	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {
 		if(const char *e = getenv("CCG_JOIN_PF")) join_pf = atoi(e);
 		if(const char *e = getenv("CCG_SCAN_FOLD")) scan_fold = atoi(e);
 		if(const char *e = getenv("CCG_SCAN_PRUNE")) scan_prune = atoi(e);
+		if(const char *e = getenv("CCG_SCAN_VBLK")) scan_vblk = atoi(e);
 		if(const char *e = getenv("CCG_S_TOP")) s_top = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_S_BANDS")) s_bands = atoi(e) >= 0 ? atoi(e) : -1;
 		if(const char *e = getenv("CCG_S_SPLIT_N")) s_split_n = atoi(e);
@@ -1053,6 +1056,22 @@ __device__ __forceinline__ void s_table(const TreeBufs &b, int n) {
 	x1 = x1 < c ? x1 : c;
 	if(lane < nS) __hip_atomic_store(b.pS_bnd + lane, x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if(lane + 64 < nS) __hip_atomic_store(b.pS_bnd + lane + 64, x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	// the requeue's V block minima (when they serve this join): suffix minima
+	// over the blocks, vsuf[g] = min over rows >= 256 g (rows of the
+	// requeue at size n + 1; row n is gone, its V never counted)
+	if(b.ctl->vtag == n) {
+		const int G = (int) cdiv(n + 1, TB);
+		double carry = DBL_MAX;
+		for(int g1 = ((G - 1) / 64) * 64; g1 >= 0; g1 -= 64) {   // 64 blocks per step, from the top
+			const int g = g1 + 63 - lane;   // lane 0 the highest block of the step
+			double x = g < G ? b.bmv[g] : DBL_MAX;
+			x = wave_incl_min(x);   // lanes 0..l: blocks g1 + 63 - l .. g1 + 63
+			x = x < carry ? x : carry;
+			if(g < G) __hip_atomic_store(b.vsuf + g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			carry = readlane_d(x, 63);
+		}
+		if(lane == 0) __hip_atomic_store(b.vsuf + G, DBL_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	if(lane == 0) {
 		__hip_atomic_store(&b.ctl->scnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1065,8 +1084,9 @@ __device__ __forceinline__ void s_table(const TreeBufs &b, int n) {
 struct SBound {
 	int ra, rb;
 	double ba, bb, m0;
-	int nS;
-	bool ok;
+	int nS, G;
+	bool ok, vb;
+	const double *vsuf;
 	// waits (bounded) for the S phase of this join; false: no pruning
 	__device__ __forceinline__ bool load(const TreeBufs &b, int n) {
 		const int lane = threadIdx.x & 63;
@@ -1086,6 +1106,9 @@ struct SBound {
 		ok = __shfl(ok, 0);
 		if(!ok) return false;   // never expected: the units then run unpruned (still exact)
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		vb = b.ctl->vtag == n;
+		G = (int) cdiv(n + 1, TB);
+		vsuf = b.vsuf;
 		ra = lane < nS ? b.pS_row[lane] : -1;
 		rb = lane + 64 < nS ? b.pS_row[lane + 64] : -1;
 		ba = lane < nS ? __hip_atomic_load(b.pS_bnd + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : m0;
@@ -1096,7 +1119,13 @@ struct SBound {
 		const int t = __popcll(__ballot(ra > r)) + __popcll(__ballot(rb > r));
 		const double xa = __shfl(ba, t - 1 < 63 ? (t - 1 < 0 ? 0 : t - 1) : 63);
 		const double xb = __shfl(bb, t - 65 < 0 ? 0 : t - 65);
-		return t == 0 ? m0 : t <= 64 ? xa : xb;
+		double x = t == 0 ? m0 : t <= 64 ? xa : xb;
+		if(vb) {   // every row of the blocks above r's
+			const int g = (r >> 8) + 1;
+			const double v = __hip_atomic_load(vsuf + (g < G ? g : G), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			x = v < x ? v : x;
+		}
+		return x;
 	}
 };
 

@@ -44,6 +44,7 @@ struct TreeCtl {
 	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
 	unsigned sready;     // = n once the scan's S bound table is written (tagged: no reset)
 	long long cells_pruned;  // listed cells the scan skipped under the S bound table
+	int vtag;            // VBLK: the matrix size whose join the requeue's bmv minima serve
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
 };
 
@@ -95,6 +96,8 @@ struct TreeBufs {
 	int *pS_row, *pS_ent, *pS_uo;   // S for the scan's pruning: rows (descending), entry index, unit prefix
 	double *pS_q, *pS_bnd;          // their Q (stale bounds), and the bound table the scan builds
 	unsigned char *eS;              // per entry: 1 for an S row
+	double *bmv, *vsuf;             // VBLK: per requeue block the minimum of V_k = max(q at the partner cell, Q_k),
+	                                // and the scan's suffix minima of them (bounds from every row above)
 	int maxu;
 };
 

@@ -847,11 +847,12 @@ __global__ __launch_bounds__(1024) void k_update_general(typename Elem<ET>::T *_
 // Row sum of j, then updateDNJ's Q/P part (dnj.c:618-709) and DNJ_popArrange
 // (dnj.c:817-975); the four (q, idx) reductions go to per-block partials that
 // the next k_dnj_select folds.
-template <int ET, bool BANDS>
+template <int ET, bool BANDS, bool VBLK = false>
 __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, int general, int exact_arg) {
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
 	__shared__ int si[5][TB / 64], sfp[TB / 64], sbp[TB / 64];
+	__shared__ double sfv[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
@@ -870,6 +871,15 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		pkk0 = b.P[k];
 	}
 	if(k < nn) vm = D[tri(nn) + k];   // row nn, moved to i
+	// VBLK: the cell at the row's partner and the partner's row sum, for the
+	// row's bound V_k of the next join's scan (prefetched: usually unchanged)
+	typename Elem<ET>::T vp = 0;
+	double sdp0 = 0.0;
+	if(VBLK && k >= 1 && k < n) {
+		const int p0 = pkk0 >= 0 && pkk0 < k ? pkk0 : 0;
+		vp = D[tri(k) + p0];
+		sdp0 = b.sD[p0];
+	}
 	const int Nm0 = b.N[nn];
 	const double sDm0 = b.sD[nn];
 	// column j of the joined pair, read by every thread (not through wave 0's
@@ -979,6 +989,35 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			}
 		}
 	}
+	// VBLK: V_k = max(q at the row's partner cell, Q_k) in the next join's
+	// state, a bound of minQpair's running min below row k whatever the
+	// reference does with it (a cell of row k is >= its fresh minimum); the
+	// block minimum, for the next scan's suffix bound over the rows above
+	double vk = DBL_MAX;
+	if(VBLK && k >= 1 && k < nn && k != i && k != j) {
+		const bool later = k > j;   // rows above j may have a new partner (j or the moved i)
+		const int pf = later ? fp : pkk0;
+		const double qf = later ? fq : qk0;
+		double d = -1.0, sp = 0.0;
+		if(pf == j && later) {
+			d = Elem<ET>::get(vj, bs);
+			sp = sdj;
+		} else if(pf == i && move && later) {
+			d = Elem<ET>::get(vm, bs);
+			sp = sDm;
+		} else if(pf == pkk0 && pkk0 >= 0 && pkk0 < k && pkk0 != i && pkk0 != j) {
+			d = Elem<ET>::get(vp, bs);
+			sp = sdp0;
+		}
+		if(0 <= d) {
+			const double q = qcrit(nn, nn, d, sDk, sp);
+			vk = q > qf ? q : qf;
+		}
+	}
+	if(VBLK) {
+		vk = readlane_d(wave_incl_min(vk), 63);
+		if(lane == 0) sfv[wid] = vk;
+	}
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
 	// fold); only when the next S has a band part
@@ -1038,6 +1077,12 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			b.cfq[blockIdx.x] = cq;
 			b.cfp[blockIdx.x] = cp;
 		}
+	}
+	if(VBLK && tid == 0) {
+		double v = sfv[0];
+		for(int w = 1; w < TB / 64; ++w) v = sfv[w] < v ? sfv[w] : v;
+		b.bmv[blockIdx.x] = v;
+		if(blockIdx.x == 0) ctl->vtag = nn;   // the join these minima serve
 	}
 	TS(4, 2);
 	TS_EXIT(4);
@@ -1596,7 +1641,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	size_t o_hg = take(nch * 8), o_hr = take(nch * 4), o_hj = take(nch * 4), o_hb = take(nch * 4);
 	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
 	size_t o_pr = take(DNJ_B * 4), o_pe = take(DNJ_B * 4), o_pu = take((DNJ_B + 1) * 4), o_pq = take(DNJ_B * 8);
-	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent);
+	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent), o_bv = take(nb * 8), o_vs = take(nb * 8);
 	if(!m) return sz;
 	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
@@ -1656,6 +1701,8 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.pS_q = (double *) (m + o_pq);
 	b.pS_bnd = (double *) (m + o_pb);
 	b.eS = (unsigned char *) (m + o_eS);
+	b.bmv = (double *) (m + o_bv);
+	b.vsuf = (double *) (m + o_vs);
 	b.maxu = (int) maxu;
 	return sz;
 }
@@ -1765,7 +1812,9 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 			k_exact_sum<><<<1, XS_NT, 0, st>>>(b, n, (int) gn);
 			kt.mark(CCG_K_XSUM);
 		}
-		if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
+		if(g_grid.bands(n - 1) && g_grid.scan_vblk && dnj_prune(n - 1, ET, GEN))
+			k_dnj_requeue<ET, true, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
+		else if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		kt.mark(CCG_K_REQUEUE);
 		return (GEN ? 5 : 4) + (prefold && !tfold) + xs;

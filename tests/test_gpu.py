@@ -690,7 +690,8 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
     (so minQpair skips it, dnj.c:78) loads nothing.  At small n through
     CCG_S_SPLIT_N / CCG_PREFOLD_N: joins and the reference-rule counters equal
     the serial oracle's, CCG_SCAN_PRUNE=0 gives the same joins, and the
-    pruned run loads no more cells."""
+    pruned run loads no more cells; with the requeue's V block minima
+    (CCG_SCAN_VBLK, the bound from every row above) fewer still."""
     from oracle import pyoracle
     from ccphylo_amd import native
     K = native.NKSTAT
@@ -707,11 +708,12 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
         D = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
     ref, rfn, rfd, rst = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1, stats=True)
     cells = {}
-    for prune in ("1", "0"):
+    for prune, vblk in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("CCG_SCAN_PRUNE", prune)
+        monkeypatch.setenv("CCG_SCAN_VBLK", vblk)   # + the requeue's V block minima
         got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
-        assert (fn, fd) == (rfn, rfd), prune
-        assert len(got) == len(ref) and (got == ref).all(), prune
-        assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), prune
-        cells[prune] = st[1]
-    assert int(rst[1]) <= cells["1"] <= cells["0"]
+        assert (fn, fd) == (rfn, rfd), (prune, vblk)
+        assert len(got) == len(ref) and (got == ref).all(), (prune, vblk)
+        assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), (prune, vblk)
+        cells[prune + vblk] = st[1]
+    assert int(rst[1]) <= cells["11"] <= cells["10"] <= cells["00"]
