@@ -29,6 +29,7 @@ struct DenseRows {
 #define JOIN_UPRE 2048   // rest-unit partials k_dnj_join prefetches into LDS
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
 #define PLAN_MAXB 256    // blocks of k_dnj_plan (one listing step of LT * FR rows each)
+#define SRDY_REP 64      // copies of the scan's S-table ready tag (pollers spread over lines)
 
 // Grid of k_dnj_scan: min(ceil(n / scan_div), scan_max).  CCG_SCAN_DIV and
 // CCG_SCAN_MAX override it (tests shrink the grid so that several grid
@@ -38,9 +39,12 @@ struct DnjGrid {
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
-	int scan_fold = 1; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=0)
-	int scan_prune = 1; // band mode: the scan rescans S first and prunes the other entries under its exact
-	                    // fresh minima (CCG_SCAN_PRUNE=0: off)
+	// measured at the headline (configs[2], 50k, profiled tree; round 4): scan + fold per join 68.3 us with
+	// k_dnj_fold, 72.4 with FoldTail, 84.2 with FoldTail + pruning (cells 2.12x -> 1.27x the reference's:
+	// the S phase and the wait for its table lengthen every wave's chain more than the pruned loads save)
+	int scan_fold = 0; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=1)
+	int scan_prune = 1; // band mode, with FoldTail: the scan rescans S first and prunes the other entries
+	                    // under its exact fresh minima (CCG_SCAN_PRUNE=0: off)
 	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
 	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {
@@ -1073,10 +1077,24 @@ __device__ __forceinline__ void s_table(const TreeBufs &b, int n) {
 		if(lane == 0) __hip_atomic_store(b.vsuf + G, DBL_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	if(lane == 0) {
-		__hip_atomic_store(&b.ctl->scnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		__hip_atomic_store(&b.ctl->sready, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if(lane == 0) __hip_atomic_store(&b.ctl->scnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	// the ready tag in SRDY_REP lines: thousands of waiting waves polling ONE
+	// line cut the chip's bandwidth (MI355X_MICROARCH.md, polling-cost)
+	if(lane < SRDY_REP)
+		__hip_atomic_store(b.srdy + 32 * lane, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the S bound table of this join is published (bounded wait; false: never
+// expected, the units then run unpruned, still exact).  ONE lane per block
+// polls (its block's copy of the tag); the block's other waves read the
+// table after a barrier this lane joins.
+__device__ __forceinline__ bool s_table_wait(const TreeBufs &b, int n) {
+	const unsigned *f = b.srdy + 32 * (blockIdx.x % SRDY_REP);
+	for(int spin = 0; spin < (1 << 18); ++spin) {
+		if(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) n) return true;
+		__builtin_amdgcn_s_sleep(4);
 	}
+	return false;
 }
 
 // The S bound table in a wave's registers (lanes t and t + 64), and the
@@ -1087,25 +1105,13 @@ struct SBound {
 	int nS, G;
 	bool ok, vb;
 	const double *vsuf;
-	// waits (bounded) for the S phase of this join; false: no pruning
-	__device__ __forceinline__ bool load(const TreeBufs &b, int n) {
+	// ready: s_table_wait's answer for this block (after a barrier)
+	__device__ __forceinline__ bool load(const TreeBufs &b, int n, bool ready) {
 		const int lane = threadIdx.x & 63;
 		nS = b.ctl->pS;
 		m0 = b.ctl->m0;
-		ok = false;
-		if(nS <= 0) return false;
-		if(lane == 0) {
-			for(int spin = 0; spin < (1 << 18); ++spin) {
-				if(__hip_atomic_load(&b.ctl->sready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) n) {
-					ok = true;
-					break;
-				}
-				__builtin_amdgcn_s_sleep(2);
-			}
-		}
-		ok = __shfl(ok, 0);
-		if(!ok) return false;   // never expected: the units then run unpruned (still exact)
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		ok = ready && nS > 0;
+		if(!ok) return false;
 		vb = b.ctl->vtag == n;
 		G = (int) cdiv(n + 1, TB);
 		vsuf = b.vsuf;
@@ -1479,7 +1485,14 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		unit(v, b.pS_ent[lo], r, c0, c0 + SEG < r ? c0 + SEG : r, false, true, s_uo[lo], s_uo[lo + 1]);
 	}
 	SBound sb;
-	bool have_sb = false;
+	bool have_sb = false, ready = false;
+	if(PRUNE && nSp && (int) blockIdx.x * (TB / 64) < nunits) {   // block-uniform: one poller per block
+		__shared__ int s_ready;
+		__syncthreads();
+		if(tid == 0) s_ready = s_table_wait(b, n);
+		__syncthreads();
+		ready = s_ready;
+	}
 	for(int u = gw; u < nunits; u += nw) {
 		const int e = u / umax, ua = e * umax;
 		const int r = lds ? erow[e] : b.crow[e];
@@ -1489,7 +1502,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		if(PRUNE && nSp) {
 			if(b.eS[e]) continue;   // ran in the S phase
 			if(!have_sb) {
-				sb.load(b, n);
+				sb.load(b, n, ready);
 				have_sb = true;
 			}
 			skip = sb.ok && !(b.cbnd[e] < sb.at(r));
@@ -1577,7 +1590,14 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 		fold_arrive(b, n, b.uq, b.uj, v, s_uo[lo], s_uo[lo + 1], q, idx, e, Tn, true);
 	}
 	SBound sb;
-	bool have_sb = false;
+	bool have_sb = false, ready = false;
+	if(PRUNE && nSp && (int) blockIdx.x * (TB / 64) < nunits) {   // block-uniform: one poller per block
+		__shared__ int s_ready;
+		__syncthreads();
+		if(tid == 0) s_ready = s_table_wait(b, n);
+		__syncthreads();
+		ready = s_ready;
+	}
 	for(int u = gw; u < nunits; u += nw) {
 		const int g = u / umax, s = u - g * umax, c0 = s * seg;
 		int r[G], c1[G];
@@ -1596,7 +1616,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 #pragma unroll
 			for(int k = 0; k < G; ++k) any = any || act[k];
 			if(any && !have_sb) {   // uniform
-				sb.load(b, n);
+				sb.load(b, n, ready);
 				have_sb = true;
 			}
 			if(any && sb.ok) {

@@ -42,7 +42,6 @@ struct TreeCtl {
 	int rtotal;          // sharded DNJ: replay entries whose accept flags k_shd_join applies
 	int pS;              // S rows whose exact fresh minima prune the scan (0: no pruning this join)
 	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
-	unsigned sready;     // = n once the scan's S bound table is written (tagged: no reset)
 	long long cells_pruned;  // listed cells the scan skipped under the S bound table
 	int vtag;            // VBLK: the matrix size whose join the requeue's bmv minima serve
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
@@ -98,6 +97,8 @@ struct TreeBufs {
 	unsigned char *eS;              // per entry: 1 for an S row
 	double *bmv, *vsuf;             // VBLK: per requeue block the minimum of V_k = max(q at the partner cell, Q_k),
 	                                // and the scan's suffix minima of them (bounds from every row above)
+	unsigned *srdy;                 // SRDY_REP copies (one 128-B line each) of the tag n the scan's S bound
+	                                // table is published with; block b polls copy b % SRDY_REP
 	int maxu;
 };
 

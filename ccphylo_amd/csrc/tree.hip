@@ -1642,6 +1642,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
 	size_t o_pr = take(DNJ_B * 4), o_pe = take(DNJ_B * 4), o_pu = take((DNJ_B + 1) * 4), o_pq = take(DNJ_B * 8);
 	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent), o_bv = take(nb * 8), o_vs = take(nb * 8);
+	size_t o_sr = take(SRDY_REP * 128);
 	if(!m) return sz;
 	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
@@ -1703,6 +1704,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.eS = (unsigned char *) (m + o_eS);
 	b.bmv = (double *) (m + o_bv);
 	b.vsuf = (double *) (m + o_vs);
+	b.srdy = (unsigned *) (m + o_sr);
 	b.maxu = (int) maxu;
 	return sz;
 }

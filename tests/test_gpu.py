@@ -696,6 +696,7 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
     from ccphylo_amd import native
     K = native.NKSTAT
     monkeypatch.setenv("CCG_SCAN_WAVE", mode)
+    monkeypatch.setenv("CCG_SCAN_FOLD", "1")   # pruning rides on the in-scan fold (off by default)
     monkeypatch.setenv("CCG_PREFOLD_N", "0")
     monkeypatch.setenv("CCG_SEG_MUL", "1")
     monkeypatch.setenv("CCG_S_SPLIT_N", "100")
