@@ -35,7 +35,14 @@ struct DenseRows {
 // CCG_SCAN_MAX override it (tests shrink the grid so that several grid
 // waves of units run at small n).
 struct DnjGrid {
-	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 8 * SEG;
+	// prefold_n: every n folds each entry's units once (k_dnj_fold + k_dnj_join_pf); round 4, measured: the
+	// headline's tree 6.61 -> 6.36 s (profiled), configs[1] 24.7k -> 25.0k joins/s, 4k Euclidean unchanged
+	int scan_div = 4, scan_max = 2048, seg_mul = 0, prefold_n = 0;
+	// below 16384 taxa the wave scan replaces the block scan while the joins list many rows: tree_run_t
+	// sets small_wave from the rows listed per join over its last 1024-join window (> adapt_rows;
+	// CCG_SCAN_ADAPT, 0: never; headline tree 6.23 -> 6.16 s at 1000, 6.11 at 500).  Clade SNP data (the headline) lists thousands of rows per join there,
+	// Euclidean matrices a few hundred (configs[1]: 246), where the block scan is 2-3 % faster
+	int small_wave = 0, adapt_rows = 500;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
@@ -58,7 +65,8 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_SCAN_DIV")) scan_div = atoi(e) > 0 ? atoi(e) : 4;
 		if(const char *e = getenv("CCG_SCAN_MAX")) scan_max = atoi(e) > 0 ? atoi(e) : 2048;
 		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
-		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 8 * SEG;
+		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_SCAN_ADAPT")) adapt_rows = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
@@ -98,7 +106,7 @@ struct DnjGrid {
 	// groups (20), where the 8-byte sD load per cell outweighs the row bytes
 	// and one sD load serves 4 rows
 	int scan_mode(int n, int et = 8) const {
-		return scan_wave >= 0 ? scan_wave : n > 16384 ? (et == 8 ? 9 : 20) : 0;
+		return scan_wave >= 0 ? scan_wave : n > 16384 || small_wave ? (et == 8 ? 9 : 20) : 0;
 	}
 	// cells per rescan unit: SEG up to 8 units per row, then growing with n
 	// (at most 8 SEG) so that a unit's fixed cost stays small beside its bytes
@@ -530,6 +538,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// most SEL_STEPS steps of 64 SEL_RPL rows (any S is exact: when the
 			// scan stops short, the rows below the examined ones are left to the
 			// listing under its bound, which never exceeds m0)
+			TS(1, 9);
 			int cnt = 0, low = n;   // rows >= low examined
 			for(int base = n - 1, step = 0; !regsel && base >= 1 && cnt < ktop && step < SEL_STEPS;
 			    base -= 64 * SEL_RPL, ++step) {
@@ -845,7 +854,6 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				for(int m = 0; m < FR; ++m) sfm |= ((fw[m >> 2] >> (8 * (m & 3))) & 1u) << m;
 			}
 			if(base == top) TS(1, 5);
-			if(base == top - LT * FR) TS(1, 9);
 			unsigned long long bm[FR];
 			unsigned sbm = 0;   // bit m: this lane's slot-m row is a band row of S
 #pragma unroll

@@ -1920,6 +1920,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 #endif
 	int n = n0;
 	int since_check = 0;
+	long long win_rows = h.rows;   // ctl->rows at the last check
 	bool stopped = false;
 	const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 	while(n > stop_n) {
@@ -1931,6 +1932,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			since_check = 0;
 			CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 			CCG_CHECK(hipStreamSynchronize(st));
+			// the next window's scan form below 16384 taxa (DnjGrid::small_wave)
+			g_grid.small_wave = g_grid.adapt_rows && h.rows - win_rows > 1024LL * g_grid.adapt_rows;
+			win_rows = h.rows;
 			if(g_progress && (n0 - n) % (16 * 1024) == 0)   // long trees (CCG_PROGRESS=1): a line per 16384 joins
 				fprintf(stderr, "ccg_tree: %d joins, n = %d, rows %lld cells %lld (reference rule %lld / %lld)\n", n0 - n,
 				        n, h.rows, h.cells, h.ref_rows, h.ref_cells);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--n", type=int, default=50_000)
     ap.add_argument("--L", type=int, default=5_000_000)
     ap.add_argument("--joins", type=int, default=0)
+    ap.add_argument("--joins-list", default="", help="comma-separated join prefixes, each timed under every setting")
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("settings", nargs="*")
     a = ap.parse_args()
@@ -39,7 +40,9 @@ def main():
     del seqs, incs
     torch.cuda.empty_cache()
     host = Dd.cpu()
-    for st_ in a.settings or [""]:
+    runs = [(s_, int(jl)) for jl in (a.joins_list.split(",") if a.joins_list else [a.joins])
+            for s_ in (a.settings or [""])]
+    for st_, max_joins in runs:
         env = dict(kv.split("=", 1) for kv in st_.split())
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
@@ -47,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         j, fn, fd, st = dev.tree_dev(Dd.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=bool(a.exact),
-                                     max_joins=a.joins, profile=True)
+                                     max_joins=max_joins, profile=True)
         dt = time.perf_counter() - t0
         kern = {name: round(st[5 + 2 * c] / 1e3 / max(len(j), 1), 2)
                 for c, name in enumerate(["init", "top", "scan", "argmin", "update", "requeue", "pop", "plan",
