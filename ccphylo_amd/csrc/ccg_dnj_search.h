@@ -43,6 +43,7 @@ struct DnjGrid {
 	// CCG_SCAN_ADAPT, 0: never; headline tree 6.23 -> 6.16 s at 1000, 6.11 at 500).  Clade SNP data (the headline) lists thousands of rows per join there,
 	// Euclidean matrices a few hundred (configs[1]: 246), where the block scan is 2-3 % faster
 	int small_wave = 0, adapt_rows = 500;
+	int sphase_b = 512;   // CCG_SPHASE_BLOCKS
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
@@ -67,6 +68,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_SEG_MUL")) seg_mul = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_ADAPT")) adapt_rows = atoi(e) > 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_SPHASE_BLOCKS")) sphase_b = atoi(e) > 0 ? atoi(e) : 512;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
@@ -130,6 +132,8 @@ struct DnjGrid {
 		b = b > DNJ_BANDS_MAX ? DNJ_BANDS_MAX : b;
 		return top(n) + b > DNJ_B ? DNJ_B - top(n) : b;
 	}
+	// k_dnj_sphase's grid (one wave per S unit, grid-stride)
+	unsigned sphase_blocks() const { return sphase_b; }
 	unsigned scan(int n) const {
 		const long long g = (n + scan_div - 1) / scan_div;
 		return (unsigned) (g < scan_max ? g : scan_max);
@@ -1146,6 +1150,9 @@ struct SBound {
 // all lanes of the wave, with the wave's (q, j) of unit u of entry e, whose
 // partials are pq / pj [ua, ub); sent: entry e is an S row of the scan's S
 // phase (its partials then live in uq / uj, indexed by the S unit)
+// CHUNKS = false (k_dnj_sphase): the entry is folded and counted into S only;
+// k_dnj_fold summarises the chunks after the scan
+template <bool CHUNKS = true>
 __device__ __forceinline__ void fold_arrive(const TreeBufs &b, int n, double *pq, int *pj, int u, int ua, int ub,
                                             double q, int j, int e, int T, bool sent) {
 	const int lane = threadIdx.x & 63;
@@ -1184,11 +1191,13 @@ __device__ __forceinline__ void fold_arrive(const TreeBufs &b, int n, double *pq
 			__hip_atomic_store(b.rf + e, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			__hip_atomic_store(b.rj + e, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			const int c = e >> 6, ce = T - (c << 6) < 64 ? T - (c << 6) : 64;
-			const unsigned seen = __hip_atomic_fetch_add(b.ccnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if((int) seen == ce - 1) {
-				chunk_done = 1;
-				__hip_atomic_store(b.ccnt + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if(CHUNKS) {
+				const int c = e >> 6, ce = T - (c << 6) < 64 ? T - (c << 6) : 64;
+				const unsigned seen = __hip_atomic_fetch_add(b.ccnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				if((int) seen == ce - 1) {
+					chunk_done = 1;
+					__hip_atomic_store(b.ccnt + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
 			}
 			if(sent) {
 				const unsigned sseen = __hip_atomic_fetch_add(&b.ctl->scnt, 1u, __ATOMIC_RELAXED,
@@ -1201,7 +1210,7 @@ __device__ __forceinline__ void fold_arrive(const TreeBufs &b, int n, double *pq
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 		s_table(b, n);
 	}
-	if(!__shfl(chunk_done, 0)) return;
+	if(!CHUNKS || !__shfl(chunk_done, 0)) return;
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 	// the chunk summary, as k_dnj_fold leaves it
 	const int c = e >> 6, e2 = (c << 6) + lane;
@@ -1351,7 +1360,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // current ones are compared (half UV, two register sets), bit 2 loads sD
 // 16 bytes at a time where the unit's aligned start is even (sD + ca 16-byte
 // aligned; uniform per unit), bit 3 doubles the loads in flight per lane.
-template <int ET, class Rows, class Tail = NoTail, int MODE = 0, bool PRUNE = false>
+template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
@@ -1361,6 +1370,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	__shared__ int erow[REPLAY_CAP];
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
+	TS_ENTRY(2);
+	TS(2, 0);
+	TS_SAMP(0);
 	const int r0 = b.crow[tid];
 	const int done = ctl->done, Tn = ctl->T;
 	if(done) return;
@@ -1369,7 +1381,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	const int umax = dnj_umax(n, seg), nunits = Tn * umax;
 	const int nSp = PRUNE ? ctl->pS : 0;
 	// (the S phase's SEG-cell units may outnumber the entries' units)
-	const int su0 = PRUNE && nSp ? b.pS_uo[nSp] : 0;
+	const int su0 = PRUNE == 1 && nSp ? b.pS_uo[nSp] : 0;
 	if((int) blockIdx.x * (TB / 64) >= (nunits > su0 ? nunits : su0)) return;
 	const bool lds = Tn <= REPLAY_CAP;
 	if(lds) {
@@ -1378,6 +1390,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	}
 	__syncthreads();
 	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	TS(2, 1);
+	TS_SAMP(1);
 	// PRUNE (band mode): the S entries' units first (the lowest waves), their
 	// exact fresh minima then bound every other entry (SBound), and an entry
 	// whose stale Q is not below the bound at its row is one minQpair skips
@@ -1385,7 +1399,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	// neither accepts nor lets into the running min
 	__shared__ int s_uo[DNJ_B + 1];
 	int su = 0;
-	if(PRUNE && nSp) {
+	if(PRUNE == 1 && nSp) {
 		for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
 		__syncthreads();
 		su = s_uo[nSp];
@@ -1480,7 +1494,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 		}
 		qarg_wave_reduce(q, idx);
-		if(PRUNE && sent) fold_arrive(b, n, b.uq, b.uj, u, sua, sub, q, idx, e, Tn, true);
+		if(PRUNE == 1 && sent) fold_arrive(b, n, b.uq, b.uj, u, sua, sub, q, idx, e, Tn, true);
 		else tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn);
 	};
 	for(int v = gw; v < su; v += nw) {   // the S phase: SEG-cell units (short, so the phase is)
@@ -1494,13 +1508,18 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	}
 	SBound sb;
 	bool have_sb = false, ready = false;
-	if(PRUNE && nSp && (int) blockIdx.x * (TB / 64) < nunits) {   // block-uniform: one poller per block
+	if(PRUNE == 1 && nSp && (int) blockIdx.x * (TB / 64) < nunits) {   // block-uniform: one poller per block
 		__shared__ int s_ready;
 		__syncthreads();
 		if(tid == 0) s_ready = s_table_wait(b, n);
 		__syncthreads();
 		ready = s_ready;
 	}
+	// PRUNE == 2: k_dnj_sphase (the launch before) rescanned S, folded its
+	// entries and left the table tagged n (plain loads after the boundary)
+	if(PRUNE == 2 && nSp) ready = b.srdy[0] == (unsigned) n;
+	int nu = 0;   // (trace: units of this wave so far)
+	(void) nu;
 	for(int u = gw; u < nunits; u += nw) {
 		const int e = u / umax, ua = e * umax;
 		const int r = lds ? erow[e] : b.crow[e];
@@ -1515,10 +1534,75 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			}
 			skip = sb.ok && !(b.cbnd[e] < sb.at(r));
 		}
+		TS_U(2 * nu);
 		unit(u, e, r, c0, c0 + seg < r ? c0 + seg : r, skip, false, 0, 0);
+		TS_U(2 * nu + 1);
+		++nu;
 	}
 	if(PRUNE && pruned && lane == 0)   // (uniform: every lane counted the same units)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
+	TS(2, 2);
+	TS_SAMP(2);
+	TS_EXIT(2);
+}
+
+// S's rescans in a launch of their own before the scan (CCG_SCAN_PRUNE=2):
+// S rows (the plan's top and band rows, pS_*) in SEG-cell units, one wave per
+// unit, each S entry folded at its last unit and the bound table built by the
+// last S entry (fold_arrive without chunk accounting, s_table), so the scan
+// that follows prunes with the table from its first unit and never waits.
+// Column/row values are those the scan would read (the plan persisted row
+// i's sD / N before this launch).
+template <int ET>
+__global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                   int n) {
+	typedef typename Elem<ET>::T T;
+	constexpr int UC = 8;
+	__shared__ int s_uo[DNJ_B + 1];
+	const TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	if(ctl->done) return;
+	const int nSp = ctl->pS, Tn = ctl->T;
+	if(nSp <= 0) return;
+	for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
+	__syncthreads();
+	const int su = s_uo[nSp];
+	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	for(int v = gw; v < su; v += nw) {
+		int lo = 0, hi = nSp;   // the S row t with s_uo[t] <= v < s_uo[t + 1]
+		while(hi - lo > 1) {
+			const int mid = (lo + hi) >> 1;
+			if(s_uo[mid] <= v) lo = mid; else hi = mid;
+		}
+		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;
+		const int c1 = c0 + SEG < r ? c0 + SEG : r;
+		const double sDr = b.sD[r];
+		const T *row = D + tri(r);
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int base = c0; base < c1; base += 64 * UC) {
+			double sk[UC];
+			T vv[UC];
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const int cc = c < c1 ? c : c1 - 1;
+				sk[m] = b.sD[cc];
+				vv[m] = row[cc];
+			}
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const double d = Elem<ET>::get(vv[m], bs);
+				const double x = qcrit(n, n, d, sDr, sk[m]);
+				const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+				q = take ? x : q;
+				idx = take ? c : idx;
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		fold_arrive<false>(b, n, b.uq, b.uj, v, s_uo[lo], s_uo[lo + 1], q, idx, e, Tn, true);
+	}
 }
 
 // Row groups (the default rescan past 16384 taxa for every element type but
@@ -1712,11 +1796,13 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 // value, the row and partner of the first entry reaching it, and whether any
 // entry is "bad" (fresh below its stale bound: minQpair's running min is then
 // not a prefix min).
+// sfold: this join's S entries (eS) were folded by k_dnj_sphase (rf / rj kept).
 template <int UNUSED = 0>
-__global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
+__global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg, int sfold = 0) {
 	const TreeCtl *ctl = b.ctl;
 	if(ctl->done) return;
 	const int T = ctl->T, lane = threadIdx.x & 63, umax = dnj_umax(n, seg);
+	sfold = sfold && ctl->pS > 0;
 	const int nc = (T + 63) >> 6;
 	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
 	for(int c = w0; c < nc; c += nw) {
@@ -1724,9 +1810,10 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
 		const bool valid = e < T;
 		const int r = valid ? b.crow[e] : 0;
 		const double bnd = valid ? b.cbnd[e] : 0.0;
-		const int ua = e * umax, ub = ua + (valid ? dcdiv(r, seg) : 0);
-		double q = DBL_MAX;
-		int idx = 0;
+		const bool sdone = sfold && valid && b.eS[e];
+		const int ua = e * umax, ub = ua + (valid && !sdone ? dcdiv(r, seg) : 0);
+		double q = sdone ? b.rf[e] : DBL_MAX;
+		int idx = sdone ? b.rj[e] : 0;
 		int u = ua;
 		for(; u + 4 <= ub; u += 4) {   // 4 units' loads in flight
 			double oq[4];
@@ -1752,7 +1839,7 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg) {
 				idx = oi;
 			}
 		}
-		if(valid) {
+		if(valid && !sdone) {
 			b.rf[e] = q;
 			b.rj[e] = idx;
 		}

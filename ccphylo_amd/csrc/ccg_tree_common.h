@@ -368,6 +368,15 @@ __device__ unsigned long long g_samp[256 * 64 * 3];
 			if(s_ >= 0 && s_ < 256) g_samp[(s_ * 64 + (blockIdx.x >> 5)) * 3 + (ph)] = rt_stamp(); \
 		}                                                                             \
 	} while(0)
+// wave 0 of every 32nd scan block: start / end stamps of its first 4 units (slots 0..7)
+__device__ unsigned long long g_uamp[256 * 64 * 8];
+#define TS_U(slot)                                                                    \
+	do {                                                                              \
+		if(threadIdx.x == 0 && (blockIdx.x & 31) == 0 && (blockIdx.x >> 5) < 64 && (slot) < 8) { \
+			int s_ = g_trace_hi - n;                                                  \
+			if(s_ >= 0 && s_ < 256) g_uamp[(s_ * 64 + (blockIdx.x >> 5)) * 8 + (slot)] = rt_stamp(); \
+		}                                                                             \
+	} while(0)
 #define TS_EXIT(kern)                                                                 \
 	do {                                                                              \
 		if(threadIdx.x == 0) {                                                        \
@@ -376,6 +385,7 @@ __device__ unsigned long long g_samp[256 * 64 * 3];
 		}                                                                             \
 	} while(0)
 #else
+#define TS_U(slot)
 #define TS_EXIT(kern)
 #define TS(kern, ph)
 #define TSW(kern, ph, th)

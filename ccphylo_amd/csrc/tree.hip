@@ -1726,10 +1726,14 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 // the scan rescans S first and prunes the other entries under S's exact
 // fresh minima: band mode, the wave scans with the fold at their last
 // arrivals, no missing entries
-static bool dnj_prune(int n, int et, bool gen) {
+// (scan_prune 1: the S phase inside the scan, with FoldTail; 2: S rescanned by
+// k_dnj_sphase, its own launch, then the wave scan with k_dnj_fold)
+static int dnj_prune(int n, int et, bool gen) {
 	const int sm = g_grid.scan_mode(n, et);
-	return g_grid.scan_prune && !gen && g_grid.bands(n) && g_grid.prefold(n) && g_grid.scan_fold &&
-	       ((sm >= 4 && sm < 20) || (sm >= 20 && sm <= 23));
+	if(gen || !g_grid.bands(n) || !g_grid.prefold(n)) return 0;
+	if(g_grid.scan_prune == 1 && g_grid.scan_fold && ((sm >= 4 && sm < 20) || (sm >= 20 && sm <= 23))) return 1;
+	if(g_grid.scan_prune == 2 && !g_grid.scan_fold && sm >= 4 && sm < 20) return 2;
+	return 0;
 }
 
 template <int ET, bool GEN>
@@ -1759,7 +1763,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		// the wave-per-unit scans fold the entries at their last arrivals
 		// (FoldTail) instead of a k_dnj_fold pass
 		const bool tfold = prefold && g_grid.scan_fold && sm >= 1;
-		const bool prune = dnj_prune(n, ET, GEN);
+		const int prune = dnj_prune(n, ET, GEN);
+		if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n);
 		if(sm >= 20 && sm <= 23 && !GEN) {
 			if(prune) {
 				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
@@ -1778,7 +1783,14 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 				else k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 			}
 		} else if(sm >= 4 && !GEN) {
-			if(prune) {
+			if(prune == 2) {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 2><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(5)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows, NoTail, 0, 2><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			} else if(prune) {
 				switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, FoldTail, M, true><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
 					SV_(1) SV_(5)
@@ -1804,7 +1816,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 			if(tfold) k_dnj_scan_w<ET, GEN, DenseRows, FoldTail><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 			else k_dnj_scan_w<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 		} else k_dnj_scan<ET, GEN><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
-		if(prefold && !tfold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg);
+		if(prefold && !tfold) k_dnj_fold<><<<FOLD_BLOCKS, TB, 0, st>>>(b, n, seg, prune == 2);
 		kt.mark(CCG_K_REST);
 		if(prefold && g_grid.join_pf) k_dnj_join_pf<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, g_grid.join_pf == 2);
 		else k_dnj_join<ET, GEN><<<gn, TB, 0, st>>>(D, bs, b, n, general, prefold, seg);
@@ -1819,7 +1831,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		else if(g_grid.bands(n - 1)) k_dnj_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		else k_dnj_requeue<ET, false><<<gn, TB, 0, st>>>(D, bs, b, n, general, exact);
 		kt.mark(CCG_K_REQUEUE);
-		return (GEN ? 5 : 4) + (prefold && !tfold) + xs;
+		return (GEN ? 5 : 4) + (prefold && !tfold) + (prune == 2) + xs;
 	}
 	if(method == CCG_TREE_HNJ) {
 		k_hnj_argmin<><<<gn, TB, 0, st>>>(b, n);
@@ -1995,7 +2007,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			// sampled scan blocks (every 32nd): start and end relative to the kernel's first entry
 			static unsigned long long sp[256 * 64 * 3];
 			CCG_CHECK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_samp), sizeof(sp), 0, hipMemcpyDeviceToHost));
-			double st_max = 0, en_max = 0, dur = 0, st_med = 0;
+			double st_max = 0, en_max = 0, dur = 0, st_med = 0, stg = 0;
 			int sc = 0, jc = 0;
 			for(int s = 0; s < 256; ++s) {
 				const unsigned long long t0 = ~tr[(s * NKT + 2) * 16 + 15];
@@ -2009,6 +2021,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 					smax = a > smax ? a : smax;
 					emax = z > emax ? z : emax;
 					dur += z - a;
+					if(e[1] >= e[0]) stg += (e[1] - e[0]) / 100.0;
 					st_med += a;
 					++sc;
 					any = 1;
@@ -2019,8 +2032,42 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 					++jc;
 				}
 			}
-			if(jc) fprintf(stderr, "  scan samples: %d joins, %.1f working blocks sampled/join; last start %.2f us, last end %.2f us, mean start %.2f, mean duration %.2f us\n",
-			                jc, (double) sc / jc, st_max / jc, en_max / jc, st_med / sc, dur / sc);
+			{
+				static unsigned long long ua[256 * 64 * 8];
+				CCG_CHECK(hipMemcpyFromSymbol(ua, HIP_SYMBOL(g_uamp), sizeof(ua), 0, hipMemcpyDeviceToHost));
+				double ud[4] = {0}, ug[4] = {0}, us0 = 0;
+				int uc[4] = {0}, gc[4] = {0}, s0c = 0;
+				for(int s = 0; s < 256; ++s) {
+					const unsigned long long t0 = ~tr[(s * NKT + 2) * 16 + 15];
+					if(!tr[(s * NKT + 2) * 16 + 15]) continue;
+					for(int q = 0; q < 64; ++q) {
+						const unsigned long long *e = ua + (s * 64 + q) * 8;
+						const unsigned long long *sp0 = sp + (s * 64 + q) * 3;
+						if(e[0] && e[0] >= t0 && sp0[0] && e[0] >= sp0[0]) {
+							us0 += (e[0] - sp0[0]) / 100.0;   // block entry -> first unit
+							++s0c;
+						}
+						for(int k = 0; k < 4; ++k) {
+							if(e[2 * k] && e[2 * k + 1] >= e[2 * k] && e[2 * k] >= t0) {
+								ud[k] += (e[2 * k + 1] - e[2 * k]) / 100.0;
+								++uc[k];
+							}
+							if(k && e[2 * k] && e[2 * k - 1] && e[2 * k] >= e[2 * k - 1] && e[2 * k] >= t0) {
+								ug[k] += (e[2 * k] - e[2 * k - 1]) / 100.0;
+								++gc[k];
+							}
+						}
+					}
+				}
+				fprintf(stderr, "  scan units (wave 0 of sampled blocks): entry->first unit %.2f us;", s0c ? us0 / s0c : 0.0);
+				for(int k = 0; k < 4; ++k)
+					fprintf(stderr, " unit%d n=%d dur %.2f gap %.2f;", k, uc[k], uc[k] ? ud[k] / uc[k] : 0.0, gc[k] ? ug[k] / gc[k] : 0.0);
+				fprintf(stderr, "\n");
+				memset(ua, 0, sizeof(ua));
+				CCG_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_uamp), ua, sizeof(ua), 0, hipMemcpyHostToDevice));
+			}
+			if(jc) fprintf(stderr, "  scan samples: %d joins, %.1f working blocks sampled/join; last start %.2f us, last end %.2f us, mean start %.2f, mean duration %.2f us (setup %.2f)\n",
+			                jc, (double) sc / jc, st_max / jc, en_max / jc, st_med / sc, dur / sc, stg / sc);
 		}
 		for(int k = 0; k < nk && cnt; ++k) {
 			if(!present[k]) continue;

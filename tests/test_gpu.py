@@ -696,7 +696,6 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
     from ccphylo_amd import native
     K = native.NKSTAT
     monkeypatch.setenv("CCG_SCAN_WAVE", mode)
-    monkeypatch.setenv("CCG_SCAN_FOLD", "1")   # pruning rides on the in-scan fold (off by default)
     monkeypatch.setenv("CCG_PREFOLD_N", "0")
     monkeypatch.setenv("CCG_SEG_MUL", "1")
     monkeypatch.setenv("CCG_S_SPLIT_N", "100")
@@ -709,12 +708,19 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
         D = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
     ref, rfn, rfd, rst = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1, stats=True)
     cells = {}
-    for prune, vblk in (("1", "1"), ("1", "0"), ("0", "0")):
+    # prune 1: the S phase inside the scan (with its fold at the last arrivals);
+    # prune 2: S rescanned by k_dnj_sphase, its own launch (wave scans only)
+    for prune, vblk, fold in (("1", "1", "1"), ("1", "0", "1"), ("2", "1", "0"), ("2", "0", "0"), ("0", "0", "0")):
         monkeypatch.setenv("CCG_SCAN_PRUNE", prune)
         monkeypatch.setenv("CCG_SCAN_VBLK", vblk)   # + the requeue's V block minima
+        monkeypatch.setenv("CCG_SCAN_FOLD", fold)
         got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
         assert (fn, fd) == (rfn, rfd), (prune, vblk)
         assert len(got) == len(ref) and (got == ref).all(), (prune, vblk)
         assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), (prune, vblk)
         cells[prune + vblk] = st[1]
     assert int(rst[1]) <= cells["11"] <= cells["10"] <= cells["00"]
+    if int(mode) < 20:   # the split form prunes exactly as the in-scan one
+        assert (cells["21"], cells["20"]) == (cells["11"], cells["10"])
+    else:
+        assert cells["21"] == cells["20"] == cells["00"]
