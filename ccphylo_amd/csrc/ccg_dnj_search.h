@@ -30,6 +30,7 @@ struct DenseRows {
 #define FOLD_BLOCKS 256  // grid of k_dnj_fold (one wave per entry, grid-stride)
 #define PLAN_MAXB 256    // blocks of k_dnj_plan (one listing step of LT * FR rows each)
 #define SRDY_REP 64      // copies of the scan's S-table ready tag (pollers spread over lines)
+#define UHIST 64         // bins of k_dnj_plan's per-block histogram of entries by unit count (umax < UHIST)
 
 // Grid of k_dnj_scan: min(ceil(n / scan_div), scan_max).  CCG_SCAN_DIV and
 // CCG_SCAN_MAX override it (tests shrink the grid so that several grid
@@ -44,6 +45,11 @@ struct DnjGrid {
 	// Euclidean matrices a few hundred (configs[1]: 246), where the block scan is 2-3 % faster
 	int small_wave = 0, adapt_rows = 500;
 	int sphase_b = 512;   // CCG_SPHASE_BLOCKS
+	int scan_cmp = 1, cmp_blocks = 1024;   // the compacted wave scan (CCG_SCAN_CMP=0: off) and its grid
+	// scan_prune 2 pays while the joins list many cells: tree_run_t keeps it on (prune_on) while the last
+	// 1024-join window listed more than prune_cells cells per join (CCG_PRUNE_CELLS; 0: always)
+	long long prune_cells = 20000000;
+	int prune_on = 1;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
@@ -51,8 +57,12 @@ struct DnjGrid {
 	// k_dnj_fold, 72.4 with FoldTail, 84.2 with FoldTail + pruning (cells 2.12x -> 1.27x the reference's:
 	// the S phase and the wait for its table lengthen every wave's chain more than the pruned loads save)
 	int scan_fold = 0; // the fold at the scan's last arrivals (FoldTail) instead of k_dnj_fold (CCG_SCAN_FOLD=1)
-	int scan_prune = 1; // band mode, with FoldTail: the scan rescans S first and prunes the other entries
-	                    // under its exact fresh minima (CCG_SCAN_PRUNE=0: off)
+	// band mode: the S rows' exact fresh minima bound the other entries, and an entry whose stale Q is not
+	// below the bound at its row is one minQpair skips (dnj.c:78): 2 (default) k_dnj_sphase rescans S,
+	// builds the table and keeps only the surviving entries for the compacted wave scan; 1: the S phase
+	// inside the scan (with FoldTail, CCG_SCAN_FOLD=1); 0: off.  Headline tree (profiled, round 4):
+	// 6.29 s off, 5.86-5.89 s with 2 while the joins list > 15-30M cells, 6.05 s with 2 throughout
+	int scan_prune = 2;
 	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
 	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {
@@ -69,6 +79,10 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_ADAPT")) adapt_rows = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SPHASE_BLOCKS")) sphase_b = atoi(e) > 0 ? atoi(e) : 512;
+		if(const char *e = getenv("CCG_SCAN_CMP")) scan_cmp = atoi(e);
+		if(const char *e = getenv("CCG_PRUNE_CELLS")) prune_cells = atoll(e) > 0 ? atoll(e) : 0;
+		prune_on = 1;
+		if(const char *e = getenv("CCG_SCAN_CMPB")) cmp_blocks = atoi(e) > 0 ? atoi(e) : 1024;
 		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
@@ -358,8 +372,10 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	const int fr = ((qdelay >> 17) & 15) + 1;
 	const int nblk = gridDim.x, bid = blockIdx.x, bstep = bid * (LT * fr), stride = nblk * (LT * fr);
 	__shared__ int s_off;
+	__shared__ int s_uh[UHIST];   // this block's entries by rescan-unit count (the compacted scan's enumeration)
 	TS_ENTRY(1);
 	TS(1, 0);
+	if(tid < UHIST) s_uh[tid] = 0;   // wave 0: before its own top-part counts; the others after the barrier
 	const int lt = tid - 64;   // listing thread (waves 1..)
 	// every row of the matrix sits in the listing's registers (one block, one
 	// step, no bands: n <= 15361): S is selected from them after the fold, by
@@ -606,10 +622,12 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			if(t0 < ntop && bid == 0) {
 				b.crow[t0] = r0;
 				b.cbnd[t0] = sQS[t0];
+				atomicAdd(&s_uh[dcdiv(r0, seg) < UHIST ? dcdiv(r0, seg) : UHIST - 1], 1);
 			}
 			if(t1 < ntop && bid == 0) {
 				b.crow[t1] = r1;
 				b.cbnd[t1] = sQS[t1];
+				atomicAdd(&s_uh[dcdiv(r1, seg) < UHIST ? dcdiv(r1, seg) : UHIST - 1], 1);
 			}
 			const long long ctop = wave_sum_int((long long) (o0 ? r0 : 0) + (o1 ? r1 : 0));
 			
@@ -743,6 +761,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				sQS[pos] = qv[m];
 				b.crow[pos] = r;
 				b.cbnd[pos] = qv[m];
+				if(bid == 0) atomicAdd(&s_uh[dcdiv(r, seg) < UHIST ? dcdiv(r, seg) : UHIST - 1], 1);
 				ctop += rows.owns(r) ? r : 0;
 			}
 		}
@@ -955,6 +974,15 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				const int r = base - (m * LT + lt);
 				const bool f = (bm[m] >> lane) & 1ull;
 				mycells += f ? r : 0;
+				{   // the unit-count histogram: this wave's 64 consecutive rows span at most two counts
+					const int rh = base - (m * LT + (wid - 1) * 64), bh0 = dcdiv(rh, seg);
+					const int bh = bh0 < UHIST ? bh0 : UHIST - 1;
+					const int ch = __popcll(__ballot(f && dcdiv(r, seg) == bh0)), ct = __popcll(bm[m]);
+					if(lane == 0) {
+						atomicAdd(&s_uh[bh], ch);
+						if(ct > ch) atomicAdd(&s_uh[bh0 - 1 < UHIST ? bh0 - 1 : UHIST - 1], ct - ch);
+					}
+				}
 				if(f) {
 					const int pos = T + s_mw[m * LW + wid - 1] +
 					                (int) __builtin_amdgcn_mbcnt_hi((unsigned) (bm[m] >> 32),
@@ -998,7 +1026,10 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		atomicAdd((unsigned long long *) &ctl->cells, (unsigned long long) mycells);
 		atomicAdd((unsigned long long *) &ctl->cells_rest, (unsigned long long) mycells);
 	}
+	__syncthreads();
+	if(tid < UHIST) b.uhist[bid * UHIST + tid] = s_uh[tid];
 	if(tid == 0) {
+		if(bid == 0) ctl->pblk = nblk;
 		if(bid == nblk - 1) ctl->T = T;   // every entry up to the last block's
 		// the rows this block listed (block 0 also the top part of S)
 		atomicAdd((unsigned long long *) &ctl->rows, (unsigned long long) (listed + (bid == 0 ? ntop : 0)));   // no read: nothing waits
@@ -1360,7 +1391,13 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // current ones are compared (half UV, two register sets), bit 2 loads sD
 // 16 bytes at a time where the unit's aligned start is even (sD + ca 16-byte
 // aligned; uniform per unit), bit 3 doubles the loads in flight per lane.
-template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0>
+// CMP (single engine, NoTail): the real units enumerated densely from the
+// plan's histogram of entries by unit count, slot-major (slot k: the E_k
+// entries with more than k units, a prefix of the descending list), and dealt
+// round-robin over a grid that is resident at once, so every wave gets the
+// same number of units to within one (grid-stride over T umax slots left
+// waves with 1 to 4+ units and a second round of blocks).
+template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0, bool CMP = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
@@ -1520,7 +1557,65 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	if(PRUNE == 2 && nSp) ready = b.srdy[0] == (unsigned) n;
 	int nu = 0;   // (trace: units of this wave so far)
 	(void) nu;
-	for(int u = gw; u < nunits; u += nw) {
+	if(CMP && PRUNE == 2 && nSp) {
+		// k_dnj_sphase left only the surviving entries, by unit-count bucket
+		// u at blist[Eall(u) ...): slot k's units are the survivors with more
+		// than k units, buckets in descending u
+		int H = 0;
+		const int pb = ctl->pblk;
+		for(int g = 0; g < pb; ++g) H += b.uhist[g * UHIST + lane];
+		const int inch = wave_incl_sum(H), Eall = __builtin_amdgcn_readlane(inch, 63) - inch;
+		const int cnt = b.bcnt[lane];
+		const int incc = wave_incl_sum(cnt), totc = __builtin_amdgcn_readlane(incc, 63);
+		const int Es = totc - incc;          // survivors with more than `lane` units
+		const int C = totc - incc + cnt;     // survivors with at least `lane` units
+		int R;
+		const int P = wave_excl_scan(Es, &R);
+		for(int v = gw; v < R; v += nw) {
+			const int k = 63 - __clzll((long long) __ballot(Es > 0 && P <= v));
+			const int j = v - __shfl(P, k);
+			const int ub = 63 - __clzll((long long) __ballot(lane > k && C > j));
+			const int p = j - (__shfl(C, ub) - __shfl(cnt, ub));
+			const int e = b.blist[__shfl(Eall, ub) + p];
+			const int r = lds ? erow[e] : b.crow[e];
+			const int c0 = k * seg;
+			TS_U(2 * nu);
+			unit(e * umax + k, e, r, c0, c0 + seg < r ? c0 + seg : r, false, false, 0, 0);
+			TS_U(2 * nu + 1);
+			++nu;
+		}
+	} else if(CMP) {
+		int H = 0;   // lane k: entries with exactly k units, summed over the plan's blocks
+		const int pb = ctl->pblk;
+		for(int g = 0; g < pb; ++g) H += b.uhist[g * UHIST + lane];
+		int tot;
+		const int inc = wave_incl_sum(H);
+		tot = __builtin_amdgcn_readlane(inc, 63);
+		const int E = tot - inc;   // entries with more than `lane` units: slot `lane`'s real units
+		int R;
+		const int P = wave_excl_scan(E, &R);
+		for(int v = gw; v < R; v += nw) {
+			const unsigned long long mk = __ballot(E > 0 && P <= v);
+			const int k = 63 - __clzll((long long) mk);
+			const int e = v - __shfl(P, k);
+			const int r = lds ? erow[e] : b.crow[e];
+			const int c0 = k * seg;
+			bool skip = false;
+			if(PRUNE == 2 && nSp) {
+				if(b.eS[e]) continue;   // rescanned by k_dnj_sphase
+				if(!have_sb) {
+					sb.load(b, n, ready);
+					have_sb = true;
+				}
+				skip = sb.ok && !(b.cbnd[e] < sb.at(r));
+			}
+			TS_U(2 * nu);
+			unit(e * umax + k, e, r, c0, c0 + seg < r ? c0 + seg : r, skip, false, 0, 0);
+			TS_U(2 * nu + 1);
+			++nu;
+		}
+	}
+	for(int u = CMP ? nunits : gw; u < nunits; u += nw) {
 		const int e = u / umax, ua = e * umax;
 		const int r = lds ? erow[e] : b.crow[e];
 		const int c0 = (u - ua) * seg;
@@ -1555,15 +1650,15 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 // i's sD / N before this launch).
 template <int ET>
 __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
-                                                   int n) {
+                                                   int n, int seg) {
 	typedef typename Elem<ET>::T T;
 	constexpr int UC = 8;
 	__shared__ int s_uo[DNJ_B + 1];
 	const TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
-	if(ctl->done) return;
+	if(ctl->done) return;   // (block-uniform)
 	const int nSp = ctl->pS, Tn = ctl->T;
-	if(nSp <= 0) return;
+	if(nSp <= 0) return;    // (block-uniform) no S this join: the scan enumerates every entry
 	for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
 	__syncthreads();
 	const int su = s_uo[nSp];
@@ -1603,6 +1698,70 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 		qarg_wave_reduce(q, idx);
 		fold_arrive<false>(b, n, b.uq, b.uj, v, s_uo[lo], s_uo[lo + 1], q, idx, e, Tn, true);
 	}
+	// ---- the other entries under the table (one lane per entry): pruned ones
+	// flagged (ePr, k_dnj_fold folds them as DBL_MAX), survivors appended to
+	// their unit-count bucket (the scan enumerates only those).  A block whose
+	// wait gives up keeps all its entries (still exact).
+	__shared__ int s_ready, s_prow[DNJ_B];
+	__shared__ double s_pbnd[DNJ_B];
+	__syncthreads();
+	if(tid == 0) s_ready = s_table_wait(b, n);
+	__syncthreads();
+	const bool ready = s_ready;
+	const double m0 = ctl->m0;
+	if(ready) {
+		for(int t = tid; t < nSp; t += TB) {
+			s_prow[t] = b.pS_row[t];
+			s_pbnd[t] = __hip_atomic_load(b.pS_bnd + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
+	__syncthreads();
+	const bool vb = ready && ctl->vtag == n;
+	const int G = (int) cdiv(n + 1, TB);
+	int H = 0;   // lane u: entries with exactly u units (the plan's histogram); bucket u starts at E (u)
+	for(int g = 0; g < ctl->pblk; ++g) H += b.uhist[g * UHIST + lane];
+	const int inc = wave_incl_sum(H), E = __builtin_amdgcn_readlane(inc, 63) - inc;
+	long long pcells = 0;   // cells of the pruned entries (stats: the scan never loads them)
+	for(int e0 = gw * 64; e0 < Tn; e0 += nw * 64) {
+		const int e = e0 + lane;
+		const bool valid = e < Tn;
+		const int r = valid ? b.crow[e] : 1;
+		const bool sE = valid && b.eS[e];
+		bool pr = false;
+		if(ready && valid && !sE) {
+			int lo = 0, hi = nSp;   // S rows above r (descending rows)
+			while(lo < hi) {
+				const int mid = (lo + hi) >> 1;
+				if(s_prow[mid] > r) lo = mid + 1; else hi = mid;
+			}
+			double bnd = lo ? s_pbnd[lo - 1] : m0;
+			if(vb) {
+				const int g = (r >> 8) + 1;
+				const double vv = __hip_atomic_load(b.vsuf + (g < G ? g : G), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				bnd = vv < bnd ? vv : bnd;
+			}
+			pr = !(b.cbnd[e] < bnd);
+		}
+		if(valid) b.ePr[e] = pr;
+		pcells += pr ? r : 0;
+		const bool surv = valid && !sE && !pr;
+		const int u0 = dcdiv(r, seg), u = u0 < UHIST ? u0 : UHIST - 1;
+		unsigned long long rem = __ballot(surv);
+		while(rem) {   // one atomic per bucket present in the wave
+			const int ld = __ffsll((long long) rem) - 1;
+			const int ub = __shfl(u, ld);
+			const unsigned long long mk = __ballot(surv && u == ub);
+			int base = 0;
+			if(lane == ld) base = atomicAdd(b.bcnt + ub, __popcll(mk));
+			base = __shfl(base, ld) + __shfl(E, ub);
+			if(surv && u == ub)
+				b.blist[base + (int) __builtin_amdgcn_mbcnt_hi((unsigned) (mk >> 32),
+				                                               __builtin_amdgcn_mbcnt_lo((unsigned) mk, 0))] = e;
+			rem &= ~mk;
+		}
+	}
+	pcells = wave_sum_int(pcells);
+	if(lane == 0 && pcells) atomicAdd((unsigned long long *) &b.ctl->cells_pruned, (unsigned long long) pcells);
 }
 
 // Row groups (the default rescan past 16384 taxa for every element type but
@@ -1803,6 +1962,8 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg, int
 	if(ctl->done) return;
 	const int T = ctl->T, lane = threadIdx.x & 63, umax = dnj_umax(n, seg);
 	sfold = sfold && ctl->pS > 0;
+	// k_dnj_sphase's bucket counts, consumed by the scan: zero for the next join
+	if(blockIdx.x == 0 && threadIdx.x < UHIST) b.bcnt[threadIdx.x] = 0;
 	const int nc = (T + 63) >> 6;
 	const int w0 = (int) (blockIdx.x * (TB / 64) + (threadIdx.x >> 6)), nw = (int) (gridDim.x * (TB / 64));
 	for(int c = w0; c < nc; c += nw) {
@@ -1810,8 +1971,8 @@ __global__ __launch_bounds__(TB) void k_dnj_fold(TreeBufs b, int n, int seg, int
 		const bool valid = e < T;
 		const int r = valid ? b.crow[e] : 0;
 		const double bnd = valid ? b.cbnd[e] : 0.0;
-		const bool sdone = sfold && valid && b.eS[e];
-		const int ua = e * umax, ub = ua + (valid && !sdone ? dcdiv(r, seg) : 0);
+		const bool sdone = sfold && valid && b.eS[e], pruned = sfold && valid && !sdone && b.ePr[e];
+		const int ua = e * umax, ub = ua + (valid && !sdone && !pruned ? dcdiv(r, seg) : 0);
 		double q = sdone ? b.rf[e] : DBL_MAX;
 		int idx = sdone ? b.rj[e] : 0;
 		int u = ua;

@@ -44,6 +44,7 @@ struct TreeCtl {
 	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
 	long long cells_pruned;  // listed cells the scan skipped under the S bound table
 	int vtag;            // VBLK: the matrix size whose join the requeue's bmv minima serve
+	int pblk;            // k_dnj_plan's block count (rows of uhist this join)
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
 };
 
@@ -97,6 +98,11 @@ struct TreeBufs {
 	unsigned char *eS;              // per entry: 1 for an S row
 	double *bmv, *vsuf;             // VBLK: per requeue block the minimum of V_k = max(q at the partner cell, Q_k),
 	                                // and the scan's suffix minima of them (bounds from every row above)
+	int *bcnt, *blist;              // k_dnj_sphase: surviving entries per unit-count bucket (zeroed by k_dnj_fold)
+	                                // and their indices, bucket u at [entries with more than u units, ...)
+	unsigned char *ePr;             // per entry: pruned by the S bound table this join (k_dnj_sphase)
+	int *uhist;                     // k_dnj_plan: per plan block, its entries by rescan-unit count (UHIST bins);
+	                                // the compacted wave scan enumerates the real units from it
 	unsigned *srdy;                 // SRDY_REP copies (one 128-B line each) of the tag n the scan's S bound
 	                                // table is published with; block b polls copy b % SRDY_REP
 	int maxu;

@@ -1642,7 +1642,8 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	size_t o_ec = take(nent * 4), o_cc = take(nch * 4);
 	size_t o_pr = take(DNJ_B * 4), o_pe = take(DNJ_B * 4), o_pu = take((DNJ_B + 1) * 4), o_pq = take(DNJ_B * 8);
 	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent), o_bv = take(nb * 8), o_vs = take(nb * 8);
-	size_t o_sr = take(SRDY_REP * 128);
+	size_t o_sr = take(SRDY_REP * 128), o_uh = take((size_t) PLAN_MAXB * UHIST * 4);
+	size_t o_bc = take(UHIST * 4), o_bl = take(ncand * 4), o_ep = take(nent);
 	if(!m) return sz;
 	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
@@ -1705,6 +1706,10 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.bmv = (double *) (m + o_bv);
 	b.vsuf = (double *) (m + o_vs);
 	b.srdy = (unsigned *) (m + o_sr);
+	b.uhist = (int *) (m + o_uh);
+	b.bcnt = (int *) (m + o_bc);
+	b.blist = (int *) (m + o_bl);
+	b.ePr = (unsigned char *) (m + o_ep);
 	b.maxu = (int) maxu;
 	return sz;
 }
@@ -1732,7 +1737,7 @@ static int dnj_prune(int n, int et, bool gen) {
 	const int sm = g_grid.scan_mode(n, et);
 	if(gen || !g_grid.bands(n) || !g_grid.prefold(n)) return 0;
 	if(g_grid.scan_prune == 1 && g_grid.scan_fold && ((sm >= 4 && sm < 20) || (sm >= 20 && sm <= 23))) return 1;
-	if(g_grid.scan_prune == 2 && !g_grid.scan_fold && sm >= 4 && sm < 20) return 2;
+	if(g_grid.scan_prune == 2 && g_grid.prune_on && !g_grid.scan_fold && sm >= 4 && sm < 20) return 2;
 	return 0;
 }
 
@@ -1764,7 +1769,7 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		// (FoldTail) instead of a k_dnj_fold pass
 		const bool tfold = prefold && g_grid.scan_fold && sm >= 1;
 		const int prune = dnj_prune(n, ET, GEN);
-		if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n);
+		if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
 		if(sm >= 20 && sm <= 23 && !GEN) {
 			if(prune) {
 				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
@@ -1783,7 +1788,24 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 				else k_dnj_scan_g<ET, 2, 8><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 			}
 		} else if(sm >= 4 && !GEN) {
-			if(prune == 2) {
+			// the compacted form (the plan's unit histogram; umax within its bins)
+			const bool cmp = g_grid.scan_cmp && prune != 1 && !tfold && dnj_umax(n, seg) < UHIST;
+			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
+			if(cmp && prune == 2) {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 2, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(5)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows, NoTail, 0, 2, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			} else if(cmp) {
+				switch(sm) {
+#define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 0, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
+					SV_(1) SV_(5)
+#undef SV_
+					default: k_dnj_scan_v<ET, DenseRows, NoTail, 0, 0, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+				}
+			} else if(prune == 2) {
 				switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 2><<<gc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
 					SV_(1) SV_(5)
@@ -1932,7 +1954,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 #endif
 	int n = n0;
 	int since_check = 0;
-	long long win_rows = h.rows;   // ctl->rows at the last check
+	long long win_rows = h.rows, win_cells = h.cells;   // ctl->rows / cells at the last check
 	bool stopped = false;
 	const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 	while(n > stop_n) {
@@ -1946,7 +1968,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			CCG_CHECK(hipStreamSynchronize(st));
 			// the next window's scan form below 16384 taxa (DnjGrid::small_wave)
 			g_grid.small_wave = g_grid.adapt_rows && h.rows - win_rows > 1024LL * g_grid.adapt_rows;
+			g_grid.prune_on = !g_grid.prune_cells || h.cells - win_cells > 1024LL * g_grid.prune_cells;
 			win_rows = h.rows;
+			win_cells = h.cells;
 			if(g_progress && (n0 - n) % (16 * 1024) == 0)   // long trees (CCG_PROGRESS=1): a line per 16384 joins
 				fprintf(stderr, "ccg_tree: %d joins, n = %d, rows %lld cells %lld (reference rule %lld / %lld)\n", n0 - n,
 				        n, h.rows, h.cells, h.ref_rows, h.ref_cells);
