@@ -700,6 +700,7 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
     monkeypatch.setenv("CCG_SEG_MUL", "1")
     monkeypatch.setenv("CCG_S_SPLIT_N", "100")
     monkeypatch.setenv("CCG_S_BANDS", str(bands))
+    monkeypatch.setenv("CCG_PRUNE_CELLS", "0")   # prune every join (not only while the listings are long)
     D = {"euc": lambda: _euclid(n, n + 3), "snp": lambda: _snp(n, n + 1), "clade": lambda: _clade_ltd(n, n + 4)}[kind]()
     bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 0.1}[et]
     if et == 4:
