@@ -1652,7 +1652,7 @@ template <int ET>
 __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int seg) {
 	typedef typename Elem<ET>::T T;
-	constexpr int UC = 8;
+	constexpr int UC = 16;   // a SEG-cell unit in two steps of loads
 	__shared__ int s_uo[DNJ_B + 1];
 	const TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
@@ -1704,6 +1704,12 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 	// wait gives up keeps all its entries (still exact).
 	__shared__ int s_ready, s_prow[DNJ_B];
 	__shared__ double s_pbnd[DNJ_B];
+	// this wave's first 64 entries, loaded before the wait (they do not depend on the table)
+	const int ef = gw * 64 + lane;
+	const bool vf = ef < Tn;
+	const int rf0 = vf ? b.crow[ef] : 1;
+	const bool sf0 = vf && b.eS[ef];
+	const double cbf = vf ? b.cbnd[ef] : 0.0;
 	__syncthreads();
 	if(tid == 0) s_ready = s_table_wait(b, n);
 	__syncthreads();
@@ -1724,9 +1730,10 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 	long long pcells = 0;   // cells of the pruned entries (stats: the scan never loads them)
 	for(int e0 = gw * 64; e0 < Tn; e0 += nw * 64) {
 		const int e = e0 + lane;
-		const bool valid = e < Tn;
-		const int r = valid ? b.crow[e] : 1;
-		const bool sE = valid && b.eS[e];
+		const bool first = e0 == gw * 64, valid = e < Tn;
+		const int r = first ? rf0 : valid ? b.crow[e] : 1;
+		const bool sE = first ? sf0 : valid && b.eS[e];
+		const double cb = first ? cbf : valid ? b.cbnd[e] : 0.0;
 		bool pr = false;
 		if(ready && valid && !sE) {
 			int lo = 0, hi = nSp;   // S rows above r (descending rows)
@@ -1740,7 +1747,7 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 				const double vv = __hip_atomic_load(b.vsuf + (g < G ? g : G), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				bnd = vv < bnd ? vv : bnd;
 			}
-			pr = !(b.cbnd[e] < bnd);
+			pr = !(cb < bnd);
 		}
 		if(valid) b.ePr[e] = pr;
 		pcells += pr ? r : 0;

@@ -24,7 +24,8 @@ import sys
 from collections import defaultdict
 
 NAMES = {"k_dnj_select": "dnj_select", "k_dnj_plan": "dnj_find", "k_dnj_scan": "dnj_scan",
-         "k_dnj_join": "update", "k_dnj_requeue": "dnj_requeue"}
+         "k_dnj_join": "update", "k_dnj_join_pf": "update", "k_dnj_requeue": "dnj_requeue",
+         "k_dnj_fold": "dnj_fold", "k_dnj_sphase": "dnj_sphase", "k_dnj_scan_v": "dnj_scan"}
 # the NJ passes (tools/perf_dnj.py 10000 nj), when present
 NJ_NAMES = {"k_nj_argmin": "nj_argmin", "k_nj_join": "nj_update", "k_nj_pop": "nj_pop"}
 
