@@ -45,6 +45,7 @@ struct DnjGrid {
 	// Euclidean matrices a few hundred (configs[1]: 246), where the block scan is 2-3 % faster
 	int small_wave = 0, adapt_rows = 500;
 	int sphase_b = 512;   // CCG_SPHASE_BLOCKS
+XX
 	int scan_cmp = 1, cmp_blocks = 1024;   // the compacted wave scan (CCG_SCAN_CMP=0: off) and its grid
 	// scan_prune 2 pays while the joins list many cells: tree_run_t keeps it on (prune_on) while the last
 	// 1024-join window listed more than prune_cells cells per join (CCG_PRUNE_CELLS; 0: always)
@@ -79,6 +80,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_ADAPT")) adapt_rows = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SPHASE_BLOCKS")) sphase_b = atoi(e) > 0 ? atoi(e) : 512;
+		if(const char *e = getenv("CCG_PLAN_HELP")) plan_help = atoi(e) >= 0 && atoi(e) < 512 ? atoi(e) : 128;
 		if(const char *e = getenv("CCG_SCAN_CMP")) scan_cmp = atoi(e);
 		if(const char *e = getenv("CCG_PRUNE_CELLS")) prune_cells = atoll(e) > 0 ? atoll(e) : 0;
 		prune_on = 1;
@@ -92,8 +94,9 @@ struct DnjGrid {
 	// k_dnj_plan's last argument: the Q-load delay (low 16 bits), bit 16 turns
 	// the register S selection off (on with CCG_PLAN_REGSEL=1)
 	// and bits 17-20 the rows per thread per listing step less one (CCG_PLAN_FR)
-	int plan_flags(bool prune = false) const {
-		return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17 | (prune ? 1 << 21 : 0);
+	int plan_flags(bool prune = false, int helpers = 0) const {
+		return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17 | (prune ? 1 << 21 : 0) |
+		       (helpers & 511) << 22;
 	}
 	// k_dnj_plan's grid: one listing step of (TBF - 64) FIND_RPT rows per block
 	// (CCG_PLAN_MULTI=0: one block walks every step, the round-2 form)
@@ -342,6 +345,170 @@ __global__ __launch_bounds__(TB) void k_dnj_prep(TreeBufs b, int n) {
 // Rows j and i of the previous join have their Q/P in the requeue partials
 // (substituted here, persisted by thread 0); the moved row i's sD/N (row n's)
 // are substituted as column and persisted for the kernels after.
+// The plan's helper blocks (scan_prune 2): once block 0 has published S
+// (shdr tagged n), S's rows are rescanned in SEG-cell units, one wave each,
+// with the moved row i's sD substituted (block 0 persists it in this very
+// launch); each S row is folded at its last unit (sfq / sfj by S index), and
+// the last S row builds the bound table (s_table's content, from sfq) and
+// publishes it (srdy).  The listing blocks never wait for them; k_dnj_compact
+// reads the table after the launch.
+__device__ __forceinline__ void s_table_h(const TreeBufs &b, int n, int nS, double m0) {
+	const int lane = threadIdx.x & 63;
+	double v[2];
+#pragma unroll
+	for(int h = 0; h < 2; ++h) {
+		const int t = lane + 64 * h;
+		v[h] = DBL_MAX;
+		if(t < nS) {
+			const double f = __hip_atomic_load(b.sfq + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			const double qt = __hip_atomic_load(b.pS_q + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			v[h] = f > qt ? f : qt;
+		}
+	}
+	double x0 = wave_incl_min(v[0]);
+	x0 = x0 < m0 ? x0 : m0;
+	const double c = readlane_d(x0, 63);
+	double x1 = wave_incl_min(v[1]);
+	x1 = x1 < c ? x1 : c;
+	if(lane < nS) __hip_atomic_store(b.pS_bnd + lane, x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if(lane + 64 < nS) __hip_atomic_store(b.pS_bnd + lane + 64, x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if(b.ctl->vtag == n) {   // the requeue's V block minima: suffix minima (written by an earlier launch)
+		const int G = (int) cdiv(n + 1, TB);
+		double carry = DBL_MAX;
+		for(int g1 = ((G - 1) / 64) * 64; g1 >= 0; g1 -= 64) {
+			const int g = g1 + 63 - lane;
+			double x = g < G ? b.bmv[g] : DBL_MAX;
+			x = wave_incl_min(x);
+			x = x < carry ? x : carry;
+			if(g < G) __hip_atomic_store(b.vsuf + g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			carry = readlane_d(x, 63);
+		}
+		if(lane == 0) __hip_atomic_store(b.vsuf + G, DBL_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if(lane < SRDY_REP)
+		__hip_atomic_store(b.srdy + 32 * lane, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int ET>
+__device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__restrict__ D, double bs,
+                                                        TreeBufs b, int n, int hb, int nh) {
+	typedef typename Elem<ET>::T T;
+	constexpr int UC = 8;
+	__shared__ int h_ok, h_nS, h_isub;
+	__shared__ double h_m0, h_sDm;
+	__shared__ int h_uo[DNJ_B + 1], h_row[DNJ_B];
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	if(b.ctl->done) return;   // (block-uniform; the plan's blocks return too)
+	if(tid == 0) {
+		bool ok = false;
+		for(int spin = 0; spin < (1 << 18); ++spin) {
+			if(__hip_atomic_load(b.shdr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned long long) n) {
+				ok = true;
+				break;
+			}
+			__builtin_amdgcn_s_sleep(4);
+		}
+		h_ok = ok;
+		if(ok) {
+			h_m0 = __longlong_as_double(
+			    (long long) __hip_atomic_load(b.shdr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+			h_sDm = __longlong_as_double(
+			    (long long) __hip_atomic_load(b.shdr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+			const unsigned long long w = __hip_atomic_load(b.shdr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			h_nS = (int) (unsigned) (w & 0xffffffffu);
+			h_isub = (int) (unsigned) (w >> 32);
+		}
+	}
+	__syncthreads();
+	if(!h_ok || h_nS <= 0) return;
+	const int nS = h_nS, isub = h_isub;
+	const double sDm = h_sDm;
+	for(int t = tid; t <= nS; t += blockDim.x) {
+		h_uo[t] = __hip_atomic_load(b.pS_uo + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if(t < nS) h_row[t] = __hip_atomic_load(b.pS_row + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	__syncthreads();
+	const int su = h_uo[nS];
+	const int nwv = blockDim.x >> 6;
+	for(int v = hb * nwv + wid; v < su; v += nh * nwv) {
+		int lo = 0, hi = nS;
+		while(hi - lo > 1) {
+			const int mid = (lo + hi) >> 1;
+			if(h_uo[mid] <= v) lo = mid; else hi = mid;
+		}
+		const int r = h_row[lo], c0 = (v - h_uo[lo]) * SEG;
+		const int c1 = c0 + SEG < r ? c0 + SEG : r;
+		const double sDr = r == isub ? sDm : b.sD[r];
+		const T *row = D + tri(r);
+		double q = DBL_MAX;
+		int idx = 0;
+		for(int base = c0; base < c1; base += 64 * UC) {
+			double sk[UC];
+			T vv[UC];
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const int cc = c < c1 ? c : c1 - 1;
+				sk[m] = b.sD[cc];
+				vv[m] = row[cc];
+			}
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				const double d = Elem<ET>::get(vv[m], bs);
+				const double x = qcrit(n, n, d, sDr, c == isub ? sDm : sk[m]);
+				const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+				q = take ? x : q;
+				idx = take ? c : idx;
+			}
+		}
+		qarg_wave_reduce(q, idx);
+		// fold S row lo at its last unit; the last S row builds the table
+		int s_done = 0;
+		if(lane == 0) {
+			const int ua = h_uo[lo], ub = h_uo[lo + 1];
+			bool last = true;
+			if(ub - ua > 1) {
+				__hip_atomic_store(b.uq + v, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				__hip_atomic_store(b.uj + v, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				const unsigned seen = __hip_atomic_fetch_add(b.ecS + lo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				last = (int) seen == ub - ua - 1;
+				if(last) {
+					for(int x0 = ua; x0 < ub; x0 += 4) {
+						double oq[4];
+						int oi[4];
+#pragma unroll
+						for(int m = 0; m < 4; ++m) {
+							const int x = x0 + m < ub ? x0 + m : ub - 1;
+							oq[m] = __hip_atomic_load(b.uq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+							oi[m] = __hip_atomic_load(b.uj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						}
+#pragma unroll
+						for(int m = 0; m < 4; ++m) {
+							if(x0 + m < ub && qarg_better(oq[m], oi[m], q, idx)) {
+								q = oq[m];
+								idx = oi[m];
+							}
+						}
+					}
+					__hip_atomic_store(b.ecS + lo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
+			}
+			if(last) {
+				__hip_atomic_store(b.sfq + lo, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				__hip_atomic_store(b.sfj + lo, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				const unsigned sseen = __hip_atomic_fetch_add(&b.ctl->scnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				s_done = (int) sseen == nS - 1;
+				if(s_done) __hip_atomic_store(&b.ctl->scnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+		}
+		if(__shfl(s_done, 0)) s_table_h(b, n, nS, h_m0);
+	}
+}
+
 template <int ET, bool GEN, class Rows, bool BANDS>
 __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                   int n, int first, Rows rows, int seg, int ktop, int kbands,
@@ -370,7 +537,14 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// fr (<= FR): rows per thread per listing step, from the flags (small n:
 	// fewer rows per block, more blocks to pull Q in)
 	const int fr = ((qdelay >> 17) & 15) + 1;
-	const int nblk = gridDim.x, bid = blockIdx.x, bstep = bid * (LT * fr), stride = nblk * (LT * fr);
+	// helper blocks (the last (qdelay >> 22) & 511 of the grid, scan_prune 2):
+	// S's rescans and the bound table while the listing blocks list
+	const int nhelp = (qdelay >> 22) & 511;
+	if((int) blockIdx.x >= (int) gridDim.x - nhelp) {
+		plan_s_helper<ET>(D, bs, b, n, (int) blockIdx.x - ((int) gridDim.x - nhelp), nhelp);
+		return;
+	}
+	const int nblk = gridDim.x - nhelp, bid = blockIdx.x, bstep = bid * (LT * fr), stride = nblk * (LT * fr);
 	__shared__ int s_off;
 	__shared__ int s_uh[UHIST];   // this block's entries by rescan-unit count (the compacted scan's enumeration)
 	TS_ENTRY(1);
@@ -384,6 +558,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// S for the scan's pruning (band mode): its rows, Q and unit prefix persisted,
 	// every entry flagged (eS) and each S row's entry index recorded
 	const bool prune = BANDS && ((qdelay >> 21) & 1);
+	const int nhelp_ = (qdelay >> 22) & 511;
 	qdelay &= 0xffff;
 	double qv[FR];
 	const int rt = top - lt;
@@ -663,25 +838,40 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				const int ua = ta < nS ? (int) dcdiv(sS[ta], SEG) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], SEG) : 0;
 				int tota, totb;
 				const int pa = wave_excl_scan(ua, &tota), pb = wave_excl_scan(ub, &totb);
+				// (write-through: the helper blocks read them in this launch)
 				if(ta < nS) {
-					b.pS_row[ta] = sS[ta];
-					b.pS_q[ta] = sQS[ta];
-					b.pS_uo[ta] = pa;
+					__hip_atomic_store(b.pS_row + ta, sS[ta], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(b.pS_q + ta, sQS[ta], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(b.pS_uo + ta, pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					if(ta < ntop) {
 						b.pS_ent[ta] = ta;
 						b.eS[ta] = 1;
 					}
 				}
 				if(tb < nS) {
-					b.pS_row[tb] = sS[tb];
-					b.pS_q[tb] = sQS[tb];
-					b.pS_uo[tb] = tota + pb;
+					__hip_atomic_store(b.pS_row + tb, sS[tb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(b.pS_q + tb, sQS[tb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(b.pS_uo + tb, tota + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					if(tb < ntop) {
 						b.pS_ent[tb] = tb;
 						b.eS[tb] = 1;
 					}
 				}
-				if(lane == 0) b.pS_uo[nS] = tota + totb;
+				if(lane == 0)
+					__hip_atomic_store(b.pS_uo + nS, tota + totb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				if(nhelp_) {   // the S header, then its tag, for the helper blocks
+					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+					if(lane == 0) {
+						__hip_atomic_store(b.shdr + 0, (unsigned long long) __double_as_longlong(m0), __ATOMIC_RELAXED,
+						                   __HIP_MEMORY_SCOPE_AGENT);
+						__hip_atomic_store(b.shdr + 1, (unsigned long long) __double_as_longlong(sDm), __ATOMIC_RELAXED,
+						                   __HIP_MEMORY_SCOPE_AGENT);
+						__hip_atomic_store(b.shdr + 2, ((unsigned long long) (unsigned) isub << 32) | (unsigned) nS,
+						                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+						__hip_atomic_store(b.shdr + 3, (unsigned long long) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					}
+				}
 			}
 			if(lane == 0) {
 				s_done = 0;
@@ -1648,7 +1838,12 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 // that follows prunes with the table from its first unit and never waits.
 // Column/row values are those the scan would read (the plan persisted row
 // i's sD / N before this launch).
-template <int ET>
+// SLOOP = false (k_dnj_compact, the default): the plan's helper blocks
+// already rescanned S and built the table; this launch copies S's fresh
+// minima to their entries and compacts the rest.  If the table is missing
+// (a helper's bounded wait gave up: never expected) every entry, S's too,
+// survives and is rescanned.
+template <int ET, bool SLOOP = true>
 __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, int seg) {
 	typedef typename Elem<ET>::T T;
@@ -1661,7 +1856,7 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 	if(nSp <= 0) return;    // (block-uniform) no S this join: the scan enumerates every entry
 	for(int t = tid; t <= nSp; t += TB) s_uo[t] = b.pS_uo[t];
 	__syncthreads();
-	const int su = s_uo[nSp];
+	const int su = SLOOP ? s_uo[nSp] : 0;
 	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
 	for(int v = gw; v < su; v += nw) {
 		int lo = 0, hi = nSp;   // the S row t with s_uo[t] <= v < s_uo[t + 1]
@@ -1711,9 +1906,15 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 	const bool sf0 = vf && b.eS[ef];
 	const double cbf = vf ? b.cbnd[ef] : 0.0;
 	__syncthreads();
-	if(tid == 0) s_ready = s_table_wait(b, n);
+	if(tid == 0) s_ready = SLOOP ? s_table_wait(b, n) : b.srdy[0] == (unsigned) n;
 	__syncthreads();
 	const bool ready = s_ready;
+	if(!SLOOP && ready && blockIdx.x == 0)   // S's fresh minima to their entries (k_dnj_fold keeps them)
+		for(int t = tid; t < nSp; t += TB) {
+			const int e = b.pS_ent[t];
+			b.rf[e] = b.sfq[t];
+			b.rj[e] = b.sfj[t];
+		}
 	const double m0 = ctl->m0;
 	if(ready) {
 		for(int t = tid; t < nSp; t += TB) {
@@ -1732,7 +1933,11 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 		const int e = e0 + lane;
 		const bool first = e0 == gw * 64, valid = e < Tn;
 		const int r = first ? rf0 : valid ? b.crow[e] : 1;
-		const bool sE = first ? sf0 : valid && b.eS[e];
+		bool sE = first ? sf0 : valid && b.eS[e];
+		if(!SLOOP && !ready && sE) {   // no table: S's entries are rescanned as any other
+			b.eS[e] = 0;
+			sE = false;
+		}
 		const double cb = first ? cbf : valid ? b.cbnd[e] : 0.0;
 		bool pr = false;
 		if(ready && valid && !sE) {

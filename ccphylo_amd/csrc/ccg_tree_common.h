@@ -101,6 +101,11 @@ struct TreeBufs {
 	int *bcnt, *blist;              // k_dnj_sphase: surviving entries per unit-count bucket (zeroed by k_dnj_fold)
 	                                // and their indices, bucket u at [entries with more than u units, ...)
 	unsigned char *ePr;             // per entry: pruned by the S bound table this join (k_dnj_sphase)
+	unsigned long long *shdr;       // k_dnj_plan's S header for its helper blocks: m0, sD of the moved row i,
+	                                // (i << 32 | |S|), then the tag n (written last, write-through)
+	double *sfq;                    // S rows' fresh minima by S index (the plan's helpers), and their
+	int *sfj;                       // partners; ecS counts each S row's arrived units
+	unsigned *ecS;
 	int *uhist;                     // k_dnj_plan: per plan block, its entries by rescan-unit count (UHIST bins);
 	                                // the compacted wave scan enumerates the real units from it
 	unsigned *srdy;                 // SRDY_REP copies (one 128-B line each) of the tag n the scan's S bound

@@ -1644,6 +1644,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	size_t o_pb = take(DNJ_B * 8), o_eS = take(nent), o_bv = take(nb * 8), o_vs = take(nb * 8);
 	size_t o_sr = take(SRDY_REP * 128), o_uh = take((size_t) PLAN_MAXB * UHIST * 4);
 	size_t o_bc = take(UHIST * 4), o_bl = take(ncand * 4), o_ep = take(nent);
+	size_t o_sh = take(128), o_sf = take(DNJ_B * 8), o_sj = take(DNJ_B * 4), o_es = take(DNJ_B * 4);
 	if(!m) return sz;
 	TreeBufs &b = *bp;
 	b.sD = (double *) (m + o_sD);
@@ -1710,6 +1711,10 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.bcnt = (int *) (m + o_bc);
 	b.blist = (int *) (m + o_bl);
 	b.ePr = (unsigned char *) (m + o_ep);
+	b.shdr = (unsigned long long *) (m + o_sh);
+	b.sfq = (double *) (m + o_sf);
+	b.sfj = (int *) (m + o_sj);
+	b.ecS = (unsigned *) (m + o_es);
 	b.maxu = (int) maxu;
 	return sz;
 }
@@ -1745,8 +1750,9 @@ template <int ET, bool GEN>
 static void enqueue_plan(hipStream_t st, typename Elem<ET>::T *D, double bs, const TreeBufs &b, int n, int first) {
 	const int seg = g_grid.seg(n);
 	const unsigned gp = g_grid.plan_blocks(n);
-	const bool prune = dnj_prune(n, ET, GEN);
-	if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags(prune));
+	const int prune = dnj_prune(n, ET, GEN);
+	const int nh = prune == 2 && g_grid.plan_help ? g_grid.plan_help : 0;   // S's rescans by helper blocks
+	if(g_grid.bands(n)) k_dnj_plan<ET, GEN, DenseRows, true><<<gp + nh, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), g_grid.bands(n), g_grid.plan_flags(prune != 0, nh));
 	else k_dnj_plan<ET, GEN, DenseRows, false><<<gp, TBF, 0, st>>>(D, bs, b, n, first, DenseRows(), seg, g_grid.top(n), 0, g_grid.plan_flags());
 }
 
@@ -1769,7 +1775,8 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		// (FoldTail) instead of a k_dnj_fold pass
 		const bool tfold = prefold && g_grid.scan_fold && sm >= 1;
 		const int prune = dnj_prune(n, ET, GEN);
-		if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
+		if(prune == 2 && g_grid.plan_help) k_dnj_sphase<ET, false><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
+		else if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
 		if(sm >= 20 && sm <= 23 && !GEN) {
 			if(prune) {
 				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
