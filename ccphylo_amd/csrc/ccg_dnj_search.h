@@ -45,7 +45,9 @@ struct DnjGrid {
 	// Euclidean matrices a few hundred (configs[1]: 246), where the block scan is 2-3 % faster
 	int small_wave = 0, adapt_rows = 500;
 	int sphase_b = 512;   // CCG_SPHASE_BLOCKS
-XX
+	// scan_prune 2: k_dnj_plan's helper blocks rescan S while the plan lists (CCG_PLAN_HELP; 0: S in
+	// k_dnj_sphase after the plan): headline tree 5.96 -> 5.71 (128) / 5.67 s (256), profiled
+	int plan_help = 256;
 	int scan_cmp = 1, cmp_blocks = 1024;   // the compacted wave scan (CCG_SCAN_CMP=0: off) and its grid
 	// scan_prune 2 pays while the joins list many cells: tree_run_t keeps it on (prune_on) while the last
 	// 1024-join window listed more than prune_cells cells per join (CCG_PRUNE_CELLS; 0: always)
@@ -80,7 +82,7 @@ XX
 		if(const char *e = getenv("CCG_PREFOLD_N")) prefold_n = atoi(e) >= 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SCAN_ADAPT")) adapt_rows = atoi(e) > 0 ? atoi(e) : 0;
 		if(const char *e = getenv("CCG_SPHASE_BLOCKS")) sphase_b = atoi(e) > 0 ? atoi(e) : 512;
-		if(const char *e = getenv("CCG_PLAN_HELP")) plan_help = atoi(e) >= 0 && atoi(e) < 512 ? atoi(e) : 128;
+		if(const char *e = getenv("CCG_PLAN_HELP")) plan_help = atoi(e) >= 0 && atoi(e) < 512 ? atoi(e) : 256;
 		if(const char *e = getenv("CCG_SCAN_CMP")) scan_cmp = atoi(e);
 		if(const char *e = getenv("CCG_PRUNE_CELLS")) prune_cells = atoll(e) > 0 ? atoll(e) : 0;
 		prune_on = 1;
