@@ -689,6 +689,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			const int r = n - 1 - (m * 64 + lane);
 			topQ[m] = r >= 1 && !regsel ? b.Q[r] : DBL_MAX;
 		}
+		// band mode: the requeue's per-256-row-block minimum Q (rows i and j
+		// excluded) of the top blocks; the S steps skip blocks whose minimum is
+		// not below m0 (no row there can qualify) and load nothing for them
+		const int gtop = (n - 1) >> 8;
+		const double gbq = BANDS && !first && lane <= 2 * SEL_STEPS && gtop - lane >= 0 ? b.bmq[gtop - lane] : -DBL_MAX;
 		const double sDm = first ? 0.0 : b.sD[n];   // row n moves to i (matrix.c:518 semantics)
 		const int Nm = first ? 0 : b.N[n];
 		if(done) {
@@ -737,8 +742,21 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			// listing under its bound, which never exceeds m0)
 			TS(1, 9);
 			int cnt = 0, low = n;   // rows >= low examined
+			// bit l: block gtop - l may hold a row with Q < m0 (its minimum, or row j / i in it)
+			const int gl = gtop - lane;
+			const unsigned long long live =
+			    __ballot(gl >= 0 && (gbq < m0 || (jsub >= 0 && (jsub >> 8) == gl) || (isub >= 0 && (isub >> 8) == gl))) |
+			    ~((2ull << (2 * SEL_STEPS)) - 1);
 			for(int base = n - 1, step = 0; !regsel && base >= 1 && cnt < ktop && step < SEL_STEPS;
 			    base -= 64 * SEL_RPL, ++step) {
+				{   // the step's rows [lo, base] lie in blocks gtop - b0 .. gtop - b1
+					const int lo = base - (64 * SEL_RPL - 1) > 1 ? base - (64 * SEL_RPL - 1) : 1;
+					const int b0 = gtop - (base >> 8), b1 = gtop - (lo >> 8);
+					if(!(live & (((2ull << b1) - 1) & ~((1ull << b0) - 1)))) {   // uniform
+						low = lo;
+						continue;
+					}
+				}
 				if(step) {
 #pragma unroll
 					for(int m = 0; m < SEL_RPL; ++m) {   // all of the step's loads in flight at once
