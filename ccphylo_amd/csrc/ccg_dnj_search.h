@@ -20,6 +20,7 @@ struct DenseRows {
                          // of this many bands below them (DnjGrid::top/bands)
 #define DNJ_BANDS_MAX 128  // CCG_S_BANDS up to this (two bands per lane of k_dnj_plan's wave 0)
 #define SEG 2048         // cells per rescan unit (TB threads x 8)
+#define SEG_S 1024       // cells per rescan unit of S's rows (pruning's S phase: shorter chains, more waves)
 #define SEL_RPL 8        // rows per lane per step of the S scan (<= 32)
 #define SEL_STEPS 8      // steps of the S scan at most (then the listing takes over)
 #define TBF 1024         // threads of k_dnj_plan (one block)
@@ -439,8 +440,8 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 			const int mid = (lo + hi) >> 1;
 			if(h_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int r = h_row[lo], c0 = (v - h_uo[lo]) * SEG;
-		const int c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int r = h_row[lo], c0 = (v - h_uo[lo]) * SEG_S;
+		const int c1 = c0 + SEG_S < r ? c0 + SEG_S : r;
 		const double sDr = r == isub ? sDm : b.sD[r];
 		const T *row = D + tri(r);
 		double q = DBL_MAX;
@@ -855,7 +856,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				// top part's entries are the list's head; its SEG-cell rescan
 				// units prefixed for the scan's S phase
 				const int ta = lane, tb = lane + 64;
-				const int ua = ta < nS ? (int) dcdiv(sS[ta], SEG) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], SEG) : 0;
+				const int ua = ta < nS ? (int) dcdiv(sS[ta], SEG_S) : 0, ub = tb < nS ? (int) dcdiv(sS[tb], SEG_S) : 0;
 				int tota, totb;
 				const int pa = wave_excl_scan(ua, &tota), pb = wave_excl_scan(ub, &totb);
 				// (write-through: the helper blocks read them in this launch)
@@ -1750,8 +1751,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 			const int mid = (lo + hi) >> 1;
 			if(s_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;
-		unit(v, b.pS_ent[lo], r, c0, c0 + SEG < r ? c0 + SEG : r, false, true, s_uo[lo], s_uo[lo + 1]);
+		const int r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG_S;
+		unit(v, b.pS_ent[lo], r, c0, c0 + SEG_S < r ? c0 + SEG_S : r, false, true, s_uo[lo], s_uo[lo + 1]);
 	}
 	SBound sb;
 	bool have_sb = false, ready = false;
@@ -1884,8 +1885,8 @@ __global__ __launch_bounds__(TB) void k_dnj_sphase(const typename Elem<ET>::T *_
 			const int mid = (lo + hi) >> 1;
 			if(s_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;
-		const int c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG_S;
+		const int c1 = c0 + SEG_S < r ? c0 + SEG_S : r;
 		const double sDr = b.sD[r];
 		const T *row = D + tri(r);
 		double q = DBL_MAX;
@@ -2043,8 +2044,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 			const int mid = (lo + hi) >> 1;
 			if(s_uo[mid] <= v) lo = mid; else hi = mid;
 		}
-		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG;   // SEG-cell S units
-		const int c1 = c0 + SEG < r ? c0 + SEG : r;
+		const int e = b.pS_ent[lo], r = b.pS_row[lo], c0 = (v - s_uo[lo]) * SEG_S;   // SEG-cell S units
+		const int c1 = c0 + SEG_S < r ? c0 + SEG_S : r;
 		const double sDr = b.sD[r];
 		const T *row = D + tri(r);
 		double q = DBL_MAX;

@@ -1594,7 +1594,7 @@ __global__ __launch_bounds__(TB) void k_hnj_update(typename Elem<ET>::T *__restr
 // returns its bytes, and with m != NULL points b's arrays into it.
 static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	const size_t nb = (size_t) cdiv(n, TB) + 1;
-	const size_t maxu = cdiv(n, SEG) + 1;
+	const size_t maxu = cdiv(n, SEG_S) + 1;   // S rows' units (SEG_S cells)
 	// every row below S may qualify: room for n entries and their units
 	const size_t ncand = (size_t) n + 257;
 	// entry e's rescan units are [e umax, (e + 1) umax) (k_dnj_scan): room for
