@@ -1801,14 +1801,14 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 			if(cmp && prune == 2) {
 				switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 2, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
-					SV_(1) SV_(5)
+					SV_(1) SV_(5) SV_(7) SV_(13)
 #undef SV_
 					default: k_dnj_scan_v<ET, DenseRows, NoTail, 0, 2, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 				}
 			} else if(cmp) {
 				switch(sm) {
 #define SV_(M) case 4 + M: k_dnj_scan_v<ET, DenseRows, NoTail, M, 0, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg); break;
-					SV_(1) SV_(5)
+					SV_(1) SV_(5) SV_(7) SV_(13)
 #undef SV_
 					default: k_dnj_scan_v<ET, DenseRows, NoTail, 0, 0, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
 				}
