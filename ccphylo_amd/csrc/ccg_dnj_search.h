@@ -144,10 +144,11 @@ struct DnjGrid {
 	// matrices are latency-bound: 128 top rows, no bands; beyond s_split_n the
 	// bands cut the rescanned cells several-fold (tools/sim_stages.c)
 	int top(int n) const {
-		// band mode: 8 top rows (round 4; 16 before): more of the top rows left to the listing and
-		// pruning under the band rows' bounds -- headline tree 5.64 -> 5.51 s profiled (engine cells 1.31 ->
-		// 1.16x the reference's), configs[3]'s first 20k joins 5.67 -> 5.62 s
-		const int t = s_top ? s_top : n > s_split_n ? 8 : DNJ_B;
+		// (round 4: 8 top rows in band mode measured the same as 16 at the headline; band mode with pruning
+		// below 16384 taxa -- CCG_S_TOP=8 CCG_S_BANDS=64 -- took its tree 5.64 -> 5.43-5.51 s profiled, engine
+		// cells 1.31 -> 1.16x, but costs configs[1]'s Euclidean trees, and switching band mode per window
+		// needs the requeue and the next plan to agree; not done)
+		const int t = s_top ? s_top : n > s_split_n ? 16 : DNJ_B;
 		return t < 1 ? 1 : t > DNJ_B ? DNJ_B : t;
 	}
 	int bands(int n) const {
