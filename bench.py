@@ -86,8 +86,8 @@ def _latest(*names):
     return os.path.join(ROOT, "profiles", names[-1])
 
 
-PMC_SUMMARY = _latest("r04_pmc.json", "r03_pmc.json", "r02_pmc.json")
-PMC_HEADLINE = _latest("r04_pmc_headline.json", "r03_pmc_headline.json")
+PMC_SUMMARY = _latest("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc.json")
+PMC_HEADLINE = _latest("r05_pmc_headline.json", "r04_pmc_headline.json", "r03_pmc_headline.json")
 SHARD_LEG_TIMEOUT_S = 600
 HEADLINE_TIMEOUT_S = 1200
 
@@ -143,20 +143,23 @@ def effective_cores():
 from tools.synth import euclid as euclid_ltd  # noqa: E402
 
 
-def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan):
+def algorithmic_bytes_total(kernel, n, s, cells_select, cells_scan, cells_help=0):
     """Compulsory HBM bytes of all launches of one class over a whole tree
     (joins at matrix sizes n .. 3); DESIGN.md, 'Roofline accounting'.
-    s = bytes per D element; the n-vectors are f64 (sD, Q) and i32 (N, P)."""
+    s = bytes per D element; the n-vectors are f64 (sD, Q) and i32 (N, P).
+    cells_help: the S cells k_dnj_plan's helper blocks rescanned (pruning,
+    single engine, stats[8 + 2 NKSTAT]): the plan's bytes, not the scan's."""
     sizes = range(3, n + 1)
     sn = float(sum(sizes))
     if kernel == "dnj_select":      # (sharded engine) rescanned D cells of S + the sD vector once
         return s * cells_select + 8.0 * sn
     if kernel == "dnj_scan":        # one GPU: every rescanned D cell (S and the rows below it) + the sD vector once
-        return s * (cells_select + cells_scan) + 8.0 * sn
+        return s * (cells_select + cells_scan - cells_help) + 8.0 * sn
     if kernel == "dnj_scan_ref":    # SURVEY 8(d): the cells the reference's minQpair rule rescans (cells_scan)
         return s * cells_scan + 8.0 * sn
     if kernel == "dnj_find":        # k_dnj_plan: Q of every row; P, the partner cell, sD of row and partner
-        return 8.0 * sn + (20.0 + s) * float(sum(min(k - 1, 960) for k in sizes))   # for the top rows
+        # for the top rows; the helpers' S rescans (row cells + the sD gathers per cell)
+        return 8.0 * sn + (20.0 + s) * float(sum(min(k - 1, 960) for k in sizes)) + (s + 8.0) * cells_help
     if kernel == "nj_argmin":       # every LT cell + sD
         return sum(s * k * (k - 1) / 2 + 8.0 * k for k in sizes)
     if kernel == "update":          # D_ik, D_kj read, D_kj written; sD, N read+written
@@ -184,7 +187,7 @@ def pmc_traffic(kernel):
         return None, None
 
 
-KERNEL_STATS = _latest("r04_kernel_stats.csv", "r03_kernel_stats.csv", "r02_kernel_stats.csv")
+KERNEL_STATS = _latest("r05_kernel_stats.csv", "r04_kernel_stats.csv", "r03_kernel_stats.csv", "r02_kernel_stats.csv")
 KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
         "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop", "exact_sum": "k_exact_sum"}
 
@@ -228,7 +231,9 @@ def roofline(stats, n, s):
             per[name] = (cnt, ns)
     name = max(per, key=lambda k: per[k][1])
     cnt, ns = per[name]
-    tot = algorithmic_bytes_total(name, n, s, stats[4 + 2 * len(KNAMES)], stats[5 + 2 * len(KNAMES)])
+    K = len(KNAMES)
+    ch = stats[8 + 2 * K] if len(stats) > 8 + 2 * K else 0   # single engine only (sharded: init bytes)
+    tot = algorithmic_bytes_total(name, n, s, stats[4 + 2 * K], stats[5 + 2 * K], ch)
     avg_s = ns / cnt / 1e9
     achieved = tot / cnt / avg_s / 1e9
     shares = {k: round(v[1] / sum(x[1] for x in per.values()), 4) for k, v in per.items()}
@@ -236,7 +241,7 @@ def roofline(stats, n, s):
     for k, (c, t) in per.items():   # every kernel class: algorithmic bytes, HIP-event and rocprof rates, PMC bytes
         if k == "init":
             continue
-        ab = algorithmic_bytes_total(k, n, s, stats[4 + 2 * len(KNAMES)], stats[5 + 2 * len(KNAMES)]) / c
+        ab = algorithmic_bytes_total(k, n, s, stats[4 + 2 * K], stats[5 + 2 * K], ch) / c
         ev = t / c / 1e9
         rp = rocprof_mean_us(k)
         kernels[k] = {"algorithmic_bytes_per_launch": round(ab, 1), "avg_launch_us": round(ev * 1e6, 3),
@@ -759,7 +764,7 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
     return out
 
 
-HEADLINE_STATS = _latest("r04_kernel_stats_headline.csv", "r03_kernel_stats_headline.csv")
+HEADLINE_STATS = _latest("r05_kernel_stats_headline.csv", "r04_kernel_stats_headline.csv", "r03_kernel_stats_headline.csv")
 HSYM = {"dist": ("k_snp_mfma2",), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan", "k_dnj_scan_g"),
         "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join_pf", "k_dnj_join"), "dnj_requeue": ("k_dnj_requeue",),
         "exact_sum": ("k_exact_sum",), "dnj_select": ("k_dnj_select",), "init": ("k_init_rows",)}
@@ -800,31 +805,38 @@ def headline_profile_evidence(kernel):
     return out
 
 
-def headline_roofline(n, L, elems, dist_kernel_ms, dist_launches, pst, world):
+def headline_roofline(n, L, positions, elems, dist_kernel_ms, dist_launches, pst, world):
     """Every kernel of the headline step with its roofline; the dominant one
     (largest device time per step) is the line's `roofline`.
-    dist: 6 flops (3 MX-fp4 MACs) per position pair, this rank's cells x L,
-    against the MX-fp4 dense peak; tree kernels: SURVEY 8(d) bytes (the
-    engine's own rescanned cells for the scans), against 8 TB/s."""
+    dist: 6 flops (3 MX-fp4 MACs) per position pair, this rank's cells x the
+    positions the kernel compares (the included ones: k_planes compacts the
+    excluded words away, so the MFMAs never see them), against the MX-fp4
+    dense peak; tree kernels: SURVEY 8(d) bytes (the engine's own rescanned
+    cells for the scans), against 8 TB/s."""
     kernels = {}
-    tf = FLOPS_PER_POSITION_PAIR * elems * float(L) / (dist_kernel_ms / 1e3) / 1e12
+    fl = FLOPS_PER_POSITION_PAIR * elems * float(positions)
+    tf = fl / (dist_kernel_ms / 1e3) / 1e12
     d = {"kernel": "k_snp_mfma2", "bound": "mfma", "achieved": round(tf, 1),
          "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4),
          "frac_of_measured_issue_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
          "step_ms": round(dist_kernel_ms, 2), "launches": dist_launches,
          "avg_launch_ms": round(dist_kernel_ms / dist_launches, 3),
-         "flops_per_launch": FLOPS_PER_POSITION_PAIR * elems * float(L) / dist_launches,
-         "algorithm": "6 flops per position pair (tetrahedron MX-fp4 form, dist = (3 L - dot) / 4), "
-                      "position pairs = LT cells x L"}
+         "flops_per_launch": fl / dist_launches,
+         "algorithm": f"6 flops per position pair (tetrahedron MX-fp4 form, dist = (3 L - dot) / 4), "
+                      f"position pairs = LT cells x {positions} included positions (of L = {L})"}
     d.update(headline_profile_evidence("dist"))
+    if d.get("rocprof_mean_us"):   # the same count over the committed rocprofv3 mean of the same command
+        d["frac_rocprof_duration"] = round(fl / dist_launches / (d["rocprof_mean_us"] * 1e-6) / 1e12 /
+                                           MFMA_FP4_DENSE_TFLOPS, 4)
     kernels["dist"] = d
     if pst is not None:
         cs, cr = pst[4 + 2 * len(KNAMES)], pst[5 + 2 * len(KNAMES)]
+        ch = pst[8 + 2 * len(KNAMES)] if world == 1 else 0   # plan helpers' S cells (single engine)
         for c, name in enumerate(KNAMES):
             cnt, ns = pst[4 + 2 * c], pst[5 + 2 * c]
             if not cnt or name == "coll":
                 continue
-            ab = algorithmic_bytes_total(name, n, 8, cs, cr) / (world if name in ("init",) else 1)
+            ab = algorithmic_bytes_total(name, n, 8, cs, cr, ch) / (world if name in ("init",) else 1)
             gbs = ab / (ns / 1e9) / 1e9
             k = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(gbs / HBM_PEAK_GBS, 5), "step_ms": round(ns / 1e6, 2), "launches": cnt,
@@ -1035,7 +1047,8 @@ def main():
     # dist launches per call (snp_launch_mfma2: 256 x 256 tiles in batches of
     # 65536; no split-K at the headline's tile count)
     tiles = (-(-n // 256)) * (-(-n // 256) + 1) // 2 // world
-    roof = headline_roofline(n, L, elems, head["dist_kernel_ms"], max(1, -(-tiles // 65536)), pst, world)
+    roof = headline_roofline(n, L, head["included_positions"], elems, head["dist_kernel_ms"],
+                             max(1, -(-tiles // 65536)), pst, world)
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
         "value": round(m * args.steps / dt, 1),

@@ -56,6 +56,10 @@ struct DnjGrid {
 	int prune_on = 1;
 	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
+	// tests only (CCG_TEST_WITHHOLD): bit 0, k_dnj_plan's block 0 never publishes its entry count (the
+	// listing blocks' look-back must time out into an error); bit 1, it never tags the S header (the
+	// helper blocks' wait must); either shortens the bounded spins so that the error comes quickly
+	int test_withhold = 0;
 	int join_pf = 1;   // with k_dnj_fold: k_dnj_join_pf (0: k_dnj_join; 2: its block-0 replay path always)
 	// measured at the headline (configs[2], 50k, profiled tree; round 4): scan + fold per join 68.3 us with
 	// k_dnj_fold, 72.4 with FoldTail, 84.2 with FoldTail + pruning (cells 2.12x -> 1.27x the reference's:
@@ -93,12 +97,14 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_REGSEL")) plan_regsel = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_FR")) plan_fr = atoi(e) < 1 ? 1 : atoi(e) > FIND_RPT ? FIND_RPT : atoi(e);
+		if(const char *e = getenv("CCG_TEST_WITHHOLD")) test_withhold = atoi(e) & 3;
 	}
-	// k_dnj_plan's last argument: the Q-load delay (low 16 bits), bit 16 turns
+	// k_dnj_plan's last argument: the Q-load delay (low 14 bits), bits 14-15 the
+	// test knob test_withhold, bit 16 turns
 	// the register S selection off (on with CCG_PLAN_REGSEL=1)
 	// and bits 17-20 the rows per thread per listing step less one (CCG_PLAN_FR)
 	int plan_flags(bool prune = false, int helpers = 0) const {
-		return (plan_qdelay & 0xffff) | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17 | (prune ? 1 << 21 : 0) |
+		return (plan_qdelay & 0x3fff) | (test_withhold & 3) << 14 | (plan_regsel ? 0 : 1 << 16) | ((plan_fr - 1) & 15) << 17 | (prune ? 1 << 21 : 0) |
 		       (helpers & 511) << 22;
 	}
 	// k_dnj_plan's grid: one listing step of (TBF - 64) FIND_RPT rows per block
@@ -399,7 +405,7 @@ __device__ __forceinline__ void s_table_h(const TreeBufs &b, int n, int nS, doub
 
 template <int ET>
 __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__restrict__ D, double bs,
-                                                        TreeBufs b, int n, int hb, int nh) {
+                                                        TreeBufs b, int n, int hb, int nh, bool tshort) {
 	typedef typename Elem<ET>::T T;
 	constexpr int UC = 8;   // (16: the plan kernel's registers spill further, 30.8 -> 33.4 us per plan at 50k)
 	__shared__ int h_ok, h_nS, h_isub;
@@ -409,7 +415,7 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 	if(b.ctl->done) return;   // (block-uniform; the plan's blocks return too)
 	if(tid == 0) {
 		bool ok = false;
-		for(int spin = 0; spin < (1 << 18); ++spin) {
+		for(int spin = 0; spin < (tshort ? 1 << 10 : 1 << 18); ++spin) {
 			if(__hip_atomic_load(b.shdr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned long long) n) {
 				ok = true;
 				break;
@@ -417,6 +423,15 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 			__builtin_amdgcn_s_sleep(4);
 		}
 		h_ok = ok;
+		if(!ok) {
+			// never expected (block 0 runs before its helpers): other helpers may
+			// already have counted S units in (ecS, scnt) that this block's units
+			// will never complete, so the bound table of this join and the
+			// counters of the next would be wrong; stop the loop with an error
+			// (tree_run_t) as k_dnj_plan's own look-back does
+			b.ctl->final_n = -1;
+			b.ctl->done = 1;
+		}
 		if(ok) {
 			h_m0 = __longlong_as_double(
 			    (long long) __hip_atomic_load(b.shdr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -548,7 +563,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// S's rescans and the bound table while the listing blocks list
 	const int nhelp = (qdelay >> 22) & 511;
 	if((int) blockIdx.x >= (int) gridDim.x - nhelp) {
-		plan_s_helper<ET>(D, bs, b, n, (int) blockIdx.x - ((int) gridDim.x - nhelp), nhelp);
+		plan_s_helper<ET>(D, bs, b, n, (int) blockIdx.x - ((int) gridDim.x - nhelp), nhelp, (qdelay >> 14) & 3);
 		return;
 	}
 	const int nblk = gridDim.x - nhelp, bid = blockIdx.x, bstep = bid * (LT * fr), stride = nblk * (LT * fr);
@@ -566,7 +581,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 	// every entry flagged (eS) and each S row's entry index recorded
 	const bool prune = BANDS && ((qdelay >> 21) & 1);
 	const int nhelp_ = (qdelay >> 22) & 511;
-	qdelay &= 0xffff;
+	// tests (DnjGrid::test_withhold): block 0 withholds its count (bit 14) or the
+	// S header's tag (bit 15); the bounded spins are then short
+	const bool wh_cnt = (qdelay >> 14) & 1, wh_hdr = (qdelay >> 15) & 1;
+	const int spin_max = wh_cnt || wh_hdr ? 1 << 12 : 1 << 24;
+	qdelay &= 0x3fff;
 	double qv[FR];
 	const int rt = top - lt;
 	bool have_rt = false;
@@ -885,6 +904,9 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				if(lane == 0)
 					__hip_atomic_store(b.pS_uo + nS, tota + totb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				if(nhelp_) {   // the S header, then its tag, for the helper blocks
+					// (S's cells, which the helpers rescan: the plan's bytes in the roofline)
+					const long long hc = wave_sum_int((long long) (ta < nS ? sS[ta] : 0) + (tb < nS ? sS[tb] : 0));
+					if(lane == 0 && hc) atomicAdd((unsigned long long *) &ctl->cells_help, (unsigned long long) hc);
 					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 					if(lane == 0) {
 						__hip_atomic_store(b.shdr + 0, (unsigned long long) __double_as_longlong(m0), __ATOMIC_RELAXED,
@@ -894,7 +916,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 						__hip_atomic_store(b.shdr + 2, ((unsigned long long) (unsigned) isub << 32) | (unsigned) nS,
 						                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 						asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-						__hip_atomic_store(b.shdr + 3, (unsigned long long) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						if(!wh_hdr)
+							__hip_atomic_store(b.shdr + 3, (unsigned long long) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					}
 				}
 			}
@@ -1147,7 +1170,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				if(nblk > 1) {
 					// publish this block's count, then the lower blocks' counts
 					// (dispatched before this block, they never wait on it)
-					if(lane == 0)
+					if(lane == 0 && !(wh_cnt && bid == 0))
 						__hip_atomic_store(b.ppub + bid, ((unsigned long long) n << 32) | (unsigned) tot,
 						                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					int off = 0;
@@ -1162,7 +1185,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 								ok = (int) (u >> 32) == n;
 							}
 							if(__all(ok)) break;
-							if(spin > (1 << 24)) {
+							if(spin > spin_max) {
 								stuck = true;
 								break;
 							}
@@ -1217,24 +1240,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			if(base - stride < 1) break;
 			__syncthreads();   // s_mw is reused by the next step
 		}
-	} else if(nblk > 1 && tid == 0) {
-		// nothing to list in this block: its count is 0, and the last block
-		// still needs the lower blocks' counts for the total
-		__hip_atomic_store(b.ppub + bid, (unsigned long long) n << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		if(bid == nblk - 1) {
-			int off = 0;
-			for(int g = 0; g < bid; ++g) {
-				unsigned long long u = 0;
-				for(int spin = 0; spin <= (1 << 24); ++spin) {
-					u = __hip_atomic_load(b.ppub + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					if((int) (u >> 32) == n) break;
-					__builtin_amdgcn_s_sleep(1);
-				}
-				off += (int) (u >> 32) == n ? (int) (u & 0xffffffffu) : 0;
-			}
-			T += off;
-		}
 	}
+	// (nothing to list: smin <= 1.  Every block took the same branch -- smin
+	// comes from the prologue every block runs on identical inputs, and
+	// plan_blocks keeps top - bstep >= 1 for every block -- so every block's
+	// count is 0 and the last block's T = ntop needs no look-back)
 	TS(1, 3);
 	mycells = wave_sum_int(mycells);
 	if(lane == 0 && mycells) {
@@ -1849,7 +1859,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		TS_U(2 * nu + 1);
 		++nu;
 	}
-	if(PRUNE && pruned && lane == 0)   // (uniform: every lane counted the same units)
+	// (uniform: every lane counted the same units; with PRUNE 2 k_dnj_sphase
+	// already counted the pruned entries' whole rows)
+	if(PRUNE == 1 && pruned && lane == 0)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
 	TS(2, 2);
 	TS_SAMP(2);
@@ -2183,6 +2195,120 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 	}
 	if(PRUNE && pruned && lane == 0)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
+}
+
+// Row groups over a dense enumeration (scan_mode 20-23 with the compacted
+// form, the single engine's default for float / u16 / u8 rows past 16384
+// taxa): the entries to rescan -- every listed entry, or with pruning
+// (PRUNE2, k_dnj_sphase ran) only the survivors k_dnj_sphase appended to
+// their unit-count buckets -- are taken in descending unit count (bucket u
+// holds the entries with exactly u units; entry order inside a bucket is
+// free) and cut into groups of G consecutive ones.  Slot k of the
+// enumeration holds the groups whose first entry has more than k units
+// (ceil(E_k / G) of them, E_k = the entries with more than k units, a prefix
+// of the order), so the real (group, unit) pairs are numbered densely,
+// slot-major, and dealt round-robin over a grid that is resident at once.
+// One wave rescans the same seg-cell column range of its group's rows
+// (k_dnj_scan_g's body: one sD load serves G rows); each row's (q, j) goes
+// to its unit partial, which k_dnj_fold folds (pruned entries and S's, which
+// k_dnj_sphase / the plan's helpers settled, have no units here).
+template <int ET, int G, int UC, bool PRUNE2>
+__global__ __launch_bounds__(TB) void k_dnj_scan_gc(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
+                                                    int n, int seg) {
+	typedef typename Elem<ET>::T T;
+	const TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int done = ctl->done, Tn = ctl->T;
+	if(done || Tn == 0) return;   // (block-uniform)
+	const int umax = dnj_umax(n, seg);
+	const int nSp = PRUNE2 ? ctl->pS : 0;
+	const bool surv = PRUNE2 && nSp > 0;   // k_dnj_sphase left the survivors in blist (else: every entry, e = p)
+	const int gw = blockIdx.x * (TB / 64) + (tid >> 6), nw = gridDim.x * (TB / 64);
+	// lane u: H = listed entries with exactly u units (the plan's histogram, summed over its blocks);
+	// bucket u's survivors sit at blist[Eall(u) ...), cnt(u) of them (k_dnj_sphase)
+	int H = 0;
+	const int pb = ctl->pblk;
+	for(int g = 0; g < pb; ++g) H += b.uhist[g * UHIST + lane];
+	const int inch = wave_incl_sum(H), Eall = __builtin_amdgcn_readlane(inch, 63) - inch;
+	const int cnt = surv ? b.bcnt[lane] : H;
+	const int incc = wave_incl_sum(cnt), totc = __builtin_amdgcn_readlane(incc, 63);
+	const int Es = totc - incc;        // entries (survivors) with more than `lane` units: a prefix of the order
+	const int C = Es + cnt;            // ... with at least `lane` units
+	const int NG = (Es + G - 1) / G;   // slot `lane`'s groups
+	int R;
+	const int PG = wave_excl_scan(NG, &R);
+	for(int v = gw; v < R; v += nw) {
+		const int k = 63 - __clzll((long long) __ballot(NG > 0 && PG <= v));   // the slot (uniform)
+		const int grp = v - __shfl(PG, k), EsK = __shfl(Es, k);
+		const int c0 = k * seg;
+		int r[G], e[G], c1[G];
+		bool act[G];
+		int cmax = c0;
+#pragma unroll
+		for(int t = 0; t < G; ++t) {
+			const int pos = grp * G + t;
+			act[t] = pos < EsK;   // (uniform) this member has unit k
+			e[t] = 0;
+			r[t] = 1;
+			if(act[t]) {
+				if(surv) {
+					// the bucket: the highest u > k with C(u) > pos (C non-increasing in u)
+					const int ub = 63 - __clzll((long long) __ballot(lane > k && C > pos));
+					const int pin = pos - (__shfl(C, ub) - __shfl(cnt, ub));
+					e[t] = b.blist[__shfl(Eall, ub) + pin];
+				} else {
+					e[t] = pos;   // the entry list is in descending rows: already in bucket order
+				}
+				r[t] = b.crow[e[t]];
+			}
+			c1[t] = act[t] ? (c0 + seg < r[t] ? c0 + seg : r[t]) : c0;
+			cmax = c1[t] > cmax ? c1[t] : cmax;
+		}
+		double sDr[G], q[G];
+		int idx[G];
+		const T *row[G];
+#pragma unroll
+		for(int t = 0; t < G; ++t) {
+			sDr[t] = act[t] ? b.sD[r[t]] : 0.0;
+			row[t] = D + tri(act[t] ? r[t] : 1);
+			q[t] = DBL_MAX;
+			idx[t] = 0;
+		}
+		for(int base = c0; base < cmax; base += 64 * UC) {
+			double sk[UC];
+			T vv[G][UC];
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+				sk[m] = b.sD[c < cmax ? c : cmax - 1];
+#pragma unroll
+				for(int t = 0; t < G; ++t) vv[t][m] = row[t][c < c1[t] ? c : (act[t] ? c1[t] - 1 : 0)];
+			}
+#pragma unroll
+			for(int m = 0; m < UC; ++m) {
+				const int c = base + 64 * m + lane;
+#pragma unroll
+				for(int t = 0; t < G; ++t) {
+					const double d = Elem<ET>::get(vv[t][m], bs);
+					const double x = qcrit(n, n, d, sDr[t], sk[m]);
+					const bool take = c < c1[t] && 0 <= d && qarg_better(x, c, q[t], idx[t]);
+					q[t] = take ? x : q[t];
+					idx[t] = take ? c : idx[t];
+				}
+			}
+		}
+#pragma unroll
+		for(int t = 0; t < G; ++t) {
+			if(!act[t]) continue;   // wave-uniform
+			double qq = q[t];
+			int ii = idx[t];
+			qarg_wave_reduce(qq, ii);
+			if(lane == 0) {
+				b.cq[e[t] * umax + k] = qq;
+				b.cj[e[t] * umax + k] = ii;
+			}
+		}
+	}
 }
 
 // ------------------------------------------------------------------ DNJ fold

@@ -43,6 +43,7 @@ struct TreeCtl {
 	int pS;              // S rows whose exact fresh minima prune the scan (0: no pruning this join)
 	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
 	long long cells_pruned;  // listed cells the scan skipped under the S bound table
+	long long cells_help;    // S cells rescanned inside k_dnj_plan by its helper blocks (scan_prune 2)
 	int vtag;            // VBLK: the matrix size whose join the requeue's bmv minima serve
 	int pblk;            // k_dnj_plan's block count (rows of uhist this join)
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)

@@ -46,7 +46,7 @@
 
 #include "ccg_dnj_search.h"
 
-static DnjGrid g_grid;   // loaded per tree run
+static thread_local DnjGrid g_grid;   // loaded per tree run (per host thread: tree_run_t adapts it per window)
 
 // ------------------------------------------------------------------ init
 // nj.c:111 initSummaD: per row, the row part (m < k) then the column part
@@ -1742,7 +1742,9 @@ static int dnj_prune(int n, int et, bool gen) {
 	const int sm = g_grid.scan_mode(n, et);
 	if(gen || !g_grid.bands(n) || !g_grid.prefold(n)) return 0;
 	if(g_grid.scan_prune == 1 && g_grid.scan_fold && ((sm >= 4 && sm < 20) || (sm >= 20 && sm <= 23))) return 1;
-	if(g_grid.scan_prune == 2 && g_grid.prune_on && !g_grid.scan_fold && sm >= 4 && sm < 20) return 2;
+	// prune 2 with the row groups: the compacted group scan (k_dnj_scan_gc) enumerates the survivors
+	const bool gcmp = sm >= 20 && sm <= 23 && g_grid.scan_cmp && dnj_umax(n, g_grid.seg(n)) < UHIST;
+	if(g_grid.scan_prune == 2 && g_grid.prune_on && !g_grid.scan_fold && ((sm >= 4 && sm < 20) || gcmp)) return 2;
 	return 0;
 }
 
@@ -1777,7 +1779,21 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int prune = dnj_prune(n, ET, GEN);
 		if(prune == 2 && g_grid.plan_help) k_dnj_sphase<ET, false><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
 		else if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
-		if(sm >= 20 && sm <= 23 && !GEN) {
+		if(sm >= 20 && sm <= 23 && !GEN && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
+			// row groups over the dense (group, unit) enumeration; with pruning, the survivors only
+			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
+			if(prune == 2) {
+				if(sm == 20) k_dnj_scan_gc<ET, 4, 8, true><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 21) k_dnj_scan_gc<ET, 8, 4, true><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 22) k_dnj_scan_gc<ET, 4, 4, true><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else k_dnj_scan_gc<ET, 2, 8, true><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+			} else {
+				if(sm == 20) k_dnj_scan_gc<ET, 4, 8, false><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 21) k_dnj_scan_gc<ET, 8, 4, false><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else if(sm == 22) k_dnj_scan_gc<ET, 4, 4, false><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+				else k_dnj_scan_gc<ET, 2, 8, false><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+			}
+		} else if(sm >= 20 && sm <= 23 && !GEN) {
 			if(prune) {
 				if(sm == 20) k_dnj_scan_g<ET, 4, 8, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
 				else if(sm == 21) k_dnj_scan_g<ET, 8, 4, true, true><<<gc, TB, 0, st>>>(D, bs, b, n, seg);
@@ -2110,7 +2126,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 #endif
 	if(h.done && h.final_n < 0) {   // k_dnj_plan's look-back timed out (never expected)
 		hipFree(w.mem);
-		ccg_set_last_msg("k_dnj_plan / k_dnj_join: a block's wait on a lower block timed out");
+		ccg_set_last_msg("k_dnj_plan / k_dnj_join: a block's bounded wait on another block timed out");
 		return CCG_EHIP;
 	}
 	*njoins = h.njoins;
@@ -2126,9 +2142,11 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
 	}
 	if(sout) {   // the loop state after the last join, as the next minQpair reads it
-		sout->n = h.done ? 0 : n;
+		// (a finished tree, n == 2, has no next join: n = 0 as for a stopped one)
+		const bool over = h.done || n <= 2;
+		sout->n = over ? 0 : n;
 		sout->cand = 0;
-		if(!h.done) {
+		if(!over) {
 			if(n != n0) {
 				// the next join's plan prologue folds the last requeue's partials
 				// into Q/P of rows j and i (and moves row n's sD/N to i) and
@@ -2162,7 +2180,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest - h.cells_pruned;
 			stats[6 + 2 * CCG_NKSTAT] = h.serial_sums;
 			stats[7 + 2 * CCG_NKSTAT] = h.chain_sums;
-			stats[8 + 2 * CCG_NKSTAT] = 0;
+			stats[8 + 2 * CCG_NKSTAT] = h.cells_help;
 			stats[9 + 2 * CCG_NKSTAT] = 0;
 			stats[10 + 2 * CCG_NKSTAT] = h.ref_rows;
 			stats[11 + 2 * CCG_NKSTAT] = h.ref_cells;

@@ -173,8 +173,10 @@ typedef struct {
  * cells rescanned by CCG_K_TOP and [5+2*CCG_NKSTAT] by CCG_K_REST;
  * [6+2*CCG_NKSTAT] exact row sums that needed the serial order,
  * [7+2*CCG_NKSTAT] of those computed by the serial chain (the parallel form
- * declined); sharded engines only: [8+2*CCG_NKSTAT] bytes this rank put into
- * the initSummaD collectives, [9+2*CCG_NKSTAT] columns whose column part
+ * declined); [8+2*CCG_NKSTAT]: single engine, the cells of S (part of [1])
+ * that k_dnj_plan's helper blocks rescanned (pruning, CCG_K_FIND's bytes);
+ * sharded engines, the bytes this rank put into the initSummaD collectives;
+ * sharded engines only: [9+2*CCG_NKSTAT] columns whose column part
  * went through the serial gather (the rest are exact sums of per-rank
  * statistics); DNJ: [10+2*CCG_NKSTAT] rows and [11+2*CCG_NKSTAT] cells that
  * the reference's own minQpair rule rescans (dnj.c:78, a row whose stored Q is
@@ -222,7 +224,8 @@ typedef struct {
  * a->max_joins joins, D_dev then holding its LT.  A run from `in` makes the
  * joins the uninterrupted run makes after the same state (bit-identical; the
  * reference has no checkpoint, so this is its loop split in two).  The single
- * GPU engine only (no sharding); out->n = 0 if the loop stopped (pos == 0). */
+ * GPU engine only (no sharding); out->n = 0 if the loop stopped (pos == 0)
+ * or finished (n == 2: no join is left to resume). */
 int ccg_tree_dev_state(ccg_ctx *ctx, const ccg_tree_args *a, void *D_dev, const ccg_dnj_state *in,
                        ccg_dnj_state *out, ccg_join *joins, int *njoins, int *final_n, double *final_d,
                        int64_t *stats);

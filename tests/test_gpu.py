@@ -721,7 +721,38 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
         assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), (prune, vblk)
         cells[prune + vblk] = st[1]
     assert int(rst[1]) <= cells["11"] <= cells["10"] <= cells["00"]
-    if int(mode) < 20:   # the split form prunes exactly as the in-scan one
-        assert (cells["21"], cells["20"]) == (cells["11"], cells["10"])
-    else:
-        assert cells["21"] == cells["20"] == cells["00"]
+    # the split form (the plan's helpers + k_dnj_sphase; for row groups the
+    # compacted group scan k_dnj_scan_gc over the survivors) prunes exactly as
+    # the in-scan one
+    assert (cells["21"], cells["20"]) == (cells["11"], cells["10"])
+    # without the compacted enumeration: the wave scan rechecks the table and
+    # k_dnj_sphase alone counts the pruned cells; row groups then
+    # run unpruned (k_dnj_scan_g)
+    monkeypatch.setenv("CCG_SCAN_PRUNE", "2")
+    monkeypatch.setenv("CCG_SCAN_VBLK", "1")
+    monkeypatch.setenv("CCG_SCAN_FOLD", "0")
+    monkeypatch.setenv("CCG_SCAN_CMP", "0")
+    got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
+    assert (fn, fd) == (rfn, rfd) and (got == ref).all()
+    assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1]))
+    assert st[1] == (cells["21"] if int(mode) < 20 else cells["00"])
+
+
+@pytest.mark.parametrize("withhold", ["1", "2"])
+def test_dnj_plan_wait_timeout_is_an_error(dev, monkeypatch, withhold):
+    """A bounded wait of k_dnj_plan that gives up stops the tree with an
+    error, never a silently different tree: CCG_TEST_WITHHOLD=1 makes block 0
+    withhold its entry count (the other listing blocks' look-back), =2 the S
+    header's tag (the helper blocks' wait for S).  CCG_PLAN_FR=1 gives several
+    listing blocks at n = 3000, band mode with pruning brings the helpers."""
+    from ccphylo_amd import CcgError
+    n = 3000
+    for k, v in (("CCG_SCAN_WAVE", "9"), ("CCG_PREFOLD_N", "0"), ("CCG_SEG_MUL", "1"), ("CCG_S_SPLIT_N", "100"),
+                 ("CCG_PRUNE_CELLS", "0"), ("CCG_PLAN_FR", "1")):
+        monkeypatch.setenv(k, v)
+    D = _clade_ltd(n, 5)
+    got, fn, _, _ = dev.tree(D, n, method=1, exact=True)   # the same settings without the knob: a tree
+    assert fn == 2 and len(got) == n - 2
+    monkeypatch.setenv("CCG_TEST_WITHHOLD", withhold)
+    with pytest.raises(CcgError):
+        dev.tree(D, n, method=1, exact=True)

@@ -162,17 +162,72 @@ def test_config2_dist_and_dnj_prefix(dev):
     _same_joins((got[0], 0, 0), (ref[0], 0, 0), "dnj configs[2] exact prefix")
 
 
-def test_config3_dnj_prefix(dev, monkeypatch):
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _config3_rank(rank, world, port, n, k, out_dir):
+    """One rank of the world-8 rehearsal: its own band shard of configs[3]'s
+    matrix built on the GPU, the sharded DNJ over gloo (HostColl)."""
+    import json
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    from tools.synth import euclid_shard_dev
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = cg.Device(0)
+    loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
+    assert loc.numel() == nt.shard_elems(n, rank, world)
+    torch.cuda.synchronize()
+    coll = nt.HostColl(dist)
+    dist.barrier()
+    t0 = time.perf_counter()
+    joins, fn, fd, st = dev.tree_shard_dev(loc.data_ptr(), n, coll, etype=4, method=cg.CCG_TREE_DNJ, exact=True,
+                                           max_joins=k, profile=True)
+    dt = time.perf_counter() - t0
+    np.save(os.path.join(out_dir, f"j{rank}.npy"), joins)
+    K = nt.NKSTAT
+    with open(os.path.join(out_dir, f"s{rank}.json"), "w") as f:
+        json.dump({"rank": rank, "shard_GB": round(loc.numel() * 4 / 1e9, 3), "tree_s": round(dt, 2),
+                   "init_coll_bytes": int(st[8 + 2 * K]), "hard_columns": int(st[9 + 2 * K]),
+                   "ref_rows": int(st[10 + 2 * K]), "ref_cells": int(st[11 + 2 * K]),
+                   "coll_calls": coll.calls, "coll_bytes": coll.bytes}, f)
+    del loc
+    dev.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config3_dnj_prefix(dev, monkeypatch, tmp_path):
     """configs[3]: N = 200k Euclidean (seed 4), float (`-p`, 80 GB), exact DNJ
     against the oracle's serial minQpair (threaded rescans, same decisions):
-    the single engine's default float path (row-group rescans k_dnj_scan_g,
-    k_dnj_fold, k_dnj_join_pf) over the first 2000 joins, and the row-sharded
-    kernels at world 1 (band layout = the packed LT) over the first 500."""
+    the single engine's default float path (row-group rescans over the
+    compacted enumeration k_dnj_scan_gc with pruning, k_dnj_fold,
+    k_dnj_join_pf) over the first 2000 joins; the row-sharded kernels at
+    world 1 (band layout = the packed LT) over the first 500; and configs[3]'s
+    own world size rehearsed on the one GPU: 8 rank processes,
+    each building its 10 GB band shard on the GPU (tools/synth.euclid_shard_dev)
+    and running ccg_tree_shard_dev over gloo (HostColl: every exchange of the
+    8-GPU run, host-staged), the first 1000 joins, every rank's joins equal to
+    the oracle's and to the single engine's.  Reference: dnj.c:985-1052."""
+    import json
     import torch
+    import torch.multiprocessing as mp
     import ccphylo_amd as cg
     from oracle import pyoracle
     from tools.synth import euclid_shard_dev
-    n, k, ks = 200_000, 2000, 500
+    n, k, ks, kw, world = 200_000, 2000, 500, 1000, 8
     got = {}
     for force, kk in (("0", k), ("1", ks)):
         monkeypatch.setenv("CCG_SHARD_FORCE", force)
@@ -183,10 +238,26 @@ def test_config3_dnj_prefix(dev, monkeypatch):
                                         max_joins=kk)
         del loc
         torch.cuda.empty_cache()
+    mp.start_processes(_config3_rank, args=(world, _free_port(), n, kw, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
     assert len(ref[0]) == k
     _same_joins((got["0"][0], 0, 0), (ref[0], 0, 0), "single engine dnj 200k float exact prefix")
     _same_joins((got["1"][0], 0, 0), (ref[0][:ks], 0, 0), "sharded dnj 200k float exact prefix")
+    recs = []
+    for r in range(world):
+        jr = np.load(tmp_path / f"j{r}.npy")
+        _same_joins((jr, 0, 0), (ref[0][:kw], 0, 0), f"world-8 rank {r} dnj 200k float exact prefix")
+        assert (jr == got["0"][0][:kw]).all()
+        recs.append(json.load(open(tmp_path / f"s{r}.json")))
+    # every rank counted the same reference-rule rescans (replicated replay)
+    assert len({(x["ref_rows"], x["ref_cells"]) for x in recs}) == 1
+    rec = {"test": "config3_world8_rehearsal", "n": n, "world": world, "joins": kw, "etype": 4, "exact": True,
+           "transport": "gloo (HostColl), 8 processes on one MI355X", "oracle_identical": True, "ranks": recs}
+    print(json.dumps(rec))
+    if os.environ.get("CCG_CONFIG4_OUT"):
+        with open(os.environ["CCG_CONFIG4_OUT"], "a") as f:
+            f.write(json.dumps(rec) + "\n")
 
 
 def test_config3_single_vs_sharded_prefix(dev, monkeypatch):
@@ -325,14 +396,34 @@ def test_config4_rank_1e6(dev, msa_1e6, rank):
     Dloc = dev.malloc(elems * 4)
     tree_b = None
     try:
-        t0 = __import__("time").perf_counter()
-        inc = dev.snp_ltd_shard(seqs, incs, n, L, Dloc, rank, world, etype=4)
-        dist_s = __import__("time").perf_counter() - t0
+        import threading
+        import time
+        # the dist's HBM high-water mark, sampled: a side thread
+        # polls hipMemGetInfo while ccg_snp_ltd_shard runs (ctypes drops the GIL)
+        low = [free0]
+        stop = threading.Event()
+
+        def poll():
+            while not stop.is_set():
+                f, _ = torch.cuda.mem_get_info()
+                low[0] = min(low[0], f)
+                time.sleep(0.002)
+        th = threading.Thread(target=poll, daemon=True)
+        th.start()
+        t0 = time.perf_counter()
+        try:
+            inc = dev.snp_ltd_shard(seqs, incs, n, L, Dloc, rank, world, etype=4)
+        finally:
+            dist_s = time.perf_counter() - t0
+            stop.set()
+            th.join()
         assert inc == int(np.unpackbits(incs.view(np.uint8)).sum())
         # the planes the dist held beside the shard: kept words (compacted) x 2 bits, rows padded to 256
         Wc = int((incs[:(L + 31) // 32] != 0).sum())
         planes = -(-n // 256) * 256 * (-(-Wc // 16) * 16) * 8
-        peak = elems * 4 + planes + (256 << 20)
+        planned = elems * 4 + planes + (256 << 20)
+        peak = free0 - low[0]   # measured: HBM this test held at the lowest free sample (shard included)
+        assert peak >= elems * 4, (peak, elems * 4)
         assert peak <= 280e9, peak
         lib = pyoracle.lib()
         rng = np.random.default_rng(rank + 1)
@@ -358,7 +449,9 @@ def test_config4_rank_1e6(dev, msa_1e6, rank):
         dev.free(Tb)
         rec = {"n": n, "L": L, "world": world, "rank": rank, "dist_s": round(dist_s, 3), "rank_cells": elems,
                "rank_taxa_pairs_per_s": round(elems / dist_s, 1), "shard_GB": round(elems * 4 / 1e9, 2),
-               "kept_words": Wc, "planes_GB": round(planes / 1e9, 2), "dist_peak_GB": round(peak / 1e9, 2),
+               "kept_words": Wc, "planes_GB": round(planes / 1e9, 2), "dist_peak_GB_measured": round(peak / 1e9, 2),
+               "dist_peak_GB_planned": round(planned / 1e9, 2),
+               "peak_source": "hipMemGetInfo polled every 2 ms on a side thread during ccg_snp_ltd_shard",
                "tree_phase_state_GB": round(tree_b / 1e9, 3),
                "tree_phase_total_GB": round((elems * 4 + tree_b) / 1e9, 2),
                "init_gather_bound_GB": round(gather_b / 1e9, 2),
