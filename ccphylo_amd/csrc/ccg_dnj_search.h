@@ -71,6 +71,9 @@ struct DnjGrid {
 	// inside the scan (with FoldTail, CCG_SCAN_FOLD=1); 0: off.  Headline tree (profiled, round 4):
 	// 6.29 s off, 5.86-5.89 s with 2 while the joins list > 15-30M cells, 6.05 s with 2 throughout
 	int scan_prune = 2;
+	// the block lower bounds (TreeBufs::lbm, lb_unit): kept by the join and the requeue from the first join
+	// of a matrix larger than lb_min_n on (CCG_SCAN_LB=0: off; CCG_LB_MIN_N), used by the compacted wave scan
+	int lb = 1, lb_min_n = 16384;
 	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
 	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {
@@ -98,6 +101,8 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PLAN_REGSEL")) plan_regsel = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_FR")) plan_fr = atoi(e) < 1 ? 1 : atoi(e) > FIND_RPT ? FIND_RPT : atoi(e);
 		if(const char *e = getenv("CCG_TEST_WITHHOLD")) test_withhold = atoi(e) & 3;
+		if(const char *e = getenv("CCG_SCAN_LB")) lb = atoi(e);
+		if(const char *e = getenv("CCG_LB_MIN_N")) lb_min_n = atoi(e);
 	}
 	// k_dnj_plan's last argument: the Q-load delay (low 14 bits), bits 14-15 the
 	// test knob test_withhold, bit 16 turns
@@ -488,36 +493,34 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 		qarg_wave_reduce(q, idx);
 		// fold S row lo at its last unit; the last S row builds the table
 		int s_done = 0;
-		if(lane == 0) {
-			const int ua = h_uo[lo], ub = h_uo[lo + 1];
-			bool last = true;
-			if(ub - ua > 1) {
+		const int ua = h_uo[lo], ub = h_uo[lo + 1];
+		int last = 1;
+		if(ub - ua > 1) {
+			if(lane == 0) {
 				__hip_atomic_store(b.uq + v, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				__hip_atomic_store(b.uj + v, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				const unsigned seen = __hip_atomic_fetch_add(b.ecS + lo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				last = (int) seen == ub - ua - 1;
-				if(last) {
-					for(int x0 = ua; x0 < ub; x0 += 4) {
-						double oq[4];
-						int oi[4];
-#pragma unroll
-						for(int m = 0; m < 4; ++m) {
-							const int x = x0 + m < ub ? x0 + m : ub - 1;
-							oq[m] = __hip_atomic_load(b.uq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-							oi[m] = __hip_atomic_load(b.uj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-						}
-#pragma unroll
-						for(int m = 0; m < 4; ++m) {
-							if(x0 + m < ub && qarg_better(oq[m], oi[m], q, idx)) {
-								q = oq[m];
-								idx = oi[m];
-							}
-						}
-					}
-					__hip_atomic_store(b.ecS + lo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-				}
+				if(last) __hip_atomic_store(b.ecS + lo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
+			last = __shfl(last, 0);
+			if(last) {
+				// the row's partials, one per lane (a top row of S has up to
+				// n / SEG_S of them): one round trip, then the wave's reduce (the
+				// total order of qarg_better makes the fold order free)
+				for(int x = ua + lane; x < ub; x += 64) {
+					const double oq = __hip_atomic_load(b.uq + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					const int oi = __hip_atomic_load(b.uj + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if(qarg_better(oq, oi, q, idx)) {
+						q = oq;
+						idx = oi;
+					}
+				}
+				qarg_wave_reduce(q, idx);
+			}
+		}
+		if(lane == 0) {
 			if(last) {
 				__hip_atomic_store(b.sfq + lo, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				__hip_atomic_store(b.sfj + lo, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1622,10 +1625,85 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // round-robin over a grid that is resident at once, so every wave gets the
 // same number of units to within one (grid-stride over T umax slots left
 // waves with 1 to 4+ units and a second round of blocks).
-template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0, bool CMP = false>
+// One rescan unit, columns [c0, c1) of row r (c0 a multiple of LBW), under
+// the block lower bounds (TreeBufs::lbm / msd): the threshold is the Q
+// criterion at the row's partner cell P[r] evaluated now -- a cell of row r,
+// so >= the row's fresh minimum f_r -- and a 64-column block whose bound
+//     lb = ((n - 2) * m_d - sD_r) - M_sD    (qcrit's operation order)
+// exceeds it holds no cell with q <= f_r (rounding is monotone, m_d <= every
+// cell, M_sD >= every column's sD), so neither the minimum nor a tie the
+// index rule could pick: it is skipped.  The other blocks are rescanned one
+// cell per lane, BB blocks in flight.  Returns the cells skipped.
+template <int ET>
+__device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
+                                       int r, int c0, int c1, double sDr, double &q, int &idx) {
+	typedef typename Elem<ET>::T T;
+	constexpr int BB = 8;
+	const int lane = threadIdx.x & 63;
+	const int pr0 = b.P[r], pr = pr0 >= 0 && pr0 < r ? pr0 : 0;
+	const int bl0 = c0 / LBW, nbk = (c1 - c0 + LBW - 1) / LBW;   // <= seg / 64 <= 256 blocks
+	// the unit's bounds (one or more per lane), loaded with the partner's
+	unsigned lbb[4];
+	double msb[4];
+#pragma unroll
+	for(int h = 0; h < 4; ++h) {
+		const int t = lane + 64 * h;
+		lbb[h] = t < nbk ? b.lbm[(long long) r * b.lbs + bl0 + t] : 0u;
+		msb[h] = t < nbk ? b.msd[bl0 + t] : 0.0;
+	}
+	const double dp = Elem<ET>::get(row[pr], bs), sp = b.sD[pr];
+	const double ub = qcrit(n, n, dp, sDr, sp);
+	unsigned long long need[4];
+#pragma unroll
+	for(int h = 0; h < 4; ++h) {
+		const int t = lane + 64 * h;
+		const double lb = qcrit(n, n, (double) __uint_as_float(lbb[h]), sDr, msb[h]);
+		need[h] = __ballot(t < nbk && !(lb > ub));
+	}
+	int loaded = 0;
+	// the needed blocks, BB at a time (wave-uniform walk of the ballot masks)
+	int h = 0;
+	while(true) {
+		int blk[BB], nb = 0;
+		while(nb < BB && h < 4) {
+			if(!need[h]) {
+				++h;
+				continue;
+			}
+			const int bit = __ffsll((long long) need[h]) - 1;
+			need[h] &= need[h] - 1;
+			blk[nb++] = bl0 + 64 * h + bit;
+		}
+		if(!nb) break;
+		T v[BB];
+		double sk[BB];
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			int c = (m < nb ? blk[m] : blk[0]) * LBW + lane;
+			c = c < c1 ? c : c1 - 1;
+			v[m] = row[c];
+			sk[m] = b.sD[c];
+		}
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const int c = (m < nb ? blk[m] : blk[0]) * LBW + lane;
+			const double d = Elem<ET>::get(v[m], bs);
+			const double x = qcrit(n, n, d, sDr, sk[m]);
+			if(m < nb && c < c1 && 0 <= d && qarg_better(x, c, q, idx)) {
+				q = x;
+				idx = c;
+			}
+		}
+		for(int m = 0; m < nb; ++m) loaded += (blk[m] + 1) * LBW < c1 ? LBW : c1 - blk[m] * LBW;
+	}
+	return (c1 - c0) - loaded;
+}
+
+template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0, bool CMP = false, bool LB = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
 	typedef typename Elem<ET>::T T;
+	static_assert(!(LB && PRUNE == 1), "the block bounds serve the compacted scan (its S units fold elsewhere)");
 	constexpr bool NTL = MODE & 1, PIPE = (MODE & 2) != 0, SDV = (MODE & 4) != 0;
 	constexpr int VEC = 16 / (int) sizeof(T), UV0 = (VEC >= 16 ? 1 : 16 / VEC) * (MODE & 8 ? 2 : 1);
 	constexpr int UV = PIPE && UV0 > 1 ? UV0 / 2 : UV0;
@@ -1666,7 +1744,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		__syncthreads();
 		su = s_uo[nSp];
 	}
-	long long pruned = 0;
+	long long pruned = 0, lbskip = 0;
 	// one unit: columns [c0, c1) of entry e's row r; S-phase units (sent) are
 	// SEG cells with their partials in uq / uj at the S unit index
 	auto unit = [&](int u, int e, int r, int c0, int c1, bool skip, bool sent, int sua, int sub) {
@@ -1679,6 +1757,14 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 		const double sDr = b.sD[r];
 		const long long ro = rows.row(r);
 		const T *row = D + ro;
+		if(LB) {   // the block lower bounds (single engine)
+			double q = DBL_MAX;
+			int idx = 0;
+			lbskip += lb_unit<ET>(row, bs, b, n, r, c0, c1, sDr, q, idx);
+			qarg_wave_reduce(q, idx);
+			tail_unit(tail, b, n, u, ua, ua + dcdiv(r, seg), r, q, idx, e, Tn);
+			return;
+		}
 		const int a = (int) ((VEC - (ro + c0) % VEC) % VEC);
 		const int ca = c0 + a < c1 ? c0 + a : c1;
 		const int nv = (c1 - ca) / VEC, ce = ca + nv * VEC;
@@ -1863,6 +1949,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	// already counted the pruned entries' whole rows)
 	if(PRUNE == 1 && pruned && lane == 0)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
+	if(LB && lbskip && lane == 0) atomicAdd((unsigned long long *) b.lbskip, (unsigned long long) lbskip);
 	TS(2, 2);
 	TS_SAMP(2);
 	TS_EXIT(2);

@@ -44,6 +44,7 @@ struct TreeCtl {
 	unsigned scnt;       // the scan's S entries folded so far (reset by the last)
 	long long cells_pruned;  // listed cells the scan skipped under the S bound table
 	long long cells_help;    // S cells rescanned inside k_dnj_plan by its helper blocks (scan_prune 2)
+	long long cells_lbskip;  // listed cells the scan skipped under the block lower bounds
 	int vtag;            // VBLK: the matrix size whose join the requeue's bmv minima serve
 	int pblk;            // k_dnj_plan's block count (rows of uhist this join)
 	int xs_why[8];       // exact row sums sent to the chain, by reason (XS_WHY_*)
@@ -112,7 +113,25 @@ struct TreeBufs {
 	unsigned *srdy;                 // SRDY_REP copies (one 128-B line each) of the tag n the scan's S bound
 	                                // table is published with; block b polls copy b % SRDY_REP
 	int maxu;
+	// block lower bounds (DNJ, single engine, no missing entries; NULL when
+	// off): lbm[r * lbs + u] = the bits of a float <= every cell of row r in
+	// columns [64u, 64u + 64) (non-negative, so the bits order as the values;
+	// kept conservative by atomicMin where a cell of a column changes),
+	// msd[u] >= sD of every column there (the next join's, left by the
+	// requeue).  The scan skips a 64-column block whose bound of the Q
+	// criterion exceeds the q at the row's partner cell.
+	unsigned *lbm;
+	double *msd;
+	long long lbs;
+	long long *lbskip;   // cells the scan skipped under the block bounds (stats)
 };
+
+#define LBW 64   // columns per block of the lower bounds (one wave)
+
+// a float <= x (x >= 0: a cell value) as order-preserving bits
+__device__ __forceinline__ unsigned lb_bits(double x) {
+	return x > 0.0 ? __float_as_uint(__double2float_rd(x)) : 0u;
+}
 
 
 // the device state of one tree run (one hipMalloc), sized for n taxa
@@ -169,6 +188,27 @@ __device__ __forceinline__ double wave_sum_fixed(double x) {
 __device__ __forceinline__ int wave_sum_int(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
 __device__ __forceinline__ long long wave_sum_int(long long v) { return readlane_l(wave_incl_sum_l(v), 63); }
 __device__ __forceinline__ int wave_min_int(int v) { return __builtin_amdgcn_readlane(wave_incl_min_i(v), 63); }
+// wave minimum of u32 / maximum of f64, the same value in every lane (all lanes active)
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#define S_(C, R)                                                          \
+	{                                                                     \
+		const unsigned t_ = (unsigned) dpp_i<C, R>((int) 0xFFFFFFFFu, (int) v); \
+		v = t_ < v ? t_ : v;                                              \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return (unsigned) __builtin_amdgcn_readlane((int) v, 63);
+}
+__device__ __forceinline__ double wave_max_d(double x) {
+#define S_(C, R)                                   \
+	{                                              \
+		const double t_ = dpp_d<C, R>(-DBL_MAX, x); \
+		x = t_ > x ? t_ : x;                       \
+	}
+	CCG_DPP_STEPS(S_)
+#undef S_
+	return readlane_d(x, 63);
+}
 
 // nj.c:42 limbLength / nj.c:81 limbLengthNeg
 static __device__ void limb_length(double *Li, double *Lj, double sDi, double sDj, int Ni_, int Nj_, double Dij, int neg) {

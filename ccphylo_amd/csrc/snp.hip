@@ -638,9 +638,43 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_band(const uint2 *__restric
 // one rank's owned rows of the band layout (k_snp_mfma_band), D indexed by
 // Shard::off.  SPLIT: word slice item % S of Wk words, exact u32 counts.
 #define TILE2 256
-#define KC2 8                          // words per LDS chunk
+#define KC2 8                          // words per LDS chunk (the default; KC2L with CCG_DIST_KC=16)
+#define KC2L 16
 #define RS2 260                        // LDS row stride (uint2): 16-byte aligned rows of 256 + pad
-#define QS2 (TILE2 * KC2 / 2 / 256)    // uint4 staged per thread per panel (4)
+
+// Super-tile order of the LT's 256 x 256 tiles (CCG_DIST_ORDER=1): super-rows
+// of 4 panel rows; inside one, column chunks of 8 panels (4 x 8 = 32 tiles,
+// one XCD's 32 CUs at a time under xcd_tile), row-major inside a chunk, then
+// the diagonal remainder J in [8F, I] row-major.  A super-row starts at the
+// same tile index as in row-major order (T(P) = 4P (4P + 1) / 2), so the
+// row-major row of t names its super-row; a super-row cut by the last panel
+// row Ihi (the end of the range) stays row-major.  The 32 tiles an XCD runs
+// together then read 4 A + 8 B panels (row-major: 1 + 32), in step along K.
+__device__ __forceinline__ void tile_ij_super(long long t, long long Ihi, int &I, int &J) {
+	int r, c;
+	tile_ij(t, r, c);
+	const long long P = r >> 2, I0 = 4 * P;
+	if(I0 + 3 > Ihi) {
+		I = r;
+		J = c;
+		return;
+	}
+	const long long u = t - I0 * (I0 + 1) / 2, F = P >> 1;   // F full chunks: J < 8F <= I0
+	if(u < 32 * F) {
+		const int v = (int) (u & 31);
+		I = (int) I0 + (v >> 3);
+		J = 8 * (int) (u >> 5) + (v & 7);
+		return;
+	}
+	long long w = u - 32 * F;
+	int i = (int) I0;
+	while(w >= i - 8 * F + 1) {
+		w -= i - 8 * F + 1;
+		++i;
+	}
+	I = i;
+	J = (int) (8 * F + w);
+}
 
 __device__ __forceinline__ v8i_t fp4_xor_spread(const v8i_t &a, const v8i_t &b) {
 	v8i_t v;
@@ -650,15 +684,16 @@ __device__ __forceinline__ v8i_t fp4_xor_spread(const v8i_t &a, const v8i_t &b) 
 	return v;
 }
 
-template <int ET, bool SPLIT, bool BAND>
+template <int ET, bool SPLIT, bool BAND, int KCW = KC2>
 __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ P, int Wp, int n, long long t0,
                                                       long long items, int S, int Wk, double nFactor, double bs,
                                                       typename Elem<ET>::T *__restrict__ D, long long rowBegin,
                                                       long long rowEnd, unsigned *__restrict__ cnt, long long cbase,
                                                       const long long *__restrict__ pfx, int npanels, int rank,
-                                                      int world) {
-	__shared__ __attribute__((aligned(16))) uint2 As[2][KC2 * RS2];
-	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KC2 * RS2];
+                                                      int world, int sorder) {
+	constexpr int QS2 = TILE2 * KCW / 2 / 256, WPR = KCW / 2;   // uint4 staged per thread per panel; per row
+	__shared__ __attribute__((aligned(16))) uint2 As[2][KCW * RS2];
+	__shared__ __attribute__((aligned(16))) uint2 Bs[2][KCW * RS2];
 	const long long item = t0 + xcd_tile(blockIdx.x, items), t = SPLIT ? item / S : item;
 	int I, J;
 	if(BAND) {   // tile t of the rank's list: panel I = last with pfx[I] <= t, J = t - pfx[I]
@@ -669,6 +704,8 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ 
 		}
 		I = lo;
 		J = (int) (t - pfx[lo]);
+	} else if(sorder) {
+		tile_ij_super(t, (rowEnd - 1) / TILE2, I, J);
 	} else {
 		tile_ij(t, I, J);
 	}
@@ -688,14 +725,14 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ 
 	uint4 va[QS2], vb[QS2];
 #pragma unroll
 	for(int q = 0; q < QS2; ++q) {
-		const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+		const int e = q * 256 + threadIdx.x, row = e / WPR, wp = e % WPR;
 		ar[q] = arow(row);
 		va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + 2 * wp);
 		vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + 2 * wp);
 	}
 #pragma unroll
 	for(int q = 0; q < QS2; ++q) {
-		const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+		const int e = q * 256 + threadIdx.x, row = e / WPR, wp = e % WPR;
 		As[0][(2 * wp) * RS2 + row] = make_uint2(va[q].x, va[q].y);
 		As[0][(2 * wp + 1) * RS2 + row] = make_uint2(va[q].z, va[q].w);
 		Bs[0][(2 * wp) * RS2 + row] = make_uint2(vb[q].x, vb[q].y);
@@ -714,19 +751,19 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ 
 #pragma unroll
 			for(int r = 0; r < 16; ++r) acc[a][c][r] = 0.0f;
 	int buf = 0;
-	for(int w0 = 0; w0 < Wl; w0 += KC2, buf ^= 1) {
-		const bool more = w0 + KC2 < Wl;
+	for(int w0 = 0; w0 < Wl; w0 += KCW, buf ^= 1) {
+		const bool more = w0 + KCW < Wl;
 		if(more) {
 #pragma unroll
 			for(int q = 0; q < QS2; ++q) {
-				const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
-				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + w0 + KC2 + 2 * wp);
-				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KC2 + 2 * wp);
+				const int e = q * 256 + threadIdx.x, row = e / WPR, wp = e % WPR;
+				va[q] = *(const uint4 *) (P + (size_t) ar[q] * Wp + wb + w0 + KCW + 2 * wp);
+				vb[q] = *(const uint4 *) (Bp + (size_t) row * Wp + w0 + KCW + 2 * wp);
 			}
 		}
 		const uint2 *Ac = As[buf], *Bc = Bs[buf];
 #pragma unroll
-		for(int s = 0; s < KC2 / 2; ++s) {
+		for(int s = 0; s < KCW / 2; ++s) {
 			const int w = 2 * s + h;   // this lane's word: its half of the step's 64 positions
 			uint2 a[4], b[4];
 #pragma unroll
@@ -773,7 +810,7 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ 
 			uint2 *An = As[buf ^ 1], *Bn = Bs[buf ^ 1];
 #pragma unroll
 			for(int q = 0; q < QS2; ++q) {
-				const int e = q * 256 + threadIdx.x, row = e >> 2, wp = e & 3;
+				const int e = q * 256 + threadIdx.x, row = e / WPR, wp = e % WPR;
 				An[(2 * wp) * RS2 + row] = make_uint2(va[q].x, va[q].y);
 				An[(2 * wp + 1) * RS2 + row] = make_uint2(va[q].z, va[q].w);
 				Bn[(2 * wp) * RS2 + row] = make_uint2(vb[q].x, vb[q].y);
@@ -1401,15 +1438,21 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 		return CCG_EHIP;
 	}
 	const long long slots = prop.multiProcessorCount;   // one block per CU
-	const int chunks = Wp / KC2;
+	// words per LDS chunk (CCG_DIST_KC=16: half the barriers, 133 KB of LDS)
+	// and the tile order (CCG_DIST_ORDER=1: super-tiles, whole LT ranges from
+	// a super-row start only)
+	const char *kce = getenv("CCG_DIST_KC"), *ore = getenv("CCG_DIST_ORDER");
+	const int kc = kce && atoi(kce) == KC2L && Wp % KC2L == 0 ? KC2L : KC2;
+	const int sorder = world == 0 && ore && atoi(ore) == 1 && (rb / TILE2) % 4 == 0;
+	const int chunks = Wp / kc;
 	int S = 1;
 	if(tiles < 16 * slots) {
 		S = (int) cdivll(16 * slots, tiles);
 		if(S > chunks / 4) S = chunks / 4;
 		if(S < 1) S = 1;
 	}
-	int Wk = (int) cdivll(chunks, S) * KC2;
-	if(Wk > MFMA_KMAX) Wk = (MFMA_KMAX / KC2) * KC2;
+	int Wk = (int) cdivll(chunks, S) * kc;
+	if(Wk > MFMA_KMAX) Wk = (MFMA_KMAX / kc) * kc;
 	S = (int) cdivll(Wp, Wk);
 	const long long batch = 1 << 16;
 	unsigned *cnt = NULL;
@@ -1427,23 +1470,32 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	for(long long t = t_begin * S; t < t_end * S; t += batch) {
 		const long long items = t_end * S - t < batch ? t_end * S - t : batch;
 		const uint2 *pl = (const uint2 *) planes;
-		if(world > 0) {
-			if(S > 1)
-				k_snp_mfma2<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
-				    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,
-				    world);
-			else
-				k_snp_mfma2<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
-				    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,
-				    world);
+#define MF2_LAUNCH(KCV)                                                                                              \
+	if(world > 0) {                                                                                                  \
+		if(S > 1)                                                                                                    \
+			k_snp_mfma2<ET, true, true, KCV><<<(unsigned) items, 256, 0, ctx->stream>>>(                             \
+			    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,  \
+			    world, 0);                                                                                           \
+		else                                                                                                         \
+			k_snp_mfma2<ET, false, true, KCV><<<(unsigned) items, 256, 0, ctx->stream>>>(                            \
+			    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels, rank,  \
+			    world, 0);                                                                                           \
+	} else {                                                                                                         \
+		if(S > 1)                                                                                                    \
+			k_snp_mfma2<ET, true, false, KCV><<<(unsigned) items, 256, 0, ctx->stream>>>(                            \
+			    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1,       \
+			    sorder);                                                                                             \
+		else                                                                                                         \
+			k_snp_mfma2<ET, false, false, KCV><<<(unsigned) items, 256, 0, ctx->stream>>>(                           \
+			    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1,       \
+			    sorder);                                                                                             \
+	}
+		if(kc == KC2L) {
+			MF2_LAUNCH(KC2L)
 		} else {
-			if(S > 1)
-				k_snp_mfma2<ET, true, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
-				    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1);
-			else
-				k_snp_mfma2<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
-				    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1);
+			MF2_LAUNCH(KC2)
 		}
+#undef MF2_LAUNCH
 		MF2_TRY(hipGetLastError());
 	}
 	if(S > 1) {

@@ -117,13 +117,22 @@ __device__ __forceinline__ void update_body(typename Elem<ET>::T *__restrict__ D
                                             double sDk, int Nk, int slot) {
 	double d = 0;
 	int cnt = 0;
+	typename Elem<ET>::T v = 0;
 	if(k < n && k != i && k != j) {
 		d = (Dik + Dkj - Dij) / 2;
 		d = d < 0 ? 0 : d;
-		D[k < j ? tri(j) + k : tri(k) + j] = Elem<ET>::put(d, 0.25, bs);
+		v = Elem<ET>::put(d, 0.25, bs);
+		D[k < j ? tri(j) + k : tri(k) + j] = v;
 		b.sD[k] = sDk - (Dik + Dkj - d);
 		b.N[k] = Nk - 1;
 		cnt = 1;
+	}
+	if(b.lbm) {   // (uniform) block bounds: row j rewritten (exact per wave), column j lowered where written
+		const bool rowj = k < j;   // k < j < i: a cell of row j
+		const unsigned x = lb_bits(Elem<ET>::get(v, bs));
+		const unsigned mn = wave_min_u32(rowj ? x : 0xFFFFFFFFu);
+		if((threadIdx.x & 63) == 0 && k < j) b.lbm[(long long) j * b.lbs + (k >> 6)] = mn;
+		if(k > j && k < n && k != i) __hip_atomic_fetch_min(b.lbm + (long long) k * b.lbs + (j >> 6), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
 	update_partials(b, n, exact, k, d, cnt, slot);
 	// exact mode: this block's row of the serial row sum (xs_join_row; the
@@ -178,6 +187,39 @@ __device__ __forceinline__ void join_tail(typename Elem<ET>::T *__restrict__ D, 
 	if(general) return;
 	update_body<ET>(D, bs, b, n, i, j, Dij, exact, k, Dik, Dkj, sDk, Nk, blockIdx.x);
 	TS(3, 5);
+}
+
+// ------------------------------------------------------------------ block lower bounds
+// TreeBufs::lbm / msd from the matrix and sD as they are (the first join, or a
+// resumed state): one wave per row, BB blocks in flight per lane; one wave per
+// 64 columns for the sD maxima
+template <int ET>
+__global__ __launch_bounds__(TB) void k_lb_init(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
+                                                TreeBufs b) {
+	constexpr int BB = 8;
+	const int lane = threadIdx.x & 63;
+	const int r = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+	if(r >= n) return;   // (wave-uniform)
+	if(r < (n + LBW - 1) / LBW) {   // the sD maxima of block r
+		const int c = r * LBW + lane;
+		const double mx = wave_max_d(c < n ? b.sD[c] : -DBL_MAX);
+		if(lane == 0) b.msd[r] = mx;
+	}
+	const typename Elem<ET>::T *row = D + tri(r);
+	const int nbk = (r + LBW - 1) / LBW;
+	for(int u0 = 0; u0 < nbk; u0 += BB) {
+		unsigned x[BB];
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const int c = (u0 + m) * LBW + lane;
+			x[m] = u0 + m < nbk && c < r ? lb_bits(Elem<ET>::get(row[c], bs)) : 0xFFFFFFFFu;
+		}
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const unsigned mn = wave_min_u32(x[m]);
+			if(lane == 0 && u0 + m < nbk) b.lbm[(long long) r * b.lbs + u0 + m] = mn;
+		}
+	}
 }
 
 // ------------------------------------------------------------------ DNJ join
@@ -989,6 +1031,17 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			}
 		}
 	}
+	if(b.lbm) {   // (uniform) block bounds of the next join: row i = the moved row, column i; sD maxima
+		const unsigned x = lb_bits(Elem<ET>::get(vm, bs));
+		if(move) {
+			const unsigned mn = wave_min_u32(k < i ? x : 0xFFFFFFFFu);
+			if(lane == 0 && k < i) b.lbm[(long long) i * b.lbs + (k >> 6)] = mn;
+			if(k > i && k < nn) __hip_atomic_fetch_min(b.lbm + (long long) k * b.lbs + (i >> 6), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		const double sf = k < nn ? (move && k == i ? sDm : sDk) : -DBL_MAX;   // sD of column k at the next join
+		const double mx = wave_max_d(sf);
+		if(lane == 0 && k < nn) b.msd[k >> 6] = mx;
+	}
 	// VBLK: V_k = max(q at the row's partner cell, Q_k) in the next join's
 	// state, a bound of minQpair's running min below row k whatever the
 	// reference does with it (a cell of row k is >= its fresh minimum); the
@@ -1716,6 +1769,10 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.sfj = (int *) (m + o_sj);
 	b.ecS = (unsigned *) (m + o_es);
 	b.maxu = (int) maxu;
+	b.lbm = NULL;   // the block bounds: tree_run_t's own allocation (single engine, DNJ)
+	b.msd = NULL;
+	b.lbs = 0;
+	b.lbskip = NULL;
 	return sz;
 }
 
@@ -1779,7 +1836,12 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int prune = dnj_prune(n, ET, GEN);
 		if(prune == 2 && g_grid.plan_help) k_dnj_sphase<ET, false><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
 		else if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
-		if(sm >= 20 && sm <= 23 && !GEN && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
+		if(b.lbm && !GEN && sm >= 4 && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
+			// the compacted wave scan under the block lower bounds (every element type)
+			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
+			if(prune == 2) k_dnj_scan_v<ET, DenseRows, NoTail, 0, 2, true, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+			else k_dnj_scan_v<ET, DenseRows, NoTail, 0, 0, true, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);
+		} else if(sm >= 20 && sm <= 23 && !GEN && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
 			// row groups over the dense (group, unit) enumeration; with pruning, the survivors only
 			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
 			if(prune == 2) {
@@ -1968,6 +2030,24 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	CCG_CHECK(hipStreamSynchronize(st));
 	// GEN = false assumes N[k] == n for every row (no missing entries ever)
 	const bool general = h.has_missing != 0 || resumed_counts;
+	// the block lower bounds (DnjGrid::lb): one allocation beside the run's
+	void *lbmem = NULL;
+	if(a->method == CCG_TREE_DNJ && !general && g_grid.lb && n0 > g_grid.lb_min_n) {
+		const long long LS = (n0 + LBW - 1) / LBW;
+		const size_t lbb = ((size_t) n0 * LS * 4 + 255) & ~(size_t) 255;
+		if(hipMalloc(&lbmem, lbb + (size_t) (LS + 1) * 8) == hipSuccess) {
+			b.lbm = (unsigned *) lbmem;
+			b.msd = (double *) ((char *) lbmem + lbb);
+			b.lbs = LS;
+			b.lbskip = &b.ctl->cells_lbskip;
+			k_lb_init<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b);
+			launches += 1;
+			CCG_CHECK(hipGetLastError());
+		} else {
+			(void) hipGetLastError();   // no room: the run goes without (the same joins)
+			lbmem = NULL;
+		}
+	}
 #ifdef CCG_TRACE
 	const char *tn = getenv("CCG_TRACE_N");
 	int trace_hi = tn ? atoi(tn) : n0 / 2;
@@ -2125,6 +2205,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	}
 #endif
 	if(h.done && h.final_n < 0) {   // k_dnj_plan's look-back timed out (never expected)
+		if(lbmem) hipFree(lbmem);
 		hipFree(w.mem);
 		ccg_set_last_msg("k_dnj_plan / k_dnj_join: a block's bounded wait on another block timed out");
 		return CCG_EHIP;
@@ -2168,7 +2249,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	}
 	if(stats) {
 		stats[0] = h.rows;
-		stats[1] = h.cells - h.cells_pruned;   // cells the scans loaded (listed, less the S-pruned ones)
+		stats[1] = h.cells - h.cells_pruned - h.cells_lbskip;   // cells the scans loaded (listed, less the pruned / bounded-out ones)
 		stats[2] = launches;
 		stats[3] = (int64_t) (ms * 1000.0);
 		if(a->profile) {
@@ -2177,7 +2258,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 				stats[5 + 2 * c] = kt.ns[c];
 			}
 			stats[4 + 2 * CCG_NKSTAT] = h.cells_top;
-			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest - h.cells_pruned;
+			stats[5 + 2 * CCG_NKSTAT] = h.cells_rest - h.cells_pruned - h.cells_lbskip;
 			stats[6 + 2 * CCG_NKSTAT] = h.serial_sums;
 			stats[7 + 2 * CCG_NKSTAT] = h.chain_sums;
 			stats[8 + 2 * CCG_NKSTAT] = h.cells_help;
@@ -2187,6 +2268,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		}
 	}
 	CCG_CHECK(hipStreamSynchronize(st));
+	if(lbmem) CCG_CHECK(hipFree(lbmem));
 	CCG_CHECK(hipFree(w.mem));
 	return CCG_OK;
 }

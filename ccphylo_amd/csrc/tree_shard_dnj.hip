@@ -5,7 +5,9 @@
 // sD, N, Q, P and the join list are replicated and every rank updates them
 // with the same arithmetic.
 //
-// Per join at matrix size n: five kernels, two collectives.
+// Per join at matrix size n: five kernels, two collectives.  (Round 5: row
+// n-1 travels in the lines' allreduce instead of a broadcast of its own --
+// one collective latency fewer per join)
 //   1. k_dnj_plan (ccg_dnj_search.h, Shard row policy): minPos, m0 and the
 //      top rows S depend on the replicated Q only, so every rank computes the
 //      same ones.  Each rank bounds minQpair's serial running min with the
@@ -17,18 +19,17 @@
 //   2. k_dnj_scan rescans the listed units; its tail (RecTail) folds each
 //      row's units into a record of the rank's own rows, indexed by the
 //      row's position among them -- one bit byte per owned band, f64 fresh
-//      q, i32 j -- and the owner of row n-1 (the pop moves it to slot i,
-//      dnj.c:817 / matrix.c:518) copies it out;
+//      q, i32 j;
 //      -> allgather of the ranks' record slots (each rank sends only its own
 //      rows' records: half the ring bytes of the round-2 allreduce-as-gather
-//      over dense row-indexed arrays) and a broadcast of row n-1 from its
-//      owner;
+//      over dense row-indexed arrays);
 //   3. k_shd_pick: every block replays minQpair's accept/reject decisions
 //      over the listed rows in descending order (replay_wave); rows that the
 //      serial scan would skip have bound >= running min, so the replay
 //      rejects them and (i, j) is the single-GPU engine's on every rank.
-//      Then each rank's pieces of lines i and j;
-//      -> allreduce-sum of lines i and j (a gather again);
+//      Then each rank's pieces of lines i and j, and row n-1 from its owner
+//      (the pop moves it to slot i, dnj.c:817 / matrix.c:518);
+//      -> allreduce-sum of lines i and j and row n-1 (a gather again);
 //   4. k_shd_join: the accepted (Q, P) updates, limbLength, updateD
 //      (nj.c:836) on every rank for every k, own cells stored, the new line j
 //      kept whole (its exact row sum: xs_join_row);
@@ -95,13 +96,8 @@ struct RecTail {
 	const typename Elem<ET>::T *D;
 	Shard sh;
 	void *R;                          // this rank's record slot
-	typename Elem<ET>::T *xm;         // row n-1 (its owner fills it; broadcast after)
 	unsigned *cnt;   // n0 zeros
-	__device__ void begin(const TreeBufs &, int n) const {
-		if(!sh.owns(n - 1)) return;
-		const typename Elem<ET>::T *row = D + sh.off(n - 1);
-		for(int k = blockIdx.x * TB + threadIdx.x; k < n - 1; k += gridDim.x * TB) xm[k] = row[k];
-	}
+	__device__ void begin(const TreeBufs &, int) const {}
 	__device__ void unit(const TreeBufs &b, int n, int u, int ua, int ub, int r, double q, int j) const {
 		if(ub - ua > 1) {
 			__hip_atomic_store(b.cq + u, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -266,7 +262,10 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 		}
 	}
 	// the pieces of lines i and j this rank's rows hold: X[k] = D(i, k),
-	// X[n + k] = D(j, k) (raw elements; zeros where another rank owns the cell)
+	// X[n + k] = D(j, k), and row n-1, X[2n + k] = D(n-1, k) (raw elements;
+	// zeros where another rank owns the cell)
+	const bool own_m = sh.owns(n - 1);
+	const typename Elem<ET>::T *rowm = D + (own_m ? sh.off(n - 1) : 0);
 	for(int k = blockIdx.x * PICK_T + tid; k < n; k += gridDim.x * PICK_T) {
 		typename Elem<ET>::T xi = 0, xj = 0;
 		if(k > i) {
@@ -281,6 +280,7 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 		}
 		X[k] = xi;
 		X[n + k] = xj;
+		X[2 * n + k] = own_m && k < n - 1 ? rowm[k] : (typename Elem<ET>::T) 0;
 	}
 	PTS(5);
 	if(dbg && blockIdx.x == 0 && threadIdx.x == 0) dbg[(n & 1023) * 8 + 6] = total;
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 
 // limbLength (nj.c:42/:81), the join record and updateD (nj.c:836) over the
 // gathered lines: every rank computes the whole new line j (kept in Xj and,
-// at k = n-1, patched into the broadcast row Xm) and stores its own cells
+// at k = n-1, patched into the gathered row Xm) and stores its own cells
 template <int ET>
 __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
                                                  Shard sh, const typename Elem<ET>::T *__restrict__ X,
@@ -592,7 +592,7 @@ struct ShdLayout {
 		};
 		const RecSlot rs0 = rec_slot(n0, world);
 		o_R = take(rec_bytes(n0));
-		o_X = take((size_t) 2 * n0 * es);
+		o_X = take((size_t) 3 * n0 * es);
 		o_Xm = take((size_t) n0 * es + 8);
 		o_Sl = take(rs0.bytes);
 		o_G = take((size_t) world * rs0.bytes);
@@ -631,7 +631,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		return CCG_ENOMEM;
 	}
 	size_t hcap = sh_init_host_bytes(n0, coll->world);
-	if((size_t) 2 * n0 * ET > hcap) hcap = (size_t) 2 * n0 * ET;
+	if((size_t) 3 * n0 * ET > hcap) hcap = (size_t) 3 * n0 * ET;
 	if(rec_bytes(n0) > hcap) hcap = rec_bytes(n0);
 	if((size_t) coll->world * rs0.bytes > hcap) hcap = (size_t) coll->world * rs0.bytes;
 	if(coll->host_staged && hipHostMalloc((void **) &h, hcap) != hipSuccess) {
@@ -697,7 +697,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
 			const unsigned gn = cdiv(n, TB), gp = cdiv(n, PICK_T) < PICK_MAXB ? cdiv(n, PICK_T) : PICK_MAXB;
-			T *Xmr = Xm;   // row n-1, broadcast by its owner
+			T *Xmr = X + 2 * (size_t) n;   // row n-1, gathered with lines i and j
 			const unsigned gc = grid.scan(n);
 			const int seg = grid.seg(n);
 			// one-phase search (k_dnj_plan): each rank lists the S rows and the
@@ -706,16 +706,15 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
-			if(grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
-			else if(grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
-			else if(grid.scan_mode(n, ET)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
-			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, Xm, pcnt});
+			if(grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			else if(grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			else if(grid.scan_mode(n, ET)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
 			kt.mark(CCG_K_REST);
 			SD_TRY(cr.allgather(Sl, G, rec_slot(n, sh.world).bytes));
-			SD_TRY(cr.bcast(Xm, Xm, (size_t) (n - 1) * ET, rec_owner(n - 1, sh.world)));
 			k_shd_pick<ET><<<gp, PICK_T, 0, st>>>(D, b, n, sh, G, X, pacc, pflag, n0, dbg);
 			kt.mark(CCG_K_UPDATE);
-			SD_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
+			SD_TRY(cr.allreduce(X, (size_t) 3 * n * ET));
 			k_shd_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr, Xj, pflag);
 			kt.mark(CCG_K_UPDATE);
 			if(grid.bands(n - 1)) k_shd_requeue<ET, true><<<gn, TB, 0, st>>>(D, bs, b, n, sh, Xmr, Xj, Sl);

@@ -738,6 +738,43 @@ def test_dnj_scan_prune(dev, monkeypatch, kind, n, et, mode, bands):
     assert st[1] == (cells["21"] if int(mode) < 20 else cells["00"])
 
 
+@pytest.mark.parametrize("kind,n,et,mode", [("clade", 3000, 8, "9"), ("euc", 2500, 8, "9"), ("euc", 2600, 4, "20"),
+                                             ("snp", 2000, 2, "20"), ("clade", 2200, 1, "9"), ("euc", 3000, 8, "4"),
+                                             ("snp", 2400, 8, "9")])
+def test_dnj_block_bounds(dev, monkeypatch, kind, n, et, mode):
+    """The scan under the block lower bounds (TreeBufs::lbm, lb_unit): a
+    64-column block is skipped when ((n-2) m_d - sD_r) - M_sD exceeds the q at
+    the row's partner cell, with the bounds kept conservatively by the join
+    (row j, column j) and the requeue (row i, column i, the sD maxima).  At
+    small n through CCG_LB_MIN_N: joins, lengths and the reference-rule
+    counters equal the serial oracle's with pruning on and off, and the
+    bounded scan loads fewer cells than the unbounded one."""
+    from oracle import pyoracle
+    from ccphylo_amd import native
+    K = native.NKSTAT
+    for k, v in (("CCG_SCAN_WAVE", mode), ("CCG_PREFOLD_N", "0"), ("CCG_SEG_MUL", "1"), ("CCG_S_SPLIT_N", "100"),
+                 ("CCG_PRUNE_CELLS", "0"), ("CCG_LB_MIN_N", "100")):
+        monkeypatch.setenv(k, v)
+    D = {"euc": lambda: _euclid(n, n + 7), "snp": lambda: _snp(n, n + 5), "clade": lambda: _clade_ltd(n, n + 6)}[kind]()
+    bs = {8: 1.0, 4: 1.0, 2: 4.0, 1: 0.1}[et]
+    if et == 4:
+        D = D.astype(np.float32)
+    elif et in (2, 1):
+        D = np.clip(D * bs + 0.5, 0, 255 if et == 1 else 65535).astype(np.uint8 if et == 1 else np.uint16)
+    ref, rfn, rfd, rst = pyoracle.tree(D, n, etype=et, byte_scale=bs, method=1, stats=True)
+    for prune in ("2", "0"):
+        monkeypatch.setenv("CCG_SCAN_PRUNE", prune)
+        cells = {}
+        for lb in ("1", "0"):
+            monkeypatch.setenv("CCG_SCAN_LB", lb)
+            got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
+            assert (fn, fd) == (rfn, rfd), (prune, lb)
+            assert len(got) == len(ref) and (got == ref).all(), (prune, lb)
+            assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), (prune, lb)
+            cells[lb] = st[1]
+        assert cells["1"] < cells["0"], (prune, cells)
+
+
 @pytest.mark.parametrize("withhold", ["1", "2"])
 def test_dnj_plan_wait_timeout_is_an_error(dev, monkeypatch, withhold):
     """A bounded wait of k_dnj_plan that gives up stops the tree with an

@@ -1,5 +1,6 @@
 """configs[3]'s late tree against the oracle (joins past 12k
-pinned by nothing).  OPT-IN (CCG_LATE=1, about 10 minutes on one MI355X;
+pinned by nothing).  In the default suite at 40k taxa (test_late_tree_resume_40k,
+well under a minute); at configs[3]'s 200k OPT-IN (CCG_LATE=1, about 10 minutes on one MI355X;
 run it with `pytest -s` so the engine's progress lines keep the call alive):
 the whole 200k float tree does not fit the default GPU suite's time, and the
 oracle's serial rule rescans ~4e9 cells per join there.
@@ -22,23 +23,37 @@ import time
 import numpy as np
 import pytest
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(not os.environ.get("CCG_LATE"), reason="opt-in: CCG_LATE=1 (about 10 minutes)")]
+pytestmark = pytest.mark.gpu
 
 
+def test_late_tree_resume_40k():
+    """The same check at a size the default GPU suite affords:
+    a 40k float Euclidean matrix (seed 4), cut at 15k joins (matrix 25k: the
+    float row groups over the compacted enumeration with pruning, k_dnj_fold
+    and the long-listing k_dnj_join_pf path run from the checkpoint on) and at
+    30k joins (matrix 10k: the small-n plan and scans); at each cut the oracle
+    continues 200 joins from the engine's state, joins and reference-rule
+    counters identical."""
+    _late_legs(40_000, [15_000, 30_000], 200, os.environ.get("CCG_LATE_OUT"))
+
+
+@pytest.mark.skipif(not os.environ.get("CCG_LATE"), reason="opt-in: CCG_LATE=1 (about 10 minutes)")
 def test_config3_late_tree_resume():
+    n = int(os.environ.get("CCG_LATE_N", 200_000))
+    cuts = [int(x) for x in os.environ.get("CCG_LATE_CUTS", "60000,120000,180000").split(",")]
+    m = int(os.environ.get("CCG_LATE_M", 200))
+    os.environ.setdefault("CCG_PROGRESS", "1")
+    _late_legs(n, cuts, m, os.environ.get("CCG_LATE_OUT"))
+
+
+def _late_legs(n, cuts, m, out):
     import torch
     import ccphylo_amd as cg
     from ccphylo_amd import native
     from oracle import pyoracle
     from tools.synth import euclid_shard_dev
     K = native.NKSTAT
-    n = int(os.environ.get("CCG_LATE_N", 200_000))
-    cuts = [int(x) for x in os.environ.get("CCG_LATE_CUTS", "60000,120000,180000").split(",")]
-    m = int(os.environ.get("CCG_LATE_M", 200))
     threads = min(16, os.cpu_count() or 4)
-    out = os.environ.get("CCG_LATE_OUT")
-    os.environ.setdefault("CCG_PROGRESS", "1")
     dev = cg.Device(0)
     D = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)   # world 1: the packed LT
     torch.cuda.synchronize()
