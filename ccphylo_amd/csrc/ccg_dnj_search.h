@@ -413,7 +413,7 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
                                                         TreeBufs b, int n, int hb, int nh, bool tshort) {
 	typedef typename Elem<ET>::T T;
 	constexpr int UC = 8;   // (16: the plan kernel's registers spill further, 30.8 -> 33.4 us per plan at 50k)
-	__shared__ int h_ok, h_nS, h_isub;
+	__shared__ int h_ok, h_nS, h_isub, h_jsub;
 	__shared__ double h_m0, h_sDm;
 	__shared__ int h_uo[DNJ_B + 1], h_row[DNJ_B];
 	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -445,11 +445,12 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 			const unsigned long long w = __hip_atomic_load(b.shdr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			h_nS = (int) (unsigned) (w & 0xffffffffu);
 			h_isub = (int) (unsigned) (w >> 32);
+			h_jsub = (int) (unsigned) __hip_atomic_load(b.shdr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 	__syncthreads();
 	if(!h_ok || h_nS <= 0) return;
-	const int nS = h_nS, isub = h_isub;
+	const int nS = h_nS, isub = h_isub, jsub = h_jsub;
 	const double sDm = h_sDm;
 	for(int t = tid; t <= nS; t += blockDim.x) {
 		h_uo[t] = __hip_atomic_load(b.pS_uo + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -470,24 +471,33 @@ __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__rest
 		const T *row = D + tri(r);
 		double q = DBL_MAX;
 		int idx = 0;
-		for(int base = c0; base < c1; base += 64 * UC) {
-			double sk[UC];
-			T vv[UC];
-#pragma unroll
-			for(int m = 0; m < UC; ++m) {
-				const int c = base + 64 * m + lane;
-				const int cc = c < c1 ? c : c1 - 1;
-				sk[m] = b.sD[cc];
-				vv[m] = row[cc];
+		if(b.lbm) {   // under the block bounds (rows j and i: no threshold yet)
+			const long long sk = lb_unit<ET>(row, bs, b, n, r, c0, c1, sDr, q, idx, isub, sDm, r == isub || r == jsub);
+			if(lane == 0 && sk) {   // the cells the helpers did not load (stats; cells_help counted whole S rows)
+				long long *slot = b.lbskip + (long long) (LB_SCAN + (hb * nwv + wid) % LB_HELP) * LB_SLOT;
+				atomicAdd((unsigned long long *) slot, (unsigned long long) sk);
+				atomicAdd((unsigned long long *) (slot + 1), (unsigned long long) sk);
 			}
+		} else {
+			for(int base = c0; base < c1; base += 64 * UC) {
+				double sk[UC];
+				T vv[UC];
 #pragma unroll
-			for(int m = 0; m < UC; ++m) {
-				const int c = base + 64 * m + lane;
-				const double d = Elem<ET>::get(vv[m], bs);
-				const double x = qcrit(n, n, d, sDr, c == isub ? sDm : sk[m]);
-				const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
-				q = take ? x : q;
-				idx = take ? c : idx;
+				for(int m = 0; m < UC; ++m) {
+					const int c = base + 64 * m + lane;
+					const int cc = c < c1 ? c : c1 - 1;
+					sk[m] = b.sD[cc];
+					vv[m] = row[cc];
+				}
+#pragma unroll
+				for(int m = 0; m < UC; ++m) {
+					const int c = base + 64 * m + lane;
+					const double d = Elem<ET>::get(vv[m], bs);
+					const double x = qcrit(n, n, d, sDr, c == isub ? sDm : sk[m]);
+					const bool take = c < c1 && 0 <= d && qarg_better(x, c, q, idx);
+					q = take ? x : q;
+					idx = take ? c : idx;
+				}
 			}
 		}
 		qarg_wave_reduce(q, idx);
@@ -857,11 +867,13 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 				if(!first) {   // persist the fold for the kernels after
 					b.Q[j] = Qj;
 					b.P[j] = Pj;
+					if(b.ubq) b.ubq[j] = INFINITY;   // new partners: the scan's threshold is unknown
 					if(move) {
 						b.Q[i] = Qi;
 						b.P[i] = Pi;
 						b.sD[i] = sDm;
 						b.N[i] = Nm;
+						if(b.ubq) b.ubq[i] = INFINITY;
 					}
 				}
 				ctl->cand = cand;
@@ -918,6 +930,8 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 						                   __HIP_MEMORY_SCOPE_AGENT);
 						__hip_atomic_store(b.shdr + 2, ((unsigned long long) (unsigned) isub << 32) | (unsigned) nS,
 						                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						__hip_atomic_store(b.shdr + 4, (unsigned long long) (unsigned) jsub, __ATOMIC_RELAXED,
+						                   __HIP_MEMORY_SCOPE_AGENT);
 						asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 						if(!wh_hdr)
 							__hip_atomic_store(b.shdr + 3, (unsigned long long) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1627,22 +1641,27 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // waves with 1 to 4+ units and a second round of blocks).
 // One rescan unit, columns [c0, c1) of row r (c0 a multiple of LBW), under
 // the block lower bounds (TreeBufs::lbm / msd): the threshold is the Q
-// criterion at the row's partner cell P[r] evaluated now -- a cell of row r,
-// so >= the row's fresh minimum f_r -- and a 64-column block whose bound
+// criterion at the row's partner cell P[r] in this join's state (ubq, left by
+// the previous requeue) -- a cell of row r, so >= the row's fresh minimum
+// f_r; +inf where unknown -- and a 64-column block whose bound
 //     lb = ((n - 2) * m_d - sD_r) - M_sD    (qcrit's operation order)
 // exceeds it holds no cell with q <= f_r (rounding is monotone, m_d <= every
 // cell, M_sD >= every column's sD), so neither the minimum nor a tie the
 // index rule could pick: it is skipped.  The other blocks are rescanned one
 // cell per lane, BB blocks in flight.  Returns the cells skipped.
+// (k_dnj_plan's helper blocks run while block 0 persists row i's sD and the
+// thresholds of rows j and i: isub / sDm substitute the column, ubinf the
+// threshold)
 template <int ET>
 __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
-                                       int r, int c0, int c1, double sDr, double &q, int &idx) {
+                                       int r, int c0, int c1, double sDr, double &q, int &idx, int isub = -1,
+                                       double sDm = 0.0, bool ubinf = false) {
 	typedef typename Elem<ET>::T T;
 	constexpr int BB = 8;
 	const int lane = threadIdx.x & 63;
-	const int pr0 = b.P[r], pr = pr0 >= 0 && pr0 < r ? pr0 : 0;
 	const int bl0 = c0 / LBW, nbk = (c1 - c0 + LBW - 1) / LBW;   // <= seg / 64 <= 256 blocks
-	// the unit's bounds (one or more per lane), loaded with the partner's
+	// the unit's bounds (one or more per lane), loaded with the threshold
+	const double ub = ubinf ? INFINITY : b.ubq[r];
 	unsigned lbb[4];
 	double msb[4];
 #pragma unroll
@@ -1651,8 +1670,6 @@ __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ 
 		lbb[h] = t < nbk ? b.lbm[(long long) r * b.lbs + bl0 + t] : 0u;
 		msb[h] = t < nbk ? b.msd[bl0 + t] : 0.0;
 	}
-	const double dp = Elem<ET>::get(row[pr], bs), sp = b.sD[pr];
-	const double ub = qcrit(n, n, dp, sDr, sp);
 	unsigned long long need[4];
 #pragma unroll
 	for(int h = 0; h < 4; ++h) {
@@ -1688,7 +1705,7 @@ __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ 
 		for(int m = 0; m < BB; ++m) {
 			const int c = (m < nb ? blk[m] : blk[0]) * LBW + lane;
 			const double d = Elem<ET>::get(v[m], bs);
-			const double x = qcrit(n, n, d, sDr, sk[m]);
+			const double x = qcrit(n, n, d, sDr, c == isub ? sDm : sk[m]);
 			if(m < nb && c < c1 && 0 <= d && qarg_better(x, c, q, idx)) {
 				q = x;
 				idx = c;
@@ -1949,7 +1966,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *_
 	// already counted the pruned entries' whole rows)
 	if(PRUNE == 1 && pruned && lane == 0)
 		atomicAdd((unsigned long long *) &ctl->cells_pruned, (unsigned long long) pruned);
-	if(LB && lbskip && lane == 0) atomicAdd((unsigned long long *) b.lbskip, (unsigned long long) lbskip);
+	if(LB && lbskip && lane == 0)   // this wave's slot (no contention)
+		atomicAdd((unsigned long long *) (b.lbskip + (long long) ((blockIdx.x * (TB / 64) + (tid >> 6)) % LB_SCAN) * LB_SLOT),
+		          (unsigned long long) lbskip);
 	TS(2, 2);
 	TS_SAMP(2);
 	TS_EXIT(2);

@@ -122,11 +122,19 @@ struct TreeBufs {
 	// criterion exceeds the q at the row's partner cell.
 	unsigned *lbm;
 	double *msd;
+	double *ubq;         // per row: the Q criterion at its partner cell in this join's state (an upper bound
+	                     // of its fresh minimum, left by the previous requeue; +inf: unknown, rows j and i)
 	long long lbs;
-	long long *lbskip;   // cells the scan skipped under the block bounds (stats)
+	long long *lbskip;   // cells skipped under the block bounds (stats): per-wave slots of LB_SLOT longs --
+	                     // field 0 the cells not loaded, field 1 those of them in S rows (the plan's helpers);
+	                     // scan waves [0, LB_SCAN), helper waves after (no same-address atomics: thousands
+	                     // of waves adding to one counter serialise at its L2 channel)
 };
 
 #define LBW 64   // columns per block of the lower bounds (one wave)
+#define LB_SLOT 16      // longs per stats slot (one 128-B line)
+#define LB_SCAN 4096    // scan wave slots
+#define LB_HELP 8192    // helper wave slots
 
 // a float <= x (x >= 0: a cell value) as order-preserving bits
 __device__ __forceinline__ unsigned lb_bits(double x) {

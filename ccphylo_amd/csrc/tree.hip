@@ -41,6 +41,7 @@
 // k_nj_pop (row sum + ltdMatrix_popArrange).
 #include <string.h>
 #include <stdio.h>
+#include <vector>
 #include <stdlib.h>
 #include "ccg_tree_common.h"
 
@@ -205,6 +206,7 @@ __global__ __launch_bounds__(TB) void k_lb_init(const typename Elem<ET>::T *__re
 		const double mx = wave_max_d(c < n ? b.sD[c] : -DBL_MAX);
 		if(lane == 0) b.msd[r] = mx;
 	}
+	if(lane == 0) b.ubq[r] = INFINITY;   // no partner-cell threshold yet: the first scan reads every block
 	const typename Elem<ET>::T *row = D + tri(r);
 	const int nbk = (r + LBW - 1) / LBW;
 	for(int u0 = 0; u0 < nbk; u0 += BB) {
@@ -917,7 +919,8 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	// row's bound V_k of the next join's scan (prefetched: usually unchanged)
 	typename Elem<ET>::T vp = 0;
 	double sdp0 = 0.0;
-	if(VBLK && k >= 1 && k < n) {
+	const bool PV = VBLK || b.ubq;   // (uniform) the partner cells are wanted
+	if(PV && k >= 1 && k < n) {
 		const int p0 = pkk0 >= 0 && pkk0 < k ? pkk0 : 0;
 		vp = D[tri(k) + p0];
 		sdp0 = b.sD[p0];
@@ -1046,8 +1049,9 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	// state, a bound of minQpair's running min below row k whatever the
 	// reference does with it (a cell of row k is >= its fresh minimum); the
 	// block minimum, for the next scan's suffix bound over the rows above
-	double vk = DBL_MAX;
-	if(VBLK && k >= 1 && k < nn && k != i && k != j) {
+	// ubq (block bounds): the same q, the next scan's threshold for row k
+	double vk = DBL_MAX, qpc = INFINITY;
+	if(PV && k >= 1 && k < nn && k != i && k != j) {
 		const bool later = k > j;   // rows above j may have a new partner (j or the moved i)
 		const int pf = later ? fp : pkk0;
 		const double qf = later ? fq : qk0;
@@ -1064,8 +1068,10 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 		}
 		if(0 <= d) {
 			const double q = qcrit(nn, nn, d, sDk, sp);
+			qpc = q;
 			vk = q > qf ? q : qf;
 		}
+		if(b.ubq) b.ubq[k] = qpc;
 	}
 	if(VBLK) {
 		vk = readlane_d(wave_incl_min(vk), 63);
@@ -1771,6 +1777,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.maxu = (int) maxu;
 	b.lbm = NULL;   // the block bounds: tree_run_t's own allocation (single engine, DNJ)
 	b.msd = NULL;
+	b.ubq = NULL;
 	b.lbs = 0;
 	b.lbskip = NULL;
 	return sz;
@@ -2035,14 +2042,21 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	if(a->method == CCG_TREE_DNJ && !general && g_grid.lb && n0 > g_grid.lb_min_n) {
 		const long long LS = (n0 + LBW - 1) / LBW;
 		const size_t lbb = ((size_t) n0 * LS * 4 + 255) & ~(size_t) 255;
-		if(hipMalloc(&lbmem, lbb + (size_t) (LS + 1) * 8) == hipSuccess) {
+		const size_t msb = ((size_t) (LS + 1) * 8 + 255) & ~(size_t) 255;
+		const size_t ubb = ((size_t) n0 * 8 + 255) & ~(size_t) 255, skb = (size_t) (LB_SCAN + LB_HELP) * LB_SLOT * 8;
+		if(hipMalloc(&lbmem, lbb + msb + ubb + skb) == hipSuccess) {
 			b.lbm = (unsigned *) lbmem;
 			b.msd = (double *) ((char *) lbmem + lbb);
+			b.ubq = (double *) ((char *) lbmem + lbb + msb);
 			b.lbs = LS;
-			b.lbskip = &b.ctl->cells_lbskip;
+			b.lbskip = (long long *) ((char *) lbmem + lbb + msb + ubb);
+			CCG_CHECK(hipMemsetAsync(b.lbskip, 0, skb, st));
 			k_lb_init<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b);
 			launches += 1;
 			CCG_CHECK(hipGetLastError());
+			// S-bound pruning no longer pays beside the bounded scan (headline tree, profiled: 4.61 s
+			// without, 4.78 s with the plan's helpers and the compaction); CCG_SCAN_PRUNE still forces it
+			if(!getenv("CCG_SCAN_PRUNE")) g_grid.scan_prune = 0;
 		} else {
 			(void) hipGetLastError();   // no room: the run goes without (the same joins)
 			lbmem = NULL;
@@ -2088,6 +2102,14 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	kt.finish();
 	CCG_CHECK(hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
 	CCG_CHECK(hipStreamSynchronize(st));
+	if(b.lbskip) {   // the bounded-out cells, from the per-wave slots
+		std::vector<long long> sl((size_t) (LB_SCAN + LB_HELP) * LB_SLOT);
+		CCG_CHECK(hipMemcpy(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost));
+		for(size_t x = 0; x < (size_t) LB_SCAN + LB_HELP; ++x) {
+			h.cells_lbskip += sl[x * LB_SLOT];
+			h.cells_help -= sl[x * LB_SLOT + 1];
+		}
+	}
 	float ms = 0;
 	CCG_CHECK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
 	if(getenv("CCG_XS_WHY"))   // diagnostics: why exact row sums fell back to the serial chain
