@@ -526,19 +526,33 @@ def make_headline_alignment(torch, n, L):
     return seqs, incs, W
 
 
-def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0):
+def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0,
+                 tree_mode="shard", pg=None):
     """The headline: dist + exact DNJ of one n x L alignment per step.
     world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
-    world > 1: ccg_snp_ltd_shard_dev into this rank's band shard,
-    ccg_tree_shard_dev over `coll` (RCCL).  Returns (timed result, the last
-    step's joins, profiled-step stats or None, alignment, the first capture_k
-    LT cells of the first step (world 1))."""
+    world > 1, tree_mode "shard": ccg_snp_ltd_shard_dev into this rank's band
+    shard, ccg_tree_shard_dev over `coll` (RCCL);
+    world > 1, tree_mode "gather": each rank's dist over its contiguous LT
+    row range (shard.lt_row_ranges, equal cells), the ranges sent to GPU 0
+    (RCCL point-to-point on the process group `pg`, straight into place in
+    its packed LT), and the single-GPU engine builds the tree there while the
+    other ranks wait (at this n a join is a latency-bound chain
+    that the sharded engine's per-join collectives only lengthen).
+    Returns (timed result, the last step's joins, profiled-step stats or None,
+    alignment, the first capture_k LT cells of the first step (world 1))."""
     import hashlib
     import ccphylo_amd as cg
     from ccphylo_amd import native as nt
+    from ccphylo_amd import shard as shd
     seqs, incs, W = make_headline_alignment(torch, n, L)
     m = n * (n - 1) // 2
-    elems = m if world == 1 else nt.shard_elems(n, rank, world)
+    gather = world > 1 and tree_mode == "gather"
+    ranges = shd.lt_row_ranges(n, world) if gather else None
+    if gather:
+        r0, r1 = ranges[rank]
+        elems = m if rank == 0 else r1 * (r1 - 1) // 2 - r0 * (r0 - 1) // 2
+    else:
+        elems = m if world == 1 else nt.shard_elems(n, rank, world)
     D = torch.empty(max(elems, 1), dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
     cap = []
@@ -547,15 +561,48 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
         t0 = time.perf_counter()
         if world == 1:
             inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr())
+        elif gather:
+            # rows [r0, r1) land at their packed offsets: rank 0 in its whole LT,
+            # the others in a buffer that starts at row r0's offset
+            base = D.data_ptr() - (0 if rank == 0 else 8 * (r0 * (r0 - 1) // 2))
+            inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, base, row_range=(r0, r1))
         else:
             inc = dev.snp_ltd_shard_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D.data_ptr(), rank, world)
         dms = dev.last_dist_ms()
+        if gather and pg is not None:   # every range to GPU 0 at once (RCCL over xGMI)
+            ops = []
+            if rank == 0:
+                for g in range(1, world):
+                    a0, a1 = ranges[g]
+                    o0, o1 = a0 * (a0 - 1) // 2, a1 * (a1 - 1) // 2
+                    if o1 > o0:
+                        ops.append(dist.P2POp(dist.irecv, D[o0:o1], g, pg))
+            elif elems:
+                ops.append(dist.P2POp(dist.isend, D[:elems], 0, pg))
+            for w_ in (dist.batch_isend_irecv(ops) if ops else []):
+                w_.wait()
+            torch.cuda.synchronize()
+        elif gather:   # gloo rehearsal (several ranks on one GPU): host-staged, rank by rank
+            torch.cuda.synchronize()
+            if rank == 0:
+                for g in range(1, world):
+                    a0, a1 = ranges[g]
+                    o0, o1 = a0 * (a0 - 1) // 2, a1 * (a1 - 1) // 2
+                    if o1 > o0:
+                        buf = torch.empty(o1 - o0, dtype=torch.float64)
+                        dist.recv(buf, src=g)
+                        D[o0:o1].copy_(buf)
+            elif elems:
+                dist.send(D[:elems].cpu(), dst=0)
+            torch.cuda.synchronize()
         t1 = time.perf_counter()
         if capture_k and not cap and world == 1:   # untimed: only in the first (warmup) step
             cap.append(D[:capture_k].cpu().numpy())
             t1 = time.perf_counter()
-        if world == 1:
+        if world == 1 or (gather and rank == 0):
             j, fn, fd, st = dev.tree_dev(D.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, profile=profile)
+        elif gather:   # the tree runs on GPU 0; this rank's part of the step is done
+            j, fn, fd, st = np.zeros(0, dtype=nt.JOIN_DTYPE), 0, 0.0, [0] * (12 + 2 * nt.NKSTAT)
         else:
             j, fn, fd, st = dev.tree_shard_dev(D.data_ptr(), n, coll, method=cg.CCG_TREE_DNJ, exact=True,
                                                profile=profile)
@@ -805,7 +852,7 @@ def headline_profile_evidence(kernel):
     return out
 
 
-def headline_roofline(n, L, positions, elems, dist_kernel_ms, dist_launches, pst, world):
+def headline_roofline(n, L, positions, elems, dist_kernel_ms, dist_launches, pst, world, single_tree=False):
     """Every kernel of the headline step with its roofline; the dominant one
     (largest device time per step) is the line's `roofline`.
     dist: 6 flops (3 MX-fp4 MACs) per position pair, this rank's cells x the
@@ -831,7 +878,7 @@ def headline_roofline(n, L, positions, elems, dist_kernel_ms, dist_launches, pst
     kernels["dist"] = d
     if pst is not None:
         cs, cr = pst[4 + 2 * len(KNAMES)], pst[5 + 2 * len(KNAMES)]
-        ch = pst[8 + 2 * len(KNAMES)] if world == 1 else 0   # plan helpers' S cells (single engine)
+        ch = pst[8 + 2 * len(KNAMES)] if world == 1 or single_tree else 0   # plan helpers' S cells (single engine)
         for c, name in enumerate(KNAMES):
             cnt, ns = pst[4 + 2 * c], pst[5 + 2 * c]
             if not cnt or name == "coll":
@@ -976,6 +1023,9 @@ def main():
                          "along this tree, DESIGN.md 4)")
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
+    ap.add_argument("--tree-mode", choices=["gather", "shard"], default="gather",
+                    help="N > 1: gather the dist's row ranges to GPU 0 for the single-GPU tree (default), or the "
+                         "row-sharded tree over RCCL (DESIGN.md 6)")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -1023,7 +1073,19 @@ def main():
         start_heartbeat()
     n, L = args.n, args.L
     m = n * (n - 1) // 2
-    elems = m if world == 1 else nt.shard_elems(n, rank, world)
+    pg = None
+    if world == 1:
+        elems = m
+    elif args.tree_mode == "gather":   # this rank's dist cells: its contiguous row range
+        from ccphylo_amd import shard as shd
+        r0_, r1_ = shd.lt_row_ranges(n, world)[rank]
+        elems = r1_ * (r1_ - 1) // 2 - r0_ * (r0_ - 1) // 2
+        if args.shard_transport == "rccl":
+            pg = dist.new_group(backend="nccl")   # RCCL point-to-point for the ranges
+        else:
+            pg = None   # gloo: the default group (host-staged rehearsal)
+    else:
+        elems = nt.shard_elems(n, rank, world)
     log(f"headline: configs[2] pipeline {n} x {L}, world {world}, {args.warmup} warmup + {args.steps} steps")
     hwd = None
     if world > 1:   # a collective that never completes ends the run with a line saying so, not a hang
@@ -1040,7 +1102,7 @@ def main():
         hwd.start()
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
-        capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0)
+        capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg)
     if hwd is not None:
         hwd.cancel()
     dt = head["dt"]
@@ -1048,7 +1110,7 @@ def main():
     # 65536; no split-K at the headline's tile count)
     tiles = (-(-n // 256)) * (-(-n // 256) + 1) // 2 // world
     roof = headline_roofline(n, L, head["included_positions"], elems, head["dist_kernel_ms"],
-                             max(1, -(-tiles // 65536)), pst, world)
+                             max(1, -(-tiles // 65536)), pst, world, single_tree=args.tree_mode == "gather")
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
         "value": round(m * args.steps / dt, 1),
@@ -1066,7 +1128,10 @@ def main():
         "config": {"workload": f"configs[2]: ccphylo dist (MSA, non-pair) + ccphylo tree -m dnj (exact row sums) "
                                f"on {n} taxa x {L / 1e6:g} Mbp, one matrix per step",
                    "n_taxa": n, "alignment_length": L, "lt": "double",
-                   "parallelism": "one GPU" if world == 1 else f"LT row bands over {world} GPUs ({transport})"},
+                   "parallelism": "one GPU" if world == 1 else
+                   (f"dist: LT row ranges over {world} GPUs, gathered to GPU 0 over {args.shard_transport} "
+                    f"point-to-point; tree: GPU 0 (single-GPU engine)" if args.tree_mode == "gather" else
+                    f"LT row bands over {world} GPUs ({transport})")},
         "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
                   "dist_taxa_pairs_per_s": round(m / head["dist_s"], 1),
                   "dist_nt_comparisons_per_s": m * float(L) / head["dist_s"],

@@ -642,6 +642,28 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		double q[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, cq1 = DBL_MAX;
 		int ix[4] = {0, -1, 0, -1}, cp1 = 0;
 		__builtin_amdgcn_s_setprio(3);   // wave 0's loads first: the fold is the critical path
+		// the band candidates' first four requeue blocks (every block of a band
+		// up to G = 256), loaded before the fold's partials so that both share
+		// one round trip; with ubq the requeue also left each block minimum's
+		// partner-cell q (bmqp), so no dependent load for it follows (round 5)
+		const bool lbq = b.ubq != nullptr;
+		double bo_q[2][4], bo_c[2][4];
+		int bo_r[2][4], bo_p[2][4];
+#pragma unroll
+		for(int h = 0; h < 2; ++h) {
+			const int k = lane + 64 * h;
+			const bool act = BANDS && !first && k < kbands;
+			const int G = (int) cdiv(n + 1, TB);
+			const int ga = act ? k * G / kbands : 0, gz = act ? (k + 1) * G / kbands : 0;
+#pragma unroll
+			for(int m = 0; m < 4; ++m) {
+				const int g = ga + m < gz ? ga + m : (gz > ga ? gz - 1 : 0);
+				bo_q[h][m] = act ? b.bmq[g] : DBL_MAX;
+				bo_r[h][m] = act ? b.bmr[g] : 0;
+				bo_p[h][m] = act ? b.bmp[g] : 0;
+				bo_c[h][m] = act && lbq ? b.bmqp[g] : INFINITY;
+			}
+		}
 		if(!first) {
 			const int G = (int) cdiv(n + 1, TB);   // k_dnj_requeue's grid at size n + 1
 			// FU requeue blocks per lane per round trip: every load of a step is
@@ -683,6 +705,7 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 		// [k G / kbands, (k + 1) G / kbands) of bands k = l and l + 64 (h = 0, 1)
 		// with its partner, and loads that partner's cell right away
 		double bcq[2] = {DBL_MAX, DBL_MAX}, bd[2] = {-1.0, -1.0}, bsr[2] = {0.0, 0.0}, bsp[2] = {0.0, 0.0};
+		double bcc[2] = {INFINITY, INFINITY};   // (with ubq) the winner's partner-cell q
 		int bcr[2] = {0, 0}, bcp[2] = {0, 0}, bnr[2] = {n, n}, bnp[2] = {n, n};
 #pragma unroll
 		for(int h = 0; h < 2; ++h) {
@@ -691,14 +714,15 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 			const int G = (int) cdiv(n + 1, TB);
 			const int ga = k * G / kbands, gz = (k + 1) * G / kbands;
 			for(int g0 = ga; g0 < gz; g0 += 4) {
-				double oq[4];
+				double oq[4], oc[4];
 				int orr[4], op[4];
 #pragma unroll
-				for(int m = 0; m < 4; ++m) {   // 4 loads in flight per array
+				for(int m = 0; m < 4; ++m) {   // 4 loads in flight per array (the first four prefetched)
 					const int g = g0 + m < gz ? g0 + m : gz - 1;
-					oq[m] = b.bmq[g];
-					orr[m] = b.bmr[g];
-					op[m] = b.bmp[g];
+					oq[m] = g0 == ga ? bo_q[h][m] : b.bmq[g];
+					orr[m] = g0 == ga ? bo_r[h][m] : b.bmr[g];
+					op[m] = g0 == ga ? bo_p[h][m] : b.bmp[g];
+					oc[m] = g0 == ga ? bo_c[h][m] : lbq ? b.bmqp[g] : INFINITY;
 				}
 #pragma unroll
 				for(int m = 0; m < 4; ++m) {
@@ -706,10 +730,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 						bcq[h] = oq[m];
 						bcr[h] = orr[m];
 						bcp[h] = op[m];
+						bcc[h] = oc[m];
 					}
 				}
 			}
-			if(bcr[h] >= 1 && rows.owns(bcr[h])) {
+			if(!lbq && bcr[h] >= 1 && rows.owns(bcr[h])) {
 				bcp[h] = bcp[h] >= 0 && bcp[h] < bcr[h] ? bcp[h] : 0;
 				bd[h] = Elem<ET>::get(D[rows.row(bcr[h]) + bcp[h]], bs);
 				bsr[h] = b.sD[bcr[h]];
@@ -837,9 +862,11 @@ __global__ __launch_bounds__(TBF) void k_dnj_plan(const typename Elem<ET>::T *__
 						const bool pm = bcp[h] == isub;
 						sS[pos] = bcr[h];
 						sQS[pos] = bcq[h];
-						sQP[pos] = 0 <= bd[h] ? qcrit(GEN ? bnr[h] : n, GEN ? (pm ? Nm : bnp[h]) : n, bd[h], bsr[h],
-						                              pm ? sDm : bsp[h])
-						                      : DBL_MAX;
+						// (with ubq: the requeue's value of the same cell; +inf -> DBL_MAX, no bound)
+						sQP[pos] = lbq ? (bcc[h] < DBL_MAX ? bcc[h] : DBL_MAX)
+						           : 0 <= bd[h] ? qcrit(GEN ? bnr[h] : n, GEN ? (pm ? Nm : bnp[h]) : n, bd[h], bsr[h],
+						                                pm ? sDm : bsp[h])
+						                        : DBL_MAX;
 					}
 					base_pos += __popcll(bm);
 				}

@@ -79,6 +79,7 @@ struct TreeBufs {
 	long long *fpart;
 	double *bmq;         // requeue: each block's min-Q row (candidates of the next S)
 	int *bmr, *bmp;      // and its partner P
+	double *bmqp;        // and (with ubq) the Q criterion at that partner cell in the next join's state
 	int *Spos;           // entry slot of each S row in the descending scan order
 	int *cslot;          // and of each rest entry (k_dnj_find)
 	double *rf;          // per rest entry: fresh (q, j) folded once by k_dnj_fold
@@ -1021,8 +1022,9 @@ __device__ void xs_join_row(const TreeBufs &b, int n, int blk, double d, unsigne
 // (with the fold's partials, one round trip instead of three): lane g < 64
 // holds block g's summary, its first XS_PRE_C crossings and first tie
 #define XS_PRE_C 2
+#define XS_PRE_H 4   // blocks' summaries prefetched per lane: every join block up to G = 256 (n = 65536)
 struct XsPre {
-	XsBlk blk;
+	XsBlk blk, bh[XS_PRE_H - 1];   // blocks lane, lane + 64 h
 	XsCross cr[XS_PRE_C];
 	XsTie ti;
 };
@@ -1034,6 +1036,9 @@ __device__ __forceinline__ void xs_prefetch(const TreeBufs &b, int G, XsPre &p) 
 		for(int c = 0; c < XS_PRE_C; ++c) p.cr[c] = b.xcr[(size_t) g * XB_CAP + c];
 		p.ti = b.xti[(size_t) g * XB_CAP_T];
 	}
+#pragma unroll
+	for(int h = 1; h < XS_PRE_H; ++h)
+		if(g + 64 * h < G) p.bh[h - 1] = b.xblk[g + 64 * h];
 }
 
 __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPre *pre, int n, int *why_out) {
@@ -1050,11 +1055,19 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 	int cob = 0, tob = 0, Rwb = 0;
 	int why = 0;
 	wave_sync();
+	// every block's summary is in registers (pre, G <= 256): the record loads
+	// of all blocks are issued together below, one round trip (round 5);
+	// otherwise block by block as they come
+	const bool allpre = pre && G <= 64 * XS_PRE_H;
+	__shared__ int bco[64 * XS_PRE_H], bto[64 * XS_PRE_H], bRw[64 * XS_PRE_H], bex[64 * XS_PRE_H];
+	__shared__ short cown[XS_CAP], town[XS_CAP_T];   // the block of each crossing / tie record
 	for(int g0 = 0; g0 < G; g0 += 64) {
-		const int g = g0 + lane;
+		const int g = g0 + lane, ph = g0 >> 6;
 		XsBlk s;
 		if(g < G) {
-			s = pre && g0 == 0 ? pre->blk : b.xblk[g];
+			s = pre && g0 == 0 ? pre->blk
+			    : allpre       ? pre->bh[ph >= 1 && ph < XS_PRE_H ? ph - 1 : 0]
+			                   : b.xblk[g];
 		} else {
 			s.tail = 0;
 			s.nc = s.nt = s.tp = s.ex0 = s.bad = 0;
@@ -1064,25 +1077,39 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 		const int co = cob + wave_excl_scan(s.nc, &tc);
 		const int to = tob + wave_excl_scan(s.nt, &tt);
 		const int Rw = Rwb + wave_excl_scan(s.tp, &tr);
-		for(int c = 0; c < s.nc && c < XB_CAP; ++c) {
-			if(co + c < XS_CAP) {
-				lc[co + c] = pre && g0 == 0 && c < XS_PRE_C ? pre->cr[c < XS_PRE_C ? c : 0] : b.xcr[(size_t) g * XB_CAP + c];
-				lcR[co + c] = Rw;
-				lcT[co + c] = to;
+		if(allpre) {   // the block's place in the record lists; the records come after the loop
+			bco[g0 + lane] = co;
+			bto[g0 + lane] = to;
+			bRw[g0 + lane] = Rw;
+			bex[g0 + lane] = s.ex0;
+			if(g < G) {
+				for(int c = 0; c < s.nc && c < XB_CAP && co + c < XS_CAP; ++c) cown[co + c] = (short) g;
+				for(int t = 0; t < s.nt && t < XB_CAP_T && to + t < XS_CAP_T; ++t) town[to + t] = (short) g;
 			}
-		}
-		for(int t = 0; t < s.nt && t < XB_CAP_T; ++t) {
-			if(to + t < XS_CAP_T) {
-				lt[to + t] = pre && g0 == 0 && t == 0 ? pre->ti : b.xti[(size_t) g * XB_CAP_T + t];
-				ltR[to + t] = Rw;
+		} else {
+			for(int c = 0; c < s.nc && c < XB_CAP; ++c) {
+				if(co + c < XS_CAP) {
+					lc[co + c] = pre && g0 == 0 && c < XS_PRE_C ? pre->cr[c < XS_PRE_C ? c : 0] : b.xcr[(size_t) g * XB_CAP + c];
+					lcR[co + c] = Rw;
+					lcT[co + c] = to;
+				}
+			}
+			for(int t = 0; t < s.nt && t < XB_CAP_T; ++t) {
+				if(to + t < XS_CAP_T) {
+					lt[to + t] = pre && g0 == 0 && t == 0 ? pre->ti : b.xti[(size_t) g * XB_CAP_T + t];
+					ltR[to + t] = Rw;
+				}
 			}
 		}
 		wave_sync();
 		if(g < G) {
-			// the block's first run must have assumed its segment's binade; its
-			// last run's sum goes to its segment (integer-valued: exact in any order)
-			const int want = co == 0 ? eH : co - 1 < XS_CAP ? lc[co - 1].x : -1;
-			why |= s.ex0 != want ? XS_WHY_EX0 : 0;
+			// the block's first run must have assumed its segment's binade (checked
+			// after the records with allpre); its last run's sum goes to its segment
+			// (integer-valued: exact in any order)
+			if(!allpre) {
+				const int want = co == 0 ? eH : co - 1 < XS_CAP ? lc[co - 1].x : -1;
+				why |= s.ex0 != want ? XS_WHY_EX0 : 0;
+			}
 			if(co + s.nc <= XS_CAP) atomicAdd(&lseg[co + s.nc], s.tail);
 			else why |= XS_WHY_CAP;
 		}
@@ -1091,6 +1118,58 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 		Rwb += tr;
 	}
 	const int nx = cob, ntot = tob;
+	if(allpre) {
+		// record q of the crossing (tie) list belongs to block cown[q] (town[q]):
+		// every lane loads its records at once, then stores them
+		auto owner = [&](const short *own, int q) { return (int) own[q]; };
+		XsCross cv[2];
+		int cg[2];
+#pragma unroll
+		for(int m = 0; m < 2; ++m) {   // XS_CAP = 128 crossings: two per lane
+			const int q = lane + 64 * m;
+			cg[m] = -1;
+			if(q < nx && q < XS_CAP) {
+				const int g = owner(cown, q);
+				cg[m] = g;
+				cv[m] = b.xcr[(size_t) g * XB_CAP + (q - bco[g])];
+			}
+		}
+		XsTie tv[XS_CAP_T / 64];
+		int tg[XS_CAP_T / 64];
+#pragma unroll
+		for(int m = 0; m < XS_CAP_T / 64; ++m) {
+			const int q = lane + 64 * m;
+			tg[m] = -1;
+			if(q < ntot && q < XS_CAP_T) {
+				const int g = owner(town, q);
+				tg[m] = g;
+				tv[m] = b.xti[(size_t) g * XB_CAP_T + (q - bto[g])];
+			}
+		}
+#pragma unroll
+		for(int m = 0; m < 2; ++m) {
+			const int q = lane + 64 * m;
+			if(cg[m] >= 0) {
+				lc[q] = cv[m];
+				lcR[q] = bRw[cg[m]];
+				lcT[q] = bto[cg[m]];
+			}
+		}
+#pragma unroll
+		for(int m = 0; m < XS_CAP_T / 64; ++m) {
+			const int q = lane + 64 * m;
+			if(tg[m] >= 0) {
+				lt[q] = tv[m];
+				ltR[q] = bRw[tg[m]];
+			}
+		}
+		wave_sync();
+		for(int g = lane; g < G; g += 64) {   // the start-binade checks of the loop above
+			const int co = bco[g];
+			const int want = co == 0 ? eH : co - 1 < XS_CAP ? lc[co - 1].x : -1;
+			why |= bex[g] != want ? XS_WHY_EX0 : 0;
+		}
+	}
 	why |= nx > XS_CAP - 1 || ntot > XS_CAP_T ? XS_WHY_CAP : 0;
 #pragma unroll
 	for(int q = 0; q < XS_NWHY; ++q) why |= __any((why >> q) & 1) ? 1 << q : 0;

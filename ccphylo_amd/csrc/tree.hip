@@ -896,7 +896,7 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
                                                     int n, int general, int exact_arg) {
 	__shared__ double sq[5][TB / 64], sfq[TB / 64];
 	__shared__ int si[5][TB / 64], sfp[TB / 64], sbp[TB / 64];
-	__shared__ double sfv[TB / 64];
+	__shared__ double sfv[TB / 64], sbq[TB / 64];
 	__shared__ double s_sd;
 	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain;
 	TreeCtl *ctl = b.ctl;
@@ -1080,15 +1080,17 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
 	// fold); only when the next S has a band part
-	double bq = DBL_MAX, bdum = 0.0;
+	// (with ubq, also the q at that partner cell: the plan then needs no load for it)
+	double bq = DBL_MAX, bqc = INFINITY;
 	int bk = 0, bp = 0;
 	if(BANDS) {
 		if(k >= 1 && k < nn && k != i && k != j) {
 			bq = k > j ? fq : qk0;
 			bk = k;
 			bp = k > j ? fp : pkk0;   // its partner, for k_dnj_plan's partner-cell bound
+			bqc = qpc;
 		}
-		qarg_wave_reduce_carry(bq, bk, bdum, bp);
+		qarg_wave_reduce_carry(bq, bk, bqc, bp);
 	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
@@ -1109,11 +1111,12 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 			sq[4][wid] = bq;
 			si[4][wid] = bk;
 			sbp[wid] = bp;
+			sbq[wid] = bqc;
 		}
 	}
 	__syncthreads();
 	if(tid < (BANDS ? 5 : 4)) {
-		double q = sq[tid][0], cq = sfq[0];
+		double q = sq[tid][0], cq = sfq[0], xq = BANDS ? sbq[0] : 0.0;
 		int ix = si[tid][0], cp = sfp[0], xp = BANDS ? sbp[0] : 0;
 		for(int w = 1; w < TB / 64; ++w) {
 			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
@@ -1121,13 +1124,17 @@ __global__ __launch_bounds__(TB) void k_dnj_requeue(typename Elem<ET>::T *__rest
 				ix = si[tid][w];
 				cq = sfq[w];
 				cp = sfp[w];
-				if(BANDS) xp = sbp[w];
+				if(BANDS) {
+					xp = sbp[w];
+					xq = sbq[w];
+				}
 			}
 		}
 		if(tid == 4) {
 			b.bmq[blockIdx.x] = q;
 			b.bmr[blockIdx.x] = ix;
 			b.bmp[blockIdx.x] = xp;
+			b.bmqp[blockIdx.x] = xq;
 		} else {
 			b.qpart[4 * blockIdx.x + tid] = q;
 			b.ipart[4 * blockIdx.x + tid] = ix;
@@ -1690,7 +1697,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	size_t o_fp = take(nq * 8), o_cfq = take(nb * 8), o_cfp = take(nb * 4);
 	size_t o_j = take((size_t) n * sizeof(ccg_join)), o_ctl = take(sizeof(TreeCtl));
 	const size_t nrf = ncand > JOIN_UPRE ? ncand : JOIN_UPRE;   // k_dnj_join prefetches JOIN_UPRE
-	size_t o_bp = take(nb * 4);
+	size_t o_bp = take(nb * 4), o_bqp = take(nb * 8);
 	size_t o_bq = take(nb * 8), o_br = take(nb * 4), o_sp = take((DNJ_B + 1) * 4), o_cs = take(ncand * 4);
 	size_t o_rf = take(nrf * 8), o_rj = take(nrf * 4);
 	size_t o_xa = take(nb * 8), o_xb = take(nb * sizeof(XsBlk)), o_xc = take(nb * XB_CAP * sizeof(XsCross));
@@ -1740,6 +1747,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.bmq = (double *) (m + o_bq);
 	b.bmr = (int *) (m + o_br);
 	b.bmp = (int *) (m + o_bp);
+	b.bmqp = (double *) (m + o_bqp);
 	b.Spos = (int *) (m + o_sp);
 	b.cslot = (int *) (m + o_cs);
 	b.rf = (double *) (m + o_rf);
@@ -2057,6 +2065,8 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			// S-bound pruning no longer pays beside the bounded scan (headline tree, profiled: 4.61 s
 			// without, 4.78 s with the plan's helpers and the compaction); CCG_SCAN_PRUNE still forces it
 			if(!getenv("CCG_SCAN_PRUNE")) g_grid.scan_prune = 0;
+			// the bounded units are short: twice the waves (headline tree 4.84 -> 4.74 s, profiled)
+			if(!getenv("CCG_SCAN_CMPB")) g_grid.cmp_blocks = 2048;
 		} else {
 			(void) hipGetLastError();   // no room: the run goes without (the same joins)
 			lbmem = NULL;

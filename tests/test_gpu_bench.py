@@ -32,12 +32,17 @@ def test_bench_world_mismatch_refused():
 
 @pytest.mark.gpu
 def test_bench_gpus2_spawned_same_joins():
+    """--gpus 2 (ranks spawned by bench.py, gloo rehearsal on one GPU) in both
+    tree modes: the dist's row ranges gathered to GPU 0 for the single-GPU
+    tree (the default), and the row-sharded tree; the same joins as --gpus 1."""
     one = _bench(["--gpus", "1"] + SMALL)
     assert one.returncode == 0, one.stderr[-3000:]
-    two = _bench(["--gpus", "2", "--shard-transport", "gloo"] + SMALL)
-    assert two.returncode == 0, two.stderr[-3000:]
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
-    l2 = json.loads(two.stdout.strip().splitlines()[-1])
-    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
-    assert l2["split"]["joins_sha256"] == l1["split"]["joins_sha256"]
-    assert l2["split"]["joins"] == l1["split"]["joins"] == 2998
+    assert l1["n_gpus"] == 1
+    for mode in ("gather", "shard"):
+        two = _bench(["--gpus", "2", "--shard-transport", "gloo", "--tree-mode", mode] + SMALL)
+        assert two.returncode == 0, (mode, two.stderr[-3000:])
+        l2 = json.loads(two.stdout.strip().splitlines()[-1])
+        assert l2["n_gpus"] == 2
+        assert l2["split"]["joins_sha256"] == l1["split"]["joins_sha256"], mode
+        assert l2["split"]["joins"] == l1["split"]["joins"] == 2998

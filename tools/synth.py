@@ -34,7 +34,17 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
         rmax = int(rows[-1])
         if rmax == 0:
             continue
-        d = torch.cdist(pts[rows], pts[:rmax], compute_mode="donot_use_mm_for_euclid_dist")
+        # elementwise, one dimension at a time: every cell's value depends on
+        # its two points only (torch.cdist's may depend on the batch's shape,
+        # so the ranks of a world-8 run and the world-1 LT disagreed in the
+        # last bit of some cells)
+        a, c = pts[rows][:, None, :], pts[:rmax][None, :, :]
+        t = a[..., 0] - c[..., 0]
+        s2 = t * t
+        for k in range(1, dim):
+            t = a[..., k] - c[..., k]
+            s2 = s2 + t * t
+        d = torch.sqrt(s2)
         mask = torch.arange(rmax, device="cuda")[None, :] < rows[:, None]
         vals = d[mask]                       # row-major: each row's prefix, rows in order
         out[pos:pos + vals.numel()] = vals
