@@ -75,6 +75,20 @@ int ccg_init(int device, ccg_ctx **out) {
 	return CCG_OK;
 }
 
+int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int flags) {
+	if(!c || mask_words < 0 || (mask_words && !cu_mask)) return CCG_EINVAL;
+	CCG_CHECK(hipSetDevice(c->device));
+	if(mask_words) {   // the engine stream again, limited to the CUs of the mask
+		hipStream_t s;
+		CCG_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t) mask_words, cu_mask));
+		CCG_CHECK(hipStreamSynchronize(c->stream));
+		CCG_CHECK(hipStreamDestroy(c->stream));
+		c->stream = s;
+	}
+	c->flags = flags;
+	return CCG_OK;
+}
+
 void ccg_destroy(ccg_ctx *c) {
 	if(!c) return;
 	hipSetDevice(c->device);
@@ -94,21 +108,21 @@ int ccg_device_info(ccg_ctx *c, char *buf, size_t len) {
 int ccg_snp_ltd_dev(ccg_ctx *c, const ccg_snp_args *a, void *D, void *N, int *inc_out) {
 	if(!c || !a || !D) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
+	CCG_DEVICE_SYNC(c);   // inputs may come from other streams (e.g. torch's)
 	return ccg_snp_dev_impl(c, a, D, N, inc_out, false);
 }
 
 int ccg_snp_ltd_shard_dev(ccg_ctx *c, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
 	if(!c || !a || !Dloc) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());
+	CCG_DEVICE_SYNC(c);
 	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out, false);
 }
 
 int ccg_snp_ltd_shard(ccg_ctx *c, const ccg_snp_args *a, int rank, int world, void *Dloc, int *inc_out) {
 	if(!c || !a || !Dloc || !a->seqs || !a->incs) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());
+	CCG_DEVICE_SYNC(c);
 	return ccg_snp_shard_dev_impl(c, a, rank, world, Dloc, inc_out, true);
 }
 
@@ -156,7 +170,7 @@ int ccg_tree_dev(ccg_ctx *c, const ccg_tree_args *a, void *D, ccg_join *joins, i
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
+	CCG_DEVICE_SYNC(c);   // inputs may come from other streams (e.g. torch's)
 	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats, NULL, NULL);
 }
 
@@ -170,7 +184,7 @@ int ccg_tree_dev_state(ccg_ctx *c, const ccg_tree_args *a, void *D, const ccg_dn
 		return CCG_EINVAL;
 	if(out && (!out->sD || !out->Q || !out->N || !out->P)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());
+	CCG_DEVICE_SYNC(c);
 	return ccg_tree_impl(c, a, D, joins, njoins, final_n, final_d, stats, in, out);
 }
 

@@ -32,7 +32,14 @@ struct ccg_ctx {
 	hipEvent_t ev0, ev1;
 	char name[256];
 	float dist_ms;   // the last dist call's pair kernels (HIP events on the engine stream)
+	int flags;       // CCG_CTX_* (ccg_ctx_configure)
 };
+// every device-pointer entry point first waits for the whole device (inputs
+// may come from other streams) unless the caller orders them itself
+#define CCG_DEVICE_SYNC(c) \
+	do { \
+		if(!((c)->flags & CCG_CTX_NOSYNC)) CCG_CHECK(hipDeviceSynchronize()); \
+	} while(0)
 
 // ---------------------------------------------------------------- numerics
 __device__ __forceinline__ int32_t cvt_i32_x86(double x) {

@@ -126,6 +126,7 @@ struct TreeBufs {
 	double *ubq;         // per row: the Q criterion at its partner cell in this join's state (an upper bound
 	                     // of its fresh minimum, left by the previous requeue; +inf: unknown, rows j and i)
 	long long lbs;
+	int xs_allpre;       // the exact walk loads every block's records at once (CCG_XS_ALLPRE=0: block by block)
 	long long *lbskip;   // cells skipped under the block bounds (stats): per-wave slots of LB_SLOT longs --
 	                     // field 0 the cells not loaded, field 1 those of them in S rows (the plan's helpers);
 	                     // scan waves [0, LB_SCAN), helper waves after (no same-address atomics: thousands
@@ -1058,7 +1059,7 @@ __device__ bool xs_walk_blocks(const TreeBufs &b, int G, double *out, const XsPr
 	// every block's summary is in registers (pre, G <= 256): the record loads
 	// of all blocks are issued together below, one round trip (round 5);
 	// otherwise block by block as they come
-	const bool allpre = pre && G <= 64 * XS_PRE_H;
+	const bool allpre = pre && G <= 64 * XS_PRE_H && b.xs_allpre;
 	__shared__ int bco[64 * XS_PRE_H], bto[64 * XS_PRE_H], bRw[64 * XS_PRE_H], bex[64 * XS_PRE_H];
 	__shared__ short cown[XS_CAP], town[XS_CAP_T];   // the block of each crossing / tie record
 	for(int g0 = 0; g0 < G; g0 += 64) {

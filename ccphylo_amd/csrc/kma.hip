@@ -479,7 +479,7 @@ int ccg_kma_ltd_dev(ccg_ctx *c, const ccg_kma_args *a, void *D, void *N, int64_t
 	if(rc) return rc;
 	if(!c || (a->n > 1 && (!D || !a->rec1 || !a->rec2 || !a->len1 || !a->len2))) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
+	CCG_DEVICE_SYNC(c);   // inputs may come from other streams (e.g. torch's)
 	return kma_run(c, a, D, N, fatal);
 }
 

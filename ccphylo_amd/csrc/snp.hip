@@ -2064,7 +2064,7 @@ extern "C" int ccg_round_decimal_dev(ccg_ctx *ctx, void *D, int64_t elems, int e
 	if(!ctx || (!D && elems) || elems < 0 || precision < 0 || precision > 22) return CCG_EINVAL;
 	if(etype != 8 && etype != 4) return CCG_EUNSUP;
 	CCG_CHECK(hipSetDevice(ctx->device));
-	CCG_CHECK(hipDeviceSynchronize());
+	CCG_DEVICE_SYNC(ctx);
 	if(!elems) return CCG_OK;
 	double P = 1.0;
 	for(int k = 0; k < precision; ++k) P *= 10.0;   // exact up to 10^22

@@ -851,14 +851,14 @@ int ccg_tree_shard_dev(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll,
 		if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 		if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 		CCG_CHECK(hipSetDevice(c->device));
-		CCG_CHECK(hipDeviceSynchronize());
+		CCG_DEVICE_SYNC(c);
 		return ccg_tree_impl(c, a, Dloc, joins, njoins, final_n, final_d, stats, NULL, NULL);
 	}
 	int rc = shard_check(c, a, coll);
 	if(rc) return rc;
 	if(!Dloc || !joins || !njoins || !final_n || !final_d) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
-	CCG_CHECK(hipDeviceSynchronize());   // inputs may come from other streams (e.g. torch's)
+	CCG_DEVICE_SYNC(c);   // inputs may come from other streams (e.g. torch's)
 	if(a->method == CCG_TREE_DNJ) {
 		ccg_coll self;
 		if(!coll) {

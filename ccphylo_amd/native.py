@@ -103,6 +103,7 @@ class Coll(C.Structure):
                 ("allreduce_sum_u8", ALLREDUCE_FN), ("broadcast", BROADCAST_FN), ("allgather", ALLGATHER_FN)]
 
 
+CCG_CTX_NOSYNC = 1
 JOIN_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("Li", np.float64), ("Lj", np.float64)])
 
 # every symbol of include/ccphylo_amd.h
@@ -113,7 +114,7 @@ ENGINE_SYMBOLS = [
     "ccg_shard_owner", "ccg_shard_row_offset", "ccg_shard_elems",
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
-    "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state", "ccg_tree_shard_bytes",
+    "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state", "ccg_tree_shard_bytes", "ccg_ctx_configure",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -156,6 +157,7 @@ def engine_lib():
         lib.ccg_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         lib.ccg_destroy.argtypes = [C.c_void_p]
         lib.ccg_destroy.restype = None
+        lib.ccg_ctx_configure.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_int, C.c_int]
         lib.ccg_strerror.argtypes = [C.c_int]
         lib.ccg_strerror.restype = C.c_char_p
         lib.ccg_device_info.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
@@ -284,6 +286,22 @@ class Device:
         if self.h:
             self.lib.ccg_destroy(self.h)
             self.h = None
+
+    def configure(self, cu_mask=None, nosync=False):
+        """ccg_ctx_configure: cu_mask (a sequence of CU indices, or None: all)
+        limits the engine stream to those compute units; nosync: the entry
+        points do not wait for the whole device first (two contexts side by
+        side: the caller orders their inputs)."""
+        words = None
+        nw = 0
+        if cu_mask is not None:
+            cus = sorted(set(int(x) for x in cu_mask))
+            nw = max(cus) // 32 + 1 if cus else 0
+            words = (C.c_uint32 * max(nw, 1))()
+            for cu in cus:
+                words[cu // 32] |= 1 << (cu % 32)
+        self._check(self.lib.ccg_ctx_configure(self.h, words, nw, CCG_CTX_NOSYNC if nosync else 0),
+                    "ccg_ctx_configure")
 
     def __enter__(self):
         return self

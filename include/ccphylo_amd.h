@@ -46,6 +46,16 @@ typedef struct ccg_ctx ccg_ctx;
 /* Opens `device` (ordinal in HIP_VISIBLE_DEVICES numbering) and creates the
  * engine stream.  Fails with CCG_ENODEV when no gfx950 device is present. */
 int ccg_init(int device, ccg_ctx **ctx);
+
+/* Optional, after ccg_init: cu_mask (mask_words 32-bit words, bit k = CU k;
+ * 0 words: unchanged) limits the context's stream to those compute units
+ * (hipExtStreamCreateWithCUMask), so that two contexts of one device can run
+ * side by side -- e.g. one matrix's dist beside the previous matrix's tree;
+ * flags CCG_CTX_NOSYNC: the device-pointer entry points do not wait for the
+ * whole device first (the caller orders its inputs; a device-wide wait would
+ * wait for the other context's work). */
+#define CCG_CTX_NOSYNC 1
+int ccg_ctx_configure(ccg_ctx *ctx, const uint32_t *cu_mask, int mask_words, int flags);
 /* HIP devices visible to this process (the multi-GPU CLI deals ranks over them) */
 int ccg_device_count(int *count);
 void ccg_destroy(ccg_ctx *ctx);
