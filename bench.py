@@ -398,7 +398,8 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "kernel": ("k_snp_mfma_pair" if pair else ("k_snp_mfma" if mode_env == "1" else "k_snp_mfma2")) if mfma
+            "kernel": (("k_snp_mfma_pair" if mode_env == "1" else "k_snp_mfma2_pair") if pair
+                       else ("k_snp_mfma" if mode_env == "1" else "k_snp_mfma2")) if mfma
             else ("k_snp_tile_pair" if pair else "k_snp_tile"),
             "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
             else valu_roofline(ops, dt, opw)}
@@ -527,7 +528,7 @@ def make_headline_alignment(torch, n, L):
 
 
 def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0,
-                 tree_mode="shard", pg=None):
+                 tree_mode="shard", pg=None, tree_cus=0):
     """The headline: dist + exact DNJ of one n x L alignment per step.
     world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
     world > 1, tree_mode "shard": ccg_snp_ltd_shard_dev into this rank's band
@@ -539,7 +540,10 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     other ranks wait (at this n a join is a latency-bound chain
     that the sharded engine's per-join collectives only lengthen).
     Returns (timed result, the last step's joins, profiled-step stats or None,
-    alignment, the first capture_k LT cells of the first step (world 1))."""
+    alignment, the first capture_k LT cells of the first step (world 1)).
+    world 1 with tree_cus > 0: the pipelined form (pipelined_leg)."""
+    if world == 1 and tree_cus > 0:
+        return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k)
     import hashlib
     import ccphylo_amd as cg
     from ccphylo_amd import native as nt
@@ -635,6 +639,90 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     del D
     torch.cuda.empty_cache()
     return res, joins, pst, (seqs, incs, W), (cap[0] if cap else None)
+
+
+def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0):
+    """The headline on one GPU as a pipeline over a stream of alignments: two
+    engine contexts on disjoint compute units (ccg_ctx_configure: the tree's
+    stream on CUs [0, tree_cus), the dist's on the rest, neither waiting for
+    the whole device) and two LT buffers, so that step k builds the tree of
+    matrix k while the dist of matrix k + 1 fills the other buffer.  The dist
+    of matrix 0 runs before the warmup; every timed step holds one whole dist
+    and one whole tree (K of each in K steps), so the rate is matrices
+    completed per second in steady state.  The joins of every step equal the
+    sequential form's (the tree is deterministic and reads only its own
+    buffer).  Same return value as pipeline_leg."""
+    import hashlib
+    import threading
+    import ccphylo_amd as cg
+    seqs, incs, W = make_headline_alignment(torch, n, L)
+    m = n * (n - 1) // 2
+    gpu = torch.cuda.current_device()
+    ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
+    tree_cus = max(1, min(tree_cus, ncu - 1))
+    ddev, tdev = cg.Device(gpu), cg.Device(gpu)
+    ddev.configure(cu_mask=list(range(tree_cus, ncu)), nosync=True)
+    tdev.configure(cu_mask=list(range(tree_cus)), nosync=True)
+    Ds = [torch.empty(m, dtype=torch.float64, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    inc0 = ddev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[0].data_ptr())   # matrix 0
+    cap = Ds[0][:capture_k].cpu().numpy() if capture_k else None
+
+    def step(k, profile=False):
+        res, err = {}, []
+
+        def run_d():
+            try:
+                t0 = time.perf_counter()
+                inc = ddev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr())
+                res["d"] = (time.perf_counter() - t0, ddev.last_dist_ms(), inc)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+
+        def run_t():
+            try:
+                t0 = time.perf_counter()
+                j, fn, fd, st = tdev.tree_dev(Ds[k % 2].data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True,
+                                              profile=profile)
+                res["t"] = (time.perf_counter() - t0, (j, fn, fd), st)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        th = [threading.Thread(target=run_d), threading.Thread(target=run_t)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if err:
+            raise err[0]
+        return res["d"][0], res["t"][0], res["d"][1], res["t"][1], res["t"][2], res["d"][2]
+
+    k = 0
+    for w in range(warmup):
+        r = step(k)
+        k += 1
+        log(f"  warmup step {w}: dist {r[0]:.2f} s beside tree {r[1]:.2f} s")
+    barrier()
+    t0 = time.perf_counter()
+    parts = []
+    for s_ in range(steps):
+        parts.append(step(k))
+        k += 1
+        log(f"  step {s_}: dist {parts[-1][0]:.2f} s beside tree {parts[-1][1]:.2f} s")
+    barrier()
+    dt = time.perf_counter() - t0
+    joins, st, inc = parts[-1][3], parts[-1][4], parts[-1][5]
+    jj, fn, fd = joins
+    sha = hashlib.sha256(np.ascontiguousarray(jj).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+    pst = step(k, profile=True)[4] if profile_tree else None   # an extra, untimed pipelined step
+    res = {"dt": dt, "dist_s": sum(p[0] for p in parts) / steps, "tree_s": sum(p[1] for p in parts) / steps,
+           "dist_kernel_ms": sum(p[2] for p in parts) / steps, "joins": len(jj), "joins_sha256": sha,
+           "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]), "included_positions": inc,
+           "pipelined": {"tree_cus": tree_cus, "dist_cus": ncu - tree_cus, "matrix0_included_positions": inc0}}
+    del Ds
+    ddev.close()
+    tdev.close()
+    torch.cuda.empty_cache()
+    return res, joins, pst, (seqs, incs, W), cap
 
 
 def refrule_cells(dev, torch, seqs, incs, n, L, W, prefix, threads):
@@ -1026,6 +1114,9 @@ def main():
     ap.add_argument("--tree-mode", choices=["gather", "shard"], default="gather",
                     help="N > 1: gather the dist's row ranges to GPU 0 for the single-GPU tree (default), or the "
                          "row-sharded tree over RCCL (DESIGN.md 6)")
+    ap.add_argument("--tree-cus", type=int, default=40,
+                    help="N = 1: the pipelined headline (pipelined_leg) with the tree on this many compute units and "
+                         "the next matrix's dist on the rest; 0: dist then tree on the whole chip, step by step")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -1102,7 +1193,8 @@ def main():
         hwd.start()
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
-        capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg)
+        capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg,
+        tree_cus=args.tree_cus if world == 1 else 0)
     if hwd is not None:
         hwd.cancel()
     dt = head["dt"]
@@ -1111,6 +1203,13 @@ def main():
     tiles = (-(-n // 256)) * (-(-n // 256) + 1) // 2 // world
     roof = headline_roofline(n, L, head["included_positions"], elems, head["dist_kernel_ms"],
                              max(1, -(-tiles // 65536)), pst, world, single_tree=args.tree_mode == "gather")
+    pipe = head.get("pipelined")
+    if pipe:   # the dist kernel ran on the dist context's share of the CUs
+        dk = roof["kernels"]["dist"]
+        dk["cus"] = pipe["dist_cus"]
+        dk["frac_of_cu_share"] = round(dk["frac"] * (pipe["dist_cus"] + pipe["tree_cus"]) / pipe["dist_cus"], 4)
+        if roof.get("kernel") == "k_snp_mfma2":
+            roof["cus"], roof["frac_of_cu_share"] = dk["cus"], dk["frac_of_cu_share"]
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",
         "value": round(m * args.steps / dt, 1),
@@ -1128,11 +1227,14 @@ def main():
         "config": {"workload": f"configs[2]: ccphylo dist (MSA, non-pair) + ccphylo tree -m dnj (exact row sums) "
                                f"on {n} taxa x {L / 1e6:g} Mbp, one matrix per step",
                    "n_taxa": n, "alignment_length": L, "lt": "double",
-                   "parallelism": "one GPU" if world == 1 else
+                   "parallelism": (f"one GPU, pipelined: tree of matrix k on CUs [0, {pipe['tree_cus']}) beside "
+                                   f"the dist of matrix k + 1 on the other {pipe['dist_cus']}" if pipe else "one GPU")
+                   if world == 1 else
                    (f"dist: LT row ranges over {world} GPUs, gathered to GPU 0 over {args.shard_transport} "
                     f"point-to-point; tree: GPU 0 (single-GPU engine)" if args.tree_mode == "gather" else
                     f"LT row bands over {world} GPUs ({transport})")},
         "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
+                  "overlap": "dist and tree walls run concurrently (pipelined)" if pipe else "sequential",
                   "dist_taxa_pairs_per_s": round(m / head["dist_s"], 1),
                   "dist_nt_comparisons_per_s": m * float(L) / head["dist_s"],
                   "tree_nj_iterations_per_s": round(head["joins"] / head["tree_s"], 1),

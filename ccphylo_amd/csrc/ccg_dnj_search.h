@@ -408,6 +408,11 @@ __device__ __forceinline__ void s_table_h(const TreeBufs &b, int n, int nS, doub
 		__hip_atomic_store(b.srdy + 32 * lane, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int ET>   // (below, with the scan)
+__device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
+                                       int r, int c0, int c1, double sDr, double &q, int &idx, int isub = -1,
+                                       double sDm = 0.0, bool ubinf = false);
+
 template <int ET>
 __device__ __forceinline__ void plan_s_helper(const typename Elem<ET>::T *__restrict__ D, double bs,
                                                         TreeBufs b, int n, int hb, int nh, bool tshort) {
@@ -1681,8 +1686,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // threshold)
 template <int ET>
 __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
-                                       int r, int c0, int c1, double sDr, double &q, int &idx, int isub = -1,
-                                       double sDm = 0.0, bool ubinf = false) {
+                                       int r, int c0, int c1, double sDr, double &q, int &idx, int isub,
+                                       double sDm, bool ubinf) {
 	typedef typename Elem<ET>::T T;
 	constexpr int BB = 8;
 	const int lane = threadIdx.x & 63;
@@ -1691,10 +1696,11 @@ __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ 
 	const double ub = ubinf ? INFINITY : b.ubq[r];
 	unsigned lbb[4];
 	double msb[4];
+	const unsigned *line = lb_line(b, r);
 #pragma unroll
 	for(int h = 0; h < 4; ++h) {
 		const int t = lane + 64 * h;
-		lbb[h] = t < nbk ? b.lbm[(long long) r * b.lbs + bl0 + t] : 0u;
+		lbb[h] = t < nbk ? line[bl0 + t] : 0u;
 		msb[h] = t < nbk ? b.msd[bl0 + t] : 0.0;
 	}
 	unsigned long long need[4];

@@ -126,6 +126,8 @@ struct TreeBufs {
 	double *ubq;         // per row: the Q criterion at its partner cell in this join's state (an upper bound
 	                     // of its fresh minimum, left by the previous requeue; +inf: unknown, rows j and i)
 	long long lbs;
+	int lbw;             // 0: lbm rows are the matrix rows; w > 0: the sharded engine's, a rank's own rows
+	                     // by position among them (bands of 8 rows dealt over w ranks, ccg_shard.h)
 	int xs_allpre;       // the exact walk loads every block's records at once (CCG_XS_ALLPRE=0: block by block)
 	long long *lbskip;   // cells skipped under the block bounds (stats): per-wave slots of LB_SLOT longs --
 	                     // field 0 the cells not loaded, field 1 those of them in S rows (the plan's helpers);
@@ -137,6 +139,12 @@ struct TreeBufs {
 #define LB_SLOT 16      // longs per stats slot (one 128-B line)
 #define LB_SCAN 4096    // scan wave slots
 #define LB_HELP 8192    // helper wave slots
+
+// row r's line of the block bounds
+__device__ __forceinline__ unsigned *lb_line(const TreeBufs &b, int r) {
+	const long long p = b.lbw ? (long long) ((r >> 3) / b.lbw) * 8 + (r & 7) : r;
+	return b.lbm + p * b.lbs;
+}
 
 // a float <= x (x >= 0: a cell value) as order-preserving bits
 __device__ __forceinline__ unsigned lb_bits(double x) {

@@ -1226,6 +1226,231 @@ __global__ __launch_bounds__(256, 2) void k_snp_mfma_pair(const uint4 *__restric
 	}
 }
 
+// k_snp_mfma2_pair: pair mode on k_snp_mfma2's 256 x 256 tiles.  The mask
+// enters the nibble's exponent instead of being and-ed in afterwards: a
+// component nibble is (sign << 3) | (m << 1), +-1.0 where the row includes the
+// position and +-0.0 where it does not, so one mask spread per word (the 0x2
+// bits, itself the fourth operand: +1 / 0) serves all four components; hi and
+// lo cost one and_or per dword on top of it and hi ^ lo one xor_or
+// ((a ^ b) | msp: the shared exponent bits cancel and are set again).  Two
+// accumulator sets (dot, n) per 32 x 32 tile, so a wave takes 128 x 64 and a
+// block of 4 waves one column half of a 256 x 256 tile (items = 2 per tile):
+// each step spreads 4 A and 2 B words (25 VALU each) for 32 MFMAs, against
+// k_snp_mfma_pair's 384 VALU for 16.  Staging as k_snp_mfma2 with uint4
+// {hi, lo, m, 0} words (99 KB of LDS at 8 words per chunk, one block per
+// CU); BAND and SPLIT as k_snp_mfma2.
+__device__ __forceinline__ v8i_t pair2_mask(uint32_t m) {
+	v8i_t v;
+	v[0] = (int) ((m << 1) & 0x22222222u);
+	v[1] = (int) (m & 0x22222222u);
+	v[2] = (int) ((m >> 1) & 0x22222222u);
+	v[3] = (int) ((m >> 2) & 0x22222222u);
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+__device__ __forceinline__ v8i_t pair2_comp(uint32_t x, const v8i_t &m) {
+	v8i_t v;
+	v[0] = (int) and_or(x << 3, 0x88888888u, (uint32_t) m[0]);
+	v[1] = (int) and_or(x << 2, 0x88888888u, (uint32_t) m[1]);
+	v[2] = (int) and_or(x << 1, 0x88888888u, (uint32_t) m[2]);
+	v[3] = (int) and_or(x, 0x88888888u, (uint32_t) m[3]);
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+__device__ __forceinline__ v8i_t pair2_xor(const v8i_t &h, const v8i_t &l, const v8i_t &m) {
+	v8i_t v;
+#pragma unroll
+	for(int q = 0; q < 4; ++q) v[q] = (int) xor_or((uint32_t) h[q], (uint32_t) l[q], (uint32_t) m[q]);
+	v[4] = v[5] = v[6] = v[7] = 0;
+	return v;
+}
+
+#define RS2P 258   // pair LDS row strides (uint4): 256 A rows, 128 B rows, + pad
+#define RS2B 130
+template <int ET, bool SPLIT, bool BAND>
+__global__ __launch_bounds__(256, 1) void k_snp_mfma2_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
+                                                           long long items, int S, int Wk, unsigned norm,
+                                                           unsigned minLength, double bs,
+                                                           typename Elem<ET>::T *__restrict__ D,
+                                                           typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
+                                                           long long rowEnd, unsigned *__restrict__ cd,
+                                                           unsigned *__restrict__ cn, long long cbase,
+                                                           const long long *__restrict__ pfx, int npanels, int rank,
+                                                           int world) {
+	constexpr int QA = TILE2 * KC2 / 256, QB = QA / 2;   // uint4 staged per thread: A panel, B half panel
+	__shared__ __attribute__((aligned(16))) uint4 As[2][KC2 * RS2P];
+	__shared__ __attribute__((aligned(16))) uint4 Bs[2][KC2 * RS2B];
+	const long long item = t0 + xcd_tile(blockIdx.x, items), th = SPLIT ? item / S : item, t = th >> 1;
+	const int half = (int) (th & 1);   // the tile's column half: B rows J * 256 + 128 half + [0, 128)
+	int I, J;
+	if(BAND) {
+		int lo = 0, hi = npanels - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
+		}
+		I = lo;
+		J = (int) (t - pfx[lo]);
+	} else {
+		tile_ij(t, I, J);
+	}
+	const int wb = SPLIT ? (int) (item % S) * Wk : 0;
+	const int Wl = SPLIT ? (wb + Wk < Wp ? Wk : Wp - wb) : Wp;
+	const auto arow = [&](int l) -> long long {
+		const long long L = (long long) I * TILE2 + l;
+		if(!BAND) return L;
+		const long long lb = L / SB, r = (lb * world + rank) * SB + (L - lb * SB);
+		return r < n ? r : 0;
+	};
+	const uint4 *Bp = P + ((size_t) J * TILE2 + 128 * half) * Wp + wb;
+	const uint4 *Ap[QA];
+	// (staging registers in arrays of 4 uint4: a larger array is left in scratch)
+	// (staging registers as native 4-dword vectors: HIP's uint4 struct copies
+	// become memcpys that keep the arrays in scratch)
+	typedef unsigned u4v __attribute__((ext_vector_type(4)));
+	u4v vaa[4], vab[4], vb[4];
+	static_assert(QA == 8 && QB == 4, "staging registers: A in two arrays of 4, B in one");
+	u4v *As4 = (u4v *) &As[0][0], *Bs4 = (u4v *) &Bs[0][0];
+	const int srow = threadIdx.x / KC2, swp = threadIdx.x % KC2;   // staged element q: row srow + 32 q, word swp
+#pragma unroll
+	for(int q = 0; q < QA; ++q) Ap[q] = P + (size_t) arow(srow + 32 * q) * Wp + wb + swp;
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		vaa[q] = *(const u4v *) Ap[q];
+		vab[q] = *(const u4v *) Ap[q + 4];
+	}
+	Bp += (size_t) srow * Wp + swp;
+#pragma unroll
+	for(int q = 0; q < QB; ++q) vb[q] = *(const u4v *) (Bp + (size_t) 32 * q * Wp);
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		As4[swp * RS2P + srow + 32 * q] = vaa[q];
+		As4[swp * RS2P + srow + 32 * (q + 4)] = vab[q];
+	}
+#pragma unroll
+	for(int q = 0; q < QB; ++q) Bs4[swp * RS2B + srow + 32 * q] = vb[q];
+	__syncthreads();
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const int wr = wid >> 1, wc = wid & 1;
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 128 * wr + l32, rb0 = 64 * wc + l32;
+	v16f_t acc[4][2], accn[4][2];
+#pragma unroll
+	for(int a = 0; a < 4; ++a)
+#pragma unroll
+		for(int c = 0; c < 2; ++c)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[a][c][r] = accn[a][c][r] = 0.0f;
+	int buf = 0;
+	for(int w0 = 0; w0 < Wl; w0 += KC2, buf ^= 1) {
+		const bool more = w0 + KC2 < Wl;
+		if(more) {
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				vaa[q] = *(const u4v *) (Ap[q] + w0 + KC2);
+				vab[q] = *(const u4v *) (Ap[q + 4] + w0 + KC2);
+			}
+#pragma unroll
+			for(int q = 0; q < QB; ++q) vb[q] = *(const u4v *) (Bp + (size_t) 32 * q * Wp + w0 + KC2);
+		}
+		const uint4 *Ac = As[buf], *Bc = Bs[buf];
+#pragma unroll
+		for(int s = 0; s < KC2 / 2; ++s) {
+			const int w = 2 * s + h;
+			uint4 av[4], bv[2];
+			v8i_t am[4], ah[4], al[4], bm[2], bh[2], bl[2];
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				av[x] = Ac[w * RS2P + ra0 + 32 * x];
+				am[x] = pair2_mask(av[x].z);
+			}
+#pragma unroll
+			for(int y = 0; y < 2; ++y) {
+				bv[y] = Bc[w * RS2B + rb0 + 32 * y];
+				bm[y] = pair2_mask(bv[y].z);
+			}
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 2; ++tb)
+					accn[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    am[ta], bm[tb], accn[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) ah[x] = pair2_comp(av[x].x, am[x]);
+#pragma unroll
+			for(int y = 0; y < 2; ++y) bh[y] = pair2_comp(bv[y].x, bm[y]);
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 2; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    ah[ta], bh[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) al[x] = pair2_comp(av[x].y, am[x]);
+#pragma unroll
+			for(int y = 0; y < 2; ++y) bl[y] = pair2_comp(bv[y].y, bm[y]);
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 2; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    al[ta], bl[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) ah[x] = pair2_xor(ah[x], al[x], am[x]);
+#pragma unroll
+			for(int y = 0; y < 2; ++y) bh[y] = pair2_xor(bh[y], bl[y], bm[y]);
+#pragma unroll
+			for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+				for(int tb = 0; tb < 2; ++tb)
+					acc[ta][tb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+					    ah[ta], bh[tb], acc[ta][tb], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, 0, MFMA_SCALE1);
+		}
+		if(more) {
+			u4v *An = (u4v *) As[buf ^ 1], *Bn = (u4v *) Bs[buf ^ 1];
+#pragma unroll
+			for(int q = 0; q < 4; ++q) {
+				An[swp * RS2P + srow + 32 * q] = vaa[q];
+				An[swp * RS2P + srow + 32 * (q + 4)] = vab[q];
+			}
+#pragma unroll
+			for(int q = 0; q < QB; ++q) Bn[swp * RS2B + srow + 32 * q] = vb[q];
+		}
+		__syncthreads();
+	}
+	// epilogue as k_snp_mfma2 (C/D row (r & 3) + 8 (r >> 2) + 4 h, column l32)
+#pragma unroll
+	for(int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const long long L = (long long) I * TILE2 + 128 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			long long i = L;
+			if(BAND) {
+				const long long lb = L / SB;
+				i = (lb * world + rank) * SB + (L - lb * SB);
+			}
+			if(i >= n || (!BAND && (i < rowBegin || i >= rowEnd))) continue;
+			const long long base = BAND ? Shard{rank, world}.off(i) : tri(i);
+#pragma unroll
+			for(int tb = 0; tb < 2; ++tb) {
+				const long long j = (long long) J * TILE2 + 128 * half + 64 * wc + 32 * tb + l32;
+				if(j < i) {
+					const int nn = (int) accn[ta][tb][r];
+					const unsigned d = (unsigned) ((3 * nn - (int) acc[ta][tb][r]) >> 2);
+					if(SPLIT) {
+						atomicAdd(&cd[base + j - cbase], d);
+						atomicAdd(&cn[base + j - cbase], (unsigned) nn);
+					} else {
+						pair_store<ET>(D, Nm, base + j, d, (uint32_t) nn, norm, minLength, bs);
+					}
+				}
+			}
+		}
+	}
+}
+
 // split-K epilogue of pair mode: the A7 store of the summed (dist, n)
 template <int ET>
 __global__ void k_snp_pair_finish(const unsigned *__restrict__ cd, const unsigned *__restrict__ cn, long long f0,
@@ -1393,9 +1618,9 @@ static int dist_kernel_choice() {
 // of the band layout (world > 0), with split-K over word slices when the
 // tiles do not fill the chip (one block per CU) or a row exceeds the
 // f32-exact slice, counts finished by k_snp_finish
-template <int ET>
+template <int ET, bool PAIR = false>
 static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, int Wp, double nFactor, void *D,
-                            long long rb, long long re, int rank, int world) {
+                            long long rb, long long re, int rank, int world, void *N = NULL) {
 	typedef typename Elem<ET>::T T;
 	const long long n = a->n;
 	long long t_begin = 0, t_end = 0, f0 = 0, f1 = 0;
@@ -1431,6 +1656,10 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 		f0 = tri(rb);
 		f1 = tri(re);
 	}
+	if(PAIR) {   // pair mode: items are tile column halves
+		t_begin *= 2;
+		t_end *= 2;
+	}
 	const long long tiles = t_end - t_begin;
 	hipDeviceProp_t prop;
 	if(hipGetDeviceProperties(&prop, ctx->device) != hipSuccess) {
@@ -1442,8 +1671,8 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	// and the tile order (CCG_DIST_ORDER=1: super-tiles, whole LT ranges from
 	// a super-row start only)
 	const char *kce = getenv("CCG_DIST_KC"), *ore = getenv("CCG_DIST_ORDER");
-	const int kc = kce && atoi(kce) == KC2L && Wp % KC2L == 0 ? KC2L : KC2;
-	const int sorder = world == 0 && ore && atoi(ore) == 1 && (rb / TILE2) % 4 == 0;
+	const int kc = !PAIR && kce && atoi(kce) == KC2L && Wp % KC2L == 0 ? KC2L : KC2;
+	const int sorder = !PAIR && world == 0 && ore && atoi(ore) == 1 && (rb / TILE2) % 4 == 0;
 	const int chunks = Wp / kc;
 	int S = 1;
 	if(tiles < 16 * slots) {
@@ -1459,17 +1688,42 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	int rc = CCG_OK;
 	// every failure below leaves through `out`, which frees d_pfx and cnt
 #define MF2_TRY(x) do { if((x) != hipSuccess) { rc = CCG_EHIP; goto out; } } while(0)
-	if(S > 1) {
-		if(hipMalloc(&cnt, (size_t) (f1 - f0) * sizeof(unsigned)) != hipSuccess) {
+	if(S > 1) {   // pair mode: dist counts, then n counts
+		const size_t cz = (size_t) (f1 - f0) * (PAIR ? 2 : 1) * sizeof(unsigned);
+		if(hipMalloc(&cnt, cz) != hipSuccess) {
 			cnt = NULL;
 			rc = CCG_ENOMEM;
 			goto out;
 		}
-		MF2_TRY(hipMemsetAsync(cnt, 0, (size_t) (f1 - f0) * sizeof(unsigned), ctx->stream));
+		MF2_TRY(hipMemsetAsync(cnt, 0, cz, ctx->stream));
 	}
 	for(long long t = t_begin * S; t < t_end * S; t += batch) {
 		const long long items = t_end * S - t < batch ? t_end * S - t : batch;
 		const uint2 *pl = (const uint2 *) planes;
+		if(PAIR) {
+			typedef typename Elem<ET>::T T;
+			const uint4 *pp = (const uint4 *) planes;
+			unsigned *cn = cnt ? cnt + (f1 - f0) : NULL;
+			T *Nn = world > 0 ? NULL : (T *) N;
+			if(world > 0 && S > 1)
+				k_snp_mfma2_pair<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pp, Wp, (int) n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D, Nn, 0, n, cnt, cn, 0,
+				    d_pfx, npanels, rank, world);
+			else if(world > 0)
+				k_snp_mfma2_pair<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pp, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D, Nn, 0, n, cnt, cn, 0,
+				    d_pfx, npanels, rank, world);
+			else if(S > 1)
+				k_snp_mfma2_pair<ET, true, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pp, Wp, (int) n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D, Nn, rb, re, cnt, cn,
+				    f0, NULL, 0, 0, 1);
+			else
+				k_snp_mfma2_pair<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+				    pp, Wp, (int) n, t, items, 1, Wp, a->norm, a->minLength, a->byteScale, (T *) D, Nn, rb, re, cnt, cn,
+				    f0, NULL, 0, 0, 1);
+			MF2_TRY(hipGetLastError());
+			continue;
+		}
 #define MF2_LAUNCH(KCV)                                                                                              \
 	if(world > 0) {                                                                                                  \
 		if(S > 1)                                                                                                    \
@@ -1500,8 +1754,13 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	}
 	if(S > 1) {
 		const long long g = cdivll(f1 - f0, 256);
-		k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, f0, f0, f1, nFactor,
-		                                                                                a->byteScale, (T *) D);
+		if(PAIR)
+			k_snp_pair_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(
+			    cnt, cnt + (f1 - f0), f0, f1, a->norm, a->minLength, a->byteScale, (T *) D,
+			    world > 0 ? (T *) NULL : (T *) N);
+		else
+			k_snp_finish<ET><<<(unsigned) (g < 65536 ? g : 65536), 256, 0, ctx->stream>>>(cnt, f0, f0, f1, nFactor,
+			                                                                                a->byteScale, (T *) D);
 		MF2_TRY(hipGetLastError());
 	}
 	MF2_TRY(hipStreamSynchronize(ctx->stream));
@@ -1549,6 +1808,8 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 	S = (int) cdivll(Wp, Wk);
 	const long long f0 = tri(rb), f1 = tri(re);
 	const long long i_begin = t_begin * S, i_end = t_end * S;
+	if(a->pair && dist_kernel_choice() == 2)   // k_snp_mfma2_pair (CCG_DIST_MFMA=1: k_snp_mfma_pair, 0: VALU tiles)
+		return snp_launch_mfma2<ET, true>(ctx, a, planes, Wp, nFactor, D, rb, re, 0, 0, N);
 	if(a->pair) {
 		unsigned *cd = NULL, *cn = NULL;
 		if(S > 1) {
@@ -1701,6 +1962,10 @@ static int snp_launch_band(ccg_ctx *ctx, const ccg_snp_args *a, const void *plan
 	// the MFMA form unless disabled (CCG_DIST_MFMA=0); a row longer than the
 	// f32-exact slice is split over word slices
 	const char *mf = getenv("CCG_DIST_MFMA");
+	if(a->pair && dist_kernel_choice() == 2) {
+		CCG_CHECK(hipFree(d_pfx));
+		return snp_launch_mfma2<ET, true>(ctx, a, planes, Wp, nFactor, D, 0, n, rank, world);
+	}
 	if(a->pair) {
 		// fsacmpair per cell, the pair tiles in the band form; split-K over word
 		// slices (as snp_launch) when the rank's tiles do not fill the chip, the

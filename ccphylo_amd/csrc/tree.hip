@@ -1787,6 +1787,7 @@ static size_t tree_layout(TreeBufs *bp, int n, char *m) {
 	b.msd = NULL;
 	b.ubq = NULL;
 	b.lbs = 0;
+	b.lbw = 0;
 	b.lbskip = NULL;
 	b.xs_allpre = !(getenv("CCG_XS_ALLPRE") && atoi(getenv("CCG_XS_ALLPRE")) == 0);
 	return sz;

@@ -41,6 +41,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
+#include <vector>
 #include "ccg_dnj_search.h"
 #include "ccg_shard.h"
 
@@ -343,10 +344,11 @@ __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restric
 	}
 	double d = 0;
 	int cnt = 0;
+	typename Elem<ET>::T v = 0;
 	if(k < n && k != i && k != j) {
 		d = (Dik + Dkj - Dij) / 2;
 		d = d < 0 ? 0 : d;
-		const typename Elem<ET>::T v = Elem<ET>::put(d, 0.25, bs);
+		v = Elem<ET>::put(d, 0.25, bs);
 		if(k > j) {
 			if(sh.owns(k)) D[sh.off(k) + j] = v;
 		} else if(sh.owns(j)) {
@@ -357,6 +359,15 @@ __global__ __launch_bounds__(TB) void k_shd_join(typename Elem<ET>::T *__restric
 		b.sD[k] = sDk - (Dik + Dkj - d);
 		b.N[k] = Nk - 1;
 		cnt = 1;
+	}
+	if(b.lbm) {   // (uniform) block bounds of the owned rows: row j rewritten, column j lowered where written
+		const unsigned x = lb_bits(Elem<ET>::get(v, bs));
+		if(sh.owns(j)) {
+			const unsigned mn = wave_min_u32(k < j ? x : 0xFFFFFFFFu);
+			if((tid & 63) == 0 && k < j) lb_line(b, j)[k >> 6] = mn;
+		}
+		if(k > j && k < n && k != i && sh.owns(k))
+			__hip_atomic_fetch_min(lb_line(b, k) + (j >> 6), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
 	update_partials(b, n, s_exact, k, d, cnt, blockIdx.x);
 	// exact mode: this block's row of the serial row sum (every rank holds
@@ -392,6 +403,16 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 		vj = Xj[k];
 	}
 	if(k < nn) vm = Xm[k];
+	// block bounds: the owned row's partner cell and the partner's row sum,
+	// for the row's threshold in the next scan (ubq, as k_dnj_requeue)
+	typename Elem<ET>::T vp = 0;
+	double sdp0 = 0.0;
+	const bool PV = b.ubq != nullptr;   // (uniform)
+	if(PV && k >= 1 && k < n && sh.owns(k)) {
+		const int p0 = pkk0 >= 0 && pkk0 < k ? pkk0 : 0;
+		vp = D[sh.off(k) + p0];
+		sdp0 = b.sD[p0];
+	}
 	const int Nm0 = b.N[nn];
 	const double sDm0 = b.sD[nn];
 	if(wid == 0) {
@@ -496,18 +517,55 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 	// this rank's record slot for the next join: its bit bytes (q and j are
 	// read only where a bit is set)
 	if((size_t) k * 4 < rec_slot(n, sh.world).f_off) ((unsigned *) R)[k] = 0;
+	if(b.lbm) {   // (uniform) block bounds of the owned rows: row i = the moved row, column i; sD maxima
+		const unsigned x = lb_bits(Elem<ET>::get(vm, bs));
+		if(move) {
+			if(sh.owns(i)) {
+				const unsigned mn = wave_min_u32(k < i ? x : 0xFFFFFFFFu);
+				if(lane == 0 && k < i) lb_line(b, i)[k >> 6] = mn;
+			}
+			if(k > i && k < nn && sh.owns(k))
+				__hip_atomic_fetch_min(lb_line(b, k) + (i >> 6), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		const double sf = k < nn ? (move && k == i ? sDm : sDk) : -DBL_MAX;   // sD of column k at the next join
+		const double mx = wave_max_d(sf);
+		if(lane == 0 && k < nn) b.msd[k >> 6] = mx;
+	}
+	// ubq: the q at the owned row's partner cell in the next join's state (the
+	// next scan's threshold for the row); +inf for the other ranks' rows
+	double qpc = INFINITY;
+	if(PV && k >= 1 && k < nn && k != i && k != j && sh.owns(k)) {
+		const bool later = k > j;   // rows above j may have a new partner (j or the moved i)
+		const int pf = later ? fp : pkk0;
+		double d = -1.0, sp = 0.0;
+		if(pf == j && later) {
+			d = Elem<ET>::get(vj, bs);
+			sp = sdj;
+		} else if(pf == i && move && later) {
+			d = Elem<ET>::get(vm, bs);
+			sp = sDm;
+		} else if(pf == pkk0 && pkk0 >= 0 && pkk0 < k && pkk0 != i && pkk0 != j) {
+			d = Elem<ET>::get(vp, bs);
+			sp = sdp0;
+		}
+		if(0 <= d) qpc = qcrit(nn, nn, d, sDk, sp);
+		b.ubq[k] = qpc;
+	}
 	// the row's bound for the next join: each block's min-Q row becomes a
 	// candidate of the next S (rows j and i take theirs from k_dnj_select's
-	// fold); only when the next S has a band part
-	double bq = DBL_MAX, bdum = 0.0;
+	// fold); only when the next S has a band part (with ubq also the q at its
+	// partner cell, k_dnj_plan's partner-cell bound: +inf for another rank's row)
+	double bq = DBL_MAX, bqc = INFINITY;
 	int bk = 0, bp = 0;
+	__shared__ double sbq[TB / 64];
 	if(BANDS) {
 		if(k >= 1 && k < nn && k != i && k != j) {
 			bq = k > j ? fq : qk0;
 			bk = k;
 			bp = k > j ? fp : pkk0;   // its partner, for k_dnj_plan's partner-cell bound
+			bqc = qpc;
 		}
-		qarg_wave_reduce_carry(bq, bk, bdum, bp);
+		qarg_wave_reduce_carry(bq, bk, bqc, bp);
 	}
 	qarg_wave_reduce(rq, rj);
 	qarg_wave_reduce_carry(pq, pk, fq, fp);
@@ -528,11 +586,12 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 			sq[4][wid] = bq;
 			si[4][wid] = bk;
 			sbp[wid] = bp;
+			sbq[wid] = bqc;
 		}
 	}
 	__syncthreads();
 	if(tid < (BANDS ? 5 : 4)) {
-		double q = sq[tid][0], cq = sfq[0];
+		double q = sq[tid][0], cq = sfq[0], xq = BANDS ? sbq[0] : 0.0;
 		int ix = si[tid][0], cp = sfp[0], xp = BANDS ? sbp[0] : 0;
 		for(int w = 1; w < TB / 64; ++w) {
 			if(qarg_better(sq[tid][w], si[tid][w], q, ix)) {
@@ -540,13 +599,17 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 				ix = si[tid][w];
 				cq = sfq[w];
 				cp = sfp[w];
-				if(BANDS) xp = sbp[w];
+				if(BANDS) {
+					xp = sbp[w];
+					xq = sbq[w];
+				}
 			}
 		}
 		if(tid == 4) {
 			b.bmq[blockIdx.x] = q;
 			b.bmr[blockIdx.x] = ix;
 			b.bmp[blockIdx.x] = xp;
+			if(PV) b.bmqp[blockIdx.x] = xq;
 		} else {
 			b.qpart[4 * blockIdx.x + tid] = q;
 			b.ipart[4 * blockIdx.x + tid] = ix;
@@ -554,6 +617,42 @@ __global__ __launch_bounds__(TB) void k_shd_requeue(typename Elem<ET>::T *__rest
 		if(tid == 1) {
 			b.cfq[blockIdx.x] = cq;
 			b.cfp[blockIdx.x] = cp;
+		}
+	}
+}
+
+// the block lower bounds of the owned rows (k_lb_init's sharded form): wave
+// w takes the rank's w-th own row, and (replicated) the sD maxima of block w
+// and the threshold +inf of row w
+template <int ET>
+__global__ __launch_bounds__(TB) void k_shd_lb_init(const typename Elem<ET>::T *__restrict__ D, int n, double bs,
+                                                    TreeBufs b, Shard sh) {
+	constexpr int BB = 8;
+	const int lane = threadIdx.x & 63;
+	const int w = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+	if(w >= n) return;   // (wave-uniform)
+	if(w < (n + LBW - 1) / LBW) {
+		const int c = w * LBW + lane;
+		const double mx = wave_max_d(c < n ? b.sD[c] : -DBL_MAX);
+		if(lane == 0) b.msd[w] = mx;
+	}
+	if(lane == 0) b.ubq[w] = INFINITY;
+	const int r = ((w >> 3) * sh.world + sh.rank) * 8 + (w & 7);
+	if(r >= n) return;
+	const typename Elem<ET>::T *row = D + sh.off(r);
+	unsigned *line = lb_line(b, r);
+	const int nbk = (r + LBW - 1) / LBW;
+	for(int u0 = 0; u0 < nbk; u0 += BB) {
+		unsigned x[BB];
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const int c = (u0 + m) * LBW + lane;
+			x[m] = u0 + m < nbk && c < r ? lb_bits(Elem<ET>::get(row[c], bs)) : 0xFFFFFFFFu;
+		}
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const unsigned mn = wave_min_u32(x[m]);
+			if(lane == 0 && u0 + m < nbk) line[u0 + m] = mn;
 		}
 	}
 }
@@ -649,6 +748,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	unsigned char *pflag = (unsigned char *) (m + o_pf), *pacc = (unsigned char *) (m + o_pa);
 	unsigned *pcnt = (unsigned *) (m + o_pc);
 	unsigned long long *dbg = NULL;
+	void *lbmem = NULL;
 	// diagnostic: k_shd_pick's phase stamps (s_memrealtime), averaged to stderr
 	if(getenv("CCG_PICK_TS")) {
 		if(hipMalloc((void **) &dbg, 1024 * 8 * 8) != hipSuccess) dbg = NULL;
@@ -692,6 +792,29 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	SD_TRY(shd_init_hnj<ET>(D, n0, bs, sh, cr, st, b, R));
 	launches += 2;
+	// the block lower bounds (DnjGrid::lb, as the single engine): a line per
+	// owned row, the sD maxima and the thresholds replicated
+	if(grid.lb && n0 > grid.lb_min_n) {
+		const long long LS = (n0 + LBW - 1) / LBW, own = (long long) cdiv(cdiv(n0, 8), sh.world) * 8;
+		const size_t lbb = ((size_t) own * LS * 4 + 255) & ~(size_t) 255;
+		const size_t msb = ((size_t) (LS + 1) * 8 + 255) & ~(size_t) 255;
+		const size_t ubb = ((size_t) n0 * 8 + 255) & ~(size_t) 255, skb = (size_t) (LB_SCAN + LB_HELP) * LB_SLOT * 8;
+		if(hipMalloc(&lbmem, lbb + msb + ubb + skb) == hipSuccess) {
+			b.lbm = (unsigned *) lbmem;
+			b.msd = (double *) ((char *) lbmem + lbb);
+			b.ubq = (double *) ((char *) lbmem + lbb + msb);
+			b.lbs = LS;
+			b.lbw = sh.world;
+			b.lbskip = (long long *) ((char *) lbmem + lbb + msb + ubb);
+			SD_HIP(hipMemsetAsync(b.lbskip, 0, skb, st));
+			k_shd_lb_init<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(D, n0, bs, b, sh);
+			SD_HIP(hipGetLastError());
+			launches += 1;
+		} else {
+			(void) hipGetLastError();   // no room: the run goes without (the same joins)
+			lbmem = NULL;
+		}
+	}
 	{
 		int since_check = 0;
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
@@ -706,7 +829,9 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
 			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
-			if(grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			if(b.lbm && grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5, 0, false, true><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			else if(b.lbm && grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>, 0, 0, false, true><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
+			else if(grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
 			else if(grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
 			else if(grid.scan_mode(n, ET)) k_dnj_scan_w<ET, false, Shard, RecTail<ET>><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
 			else k_dnj_scan<ET, false><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
@@ -767,9 +892,14 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 		SD_HIP(hipStreamSynchronize(st));
 		*final_d = (ET == 8 || ET == 4) ? (double) v : v / bs;
 	}
+	if(b.lbskip) {   // the bounded-out cells, from the per-wave slots
+		std::vector<long long> sl((size_t) LB_SCAN * LB_SLOT);
+		SD_HIP(hipMemcpy(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost));
+		for(size_t x = 0; x < (size_t) LB_SCAN; ++x) hc.cells_lbskip += sl[x * LB_SLOT];
+	}
 	if(stats) {
 		stats[0] = hc.rows;
-		stats[1] = hc.cells;
+		stats[1] = hc.cells - hc.cells_lbskip;   // cells the scans loaded
 		stats[2] = launches;
 		stats[3] = (int64_t) (ms * 1000.0);
 		if(a->profile) {
@@ -778,7 +908,7 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 				stats[5 + 2 * c] = kt.ns[c];
 			}
 			stats[4 + 2 * CCG_NKSTAT] = hc.cells_top;
-			stats[5 + 2 * CCG_NKSTAT] = hc.cells_rest;
+			stats[5 + 2 * CCG_NKSTAT] = hc.cells_rest - hc.cells_lbskip;
 			stats[6 + 2 * CCG_NKSTAT] = hc.serial_sums;
 			stats[7 + 2 * CCG_NKSTAT] = hc.chain_sums;
 			stats[8 + 2 * CCG_NKSTAT] = istat.coll_bytes;
@@ -793,6 +923,7 @@ out:
 	if(rc != CCG_OK) kt.on = false;
 	hipStreamSynchronize(st);
 	if(h) hipHostFree(h);
+	if(lbmem) hipFree(lbmem);
 	hipFree(m);
 	hipFree(w.mem);
 	return rc;

@@ -182,9 +182,11 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
                                               (1100, 65, 8, None, True), (70, 6_000_000, 8, None, False),
                                               (40, 5_800_000, 4, None, True),
                                               # enough 256 x 256 tiles that k_snp_mfma2 runs without split-K
-                                              (24000, 640, 4, None, False), (20000, 1000, 8, (3000, 17001), False)])
+                                              (24000, 640, 4, None, False), (20000, 1000, 8, (3000, 17001), False),
+                                              # and k_snp_mfma2_pair (column halves of 256 x 256 tiles) likewise
+                                              (17000, 640, 8, None, True), (16500, 300, 4, (2000, 16001), True)])
 def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
-    """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma, k_snp_mfma_pair:
+    """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma / k_snp_mfma2, k_snp_mfma_pair / k_snp_mfma2_pair:
     tetrahedron +-1 vectors in MX-fp4, dist = (3 L - dot) / 4, in pair mode
     masked with n from a fourth component) give the VALU tile kernels'
     matrices (and N) bit for bit: odd sizes, row ranges, split-K slices, every element type (the

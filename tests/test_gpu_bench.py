@@ -32,13 +32,22 @@ def test_bench_world_mismatch_refused():
 
 @pytest.mark.gpu
 def test_bench_gpus2_spawned_same_joins():
-    """--gpus 2 (ranks spawned by bench.py, gloo rehearsal on one GPU) in both
+    """--gpus 1 pipelined and sequential; --gpus 2 (ranks spawned by bench.py, gloo rehearsal on one GPU) in both
     tree modes: the dist's row ranges gathered to GPU 0 for the single-GPU
     tree (the default), and the row-sharded tree; the same joins as --gpus 1."""
     one = _bench(["--gpus", "1"] + SMALL)
     assert one.returncode == 0, one.stderr[-3000:]
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
     assert l1["n_gpus"] == 1
+    # one GPU: the pipelined form (tree beside the next matrix's dist, two LT
+    # buffers in turn over warmup + 2 steps) and the sequential one agree
+    pipe = _bench(["--gpus", "1"] + SMALL + ["--steps", "2", "--warmup", "1"])
+    seq = _bench(["--gpus", "1", "--tree-cus", "0"] + SMALL)
+    for p in (pipe, seq):
+        assert p.returncode == 0, p.stderr[-3000:]
+    lp, ls = (json.loads(p.stdout.strip().splitlines()[-1]) for p in (pipe, seq))
+    assert "pipelined" in lp["config"]["parallelism"] and "pipelined" not in ls["config"]["parallelism"]
+    assert lp["split"]["joins_sha256"] == ls["split"]["joins_sha256"] == l1["split"]["joins_sha256"]
     for mode in ("gather", "shard"):
         two = _bench(["--gpus", "2", "--shard-transport", "gloo", "--tree-mode", mode] + SMALL)
         assert two.returncode == 0, (mode, two.stderr[-3000:])

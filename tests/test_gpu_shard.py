@@ -185,6 +185,38 @@ def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport,
         assert len(j) == len(ref_j) and (j == ref_j).all()
 
 
+@pytest.mark.parametrize("world,kind,et,mode", [(1, "euc", 8, "9"), (1, "clade", 4, "20"), (3, "euc", 8, "9"),
+                                                (2, "clade", 4, "20"), (8, "snp", 8, "9")])
+def test_shard_block_bounds(dev, monkeypatch, tmp_path, world, kind, et, mode):
+    """The sharded engine's scan under the block lower bounds (a line per
+    owned row, kept by k_shd_join / k_shd_requeue; thresholds and the plan's
+    band partner-cell bound from the requeue): at small n through
+    CCG_LB_MIN_N the joins equal the single engine's (itself equal to the
+    oracle with the bounds, test_dnj_block_bounds), and at world 1 the bounded
+    scan loads fewer cells than the unbounded one."""
+    for k, v in (("CCG_SCAN_WAVE", mode), ("CCG_SEG_MUL", "1"), ("CCG_S_SPLIT_N", "100"), ("CCG_LB_MIN_N", "100")):
+        monkeypatch.setenv(k, v)
+    n = {1: 2500, 2: 1800, 3: 2000, 8: 1500}[world]
+    D, bs = _typed(_data(kind, n), et)
+    monkeypatch.setenv("CCG_SCAN_LB", "0")
+    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True)[:3]
+    cells = {}
+    for lb in ("1", "0"):
+        monkeypatch.setenv("CCG_SCAN_LB", lb)
+        if world == 1:
+            j, fn, fd, st = dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
+            _same((j, fn, fd), ref)
+            cells[lb] = st[1]
+        elif lb == "1":
+            mp.start_processes(_rank_main, args=(world, _free_port(), n, kind, et, True, "gloo", 1, str(tmp_path)),
+                               nprocs=world, join=True, start_method="spawn")
+            for r in range(world):
+                fn, fd = np.load(tmp_path / f"f{r}.npy")
+                _same((np.load(tmp_path / f"j{r}.npy"), int(fn), fd), ref)
+    if world == 1:
+        assert cells["1"] < cells["0"], cells
+
+
 @pytest.mark.parametrize("kind,et,n,max_hard", [("snp", 8, 1500, 0), ("clade", 4, 1200, 0), ("snp", 2, 900, 0),
                                                  ("euc", 4, 2000, 100), ("euc", 8, 1600, 1600)])
 @pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
@@ -313,12 +345,12 @@ def test_dist_shard_to_tree_in_place(dev):
 @pytest.mark.parametrize("n,L,et,proxi", [(300, 4000, 8, 0), (517, 2049, 4, 0), (129, 1000, 2, 0), (260, 3000, 8, 20),
                                           (75, 700, 4, 5)])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-@pytest.mark.parametrize("mfma", ["1", "0"])
+@pytest.mark.parametrize("mfma", ["2", "1", "0"])
 def test_dist_shard_layout_pair(dev, monkeypatch, n, L, et, proxi, world, mfma):
     """Pair mode (cmpairFsaThrd, fsacmp.c:587; -P: maskProxi fsacmp.c:355)
     into the band shards: each rank's buffer equals the band extract of the
     full pair-mode LT (itself checked against the oracle and goldens), with
-    the MFMA (k_snp_mfma_pair) and VALU (k_snp_tile_pair) band forms."""
+    the MFMA (k_snp_mfma2_pair, k_snp_mfma_pair) and VALU (k_snp_tile_pair) band forms."""
     import ccphylo_amd as cg
     monkeypatch.setenv("CCG_DIST_MFMA", mfma)
     from ccphylo_amd import native as nt
