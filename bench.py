@@ -544,6 +544,8 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     world 1 with tree_cus > 0: the pipelined form (pipelined_leg)."""
     if world == 1 and tree_cus > 0:
         return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k)
+    if world > 1 and tree_mode == "gather-pipelined":
+        return gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, barrier, pg, profile_tree)
     import hashlib
     import ccphylo_amd as cg
     from ccphylo_amd import native as nt
@@ -723,6 +725,132 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     tdev.close()
     torch.cuda.empty_cache()
     return res, joins, pst, (seqs, incs, W), cap
+
+
+def gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, barrier, pg, profile_tree=True):
+    """The headline at N > 1 as a pipeline over a stream of alignments: rank 0
+    builds the tree of matrix k on its whole chip while ranks 1 .. N-1
+    compute the dist of matrix k + 1 over contiguous LT row ranges of equal
+    cells (shard.lt_row_ranges over N - 1 ranks) and send them into rank 0's
+    other LT buffer (RCCL point-to-point on `pg`; gloo host-staged when pg is
+    None).  Every timed step holds one whole dist and one whole tree.  Rank
+    0's context does not wait for the whole device at its entry points
+    (ccg_ctx_configure nosync): the receives run beside the tree.  Same
+    return value as pipeline_leg; the dist figures are rank 1's."""
+    import hashlib
+    import threading
+    import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
+    from ccphylo_amd import shard as shd
+    seqs, incs, W = make_headline_alignment(torch, n, L)
+    m = n * (n - 1) // 2
+    ranges = [(0, 0)] + shd.lt_row_ranges(n, world - 1)   # rank 0: the tree only
+
+    def off(r):
+        return r * (r - 1) // 2 if r > 0 else 0
+    r0, r1 = ranges[rank]
+    elems = off(r1) - off(r0)
+    if rank == 0:
+        dev.configure(nosync=True)
+        Ds = [torch.empty(m, dtype=torch.float64, device="cuda") for _ in range(2)]
+    else:
+        Dl = torch.empty(max(elems, 1), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    cur = torch.cuda.current_stream()
+
+    def dist_part():
+        t0 = time.perf_counter()
+        inc = dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Dl.data_ptr() - 8 * off(r0),
+                              row_range=(r0, r1))
+        return time.perf_counter() - t0, dev.last_dist_ms(), inc
+
+    def transfer(k):   # matrix k's row ranges into rank 0's buffer k % 2
+        if pg is not None:
+            ops = []
+            if rank == 0:
+                for g in range(1, world):
+                    a0, a1 = ranges[g]
+                    if off(a1) > off(a0):
+                        ops.append(dist.P2POp(dist.irecv, Ds[k % 2][off(a0):off(a1)], g, pg))
+            elif elems:
+                ops.append(dist.P2POp(dist.isend, Dl[:elems], 0, pg))
+            for w_ in (dist.batch_isend_irecv(ops) if ops else []):
+                w_.wait()
+            cur.synchronize()   # this stream only: rank 0's tree runs on the engine's own stream
+        elif rank == 0:
+            for g in range(1, world):
+                a0, a1 = ranges[g]
+                if off(a1) > off(a0):
+                    buf = torch.empty(off(a1) - off(a0), dtype=torch.float64)
+                    dist.recv(buf, src=g)
+                    Ds[k % 2][off(a0):off(a1)].copy_(buf)
+            cur.synchronize()
+        elif elems:
+            dist.send(Dl[:elems].cpu(), dst=0)
+
+    def step(k, profile=False):
+        """tree of matrix k (rank 0) beside the dist and transfer of matrix k + 1"""
+        if rank == 0:
+            res, err = {}, []
+
+            def run_t():
+                try:
+                    t0 = time.perf_counter()
+                    j, fn, fd, st = dev.tree_dev(Ds[k % 2].data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True,
+                                                 profile=profile)
+                    res["t"] = (time.perf_counter() - t0, (j, fn, fd), st)
+                except Exception as e:  # noqa: BLE001
+                    err.append(e)
+            th = threading.Thread(target=run_t)
+            th.start()
+            transfer(k + 1)
+            th.join()
+            if err:
+                raise err[0]
+            return 0.0, res["t"][0], 0.0, res["t"][1], res["t"][2], 0
+        ds, dms, inc = dist_part()
+        transfer(k + 1)
+        return ds, 0.0, dms, (np.zeros(0, dtype=nt.JOIN_DTYPE), 0, 0.0), [0] * (12 + 2 * nt.NKSTAT), inc
+
+    if rank != 0:
+        dist_part()
+    transfer(0)   # matrix 0
+    k = 0
+    for w in range(warmup):
+        r = step(k)
+        k += 1
+        log(f"  warmup step {w}: dist {r[0]:.2f} s beside tree {r[1]:.2f} s")
+    barrier()
+    t0 = time.perf_counter()
+    parts = []
+    for s_ in range(steps):
+        parts.append(step(k))
+        k += 1
+        log(f"  step {s_}: dist {parts[-1][0]:.2f} s beside tree {parts[-1][1]:.2f} s")
+    barrier()
+    dt = shard_max(time.perf_counter() - t0, dist)
+    joins, st = parts[-1][3], parts[-1][4]
+    jj, fn, fd = joins
+    sha = hashlib.sha256(np.ascontiguousarray(jj).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+    pst = step(k, profile=True)[4] if profile_tree else None
+    barrier()
+    # rank 1's dist figures (the ranks' shares are equal) for rank 0's line
+    mine = [sum(p[0] for p in parts) / steps, sum(p[2] for p in parts) / steps, parts[-1][5], elems]
+    allv = [None] * world
+    dist.all_gather_object(allv, mine)
+    d1 = allv[1]
+    tree_s = sum(p[1] for p in parts) / steps
+    res = {"dt": dt, "dist_s": d1[0], "tree_s": tree_s, "dist_kernel_ms": d1[1], "joins": len(jj),
+           "joins_sha256": sha, "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]),
+           "included_positions": d1[2], "dist_elems": d1[3],
+           "gather_pipelined": {"dist_ranks": world - 1, "tree_rank": 0}}
+    if rank == 0:
+        del Ds
+        dev.configure()   # the extras after this leg order their inputs by device-wide waits again
+    else:
+        del Dl
+    torch.cuda.empty_cache()
+    return res, joins, pst, (seqs, incs, W), None
 
 
 def refrule_cells(dev, torch, seqs, incs, n, L, W, prefix, threads):
@@ -1111,9 +1239,11 @@ def main():
                          "along this tree, DESIGN.md 4)")
     ap.add_argument("--shard-transport", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: host-staged (rehearsal of several ranks on one GPU)")
-    ap.add_argument("--tree-mode", choices=["gather", "shard"], default="gather",
-                    help="N > 1: gather the dist's row ranges to GPU 0 for the single-GPU tree (default), or the "
-                         "row-sharded tree over RCCL (DESIGN.md 6)")
+    ap.add_argument("--tree-mode", choices=["gather-pipelined", "gather", "shard"], default="gather-pipelined",
+                    help="N > 1: GPU 0 builds each matrix's tree while GPUs 1 .. N-1 compute the next matrix's "
+                         "dist and send it over (default, gather_pipelined_leg); gather: every GPU's dist rows "
+                         "gathered to GPU 0, then its tree, step by step; shard: the row-sharded tree over RCCL "
+                         "(DESIGN.md 6)")
     ap.add_argument("--tree-cus", type=int, default=40,
                     help="N = 1: the pipelined headline (pipelined_leg) with the tree on this many compute units and "
                          "the next matrix's dist on the rest; 0: dist then tree on the whole chip, step by step")
@@ -1167,7 +1297,7 @@ def main():
     pg = None
     if world == 1:
         elems = m
-    elif args.tree_mode == "gather":   # this rank's dist cells: its contiguous row range
+    elif args.tree_mode.startswith("gather"):   # this rank's dist cells: its contiguous row range
         from ccphylo_amd import shard as shd
         r0_, r1_ = shd.lt_row_ranges(n, world)[rank]
         elems = r1_ * (r1_ - 1) // 2 - r0_ * (r0_ - 1) // 2
@@ -1201,8 +1331,8 @@ def main():
     # dist launches per call (snp_launch_mfma2: 256 x 256 tiles in batches of
     # 65536; no split-K at the headline's tile count)
     tiles = (-(-n // 256)) * (-(-n // 256) + 1) // 2 // world
-    roof = headline_roofline(n, L, head["included_positions"], elems, head["dist_kernel_ms"],
-                             max(1, -(-tiles // 65536)), pst, world, single_tree=args.tree_mode == "gather")
+    roof = headline_roofline(n, L, head["included_positions"], head.get("dist_elems", elems), head["dist_kernel_ms"],
+                             max(1, -(-tiles // 65536)), pst, world, single_tree=args.tree_mode.startswith("gather"))
     pipe = head.get("pipelined")
     if pipe:   # the dist kernel ran on the dist context's share of the CUs
         dk = roof["kernels"]["dist"]
@@ -1230,11 +1360,15 @@ def main():
                    "parallelism": (f"one GPU, pipelined: tree of matrix k on CUs [0, {pipe['tree_cus']}) beside "
                                    f"the dist of matrix k + 1 on the other {pipe['dist_cus']}" if pipe else "one GPU")
                    if world == 1 else
-                   (f"dist: LT row ranges over {world} GPUs, gathered to GPU 0 over {args.shard_transport} "
+                   (f"pipelined: GPU 0 builds the tree of matrix k (single-GPU engine) while GPUs 1..{world - 1} "
+                    f"compute the dist of matrix k + 1 over LT row ranges and send them to GPU 0 over "
+                    f"{args.shard_transport} point-to-point" if args.tree_mode == "gather-pipelined" else
+                    f"dist: LT row ranges over {world} GPUs, gathered to GPU 0 over {args.shard_transport} "
                     f"point-to-point; tree: GPU 0 (single-GPU engine)" if args.tree_mode == "gather" else
                     f"LT row bands over {world} GPUs ({transport})")},
         "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
-                  "overlap": "dist and tree walls run concurrently (pipelined)" if pipe else "sequential",
+                  "overlap": "dist and tree walls run concurrently (pipelined)"
+                             if pipe or head.get("gather_pipelined") else "sequential",
                   "dist_taxa_pairs_per_s": round(m / head["dist_s"], 1),
                   "dist_nt_comparisons_per_s": m * float(L) / head["dist_s"],
                   "tree_nj_iterations_per_s": round(head["joins"] / head["tree_s"], 1),

@@ -228,7 +228,87 @@ __global__ __launch_bounds__(PICK_T) void k_shd_pick(const typename Elem<ET>::T 
 	__syncthreads();
 	PTS(3);
 	const bool writer = blockIdx.x == 0;
-	if(tid < 64) {
+	// Without a "bad" entry (fresh below its stale bound) minQpair's running
+	// min is a prefix min (replay_wave's comment), so the whole block decides
+	// at once from per-thread summaries of contiguous entry runs (minimum
+	// fresh value, any bad), as k_dnj_join_pf does from k_dnj_fold's 64-entry
+	// chunk summaries: a block prefix-min gives each run its running min on
+	// entry, the accept decisions follow in the run, and the pair is the
+	// first entry reaching the overall minimum.  With a bad entry wave 0
+	// replays serially (replay_wave).
+	const int per2 = (total + PICK_T - 1) / PICK_T, a0 = tid * per2, a1 = a0 + per2 < total ? a0 + per2 : total;
+	double tmin = DBL_MAX;
+	int tbad = 0;
+	for(int e = a0; e < a1; ++e) {
+		const double f = x_f[e];
+		tbad |= !(f >= x_b[e]);
+		tmin = f < tmin ? f : tmin;
+	}
+	if(!__syncthreads_or(tbad)) {
+		__shared__ double s_wm[PICK_T / 64];
+		__shared__ int s_wf[PICK_T / 64];
+		__shared__ long long s_na[PICK_T / 64], s_ca[PICK_T / 64];
+		const int lane = tid & 63, wid = tid >> 6;
+		const double inc = wave_incl_min(tmin);
+		if(lane == 63) s_wm[wid] = inc;
+		__syncthreads();
+		double carry = m0, cm = m0;
+#pragma unroll
+		for(int w = 0; w < PICK_T / 64; ++w) {
+			if(w < wid) carry = s_wm[w] < carry ? s_wm[w] : carry;
+			cm = s_wm[w] < cm ? s_wm[w] : cm;
+		}
+		const double ex = dpp_d<DPP_WAVE_SHR1, 0xF>(DBL_MAX, inc);
+		double run = ex < carry ? ex : carry;   // the running min before this thread's run
+		long long nacc = 0, cacc = 0;
+		int first = 0x7fffffff;
+		for(int e = a0; e < a1; ++e) {
+			const double f = x_f[e];
+			const bool acc = x_b[e] < run;
+			if(acc) {
+				++nacc;
+				cacc += x_row[e];
+			}
+			if(writer) acc_out[e] = acc;   // applied by k_shd_join
+			if(f == cm && e < first) first = e;
+			run = f < run ? f : run;
+		}
+		first = wave_min_int(cm < m0 ? first : 0x7fffffff);
+		nacc = wave_sum_int(nacc);
+		cacc = wave_sum_int(cacc);
+		if(lane == 0) {
+			s_wf[wid] = first;
+			s_na[wid] = nacc;
+			s_ca[wid] = cacc;
+		}
+		__syncthreads();
+		if(tid == 0) {
+			int fe = 0x7fffffff;
+			long long na = 0, ca = 0;
+			for(int w = 0; w < PICK_T / 64; ++w) {
+				fe = s_wf[w] < fe ? s_wf[w] : fe;
+				na += s_na[w];
+				ca += s_ca[w];
+			}
+			const int pi = fe < 0x7fffffff ? x_row[fe] : pos_i, pj = fe < 0x7fffffff ? x_j[fe] : pos_j;
+			s_i = pi;
+			s_j = pj;
+			if(writer) {
+				if(na) {   // minQpair's own rescans (ctl->ref_rows / ref_cells)
+					atomicAdd((unsigned long long *) &ctl->ref_rows, (unsigned long long) na);
+					atomicAdd((unsigned long long *) &ctl->ref_cells, (unsigned long long) ca);
+				}
+				if(pi == 0 && pj == 0) {
+					ctl->done = 1;
+					ctl->final_n = n;
+				} else {
+					ctl->i = pi;
+					ctl->j = pj;
+				}
+				ctl->rtotal = total;
+			}
+		}
+	} else if(tid < 64) {
 		int pi = pos_i, pj = pos_j;
 		bool had_bad;
 		if(lds) replay_wave(total, m0, e_row, e_j, e_b, e_f, e_acc, writer, b, pi, pj, &had_bad, n, acc_out);

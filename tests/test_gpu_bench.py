@@ -32,9 +32,11 @@ def test_bench_world_mismatch_refused():
 
 @pytest.mark.gpu
 def test_bench_gpus2_spawned_same_joins():
-    """--gpus 1 pipelined and sequential; --gpus 2 (ranks spawned by bench.py, gloo rehearsal on one GPU) in both
-    tree modes: the dist's row ranges gathered to GPU 0 for the single-GPU
-    tree (the default), and the row-sharded tree; the same joins as --gpus 1."""
+    """--gpus 1 pipelined and sequential; --gpus 2 (ranks spawned by bench.py,
+    gloo rehearsal on one GPU) in every tree mode: GPU 0's tree beside the
+    other ranks' next dist (the default), the dist's row ranges gathered to
+    GPU 0 for the single-GPU tree step by step, and the row-sharded tree; the
+    same joins as --gpus 1."""
     one = _bench(["--gpus", "1"] + SMALL)
     assert one.returncode == 0, one.stderr[-3000:]
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
@@ -48,7 +50,7 @@ def test_bench_gpus2_spawned_same_joins():
     lp, ls = (json.loads(p.stdout.strip().splitlines()[-1]) for p in (pipe, seq))
     assert "pipelined" in lp["config"]["parallelism"] and "pipelined" not in ls["config"]["parallelism"]
     assert lp["split"]["joins_sha256"] == ls["split"]["joins_sha256"] == l1["split"]["joins_sha256"]
-    for mode in ("gather", "shard"):
+    for mode in ("gather-pipelined", "gather", "shard"):
         two = _bench(["--gpus", "2", "--shard-transport", "gloo", "--tree-mode", mode] + SMALL)
         assert two.returncode == 0, (mode, two.stderr[-3000:])
         l2 = json.loads(two.stdout.strip().splitlines()[-1])
