@@ -40,6 +40,7 @@ default -- the whole tree is profiles/r03_config3_whole_tree.json: the
 single-GPU engine at N = 1, sharded over RCCL at N > 1) and the sharded NJ.
 """
 import argparse
+import hashlib
 import json
 import os
 import re
@@ -1244,9 +1245,10 @@ def main():
                          "dist and send it over (default, gather_pipelined_leg); gather: every GPU's dist rows "
                          "gathered to GPU 0, then its tree, step by step; shard: the row-sharded tree over RCCL "
                          "(DESIGN.md 6)")
-    ap.add_argument("--tree-cus", type=int, default=40,
+    ap.add_argument("--tree-cus", type=int, default=64,
                     help="N = 1: the pipelined headline (pipelined_leg) with the tree on this many compute units and "
-                         "the next matrix's dist on the rest; 0: dist then tree on the whole chip, step by step")
+                         "the next matrix's dist on the rest (64: tools/overlap.py, 50k x 5 Mbp per matrix 7.59 s "
+                         "against 7.71-7.90 s at 32-56 CUs); 0: dist then tree on the whole chip, step by step")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -1393,6 +1395,27 @@ def main():
         except Exception as e:  # noqa: BLE001
             result["cpu_baseline"] = {"error": str(e)}
     extras = result.setdefault("extras", {}) if not args.no_extras else None
+    if extras is not None and world == 1 and pipe:
+        # the same matrix step by step on the whole chip (dist, then tree): one matrix's latency
+        log("headline, sequential form (one step, whole chip)")
+        try:
+            D1 = torch.empty(m, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D1.data_ptr())
+            t1 = time.perf_counter()
+            j1, fn1, fd1, _ = dev.tree_dev(D1.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
+            t2 = time.perf_counter()
+            del D1
+            torch.cuda.empty_cache()
+            sha1 = hashlib.sha256(np.ascontiguousarray(j1).tobytes() + np.array([fn1, fd1]).tobytes()).hexdigest()[:16]
+            extras["headline_sequential"] = {
+                "s_per_matrix": round(t2 - t0, 3), "dist_s": round(t1 - t0, 3), "tree_s": round(t2 - t1, 3),
+                "taxa_pairs_per_s": round(m / (t2 - t0), 1), "joins_sha256": sha1,
+                "note": "one matrix's latency, dist then tree on all CUs; the line's value is the pipelined "
+                        "steady state (each step one whole dist and one whole tree, on disjoint CUs)"}
+        except Exception as e:  # noqa: BLE001
+            extras["headline_sequential"] = {"error": str(e)}
     if extras is not None and rank == 0 and world == 1:
         log(f"reference-rule cells on a {args.refrule_prefix}-join prefix of the headline tree (oracle)")
         try:

@@ -128,7 +128,7 @@ struct TreeBufs {
 	long long lbs;
 	int lbw;             // 0: lbm rows are the matrix rows; w > 0: the sharded engine's, a rank's own rows
 	                     // by position among them (bands of 8 rows dealt over w ranks, ccg_shard.h)
-	int xs_allpre;       // the exact walk loads every block's records at once (CCG_XS_ALLPRE=0: block by block)
+	int xs_allpre;       // the exact walk loads every block's records at once (CCG_XS_ALLPRE=1; default block by block)
 	long long *lbskip;   // cells skipped under the block bounds (stats): per-wave slots of LB_SLOT longs --
 	                     // field 0 the cells not loaded, field 1 those of them in S rows (the plan's helpers);
 	                     // scan waves [0, LB_SCAN), helper waves after (no same-address atomics: thousands

@@ -777,6 +777,22 @@ def test_dnj_block_bounds(dev, monkeypatch, kind, n, et, mode):
         assert cells["1"] < cells["0"], (prune, cells)
 
 
+@pytest.mark.parametrize("allpre", ["1", "0"])
+@pytest.mark.parametrize("kind", ["euc", "clade"])
+def test_exact_walk_forms(dev, monkeypatch, allpre, kind):
+    """The exact row sum's walk over the binade records (xs_walk_blocks), with
+    every block's records loaded at once (CCG_XS_ALLPRE=1) and block by block
+    (the default): whole exact DNJ trees equal the serial oracle's."""
+    from oracle import pyoracle
+    monkeypatch.setenv("CCG_XS_ALLPRE", allpre)
+    n = 2500
+    D = _euclid(n, n + 11) if kind == "euc" else _clade_ltd(n, n + 12)
+    ref, rfn, rfd = pyoracle.tree(D, n, method=1)
+    got, fn, fd, _ = dev.tree(D, n, method=1, exact=True)
+    assert (fn, fd) == (rfn, rfd)
+    assert len(got) == len(ref) and (got == ref).all()
+
+
 @pytest.mark.parametrize("withhold", ["1", "2"])
 def test_dnj_plan_wait_timeout_is_an_error(dev, monkeypatch, withhold):
     """A bounded wait of k_dnj_plan that gives up stops the tree with an

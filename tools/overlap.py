@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--layout", choices=["stride", "low"], default="stride",
                     help="stride: CUs c with c % 8 == 0 (.. ), low: CUs 0 .. k-1")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--profile", action="store_true", help="per-join kernel times of the tree, masked and whole chip")
     a = ap.parse_args()
     import torch
     import ccphylo_amd as cg
@@ -51,10 +52,14 @@ def main():
         d.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[k % 2].data_ptr())
         return time.perf_counter() - t0
 
-    def tree(d, k):
+    def tree(d, k, prof=None):
         t0 = time.perf_counter()
-        j, fn, fd, _ = d.tree_dev(Ds[k % 2].data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
+        j, fn, fd, st = d.tree_dev(Ds[k % 2].data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True, profile=prof is not None)
         sha = hashlib.sha256(np.ascontiguousarray(j).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+        if prof is not None:   # per-join microseconds by kernel class (HIP events)
+            from ccphylo_amd import native as nt
+            prof.update({name: round(st[5 + 2 * c] / 1e3 / max(len(j), 1), 2)
+                         for c, name in enumerate(nt.KSTAT_NAMES) if st[4 + 2 * c]})
         return time.perf_counter() - t0, sha
 
     out = {"n": n, "L": L, "cus": ncu, "tree_cus": tcus, "layout": a.layout}
@@ -68,6 +73,14 @@ def main():
     r = {"dist_masked_s": round(dist(dd, 0), 3)}
     ts, sha = tree(dt, 0)
     r["tree_masked_s"] = round(ts, 3)
+    if a.profile:
+        prof = {}
+        dist(dd, 0)
+        tree(dt, 0, prof)
+        full = {}
+        dist(dev, 0)
+        tree(dev, 0, full)
+        r["us_per_join_masked"], r["us_per_join_all"] = prof, full
     r["sha_same"] = sha == sha0
     print(json.dumps(r), flush=True)
     dist(dd, 0)   # matrix 0 ready for the first pipelined tree

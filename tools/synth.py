@@ -14,12 +14,14 @@ def euclid(n, seed=1, dim=8):
     return np.round(D * 1e9) / 1e9
 
 
-def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=512, dtype=None):
+def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=512, dtype=None, cdist=False):
     """This rank's row bands (ccg_tree_shard_dev layout: bands of `band` rows
     dealt round-robin, owned rows back to back, row r = D(r, 0..r-1)) of the
     Euclidean distances between n points of U[0,1)^dim, computed on the GPU.
     Every rank draws the same points (CPU generator, fixed seed); computed in
-    double, stored as `dtype` (default float64; float32 = `-p`)."""
+    double, stored as `dtype` (default float64; float32 = `-p`).  cdist: the
+    round-4 form (torch.cdist per chunk of rows), kept to reproduce that
+    round's configs[3] matrix."""
     g = torch.Generator().manual_seed(seed)
     pts = torch.rand((n, dim), generator=g, dtype=torch.float64).cuda()
     nb = (n + band - 1) // band
@@ -38,13 +40,16 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
         # its two points only (torch.cdist's may depend on the batch's shape,
         # so the ranks of a world-8 run and the world-1 LT disagreed in the
         # last bit of some cells)
-        a, c = pts[rows][:, None, :], pts[:rmax][None, :, :]
-        t = a[..., 0] - c[..., 0]
-        s2 = t * t
-        for k in range(1, dim):
-            t = a[..., k] - c[..., k]
-            s2 = s2 + t * t
-        d = torch.sqrt(s2)
+        if cdist:
+            d = torch.cdist(pts[rows], pts[:rmax], compute_mode="donot_use_mm_for_euclid_dist")
+        else:
+            a, c = pts[rows][:, None, :], pts[:rmax][None, :, :]
+            t = a[..., 0] - c[..., 0]
+            s2 = t * t
+            for k in range(1, dim):
+                t = a[..., k] - c[..., k]
+                s2 = s2 + t * t
+            d = torch.sqrt(s2)
         mask = torch.arange(rmax, device="cuda")[None, :] < rows[:, None]
         vals = d[mask]                       # row-major: each row's prefix, rows in order
         out[pos:pos + vals.numel()] = vals
