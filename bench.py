@@ -529,7 +529,7 @@ def make_headline_alignment(torch, n, L):
 
 
 def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0,
-                 tree_mode="shard", pg=None, tree_cus=0):
+                 tree_mode="shard", pg=None, tree_cus=0, tree_layout="low"):
     """The headline: dist + exact DNJ of one n x L alignment per step.
     world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
     world > 1, tree_mode "shard": ccg_snp_ltd_shard_dev into this rank's band
@@ -544,7 +544,7 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     alignment, the first capture_k LT cells of the first step (world 1)).
     world 1 with tree_cus > 0: the pipelined form (pipelined_leg)."""
     if world == 1 and tree_cus > 0:
-        return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k)
+        return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k, tree_layout)
     if world > 1 and tree_mode == "gather-pipelined":
         return gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, barrier, pg, profile_tree)
     import hashlib
@@ -644,7 +644,16 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     return res, joins, pst, (seqs, incs, W), (cap[0] if cap else None)
 
 
-def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0):
+def tree_cu_set(ncu, k, layout):
+    """The tree context's compute units: the first k (layout "low"), or k / 8
+    at the start of each of the 8 equal CU groups ("xcd")."""
+    if layout == "xcd":
+        per = max(1, k // 8)
+        return [g * (ncu // 8) + i for g in range(8) for i in range(per)]
+    return list(range(k))
+
+
+def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0, layout="low"):
     """The headline on one GPU as a pipeline over a stream of alignments: two
     engine contexts on disjoint compute units (ccg_ctx_configure: the tree's
     stream on CUs [0, tree_cus), the dist's on the rest, neither waiting for
@@ -663,9 +672,11 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     gpu = torch.cuda.current_device()
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
     tree_cus = max(1, min(tree_cus, ncu - 1))
+    tset = tree_cu_set(ncu, tree_cus, layout)
     ddev, tdev = cg.Device(gpu), cg.Device(gpu)
-    ddev.configure(cu_mask=list(range(tree_cus, ncu)), nosync=True)
-    tdev.configure(cu_mask=list(range(tree_cus)), nosync=True)
+    ddev.configure(cu_mask=[c for c in range(ncu) if c not in set(tset)], nosync=True)
+    tdev.configure(cu_mask=tset, nosync=True)
+    tree_cus = len(tset)
     Ds = [torch.empty(m, dtype=torch.float64, device="cuda") for _ in range(2)]
     torch.cuda.synchronize()
     inc0 = ddev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[0].data_ptr())   # matrix 0
@@ -720,7 +731,8 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     res = {"dt": dt, "dist_s": sum(p[0] for p in parts) / steps, "tree_s": sum(p[1] for p in parts) / steps,
            "dist_kernel_ms": sum(p[2] for p in parts) / steps, "joins": len(jj), "joins_sha256": sha,
            "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]), "included_positions": inc,
-           "pipelined": {"tree_cus": tree_cus, "dist_cus": ncu - tree_cus, "matrix0_included_positions": inc0}}
+           "pipelined": {"tree_cus": tree_cus, "dist_cus": ncu - tree_cus, "layout": layout,
+                         "matrix0_included_positions": inc0}}
     del Ds
     ddev.close()
     tdev.close()
@@ -1249,6 +1261,8 @@ def main():
                     help="N = 1: the pipelined headline (pipelined_leg) with the tree on this many compute units and "
                          "the next matrix's dist on the rest (64: tools/overlap.py, 50k x 5 Mbp per matrix 7.59 s "
                          "against 7.71-7.90 s at 32-56 CUs); 0: dist then tree on the whole chip, step by step")
+    ap.add_argument("--tree-layout", choices=["low", "xcd"], default="low",
+                    help="which CUs the pipelined tree takes: the first --tree-cus, or --tree-cus / 8 in each XCD")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -1326,7 +1340,7 @@ def main():
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg,
-        tree_cus=args.tree_cus if world == 1 else 0)
+        tree_cus=args.tree_cus if world == 1 else 0, tree_layout=args.tree_layout)
     if hwd is not None:
         hwd.cancel()
     dt = head["dt"]
@@ -1359,8 +1373,9 @@ def main():
         "config": {"workload": f"configs[2]: ccphylo dist (MSA, non-pair) + ccphylo tree -m dnj (exact row sums) "
                                f"on {n} taxa x {L / 1e6:g} Mbp, one matrix per step",
                    "n_taxa": n, "alignment_length": L, "lt": "double",
-                   "parallelism": (f"one GPU, pipelined: tree of matrix k on CUs [0, {pipe['tree_cus']}) beside "
-                                   f"the dist of matrix k + 1 on the other {pipe['dist_cus']}" if pipe else "one GPU")
+                   "parallelism": (f"one GPU, pipelined: tree of matrix k on {pipe['tree_cus']} CUs "
+                                   f"({pipe['layout']} layout) beside the dist of matrix k + 1 on the other "
+                                   f"{pipe['dist_cus']}" if pipe else "one GPU")
                    if world == 1 else
                    (f"pipelined: GPU 0 builds the tree of matrix k (single-GPU engine) while GPUs 1..{world - 1} "
                     f"compute the dist of matrix k + 1 over LT row ranges and send them to GPU 0 over "

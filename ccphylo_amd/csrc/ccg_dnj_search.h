@@ -408,6 +408,12 @@ __device__ __forceinline__ void s_table_h(const TreeBufs &b, int n, int nS, doub
 		__hip_atomic_store(b.srdy + 32 * lane, (unsigned) n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef LB_BB_D
+#define LB_BB_D 8    // lb_unit's blocks in flight per lane, double rows
+#endif
+#ifndef LB_BB_N
+#define LB_BB_N 8    // and narrower rows (float, u16, u8)
+#endif
 template <int ET>   // (below, with the scan)
 __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
                                        int r, int c0, int c1, double sDr, double &q, int &idx, int isub = -1,
@@ -1689,7 +1695,7 @@ __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ 
                                        int r, int c0, int c1, double sDr, double &q, int &idx, int isub,
                                        double sDm, bool ubinf) {
 	typedef typename Elem<ET>::T T;
-	constexpr int BB = 8;
+	constexpr int BB = ET == 8 ? LB_BB_D : LB_BB_N;   // blocks in flight per lane
 	const int lane = threadIdx.x & 63;
 	const int bl0 = c0 / LBW, nbk = (c1 - c0 + LBW - 1) / LBW;   // <= seg / 64 <= 256 blocks
 	// the unit's bounds (one or more per lane), loaded with the threshold

@@ -25,8 +25,9 @@ def main():
     ap.add_argument("--n", type=int, default=50_000)
     ap.add_argument("--L", type=int, default=5_000_000)
     ap.add_argument("--tree-cus", type=int, default=32)
-    ap.add_argument("--layout", choices=["stride", "low"], default="stride",
-                    help="stride: CUs c with c % 8 == 0 (.. ), low: CUs 0 .. k-1")
+    ap.add_argument("--layout", choices=["stride", "low", "xcd"], default="low",
+                    help="stride: every (cus / k)-th CU; low: CUs 0 .. k-1; xcd: k / 8 CUs at the start of each "
+                         "32-CU group (one per XCD if the mask's CU numbering is XCD-major)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--profile", action="store_true", help="per-join kernel times of the tree, masked and whole chip")
     a = ap.parse_args()
@@ -38,6 +39,9 @@ def main():
     if a.layout == "stride":
         step = ncu // a.tree_cus
         tcus = [c for c in range(ncu) if c % step == 0][:a.tree_cus]
+    elif a.layout == "xcd":
+        per = max(1, a.tree_cus // 8)
+        tcus = [g * (ncu // 8) + i for g in range(8) for i in range(per)]
     else:
         tcus = list(range(a.tree_cus))
     dcus = [c for c in range(ncu) if c not in set(tcus)]
