@@ -848,11 +848,12 @@ def gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, bar
     pst = step(k, profile=True)[4] if profile_tree else None
     barrier()
     # rank 1's dist figures (the ranks' shares are equal) for rank 0's line
-    mine = [sum(p[0] for p in parts) / steps, sum(p[2] for p in parts) / steps, parts[-1][5], elems]
+    mine = [sum(p[0] for p in parts) / steps, sum(p[2] for p in parts) / steps, parts[-1][5], elems,
+            sum(p[1] for p in parts) / steps]
     allv = [None] * world
     dist.all_gather_object(allv, mine)
     d1 = allv[1]
-    tree_s = sum(p[1] for p in parts) / steps
+    tree_s = allv[0][4]   # rank 0's (every rank reports the same line fields)
     res = {"dt": dt, "dist_s": d1[0], "tree_s": tree_s, "dist_kernel_ms": d1[1], "joins": len(jj),
            "joins_sha256": sha, "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]),
            "included_positions": d1[2], "dist_elems": d1[3],
@@ -1386,9 +1387,9 @@ def main():
         "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
                   "overlap": "dist and tree walls run concurrently (pipelined)"
                              if pipe or head.get("gather_pipelined") else "sequential",
-                  "dist_taxa_pairs_per_s": round(m / head["dist_s"], 1),
-                  "dist_nt_comparisons_per_s": m * float(L) / head["dist_s"],
-                  "tree_nj_iterations_per_s": round(head["joins"] / head["tree_s"], 1),
+                  "dist_taxa_pairs_per_s": round(m / max(head["dist_s"], 1e-9), 1),
+                  "dist_nt_comparisons_per_s": m * float(L) / max(head["dist_s"], 1e-9),
+                  "tree_nj_iterations_per_s": round(head["joins"] / max(head["tree_s"], 1e-9), 1),
                   "joins": head["joins"], "joins_sha256": head["joins_sha256"],
                   "rows_rescanned": head["rows_rescanned"], "cells_rescanned": head["cells_rescanned"],
                   "included_positions": head["included_positions"]},
