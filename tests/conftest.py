@@ -33,6 +33,32 @@ def _built():
     ensure_built()
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _heartbeat(request):
+    """GPU sessions: a line every 30 s in gpurun_out/pytest_heartbeat.log
+    naming the running test, so that a long test (the configs[3] world-8
+    rehearsal runs minutes with its output captured) is not taken for a hung
+    run by a watchdog that watches the run's output files."""
+    import threading
+    import time
+    if "gpu" not in (request.config.getoption("-m") or "") or "not gpu" in (request.config.getoption("-m") or ""):
+        yield
+        return
+    path = os.path.join(ROOT, "gpurun_out", "pytest_heartbeat.log")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    stop = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not stop.wait(30.0):
+            with open(path, "a") as f:
+                f.write(f"{time.time() - t0:.0f} s {os.environ.get('PYTEST_CURRENT_TEST', '')}\n")
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+
+
 def golden_cases(kind=None):
     with open(os.path.join(GOLDEN, "golden.json")) as f:
         cases = json.load(f)["cases"]
