@@ -85,7 +85,10 @@ def _snp(n, seed, L=4000):
         rows.append(p)
     X = np.array(rows)
     i, j = np.tril_indices(n, -1)
-    return (X[i] != X[j]).sum(1).astype(np.float64)
+    # differing sites = L - sites equal, the equal ones counted per code by a
+    # matrix product (exact integers in f64; the pairwise compare took seconds)
+    same = sum((X == c).astype(np.float64) @ (X == c).astype(np.float64).T for c in range(4))
+    return L - same[i, j]
 
 
 @pytest.mark.parametrize("n,kind,method", [(600, "euc", 1), (600, "euc", 0), (1500, "snp", 1), (1500, "snp", 0),

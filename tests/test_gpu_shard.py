@@ -46,7 +46,8 @@ def _snp(n, seed, L=3000):
     X = rng.integers(0, 4, (n, L))
     X[rng.random((n, L)) < 0.7] = 0        # shared sites: many equal distances
     i, j = np.tril_indices(n, -1)
-    return (X[i] != X[j]).sum(1).astype(np.float64)
+    same = sum((X == c).astype(np.float64) @ (X == c).astype(np.float64).T for c in range(4))
+    return L - same[i, j]                  # differing sites (exact integers in f64)
 
 
 def _typed(D, et):
