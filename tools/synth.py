@@ -30,10 +30,11 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
     out = torch.empty(max(sum(sizes), 1), dtype=dtype or torch.float64, device="cuda")
     per = max(1, chunk_rows // band)
     pos = 0
-    for c in range(0, len(mine), per):
-        bands = mine[c:c + per]
-        rows = torch.cat([torch.arange(b * band, min(b * band + band, n), device="cuda") for b in bands])
-        rmax = int(rows[-1])
+    for c0 in range(0, len(mine), per):
+        bands = mine[c0:c0 + per]
+        rows_h = [r for b in bands for r in range(b * band, min(b * band + band, n))]
+        rows = torch.tensor(rows_h, device="cuda")
+        rmax = rows_h[-1]
         if rmax == 0:
             continue
         # elementwise, one dimension at a time: every cell's value depends on
@@ -50,8 +51,9 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
                 t = a[..., k] - c[..., k]
                 s2 = s2 + t * t
             d = torch.sqrt(s2)
-        mask = torch.arange(rmax, device="cuda")[None, :] < rows[:, None]
-        vals = d[mask]                       # row-major: each row's prefix, rows in order
+        # row-major: each row's prefix, rows in order (views concatenated: a
+        # boolean-mask select of this size crashed torch inside a long process)
+        vals = torch.cat([d[i, :r] for i, r in enumerate(rows_h) if r > 0])
         out[pos:pos + vals.numel()] = vals
         pos += vals.numel()
     assert pos == sum(sizes)
