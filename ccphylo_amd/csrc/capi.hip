@@ -82,8 +82,13 @@ int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int f
 		hipStream_t s;
 		CCG_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t) mask_words, cu_mask));
 		CCG_CHECK(hipStreamSynchronize(c->stream));
-		CCG_CHECK(hipStreamDestroy(c->stream));
+		// a CU-masked stream is never destroyed: on this ROCm image, destroying
+		// one left the next kernel launched on another stream of the process
+		// (torch's) to segfault in the runtime (tools/cu_mask_probe.py); it is
+		// released with the process
+		if(!c->masked) CCG_CHECK(hipStreamDestroy(c->stream));
 		c->stream = s;
+		c->masked = 1;
 	}
 	c->flags = flags;
 	return CCG_OK;
@@ -95,7 +100,7 @@ void ccg_destroy(ccg_ctx *c) {
 	hipStreamSynchronize(c->stream);
 	hipEventDestroy(c->ev0);
 	hipEventDestroy(c->ev1);
-	hipStreamDestroy(c->stream);
+	if(!c->masked) hipStreamDestroy(c->stream);   // (a CU-masked one stays: ccg_ctx_configure)
 	free(c);
 }
 

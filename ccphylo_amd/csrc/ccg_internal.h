@@ -33,6 +33,7 @@ struct ccg_ctx {
 	char name[256];
 	float dist_ms;   // the last dist call's pair kernels (HIP events on the engine stream)
 	int flags;       // CCG_CTX_* (ccg_ctx_configure)
+	int masked;      // the stream was created with a CU mask (never destroyed: see ccg_ctx_configure)
 };
 // every device-pointer entry point first waits for the whole device (inputs
 // may come from other streams) unless the caller orders them itself
