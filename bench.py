@@ -1514,3 +1514,9 @@ def main():
 
 if __name__ == "__main__":
     main()
+    # leave without the runtime's exit-time teardown: with the pipelined
+    # leg's CU-masked streams alive (never destroyed, ccg_ctx_configure) the
+    # HIP teardown in __cxa_finalize segfaulted after the line was printed
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
