@@ -644,6 +644,9 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     return res, joins, pst, (seqs, incs, W), (cap[0] if cap else None)
 
 
+_MASKED_STREAMS = False   # set once pipelined_leg has made CU-masked engine streams
+
+
 def tree_cu_set(ncu, k, layout):
     """The tree context's compute units: the first k (layout "low"), or k / 8
     at the start of each of the 8 equal CU groups ("xcd")."""
@@ -673,6 +676,8 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
     tree_cus = max(1, min(tree_cus, ncu - 1))
     tset = tree_cu_set(ncu, tree_cus, layout)
+    global _MASKED_STREAMS
+    _MASKED_STREAMS = True
     ddev, tdev = cg.Device(gpu), cg.Device(gpu)
     ddev.configure(cu_mask=[c for c in range(ncu) if c not in set(tset)], nosync=True)
     tdev.configure(cu_mask=tset, nosync=True)
@@ -1514,9 +1519,12 @@ def main():
 
 if __name__ == "__main__":
     main()
-    # leave without the runtime's exit-time teardown: with the pipelined
-    # leg's CU-masked streams alive (never destroyed, ccg_ctx_configure) the
-    # HIP teardown in __cxa_finalize segfaulted after the line was printed
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(0)
+    if _MASKED_STREAMS and not os.environ.get("CCG_BENCH_CLEAN_EXIT"):
+        # leave without the runtime's exit-time teardown: with the pipelined
+        # leg's CU-masked streams alive (never destroyed, ccg_ctx_configure)
+        # the HIP teardown in __cxa_finalize segfaulted after the line was
+        # printed.  (Profilers that write their files at exit run with
+        # CCG_BENCH_CLEAN_EXIT=1, tools/profile_r05.sh.)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)

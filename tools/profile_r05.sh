@@ -9,6 +9,7 @@
 #   removed (a 50k-join tree's are too big to ship); summaries go to profiles/.
 set -e
 export TMPDIR=/tmp
+export CCG_BENCH_CLEAN_EXIT=1   # bench.py's normal exit: rocprofv3 writes its files at exit
 O=gpurun_out/prof_r05
 mkdir -p $O
 trap 'rc=$?; echo "exit $rc"; rm -rf $O/*/run_kernel_trace.csv $O/*/run_counter_collection.csv $O/*/*.db $O/*/*/' EXIT
