@@ -172,8 +172,8 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir
                                                                     (1, 900, "euc", 8, True, "rccl", 1),
                                                                     # world 8, the driver's node size, rehearsed as 8
                                                                     # processes on the one GPU
-                                                                    (8, 2000, "euc", 8, True, "gloo", 1),
-                                                                    (8, 1100, "snp", 8, True, "gloo", 0)])
+                                                                    (8, 1200, "euc", 8, True, "gloo", 1),
+                                                                    (8, 800, "snp", 8, True, "gloo", 0)])
 def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport, method):
     D, bs = _typed(_data(kind, n), et)
     ref_j, ref_fn, ref_fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=method, exact=exact)
