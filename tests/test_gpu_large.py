@@ -190,6 +190,7 @@ def _config3_rank(rank, world, port, n, k, out_dir):
     loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
     assert loc.numel() == nt.shard_elems(n, rank, world)
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()   # the generator's temporaries: 8 ranks share the one GPU
     coll = nt.HostColl(dist)
     dist.barrier()
     t0 = time.perf_counter()
@@ -238,6 +239,9 @@ def test_config3_dnj_prefix(dev, monkeypatch, tmp_path):
                                         max_joins=kk)
         del loc
         torch.cuda.empty_cache()
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()   # this process's cached blocks (earlier tests') back to the device for the 8 ranks
     mp.start_processes(_config3_rank, args=(world, _free_port(), n, kw, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
