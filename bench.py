@@ -512,13 +512,13 @@ def headline_cpu_baseline(dev, seqs_host, incs_host, L, gpu_cells, tmpdir, m=256
                       f"the reference's"}
 
 
-def make_headline_alignment(torch, n, L):
+def make_headline_alignment(torch, n, L, seed=3):
     """configs[2]: tools/config3.make_packed's tree-like alignment (512 clades,
     ~0.8% of codes flipped per taxon) on this GPU, every 10th word excluded
     (the 'N columns'); the same bytes on every rank."""
     from tools.config3 import make_packed
     W = L // 32 + 1
-    seqs = make_packed(torch, n, W)
+    seqs = make_packed(torch, n, W, seed=seed)
     incs = torch.full((W,), -1, dtype=torch.int32, device="cuda")
     incs[::10] = 0
     incs[(L + 31) // 32:] = 0
@@ -529,7 +529,7 @@ def make_headline_alignment(torch, n, L):
 
 
 def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0,
-                 tree_mode="shard", pg=None, tree_cus=0, tree_layout="low"):
+                 tree_mode="shard", pg=None, tree_cus=0, tree_layout="low", seed=3):
     """The headline: dist + exact DNJ of one n x L alignment per step.
     world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
     world > 1, tree_mode "shard": ccg_snp_ltd_shard_dev into this rank's band
@@ -542,7 +542,8 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     that the sharded engine's per-join collectives only lengthen).
     Returns (timed result, the last step's joins, profiled-step stats or None,
     alignment, the first capture_k LT cells of the first step (world 1)).
-    world 1 with tree_cus > 0: the pipelined form (pipelined_leg)."""
+    world 1 with tree_cus > 0: the pipelined form (pipelined_leg, alignments
+    of seeds 3 and 4 in turn); otherwise the alignment of `seed`."""
     if world == 1 and tree_cus > 0:
         return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k, tree_layout)
     if world > 1 and tree_mode == "gather-pipelined":
@@ -551,7 +552,7 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     import ccphylo_amd as cg
     from ccphylo_amd import native as nt
     from ccphylo_amd import shard as shd
-    seqs, incs, W = make_headline_alignment(torch, n, L)
+    seqs, incs, W = make_headline_alignment(torch, n, L, seed=seed)
     m = n * (n - 1) // 2
     gather = world > 1 and tree_mode == "gather"
     ranges = shd.lt_row_ranges(n, world) if gather else None
@@ -644,12 +645,11 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     return res, joins, pst, (seqs, incs, W), (cap[0] if cap else None)
 
 
-_MASKED_STREAMS = False   # set once pipelined_leg has made CU-masked engine streams
-
-
 def tree_cu_set(ncu, k, layout):
-    """The tree context's compute units: the first k (layout "low"), or k / 8
-    at the start of each of the 8 equal CU groups ("xcd")."""
+    """The tree context's compute units.  Mask bit c runs on XCD c % 8 (slot
+    c // 8 there; tools/micro/cu_mask.hip, profiles/r06_cu_mask_map.txt), so
+    "low" (bits 0 .. k-1) already gives every XCD k / 8 CUs; "xcd" takes
+    bits 0 .. k/8 - 1 of each 32-bit word, another k / 8 CUs per XCD."""
     if layout == "xcd":
         per = max(1, k // 8)
         return [g * (ncu // 8) + i for g in range(8) for i in range(per)]
@@ -659,32 +659,35 @@ def tree_cu_set(ncu, k, layout):
 def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0, layout="low"):
     """The headline on one GPU as a pipeline over a stream of alignments: two
     engine contexts on disjoint compute units (ccg_ctx_configure: the tree's
-    stream on CUs [0, tree_cus), the dist's on the rest, neither waiting for
-    the whole device) and two LT buffers, so that step k builds the tree of
-    matrix k while the dist of matrix k + 1 fills the other buffer.  The dist
-    of matrix 0 runs before the warmup; every timed step holds one whole dist
-    and one whole tree (K of each in K steps), so the rate is matrices
-    completed per second in steady state.  The joins of every step equal the
-    sequential form's (the tree is deterministic and reads only its own
-    buffer).  Same return value as pipeline_leg."""
+    stream on CUs [0, tree_cus), 8 per XCD, the dist's on the rest, neither
+    waiting for the whole device) and two LT buffers, so that step k builds
+    the tree of matrix k while the dist of matrix k + 1 fills the other
+    buffer.  The stream alternates two distinct alignments (seeds 3 and 4):
+    matrix k is alignment k % 2's, so consecutive steps really are different
+    matrices.  The dist of matrix 0 runs before the warmup; every timed step
+    holds one whole dist and one whole tree (K of each in K steps), so the
+    rate is matrices completed per second in steady state.  tree_s / dist_s
+    are each context's device time (HIP events on its own stream); the thread
+    walls are reported beside them.  Same return value as pipeline_leg, plus
+    res["alignments"] (both) and res["joins_sha256_by_alignment"]."""
     import hashlib
     import threading
     import ccphylo_amd as cg
-    seqs, incs, W = make_headline_alignment(torch, n, L)
+    aligns = [make_headline_alignment(torch, n, L, seed=3), make_headline_alignment(torch, n, L, seed=4)]
+    W = aligns[0][2]
     m = n * (n - 1) // 2
     gpu = torch.cuda.current_device()
     ncu = torch.cuda.get_device_properties(gpu).multi_processor_count
     tree_cus = max(1, min(tree_cus, ncu - 1))
     tset = tree_cu_set(ncu, tree_cus, layout)
-    global _MASKED_STREAMS
-    _MASKED_STREAMS = True
     ddev, tdev = cg.Device(gpu), cg.Device(gpu)
     ddev.configure(cu_mask=[c for c in range(ncu) if c not in set(tset)], nosync=True)
     tdev.configure(cu_mask=tset, nosync=True)
     tree_cus = len(tset)
     Ds = [torch.empty(m, dtype=torch.float64, device="cuda") for _ in range(2)]
     torch.cuda.synchronize()
-    inc0 = ddev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[0].data_ptr())   # matrix 0
+    s0, i0, _ = aligns[0]
+    inc0 = ddev.snp_ltd_dev(s0.data_ptr(), i0.data_ptr(), n, L, W, Ds[0].data_ptr())   # matrix 0
     cap = Ds[0][:capture_k].cpu().numpy() if capture_k else None
 
     def step(k, profile=False):
@@ -692,8 +695,9 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
 
         def run_d():
             try:
+                sq, ic, _ = aligns[(k + 1) % 2]
                 t0 = time.perf_counter()
-                inc = ddev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr())
+                inc = ddev.snp_ltd_dev(sq.data_ptr(), ic.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr())
                 res["d"] = (time.perf_counter() - t0, ddev.last_dist_ms(), inc)
             except Exception as e:  # noqa: BLE001
                 err.append(e)
@@ -713,36 +717,48 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
             x.join()
         if err:
             raise err[0]
-        return res["d"][0], res["t"][0], res["d"][1], res["t"][1], res["t"][2], res["d"][2]
+        # walls, the dist's kernel ms, joins, stats, included positions, the tree's device s (HIP events)
+        return (res["d"][0], res["t"][0], res["d"][1], res["t"][1], res["t"][2], res["d"][2],
+                res["t"][2][3] / 1e6)
+
+    def sha_of(joins):
+        jj, fn, fd = joins
+        return hashlib.sha256(np.ascontiguousarray(jj).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
 
     k = 0
     for w in range(warmup):
         r = step(k)
         k += 1
-        log(f"  warmup step {w}: dist {r[0]:.2f} s beside tree {r[1]:.2f} s")
+        log(f"  warmup step {w}: dist {r[0]:.2f} s beside tree {r[1]:.2f} s (device {r[6]:.2f} s)")
     barrier()
     t0 = time.perf_counter()
     parts = []
+    shas = {}
     for s_ in range(steps):
         parts.append(step(k))
+        shas.setdefault(k % 2, set()).add(sha_of(parts[-1][3]))
         k += 1
-        log(f"  step {s_}: dist {parts[-1][0]:.2f} s beside tree {parts[-1][1]:.2f} s")
+        log(f"  step {s_}: dist {parts[-1][0]:.2f} s beside tree {parts[-1][1]:.2f} s "
+            f"(tree device {parts[-1][6]:.2f} s, dist kernels {parts[-1][2] / 1e3:.2f} s)")
     barrier()
     dt = time.perf_counter() - t0
     joins, st, inc = parts[-1][3], parts[-1][4], parts[-1][5]
-    jj, fn, fd = joins
-    sha = hashlib.sha256(np.ascontiguousarray(jj).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
+    # the line's sha: alignment 0's (the sequential form's default matrix)
+    sha = sorted(shas[0])[0] if 0 in shas else sha_of(joins)
     pst = step(k, profile=True)[4] if profile_tree else None   # an extra, untimed pipelined step
-    res = {"dt": dt, "dist_s": sum(p[0] for p in parts) / steps, "tree_s": sum(p[1] for p in parts) / steps,
-           "dist_kernel_ms": sum(p[2] for p in parts) / steps, "joins": len(jj), "joins_sha256": sha,
+    res = {"dt": dt, "dist_s": sum(p[2] for p in parts) / steps / 1e3, "tree_s": sum(p[6] for p in parts) / steps,
+           "dist_wall_s": sum(p[0] for p in parts) / steps, "tree_wall_s": sum(p[1] for p in parts) / steps,
+           "dist_kernel_ms": sum(p[2] for p in parts) / steps, "joins": len(joins[0]), "joins_sha256": sha,
+           "joins_sha256_by_alignment": {str(a): sorted(v) for a, v in shas.items()},
            "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]), "included_positions": inc,
+           "alignments": aligns,
            "pipelined": {"tree_cus": tree_cus, "dist_cus": ncu - tree_cus, "layout": layout,
-                         "matrix0_included_positions": inc0}}
+                         "matrix0_included_positions": inc0, "alignment_seeds": [3, 4]}}
     del Ds
     ddev.close()
     tdev.close()
     torch.cuda.empty_cache()
-    return res, joins, pst, (seqs, incs, W), cap
+    return res, joins, pst, aligns[0], cap
 
 
 def gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, barrier, pg, profile_tree=True):
@@ -1268,7 +1284,10 @@ def main():
                          "the next matrix's dist on the rest (64: tools/overlap.py, 50k x 5 Mbp per matrix 7.59 s "
                          "against 7.71-7.90 s at 32-56 CUs); 0: dist then tree on the whole chip, step by step")
     ap.add_argument("--tree-layout", choices=["low", "xcd"], default="low",
-                    help="which CUs the pipelined tree takes: the first --tree-cus, or --tree-cus / 8 in each XCD")
+                    help="which CUs the pipelined tree takes: mask bits 0 .. --tree-cus - 1, or the first "
+                         "--tree-cus / 8 bits of each 32-bit mask word (both --tree-cus / 8 CUs per XCD)")
+    ap.add_argument("--headline-seed", type=int, default=3,
+                    help="the alignment's seed in the sequential forms (the pipelined one alternates 3 and 4)")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -1346,7 +1365,7 @@ def main():
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg,
-        tree_cus=args.tree_cus if world == 1 else 0, tree_layout=args.tree_layout)
+        tree_cus=args.tree_cus if world == 1 else 0, tree_layout=args.tree_layout, seed=args.headline_seed)
     if hwd is not None:
         hwd.cancel()
     dt = head["dt"]
@@ -1390,12 +1409,16 @@ def main():
                     f"point-to-point; tree: GPU 0 (single-GPU engine)" if args.tree_mode == "gather" else
                     f"LT row bands over {world} GPUs ({transport})")},
         "split": {"dist_s": round(head["dist_s"], 3), "tree_s": round(head["tree_s"], 3),
-                  "overlap": "dist and tree walls run concurrently (pipelined)"
-                             if pipe or head.get("gather_pipelined") else "sequential",
+                  "overlap": "dist and tree run concurrently (pipelined); dist_s / tree_s: each context's device "
+                             "time (HIP events on its stream)" if pipe else
+                             "dist and tree walls run concurrently (pipelined)"
+                             if head.get("gather_pipelined") else "sequential",
                   "dist_taxa_pairs_per_s": round(m / max(head["dist_s"], 1e-9), 1),
                   "dist_nt_comparisons_per_s": m * float(L) / max(head["dist_s"], 1e-9),
                   "tree_nj_iterations_per_s": round(head["joins"] / max(head["tree_s"], 1e-9), 1),
                   "joins": head["joins"], "joins_sha256": head["joins_sha256"],
+                  **({"dist_wall_s": round(head["dist_wall_s"], 3), "tree_wall_s": round(head["tree_wall_s"], 3),
+                      "joins_sha256_by_alignment": head["joins_sha256_by_alignment"]} if pipe else {}),
                   "rows_rescanned": head["rows_rescanned"], "cells_rescanned": head["cells_rescanned"],
                   "included_positions": head["included_positions"]},
         "roofline": roof,
@@ -1418,23 +1441,34 @@ def main():
     extras = result.setdefault("extras", {}) if not args.no_extras else None
     if extras is not None and world == 1 and pipe:
         # the same matrix step by step on the whole chip (dist, then tree): one matrix's latency
-        log("headline, sequential form (one step, whole chip)")
+        log("headline, sequential form (each alignment once, whole chip)")
         try:
             D1 = torch.empty(m, dtype=torch.float64, device="cuda")
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            dev.snp_ltd_dev(seqs.data_ptr(), incs.data_ptr(), n, L, W, D1.data_ptr())
-            t1 = time.perf_counter()
-            j1, fn1, fd1, _ = dev.tree_dev(D1.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
-            t2 = time.perf_counter()
+            seq = {}
+            for a_, (sq_, ic_, _) in enumerate(head["alignments"]):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                dev.snp_ltd_dev(sq_.data_ptr(), ic_.data_ptr(), n, L, W, D1.data_ptr())
+                t1 = time.perf_counter()
+                j1, fn1, fd1, _ = dev.tree_dev(D1.data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True)
+                t2 = time.perf_counter()
+                sha1 = hashlib.sha256(np.ascontiguousarray(j1).tobytes() +
+                                      np.array([fn1, fd1]).tobytes()).hexdigest()[:16]
+                seq[str(a_)] = {"s_per_matrix": round(t2 - t0, 3), "dist_s": round(t1 - t0, 3),
+                                "tree_s": round(t2 - t1, 3), "joins_sha256": sha1}
             del D1
             torch.cuda.empty_cache()
-            sha1 = hashlib.sha256(np.ascontiguousarray(j1).tobytes() + np.array([fn1, fd1]).tobytes()).hexdigest()[:16]
+            pipe_sha = head["joins_sha256_by_alignment"]
+            s_mean = sum(v["s_per_matrix"] for v in seq.values()) / len(seq)
             extras["headline_sequential"] = {
-                "s_per_matrix": round(t2 - t0, 3), "dist_s": round(t1 - t0, 3), "tree_s": round(t2 - t1, 3),
-                "taxa_pairs_per_s": round(m / (t2 - t0), 1), "joins_sha256": sha1,
-                "note": "one matrix's latency, dist then tree on all CUs; the line's value is the pipelined "
-                        "steady state (each step one whole dist and one whole tree, on disjoint CUs)"}
+                "s_per_matrix": round(s_mean, 3), "taxa_pairs_per_s": round(m / s_mean, 1),
+                "dist_s": seq["0"]["dist_s"], "tree_s": seq["0"]["tree_s"], "joins_sha256": seq["0"]["joins_sha256"],
+                "by_alignment": seq,
+                "pipelined_joins_match": all(pipe_sha.get(a_, [v["joins_sha256"]]) == [v["joins_sha256"]]
+                                             for a_, v in seq.items()),
+                "note": "one matrix's latency, dist then tree on all CUs, for each of the two alignments; the "
+                        "line's value is the pipelined steady state (each step one whole dist and one whole tree, "
+                        "on disjoint CUs, the matrices alternating between the two alignments)"}
         except Exception as e:  # noqa: BLE001
             extras["headline_sequential"] = {"error": str(e)}
     if extras is not None and rank == 0 and world == 1:
@@ -1445,6 +1479,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             extras["refrule_config2_prefix"] = {"error": str(e)}
     del seqs, incs
+    head.pop("alignments", None)
     torch.cuda.empty_cache()
     if extras is not None:
         if rank == 0 and world == 1:
@@ -1482,11 +1517,15 @@ def main():
         import threading
 
         def _timeout():
+            # a hung collective: the line (with the legs marked) still prints,
+            # and the process fails, so the driver's rc says so
             if rank == 0:
                 for leg in ("dnj_sharded", "nj_sharded"):
                     extras.setdefault(leg, {"error": f"timed out after {SHARD_LEG_TIMEOUT_S} s"})
                 print(json.dumps(result), flush=True)
-            os._exit(0)
+            sys.stderr.write(f"bench.py: a sharded leg did not finish in {SHARD_LEG_TIMEOUT_S} s\n")
+            sys.stderr.flush()
+            os._exit(4)
         wd = threading.Timer(SHARD_LEG_TIMEOUT_S, _timeout)
         wd.daemon = True
         wd.start()
@@ -1519,12 +1558,3 @@ def main():
 
 if __name__ == "__main__":
     main()
-    if _MASKED_STREAMS and not os.environ.get("CCG_BENCH_CLEAN_EXIT"):
-        # leave without the runtime's exit-time teardown: with the pipelined
-        # leg's CU-masked streams alive (never destroyed, ccg_ctx_configure)
-        # the HIP teardown in __cxa_finalize segfaulted after the line was
-        # printed.  (Profilers that write their files at exit run with
-        # CCG_BENCH_CLEAN_EXIT=1, tools/profile_r05.sh.)
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)

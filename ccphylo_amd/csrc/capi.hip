@@ -11,7 +11,9 @@ int ccg_tree_impl(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *join
                   double *final_d, int64_t *stats, const ccg_dnj_state *sin, ccg_dnj_state *sout);
 int ccg_selftest_row_sum_impl(ccg_ctx *ctx, const double *c, int n, double *out, int *parallel);
 
-static char g_last_error[512];
+// per host thread, like the tree's grid state: two contexts driven from two
+// threads (the pipelined bench) keep their own messages
+static thread_local char g_last_error[512];
 
 void ccg_set_last_error(hipError_t e, const char *what, const char *file, int line) {
 	snprintf(g_last_error, sizeof(g_last_error), "%s (%d) in %s at %s:%d", hipGetErrorString(e), (int) e, what, file,
@@ -22,6 +24,27 @@ void ccg_set_last_error(hipError_t e, const char *what, const char *file, int li
 void ccg_set_last_msg(const char *msg) {
 	snprintf(g_last_error, sizeof(g_last_error), "%s", msg);
 	fprintf(stderr, "ccphylo_amd: %s\n", g_last_error);
+}
+
+int ccg_ctx_workspace(ccg_ctx *c, int k, size_t bytes, void **p) {
+	if(c->ws[k] && c->ws_bytes[k] >= bytes) {
+		*p = c->ws[k];
+		return CCG_OK;
+	}
+	if(c->ws[k]) {   // grow: the only hipFree of a tree run, at a context's first run of a larger tree
+		CCG_CHECK(hipStreamSynchronize(c->stream));
+		CCG_CHECK(hipFree(c->ws[k]));
+		c->ws[k] = NULL;
+		c->ws_bytes[k] = 0;
+	}
+	if(hipMalloc(&c->ws[k], bytes) != hipSuccess) {   // quietly: the block bounds' slot is optional
+		(void) hipGetLastError();
+		c->ws[k] = NULL;
+		return CCG_ENOMEM;
+	}
+	c->ws_bytes[k] = bytes;
+	*p = c->ws[k];
+	return CCG_OK;
 }
 
 extern "C" {
@@ -78,17 +101,34 @@ int ccg_init(int device, ccg_ctx **out) {
 int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int flags) {
 	if(!c || mask_words < 0 || (mask_words && !cu_mask)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
+	hipStream_t s = NULL;
 	if(mask_words) {   // the engine stream again, limited to the CUs of the mask
-		hipStream_t s;
+		// mask bit k runs on XCD k % nx (slot k / nx within it), and an XCD
+		// whose share of the mask is empty runs on ALL of its CUs
+		// (profiles/r06_cu_mask_map.txt): such a mask does not limit the stream
+		hipDeviceProp_t p;
+		CCG_CHECK(hipGetDeviceProperties(&p, c->device));
+		const int ncu = p.multiProcessorCount, nx = ncu >= 32 ? ncu / 32 : 1;
+		for(int x = 0; x < nx; ++x) {
+			bool any = false;
+			for(int k = x; k < ncu && k < 32 * mask_words && !any; k += nx) any = (cu_mask[k / 32] >> (k % 32)) & 1u;
+			if(!any) {
+				snprintf(g_last_error, sizeof(g_last_error),
+				         "ccg_ctx_configure: the CU mask leaves XCD %d (mask bits k with k %% %d == %d) without a CU; "
+				         "that XCD would run on all of its CUs",
+				         x, nx, x);
+				return CCG_EINVAL;
+			}
+		}
 		CCG_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t) mask_words, cu_mask));
+	} else if(c->masked) {   // back to the whole chip
+		CCG_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+	}
+	if(s) {
 		CCG_CHECK(hipStreamSynchronize(c->stream));
-		// a CU-masked stream is never destroyed: on this ROCm image, destroying
-		// one left the next kernel launched on another stream of the process
-		// (torch's) to segfault in the runtime (tools/cu_mask_probe.py); it is
-		// released with the process
-		if(!c->masked) CCG_CHECK(hipStreamDestroy(c->stream));
+		CCG_CHECK(hipStreamDestroy(c->stream));
 		c->stream = s;
-		c->masked = 1;
+		c->masked = mask_words != 0;
 	}
 	c->flags = flags;
 	return CCG_OK;
@@ -98,9 +138,11 @@ void ccg_destroy(ccg_ctx *c) {
 	if(!c) return;
 	hipSetDevice(c->device);
 	hipStreamSynchronize(c->stream);
+	for(int k = 0; k < 2; ++k)
+		if(c->ws[k]) hipFree(c->ws[k]);
 	hipEventDestroy(c->ev0);
 	hipEventDestroy(c->ev1);
-	if(!c->masked) hipStreamDestroy(c->stream);   // (a CU-masked one stays: ccg_ctx_configure)
+	hipStreamDestroy(c->stream);
 	free(c);
 }
 

@@ -1690,6 +1690,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_w(const typename Elem<ET>::T *_
 // (k_dnj_plan's helper blocks run while block 0 persists row i's sD and the
 // thresholds of rows j and i: isub / sDm substitute the column, ubinf the
 // threshold)
+// a unit spans at most DnjGrid::seg's cap of 8 SEG cells (or SEG_S): lb_unit's
+// four 64-lane bound loads must cover all of its blocks
+static_assert(8 * SEG <= 4 * 64 * LBW && SEG_S <= 4 * 64 * LBW, "lb_unit loads at most 256 block bounds per unit");
 template <int ET>
 __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ row, double bs, const TreeBufs &b, int n,
                                        int r, int c0, int c1, double sDr, double &q, int &idx, int isub,

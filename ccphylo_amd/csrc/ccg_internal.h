@@ -33,8 +33,15 @@ struct ccg_ctx {
 	char name[256];
 	float dist_ms;   // the last dist call's pair kernels (HIP events on the engine stream)
 	int flags;       // CCG_CTX_* (ccg_ctx_configure)
-	int masked;      // the stream was created with a CU mask (never destroyed: see ccg_ctx_configure)
+	int masked;      // the stream was created with a CU mask (ccg_ctx_configure)
+	// the tree's device workspaces, kept across runs (grown on demand, freed
+	// by ccg_destroy): a tree run then makes no hipFree, which waits for every
+	// stream of the device, so a CCG_CTX_NOSYNC context never waits for another
+	void *ws[2];
+	size_t ws_bytes[2];
 };
+// slot k of the context's workspace cache, at least `bytes` long
+int ccg_ctx_workspace(ccg_ctx *c, int k, size_t bytes, void **p);
 // every device-pointer entry point first waits for the whole device (inputs
 // may come from other streams) unless the caller orders them itself
 #define CCG_DEVICE_SYNC(c) \

@@ -1807,6 +1807,18 @@ int ccg_tree_alloc(TreeWork *w, int n, hipStream_t st) {
 	return CCG_OK;
 }
 
+// the single engine's workspace: the context's cached slot 0 (no hipFree per run)
+static int tree_alloc_ctx(ccg_ctx *c, TreeWork *w, int n) {
+	const size_t sz = tree_layout(NULL, n, NULL);
+	void *m;
+	const int rc = ccg_ctx_workspace(c, 0, sz, &m);
+	if(rc) return rc;
+	CCG_CHECK(hipMemsetAsync(m, 0, sz, c->stream));
+	w->mem = m;
+	tree_layout(&w->b, n, (char *) m);
+	return CCG_OK;
+}
+
 // DNJ: k_dnj_plan of the join at matrix size n (first: the run's first join,
 // whose candidate k_dnj_prep or a resumed state left in ctl)
 // the scan rescans S first and prunes the other entries under S's exact
@@ -2003,7 +2015,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	g_grid = DnjGrid();
 	g_grid.load();
 	g_progress = getenv("CCG_PROGRESS") != nullptr;
-	int rc = ccg_tree_alloc(&w, n0, st);
+	int rc = tree_alloc_ctx(ctx, &w, n0);
 	if(rc) return rc;
 	TreeBufs b = w.b;
 	TreeCtl init;
@@ -2056,7 +2068,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		const size_t lbb = ((size_t) n0 * LS * 4 + 255) & ~(size_t) 255;
 		const size_t msb = ((size_t) (LS + 1) * 8 + 255) & ~(size_t) 255;
 		const size_t ubb = ((size_t) n0 * 8 + 255) & ~(size_t) 255, skb = (size_t) (LB_SCAN + LB_HELP) * LB_SLOT * 8;
-		if(hipMalloc(&lbmem, lbb + msb + ubb + skb) == hipSuccess) {
+		if(ccg_ctx_workspace(ctx, 1, lbb + msb + ubb + skb, &lbmem) == CCG_OK) {
 			b.lbm = (unsigned *) lbmem;
 			b.msd = (double *) ((char *) lbmem + lbb);
 			b.ubq = (double *) ((char *) lbmem + lbb + msb);
@@ -2118,7 +2130,9 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	CCG_CHECK(hipStreamSynchronize(st));
 	if(b.lbskip) {   // the bounded-out cells, from the per-wave slots
 		std::vector<long long> sl((size_t) (LB_SCAN + LB_HELP) * LB_SLOT);
-		CCG_CHECK(hipMemcpy(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost));
+		// on the context's stream (a null-stream copy would wait for every blocking stream of the device)
+		CCG_CHECK(hipMemcpyAsync(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost, st));
+		CCG_CHECK(hipStreamSynchronize(st));
 		for(size_t x = 0; x < (size_t) LB_SCAN + LB_HELP; ++x) {
 			h.cells_lbskip += sl[x * LB_SLOT];
 			h.cells_help -= sl[x * LB_SLOT + 1];
@@ -2241,8 +2255,6 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	}
 #endif
 	if(h.done && h.final_n < 0) {   // k_dnj_plan's look-back timed out (never expected)
-		if(lbmem) hipFree(lbmem);
-		hipFree(w.mem);
 		ccg_set_last_msg("k_dnj_plan / k_dnj_join: a block's bounded wait on another block timed out");
 		return CCG_EHIP;
 	}
@@ -2304,9 +2316,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 		}
 	}
 	CCG_CHECK(hipStreamSynchronize(st));
-	if(lbmem) CCG_CHECK(hipFree(lbmem));
-	CCG_CHECK(hipFree(w.mem));
-	return CCG_OK;
+	return CCG_OK;   // the workspaces stay with the context (ccg_ctx_workspace)
 }
 
 // ------------------------------------------------------------------ self-test of the exact row sum

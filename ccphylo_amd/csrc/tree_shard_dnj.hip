@@ -940,7 +940,9 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	kt.finish();
 	if(dbg) {
 		static thread_local unsigned long long hd[1024 * 8];
-		if(hipMemcpy(hd, dbg, sizeof(hd), hipMemcpyDeviceToHost) != hipSuccess) memset(hd, 0, sizeof(hd));
+		if(hipMemcpyAsync(hd, dbg, sizeof(hd), hipMemcpyDeviceToHost, st) != hipSuccess ||
+		   hipStreamSynchronize(st) != hipSuccess)
+			memset(hd, 0, sizeof(hd));
 		double acc[8] = {0};
 		int cnt = 0;
 		for(int s_ = 0; s_ < 1024; ++s_) {
@@ -974,7 +976,8 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 	}
 	if(b.lbskip) {   // the bounded-out cells, from the per-wave slots
 		std::vector<long long> sl((size_t) LB_SCAN * LB_SLOT);
-		SD_HIP(hipMemcpy(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost));
+		SD_HIP(hipMemcpyAsync(sl.data(), b.lbskip, sl.size() * 8, hipMemcpyDeviceToHost, st));
+		SD_HIP(hipStreamSynchronize(st));
 		for(size_t x = 0; x < (size_t) LB_SCAN; ++x) hc.cells_lbskip += sl[x * LB_SLOT];
 	}
 	if(stats) {

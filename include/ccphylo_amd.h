@@ -48,9 +48,12 @@ typedef struct ccg_ctx ccg_ctx;
 int ccg_init(int device, ccg_ctx **ctx);
 
 /* Optional, after ccg_init: cu_mask (mask_words 32-bit words, bit k = CU k;
- * 0 words: unchanged) limits the context's stream to those compute units
- * (hipExtStreamCreateWithCUMask), so that two contexts of one device can run
- * side by side -- e.g. one matrix's dist beside the previous matrix's tree;
+ * 0 words: the whole chip again) limits the context's stream to those compute
+ * units (hipExtStreamCreateWithCUMask), so that two contexts of one device can
+ * run side by side -- e.g. one matrix's dist beside the previous matrix's tree.
+ * On gfx950 bit k is a CU of XCD k % 8 (the first 64 bits: 8 CUs per XCD);
+ * a mask that leaves an XCD without a CU is CCG_EINVAL (that XCD would run
+ * unmasked).  May be called again; the previous stream is drained first.
  * flags CCG_CTX_NOSYNC: the device-pointer entry points do not wait for the
  * whole device first (the caller orders its inputs; a device-wide wait would
  * wait for the other context's work). */

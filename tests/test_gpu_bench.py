@@ -50,6 +50,16 @@ def test_bench_gpus2_spawned_same_joins():
     lp, ls = (json.loads(p.stdout.strip().splitlines()[-1]) for p in (pipe, seq))
     assert "pipelined" in lp["config"]["parallelism"] and "pipelined" not in ls["config"]["parallelism"]
     assert lp["split"]["joins_sha256"] == ls["split"]["joins_sha256"] == l1["split"]["joins_sha256"]
+    # the pipelined stream alternates two alignments (seeds 3, 4): each one's
+    # tree is the sequential form's tree of that alignment, and they differ
+    seq4 = _bench(["--gpus", "1", "--tree-cus", "0", "--headline-seed", "4"] + SMALL)
+    assert seq4.returncode == 0, seq4.stderr[-3000:]
+    l4 = json.loads(seq4.stdout.strip().splitlines()[-1])
+    by = lp["split"]["joins_sha256_by_alignment"]
+    assert by == {"0": [ls["split"]["joins_sha256"]], "1": [l4["split"]["joins_sha256"]]}
+    assert by["0"] != by["1"]
+    # tree_s is the tree context's device time, not the dist's wall
+    assert 0 < lp["split"]["tree_s"] <= lp["split"]["tree_wall_s"] + 1e-3
     for mode in ("gather-pipelined", "gather", "shard"):
         two = _bench(["--gpus", "2", "--shard-transport", "gloo", "--tree-mode", mode] + SMALL)
         assert two.returncode == 0, (mode, two.stderr[-3000:])
