@@ -999,16 +999,26 @@ def nj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=100_000,
             "coll_us_per_join": round(pst[5 + 2 * 8] / 1e3 / (joins + 1), 2) if pst[4 + 2 * 8] else 0.0}
 
 
-def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=200_000, joins=0, exact=True):
+def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=200_000, joins=0, exact=True,
+                    profile_joins=2000):
     """configs[3]: DNJ on ONE n-taxon Euclidean matrix (n = 200k, float =
     `-p`: 80 GB), the WHOLE tree (joins = 0) with exact row sums.  world 1:
     the single-GPU engine on the packed LT (ccg_tree_shard_dev at world 1);
     world > 1: rank g holds the row bands g, g + world, ... and the ranks
-    exchange over `coll` (RCCL) -- strong scaling of one tree."""
+    exchange over `coll` (RCCL) -- strong scaling of one tree.  A second,
+    profiled run of the first `profile_joins` joins gives each rank's device
+    time per join by kernel class (HIP events on the engine stream; the
+    collectives' class is their device time on that stream), reported for
+    rank 0 and as the max over ranks; the aggregate HBM fraction counts the
+    cells every rank's scans loaded (4 B each) plus the O(n) vectors."""
     import hashlib
     import ccphylo_amd as cg
+    from ccphylo_amd import native as nt
     from tools.synth import euclid_shard_dev
     loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
+    work = torch.empty_like(loc) if profile_joins else None
+    if work is not None:
+        work.copy_(loc)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -1017,16 +1027,39 @@ def dnj_shard_extra(dev, torch, rank=0, world=1, dist=None, coll=None, n=200_000
                                        max_joins=joins)
     dt = shard_max(time.perf_counter() - t0, dist)
     del loc
-    torch.cuda.empty_cache()
     sha = hashlib.sha256(np.ascontiguousarray(j).tobytes() + np.array([fn, fd]).tobytes()).hexdigest()[:16]
-    return {"joins_per_s": round(len(j) / dt, 2), "ms_per_join": round(1000 * dt / max(len(j), 1), 4),
-            "joins": len(j), "n": n, "world": world, "seconds": round(dt, 3), "joins_sha256": sha,
-            "rows_rescanned_rank0": int(st[0]), "cells_rescanned_rank0": int(st[1]),
-            "row_sums": "exact" if exact else "fast",
-            "config": f"configs[3]: DNJ (-m dnj) on one N={n} Euclidean matrix (float, "
-                      f"{4 * n * (n - 1) / 2 / 1e9:.0f} GB), " +
-                      ("the single-GPU engine" if world == 1 else f"its LT row bands dealt over {world} GPUs (RCCL)") +
-                      f"; {'the whole tree' if not joins else f'first {joins} joins'}, init included"}
+    cells_all = float(st[1]) if dist is None else shard_sum(float(st[1]), dist)
+    # algorithmic bytes: the cells the scans loaded + per join ~ (4 s + 40) n of vectors and line updates
+    algo = 4.0 * cells_all + sum(56.0 * (n - k) for k in range(len(j)))
+    res = {"joins_per_s": round(len(j) / dt, 2), "ms_per_join": round(1000 * dt / max(len(j), 1), 4),
+           "joins": len(j), "n": n, "world": world, "seconds": round(dt, 3), "joins_sha256": sha,
+           "rows_rescanned_rank0": int(st[0]), "cells_rescanned_rank0": int(st[1]),
+           "cells_rescanned_all_ranks": int(cells_all),
+           "hbm_GBps_aggregate": round(algo / dt / 1e9, 1),
+           "hbm_frac_aggregate": round(algo / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
+           "row_sums": "exact" if exact else "fast",
+           "config": f"configs[3]: DNJ (-m dnj) on one N={n} Euclidean matrix (float, "
+                     f"{4 * n * (n - 1) / 2 / 1e9:.0f} GB), " +
+                     ("the single-GPU engine" if world == 1 else f"its LT row bands dealt over {world} GPUs (RCCL)") +
+                     f"; {'the whole tree' if not joins else f'first {joins} joins'}, init included"}
+    if work is not None:
+        pj = min(profile_joins, len(j)) if len(j) else profile_joins
+        if dist is not None:
+            dist.barrier()
+        _, _, _, ps = dev.tree_shard_dev(work.data_ptr(), n, coll, etype=4, method=cg.CCG_TREE_DNJ, exact=exact,
+                                         max_joins=pj, profile=True)
+        per, mx = {}, {}
+        for c, nm in enumerate(KNAMES):   # every class on every rank, in one order (the max is a collective)
+            us = ps[5 + 2 * c] / 1e3 / pj if ps[4 + 2 * c] else 0.0
+            m_ = shard_max(us, dist)
+            if nm != "init" and m_ > 0:
+                per[nm], mx[nm] = round(us, 2), round(m_, 2)
+        res["device_us_per_join_rank0"] = {"joins": pj, **per}
+        res["device_us_per_join_max_over_ranks"] = mx
+        res["device_us_per_join_total_rank0"] = round(sum(per.values()), 2)
+        del work
+    torch.cuda.empty_cache()
+    return res
 
 
 def shard_max(x, dist):
@@ -1034,6 +1067,13 @@ def shard_max(x, dist):
         return x
     from ccphylo_amd import shard
     return shard.reduce_max(x, dist)
+
+
+def shard_sum(x, dist):
+    if dist is None:
+        return x
+    from ccphylo_amd import shard
+    return shard.reduce_sum(x, dist)
 
 
 def reference_tree_parity(D, n, exact_joins, fast_joins, td):

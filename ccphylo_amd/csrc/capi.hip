@@ -126,7 +126,14 @@ int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int f
 	}
 	if(s) {
 		CCG_CHECK(hipStreamSynchronize(c->stream));
-		CCG_CHECK(hipStreamDestroy(c->stream));
+		// a CU-masked stream is drained but never destroyed: on this ROCm
+		// (7.2, gfx950) destroying one leaves the runtime to hand a dead
+		// hardware queue to a later stream, whose kernels then never complete
+		// (the pure-HIP reproducer `tools/micro/cu_mask engine 2 8 1 1 0 0`:
+		// the second stream created after the destroy hangs; a plain stream
+		// destroyed the same way, or the masked one kept, run clean:
+		// profiles/r06_cu_mask_destroy.txt).  It is released with the process.
+		if(!c->masked) CCG_CHECK(hipStreamDestroy(c->stream));
 		c->stream = s;
 		c->masked = mask_words != 0;
 	}
@@ -142,7 +149,7 @@ void ccg_destroy(ccg_ctx *c) {
 		if(c->ws[k]) hipFree(c->ws[k]);
 	hipEventDestroy(c->ev0);
 	hipEventDestroy(c->ev1);
-	hipStreamDestroy(c->stream);
+	if(!c->masked) hipStreamDestroy(c->stream);   // (a CU-masked one stays: ccg_ctx_configure)
 	free(c);
 }
 

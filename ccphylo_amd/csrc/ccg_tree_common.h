@@ -1363,6 +1363,8 @@ struct KTimer {
 	int used;
 	long long cnt[CCG_NKSTAT], ns[CCG_NKSTAT];
 	void init(hipStream_t s, bool enable) {
+		if(on)   // a previous profiled run that ended early (an error return) still holds its events
+			for(int k = 0; k < 1025; ++k) hipEventDestroy(ev[k]);
 		on = enable;
 		st = s;
 		used = 0;

@@ -1003,7 +1003,10 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 out:
 #undef SD_TRY
 #undef SD_HIP
-	if(rc != CCG_OK) kt.on = false;
+	if(rc != CCG_OK && kt.on) {   // the profiled run ended early: release its events
+		for(int k = 0; k < 1025; ++k) hipEventDestroy(kt.ev[k]);
+		kt.on = false;
+	}
 	hipStreamSynchronize(st);
 	if(h) hipHostFree(h);
 	if(lbmem) hipFree(lbmem);

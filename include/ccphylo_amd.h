@@ -54,6 +54,9 @@ int ccg_init(int device, ccg_ctx **ctx);
  * On gfx950 bit k is a CU of XCD k % 8 (the first 64 bits: 8 CUs per XCD);
  * a mask that leaves an XCD without a CU is CCG_EINVAL (that XCD would run
  * unmasked).  May be called again; the previous stream is drained first.
+ * A CU-masked stream is never destroyed (a ROCm 7.2 runtime defect: a later
+ * stream's kernels hang after one is destroyed; tools/micro/cu_mask.hip), so
+ * each masked configuration keeps one HIP stream until the process exits.
  * flags CCG_CTX_NOSYNC: the device-pointer entry points do not wait for the
  * whole device first (the caller orders its inputs; a device-wide wait would
  * wait for the other context's work). */

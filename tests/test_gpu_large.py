@@ -199,8 +199,15 @@ def _config3_rank(rank, world, port, n, k, out_dir):
     dt = time.perf_counter() - t0
     np.save(os.path.join(out_dir, f"j{rank}.npy"), joins)
     K = nt.NKSTAT
+    # device time per join by kernel class (HIP events on this rank's stream;
+    # host-staged collectives: the class holds the staging copies, not the host wait)
+    names = ["init", "dnj_select", "dnj_scan", "nj_argmin", "update", "dnj_requeue", "nj_pop", "dnj_find", "coll",
+             "exact_sum"]
+    dev_us = {nm: round(st[5 + 2 * c] / 1e3 / max(len(joins), 1), 2) for c, nm in enumerate(names)
+              if st[4 + 2 * c] and nm != "init"}
     with open(os.path.join(out_dir, f"s{rank}.json"), "w") as f:
         json.dump({"rank": rank, "shard_GB": round(loc.numel() * 4 / 1e9, 3), "tree_s": round(dt, 2),
+                   "device_us_per_join": dev_us, "device_s": round(st[3] / 1e6, 3),
                    "init_coll_bytes": int(st[8 + 2 * K]), "hard_columns": int(st[9 + 2 * K]),
                    "ref_rows": int(st[10 + 2 * K]), "ref_cells": int(st[11 + 2 * K]),
                    "coll_calls": coll.calls, "coll_bytes": coll.bytes}, f)

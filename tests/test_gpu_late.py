@@ -43,10 +43,12 @@ def test_config3_late_tree_resume():
     cuts = [int(x) for x in os.environ.get("CCG_LATE_CUTS", "60000,120000,180000").split(",")]
     m = int(os.environ.get("CCG_LATE_M", 200))
     os.environ.setdefault("CCG_PROGRESS", "1")
-    _late_legs(n, cuts, m, os.environ.get("CCG_LATE_OUT"))
+    # CCG_LATE_GEN=cdist: round 4's torch.cdist matrix (its reference rule
+    # rescans ~1.7e9 cells per join: give it fewer joins per cut)
+    _late_legs(n, cuts, m, os.environ.get("CCG_LATE_OUT"), cdist=os.environ.get("CCG_LATE_GEN") == "cdist")
 
 
-def _late_legs(n, cuts, m, out):
+def _late_legs(n, cuts, m, out, cdist=False):
     import torch
     import ccphylo_amd as cg
     from ccphylo_amd import native
@@ -55,7 +57,7 @@ def _late_legs(n, cuts, m, out):
     K = native.NKSTAT
     threads = min(16, os.cpu_count() or 4)
     dev = cg.Device(0)
-    D = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32)   # world 1: the packed LT
+    D = euclid_shard_dev(torch, n, 0, 1, dtype=torch.float32, cdist=cdist)   # world 1: the packed LT
     torch.cuda.synchronize()
     state, done, t_gpu = None, 0, 0.0
     for k in cuts:
@@ -78,7 +80,8 @@ def _late_legs(n, cuts, m, out):
         to = time.perf_counter() - t0
         del cells, ost
         same = len(gj) == len(rj) == m and bool((gj == rj).all())
-        rec = {"n": n, "cut": k, "matrix_size": cur, "joins_compared": m, "joins_identical": same,
+        rec = {"n": n, "generator": "torch.cdist (round 4)" if cdist else "elementwise (round 5)", "cut": k,
+               "matrix_size": cur, "joins_compared": m, "joins_identical": same,
                "engine_reference_rule_rows_cells": [int(gs[10 + 2 * K]), int(gs[11 + 2 * K])],
                "oracle_rows_cells": [int(rs[0]), int(rs[1])],
                "engine_rows_cells": [int(gs[0]), int(gs[1])],

@@ -15,8 +15,13 @@
 //                          created after it and on the null stream
 //   exit WORDS             create a masked stream, run on it, and return from
 //                          main with the stream alive (runtime teardown)
-//   engine WORDS POOL      the engine probe's stream sequence, then POOL
-//                          priority streams as torch creates them
+//   engine WORDS POOL [MASK DESTROY PRIO TEARDOWN]
+//                          the engine probe's stream sequence, then POOL
+//                          streams as torch creates them (PRIO: alternating
+//                          high / low priority), a kernel on each; MASK 0: a
+//                          plain stream in the masked one's place; DESTROY 0:
+//                          it stays; TEARDOWN 1: return from main with every
+//                          stream alive
 //
 // hipcc --offload-arch=gfx950 -O3 -o tools/micro/cu_mask tools/micro/cu_mask.hip
 #include <hip/hip_runtime.h>
@@ -184,7 +189,7 @@ static int run_destroy(int words, bool teardown) {
 // a masked one, the plain one destroyed), work on the masked stream, the
 // masked stream destroyed; then what torch does at its first use: a pool of
 // streams at two priorities, a kernel on each
-static int run_engine_seq(int words, int pool) {
+static int run_engine_seq(int words, int pool, int use_mask, int destroy, int prio, int teardown) {
 	std::vector<uint32_t> m(words, 0u);
 	for(int c = 0; c < 64; ++c)
 		if(c / 32 < words) m[c / 32] |= 1u << (c % 32);
@@ -198,7 +203,8 @@ static int run_engine_seq(int words, int pool) {
 	hipEvent_t e0, e1;
 	CK(hipEventCreate(&e0));
 	CK(hipEventCreate(&e1));
-	CK(hipExtStreamCreateWithCUMask(&ms, (uint32_t) words, m.data()));
+	if(use_mask) CK(hipExtStreamCreateWithCUMask(&ms, (uint32_t) words, m.data()));
+	else CK(hipStreamCreateWithFlags(&ms, hipStreamNonBlocking));
 	CK(hipStreamSynchronize(b));
 	CK(hipStreamDestroy(b));
 	CK(hipEventRecord(e0, ms));
@@ -207,18 +213,22 @@ static int run_engine_seq(int words, int pool) {
 	CK(hipStreamSynchronize(ms));
 	CK(hipEventDestroy(e0));
 	CK(hipEventDestroy(e1));
-	CK(hipStreamDestroy(ms));
-	printf("engine-seq words=%d: 3000 kernels on the masked stream, stream destroyed\n", words);
+	if(destroy) CK(hipStreamDestroy(ms));
+	printf("engine-seq words=%d mask=%d destroy=%d prio=%d: 3000 kernels on the stream%s\n", words, use_mask, destroy,
+	       prio, destroy ? ", stream destroyed" : ", stream kept");
 	fflush(stdout);
 	int lo = 0, hi = 0;
 	CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
 	std::vector<hipStream_t> ps;
 	for(int k = 0; k < pool; ++k) {
 		hipStream_t s;
-		CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, k % 2 ? hi : lo));
+		CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio && k % 2 ? hi : lo));
 		ps.push_back(s);
 		k_touch<<<n / 256, 256, 0, s>>>(d, n);
 		CK(hipGetLastError());
+		CK(hipStreamSynchronize(s));
+		printf("  stream %d (priority %d): kernel done\n", k, prio && k % 2 ? hi : lo);
+		fflush(stdout);
 	}
 	CK(hipDeviceSynchronize());
 	printf("engine-seq: %d priority streams created after it, a kernel on each ok\n", pool);
@@ -231,6 +241,12 @@ static int run_engine_seq(int words, int pool) {
 	int bad = 0;
 	for(int i = 0; i < n; ++i) bad += h[i] != 3000 + pool + 2;
 	printf("engine-seq: values %s\n", bad ? "WRONG" : "ok");
+	fflush(stdout);
+	if(teardown) {
+		printf("engine-seq: returning from main with the streams alive\n");
+		fflush(stdout);
+		return bad ? 1 : 0;
+	}
 	for(hipStream_t s : ps) CK(hipStreamDestroy(s));
 	CK(hipStreamDestroy(a));
 	CK(hipFree(d));
@@ -245,7 +261,9 @@ int main(int argc, char **argv) {
 	if(!strcmp(argv[1], "map") && argc >= 4) return run_map(argv[2], atoi(argv[3]), argc > 4 ? atoi(argv[4]) : 0);
 	if(!strcmp(argv[1], "destroy")) return run_destroy(argc > 2 ? atoi(argv[2]) : 8, false);
 	if(!strcmp(argv[1], "exit")) return run_destroy(argc > 2 ? atoi(argv[2]) : 8, true);
-	if(!strcmp(argv[1], "engine")) return run_engine_seq(argc > 2 ? atoi(argv[2]) : 2, argc > 3 ? atoi(argv[3]) : 64);
+	if(!strcmp(argv[1], "engine"))
+		return run_engine_seq(argc > 2 ? atoi(argv[2]) : 2, argc > 3 ? atoi(argv[3]) : 64, argc > 4 ? atoi(argv[4]) : 1,
+		                      argc > 5 ? atoi(argv[5]) : 1, argc > 6 ? atoi(argv[6]) : 1, argc > 7 ? atoi(argv[7]) : 0);
 	fprintf(stderr, "unknown mode\n");
 	return 2;
 }
