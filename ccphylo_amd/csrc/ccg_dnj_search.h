@@ -74,6 +74,10 @@ struct DnjGrid {
 	// the block lower bounds (TreeBufs::lbm, lb_unit): kept by the join and the requeue from the first join
 	// of a matrix larger than lb_min_n on (CCG_SCAN_LB=0: off; CCG_LB_MIN_N), used by the compacted wave scan
 	int lb = 1, lb_min_n = 16384;
+	// with the bounds, the row-group scan modes (20-23: float / u16 / u8 rows) rescan bounded row groups
+	// (k_dnj_scan_gc<LB>, lb_unit_g: one column-sum load per lane for the group's rows needing a block)
+	// instead of one bounded row per wave (CCG_LB_GROUPS=0: the single-row form)
+	int lb_groups = 1;
 	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
 	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {
@@ -103,6 +107,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_TEST_WITHHOLD")) test_withhold = atoi(e) & 3;
 		if(const char *e = getenv("CCG_SCAN_LB")) lb = atoi(e);
 		if(const char *e = getenv("CCG_LB_MIN_N")) lb_min_n = atoi(e);
+		if(const char *e = getenv("CCG_LB_GROUPS")) lb_groups = atoi(e);
 	}
 	// k_dnj_plan's last argument: the Q-load delay (low 14 bits), bits 14-15 the
 	// test knob test_withhold, bit 16 turns
@@ -1758,6 +1763,101 @@ __device__ __forceinline__ int lb_unit(const typename Elem<ET>::T *__restrict__ 
 	return (c1 - c0) - loaded;
 }
 
+// lb_unit over a row group: the same column range [c0, c1_k)
+// of G rows, each row's 64-column blocks tested against its own threshold
+// exactly as lb_unit does, and the union of the rows' needed blocks walked BB
+// at a time: one 8-byte column-sum load per lane serves every row of the
+// group that needs the block, and a row loads its cells only in the blocks it
+// needs itself.  So each row's fresh minimum (and the cells it counts as
+// loaded) equals lb_unit's for that row, while the column sums cost 8 / (rows
+// needing the block) bytes per cell instead of 8.  Returns the cells skipped
+// over the group's active rows.
+template <int ET, int G>
+__device__ __forceinline__ long long lb_unit_g(const typename Elem<ET>::T *const (&row)[G], double bs, const TreeBufs &b,
+                                               int n, const int (&r)[G], const bool (&act)[G], int c0,
+                                               const int (&c1)[G], int cmax, const double (&sDr)[G], double (&q)[G],
+                                               int (&idx)[G]) {
+	typedef typename Elem<ET>::T T;
+	constexpr int BB = ET == 8 ? LB_BB_D : LB_BB_N;
+	const int lane = threadIdx.x & 63;
+	const int bl0 = c0 / LBW, nbkm = (cmax - c0 + LBW - 1) / LBW;   // <= seg / 64 <= 256 blocks
+	double msb[4];
+#pragma unroll
+	for(int h = 0; h < 4; ++h) {
+		const int t = lane + 64 * h;
+		msb[h] = t < nbkm ? b.msd[bl0 + t] : 0.0;
+	}
+	unsigned long long need[G][4], any[4] = {0, 0, 0, 0};
+#pragma unroll
+	for(int k = 0; k < G; ++k) {
+		const int nbk = act[k] ? (c1[k] - c0 + LBW - 1) / LBW : 0;
+		const double ub = act[k] ? b.ubq[r[k]] : 0.0;
+		const unsigned *line = lb_line(b, act[k] ? r[k] : 1);
+#pragma unroll
+		for(int h = 0; h < 4; ++h) {
+			const int t = lane + 64 * h;
+			const unsigned lbv = t < nbk ? line[bl0 + t] : 0u;
+			const double lb = qcrit(n, n, (double) __uint_as_float(lbv), sDr[k], msb[h]);
+			need[k][h] = __ballot(t < nbk && !(lb > ub));
+			any[h] |= need[k][h];
+		}
+	}
+	long long loaded = 0;
+	int h = 0;
+	while(true) {
+		int blk[BB], nb = 0;
+		while(nb < BB && h < 4) {
+			if(!any[h]) {
+				++h;
+				continue;
+			}
+			const int bit = __ffsll((long long) any[h]) - 1;
+			any[h] &= any[h] - 1;
+			blk[nb++] = 64 * h + bit;   // relative to bl0
+		}
+		if(!nb) break;
+		double sk[BB];
+		T v[G][BB];
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const int t = m < nb ? blk[m] : blk[0];
+			int c = (bl0 + t) * LBW + lane;
+			sk[m] = b.sD[c < cmax ? c : cmax - 1];
+#pragma unroll
+			for(int k = 0; k < G; ++k) {
+				v[k][m] = 0;
+				if((need[k][t >> 6] >> (t & 63)) & 1)   // (uniform) row k needs this block
+					v[k][m] = row[k][c < c1[k] ? c : c1[k] - 1];
+			}
+		}
+#pragma unroll
+		for(int m = 0; m < BB; ++m) {
+			const int t = m < nb ? blk[m] : blk[0];
+			const int c = (bl0 + t) * LBW + lane;
+#pragma unroll
+			for(int k = 0; k < G; ++k) {
+				if(m >= nb || !((need[k][t >> 6] >> (t & 63)) & 1)) continue;   // uniform
+				const double d = Elem<ET>::get(v[k][m], bs);
+				const double x = qcrit(n, n, d, sDr[k], sk[m]);
+				if(c < c1[k] && 0 <= d && qarg_better(x, c, q[k], idx[k])) {
+					q[k] = x;
+					idx[k] = c;
+				}
+			}
+		}
+		for(int m = 0; m < nb; ++m) {
+			const int c = (bl0 + blk[m]) * LBW;
+#pragma unroll
+			for(int k = 0; k < G; ++k)
+				if((need[k][blk[m] >> 6] >> (blk[m] & 63)) & 1) loaded += c + LBW < c1[k] ? LBW : c1[k] - c;
+		}
+	}
+	long long span = 0;
+#pragma unroll
+	for(int k = 0; k < G; ++k) span += act[k] ? c1[k] - c0 : 0;
+	return span - loaded;
+}
+
 template <int ET, class Rows, class Tail = NoTail, int MODE = 0, int PRUNE = 0, bool CMP = false, bool LB = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_v(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                    int n, Rows rows, int seg, Tail tail = Tail()) {
@@ -2360,10 +2460,13 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_g(const typename Elem<ET>::T *_
 // (k_dnj_scan_g's body: one sD load serves G rows); each row's (q, j) goes
 // to its unit partial, which k_dnj_fold folds (pruned entries and S's, which
 // k_dnj_sphase / the plan's helpers settled, have no units here).
-template <int ET, int G, int UC, bool PRUNE2>
+// LB: each group's unit under the block lower bounds (lb_unit_g; the single
+// engine with TreeBufs::lbm, no pruning)
+template <int ET, int G, int UC, bool PRUNE2, bool LB = false>
 __global__ __launch_bounds__(TB) void k_dnj_scan_gc(const typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b,
                                                     int n, int seg) {
 	typedef typename Elem<ET>::T T;
+	static_assert(!(LB && PRUNE2), "the bounded row groups run without S-bound pruning");
 	const TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int done = ctl->done, Tn = ctl->T;
@@ -2385,6 +2488,7 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_gc(const typename Elem<ET>::T *
 	const int NG = (Es + G - 1) / G;   // slot `lane`'s groups
 	int R;
 	const int PG = wave_excl_scan(NG, &R);
+	long long lbskip = 0;
 	for(int v = gw; v < R; v += nw) {
 		const int k = 63 - __clzll((long long) __ballot(NG > 0 && PG <= v));   // the slot (uniform)
 		const int grp = v - __shfl(PG, k), EsK = __shfl(Es, k);
@@ -2422,7 +2526,8 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_gc(const typename Elem<ET>::T *
 			q[t] = DBL_MAX;
 			idx[t] = 0;
 		}
-		for(int base = c0; base < cmax; base += 64 * UC) {
+		if(LB) lbskip += lb_unit_g<ET, G>(row, bs, b, n, r, act, c0, c1, cmax, sDr, q, idx);
+		for(int base = c0; !LB && base < cmax; base += 64 * UC) {
 			double sk[UC];
 			T vv[G][UC];
 #pragma unroll
@@ -2457,6 +2562,9 @@ __global__ __launch_bounds__(TB) void k_dnj_scan_gc(const typename Elem<ET>::T *
 			}
 		}
 	}
+	if(LB && lbskip && lane == 0)   // this wave's slot (no contention), as k_dnj_scan_v
+		atomicAdd((unsigned long long *) (b.lbskip + (long long) ((blockIdx.x * (TB / 64) + (tid >> 6)) % LB_SCAN) * LB_SLOT),
+		          (unsigned long long) lbskip);
 }
 
 // ------------------------------------------------------------------ DNJ fold

@@ -1867,7 +1867,12 @@ static int enqueue_iteration(hipStream_t st, typename Elem<ET>::T *D, double bs,
 		const int prune = dnj_prune(n, ET, GEN);
 		if(prune == 2 && g_grid.plan_help) k_dnj_sphase<ET, false><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
 		else if(prune == 2) k_dnj_sphase<ET><<<g_grid.sphase_blocks(), TB, 0, st>>>(D, bs, b, n, seg);
-		if(b.lbm && !GEN && sm >= 4 && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
+		if(b.lbm && !GEN && sm >= 20 && sm <= 23 && g_grid.lb_groups && g_grid.scan_cmp && !tfold && prune == 0 &&
+		   dnj_umax(n, seg) < UHIST) {
+			// bounded row groups (float / u16 / u8 rows): 4 rows per wave share each column-sum load
+			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
+			k_dnj_scan_gc<ET, 4, 8, false, true><<<gcc, TB, 0, st>>>(D, bs, b, n, seg);
+		} else if(b.lbm && !GEN && sm >= 4 && g_grid.scan_cmp && !tfold && prune != 1 && dnj_umax(n, seg) < UHIST) {
 			// the compacted wave scan under the block lower bounds (every element type)
 			const unsigned gcc = gc < (unsigned) g_grid.cmp_blocks ? gc : (unsigned) g_grid.cmp_blocks;
 			if(prune == 2) k_dnj_scan_v<ET, DenseRows, NoTail, 0, 2, true, true><<<gcc, TB, 0, st>>>(D, bs, b, n, DenseRows(), seg);

@@ -770,14 +770,19 @@ def test_dnj_block_bounds(dev, monkeypatch, kind, n, et, mode):
     for prune in ("2", "0"):
         monkeypatch.setenv("CCG_SCAN_PRUNE", prune)
         cells = {}
-        for lb in ("1", "0"):
-            monkeypatch.setenv("CCG_SCAN_LB", lb)
+        # row-group modes unpruned: the bounded row groups (lb_unit_g, "1g") and one bounded row per wave ("1")
+        forms = ("1g", "1", "0") if int(mode) >= 20 and prune == "0" else ("1", "0")
+        for lb in forms:
+            monkeypatch.setenv("CCG_SCAN_LB", lb[0])
+            monkeypatch.setenv("CCG_LB_GROUPS", "1" if lb == "1g" else "0")
             got, fn, fd, st = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True, profile=True)
             assert (fn, fd) == (rfn, rfd), (prune, lb)
             assert len(got) == len(ref) and (got == ref).all(), (prune, lb)
             assert (st[10 + 2 * K], st[11 + 2 * K]) == (int(rst[0]), int(rst[1])), (prune, lb)
             cells[lb] = st[1]
         assert cells["1"] < cells["0"], (prune, cells)
+        if "1g" in cells:   # each row loads exactly the blocks lb_unit loads for it
+            assert cells["1g"] == cells["1"], cells
 
 
 @pytest.mark.parametrize("allpre", ["1", "0"])
