@@ -2,6 +2,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
+#include <mutex>
+#include <vector>
 #include "ccg_internal.h"
 
 int ccg_snp_dev_impl(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *inc_out, bool host_in);
@@ -98,6 +100,11 @@ int ccg_init(int device, ccg_ctx **out) {
 	return CCG_OK;
 }
 
+// every CU-masked stream the process made (never destroyed before ccg_shutdown)
+static std::mutex g_masked_mu;
+static std::vector<hipStream_t> g_masked;
+static bool g_shut = false;   // ccg_shutdown ran: a masked context's stream is gone
+
 int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int flags) {
 	if(!c || mask_words < 0 || (mask_words && !cu_mask)) return CCG_EINVAL;
 	CCG_CHECK(hipSetDevice(c->device));
@@ -134,6 +141,10 @@ int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int f
 		// destroyed the same way, or the masked one kept, run clean:
 		// profiles/r06_cu_mask_destroy.txt).  It is released with the process.
 		if(!c->masked) CCG_CHECK(hipStreamDestroy(c->stream));
+		if(mask_words) {   // parked for ccg_shutdown
+			std::lock_guard<std::mutex> g(g_masked_mu);
+			g_masked.push_back(s);
+		}
 		c->stream = s;
 		c->masked = mask_words != 0;
 	}
@@ -144,13 +155,24 @@ int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int f
 void ccg_destroy(ccg_ctx *c) {
 	if(!c) return;
 	hipSetDevice(c->device);
-	hipStreamSynchronize(c->stream);
+	if(!(c->masked && g_shut)) hipStreamSynchronize(c->stream);
 	for(int k = 0; k < 2; ++k)
 		if(c->ws[k]) hipFree(c->ws[k]);
 	hipEventDestroy(c->ev0);
 	hipEventDestroy(c->ev1);
 	if(!c->masked) hipStreamDestroy(c->stream);   // (a CU-masked one stays: ccg_ctx_configure)
 	free(c);
+}
+
+int ccg_shutdown(void) {
+	std::lock_guard<std::mutex> g(g_masked_mu);
+	int rc = CCG_OK;
+	for(hipStream_t s : g_masked) {
+		if(hipStreamSynchronize(s) != hipSuccess || hipStreamDestroy(s) != hipSuccess) rc = CCG_EHIP;
+	}
+	g_masked.clear();
+	g_shut = true;
+	return rc;
 }
 
 int ccg_device_info(ccg_ctx *c, char *buf, size_t len) {

@@ -74,10 +74,13 @@ struct DnjGrid {
 	// the block lower bounds (TreeBufs::lbm, lb_unit): kept by the join and the requeue from the first join
 	// of a matrix larger than lb_min_n on (CCG_SCAN_LB=0: off; CCG_LB_MIN_N), used by the compacted wave scan
 	int lb = 1, lb_min_n = 16384;
-	// with the bounds, the row-group scan modes (20-23: float / u16 / u8 rows) rescan bounded row groups
-	// (k_dnj_scan_gc<LB>, lb_unit_g: one column-sum load per lane for the group's rows needing a block)
-	// instead of one bounded row per wave (CCG_LB_GROUPS=0: the single-row form)
-	int lb_groups = 1;
+	// with the bounds, the row-group scan modes (20-23: float / u16 / u8 rows) may rescan bounded row groups
+	// (CCG_LB_GROUPS=1: k_dnj_scan_gc<LB>, lb_unit_g: one column-sum load per lane for the group's rows
+	// needing a block) instead of one bounded row per wave.  Measured (round 6, configs[3] on round 4's
+	// cdist matrix, first 40k joins, the same cells): scan 40.9 s against 17.2 s for one row per wave --
+	// the bounded scan is latency-bound, and the group form has a quarter of the units at 131 VGPRs
+	// (3 waves/SIMD) against 68 (7): off by default
+	int lb_groups = 0;
 	int scan_vblk = 1;  // with pruning: also the bound from every row above (the requeue's per-block
 	                    // minima of V_k = max(q at the partner cell, Q_k)) (CCG_SCAN_VBLK=0: off)
 	void load() {

@@ -115,6 +115,7 @@ ENGINE_SYMBOLS = [
     "ccg_rccl_unique_id", "ccg_rccl_open", "ccg_rccl_close", "ccg_rccl_abort", "ccg_tree_shard", "ccg_tree_shard_dev",
     "ccg_kma_ltd", "ccg_kma_ltd_dev", "ccg_snp_ltd_shard_dev", "ccg_snp_ltd_shard", "ccg_selftest_row_sum",
     "ccg_round_decimal_dev", "ccg_last_dist_ms", "ccg_tree_dev_state", "ccg_tree_shard_bytes", "ccg_ctx_configure",
+    "ccg_shutdown",
 ]
 # every symbol of include/ccphylo_host.h
 HOST_SYMBOLS = [
@@ -302,6 +303,8 @@ class Device:
                 words[cu // 32] |= 1 << (cu % 32)
         self._check(self.lib.ccg_ctx_configure(self.h, words, nw, CCG_CTX_NOSYNC if nosync else 0),
                     "ccg_ctx_configure")
+        if nw:
+            _register_shutdown(self.lib)
 
     def __enter__(self):
         return self
@@ -668,6 +671,18 @@ class RcclColl:
     def close(self):
         if self.c.user:
             self.lib.ccg_rccl_close(C.byref(self.c))
+
+
+_SHUTDOWN = []
+
+
+def _register_shutdown(lib):
+    """At interpreter exit (after the last GPU work), release the CU-masked
+    streams the engine keeps (ccg_shutdown)."""
+    if not _SHUTDOWN:
+        import atexit
+        _SHUTDOWN.append(lib)
+        atexit.register(lambda: lib.ccg_shutdown())
 
 
 # ---------------------------------------------------------------- host API

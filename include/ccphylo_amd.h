@@ -62,6 +62,13 @@ int ccg_init(int device, ccg_ctx **ctx);
  * wait for the other context's work). */
 #define CCG_CTX_NOSYNC 1
 int ccg_ctx_configure(ccg_ctx *ctx, const uint32_t *cu_mask, int mask_words, int flags);
+/* Process end, after the last HIP work of the process: destroys the CU-masked
+ * streams ccg_ctx_configure kept (no HIP stream may be created afterwards;
+ * contexts configured with a mask are unusable).  Optional: without it they
+ * go with the process (ccphylo_amd's Python layer calls it at exit; under
+ * rocprofv3 a Python + torch process that still held masked streams at
+ * teardown segfaulted in __cxa_finalize, profiles/r06_exit_rocprof.txt). */
+int ccg_shutdown(void);
 /* HIP devices visible to this process (the multi-GPU CLI deals ranks over them) */
 int ccg_device_count(int *count);
 void ccg_destroy(ccg_ctx *ctx);
