@@ -477,3 +477,24 @@ def test_config4_rank_1e6(dev, msa_1e6, rank):
         assert free2 > 1e9
     finally:
         dev.free(Dloc)
+
+
+@pytest.mark.skipif(not os.environ.get("CCG_HEADLINE_PIN"),
+                    reason="opt-in: CCG_HEADLINE_PIN=1 (about 6 minutes with 16 host cores; run with -s)")
+def test_config2_headline_whole_tree_vs_oracle(tmp_path):
+    """The bench's own configs[2] matrix (50k x 5 Mbp, seed 3, GPU dist), 64
+    LT cells against orc_fsacmp, then the engine's whole exact DNJ tree
+    against the oracle's serial-decision DNJ on the same LT (host threads):
+    every join, both branch lengths, the final pair (tools/parity_headline.py;
+    profiles/r06_parity_headline.jsonl).  Reference: dnj.c:43-128, :985-1052."""
+    import json
+    import subprocess
+    import sys
+    out = tmp_path / "pin.jsonl"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "tools", "parity_headline.py"), "--start", "0",
+                        "--budget", "1e9", "--threads", str(THREADS), "--out", str(out)], cwd=root, timeout=1500)
+    assert p.returncode == 0
+    rec = json.loads(out.read_text().splitlines()[-1])
+    assert rec["cells_identical"] and rec["joins_identical"] and rec["final_identical"], rec
+    assert rec["joins_compared"] == 49_998
