@@ -906,8 +906,12 @@ static int tree_shard_dnj_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_
 			// one-phase search (k_dnj_plan): each rank lists the S rows and the
 			// rows below S it owns, under the bound of its own S rows' partner
 			// cells (a subset of S: looser, still exact after the replay)
-			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
-			else k_dnj_plan<ET, false, Shard, false><<<1, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
+			// the listing over a grid of blocks with the decoupled look-back past 15361 taxa, as on one GPU:
+			// every rank walks all n rows for its owned ones (round 6: one block took 140 us per join at
+			// 200k, tools/shard_cost.py)
+			const unsigned gpl = grid.plan_blocks(n);
+			if(grid.bands(n)) k_dnj_plan<ET, false, Shard, true><<<gpl, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), grid.bands(n), grid.plan_flags());
+			else k_dnj_plan<ET, false, Shard, false><<<gpl, TBF, 0, st>>>(D, bs, b, n, n == n0, sh, seg, grid.top(n), 0, grid.plan_flags());
 			kt.mark(CCG_K_FIND);
 			if(b.lbm && grid.scan_mode(n, ET) == 9) k_dnj_scan_v<ET, Shard, RecTail<ET>, 5, 0, false, true><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});
 			else if(b.lbm && grid.scan_mode(n, ET) >= 4) k_dnj_scan_v<ET, Shard, RecTail<ET>, 0, 0, false, true><<<gc, TB, 0, st>>>(D, bs, b, n, sh, seg, RecTail<ET>{D, sh, Sl, pcnt});

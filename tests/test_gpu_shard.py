@@ -433,3 +433,25 @@ def test_shard_device_transport_world1(dev, method, native_allgather):
     assert (got[1], got[2]) == (want[1], want[2])
     assert len(got[0]) == len(want[0]) and (got[0] == want[0]).all()
     assert coll.calls["allgather" if native_allgather else "allreduce"] > 0
+
+
+@pytest.mark.parametrize("world,n,kind,et", [(1, 3000, "euc", 8), (3, 2600, "clade", 4), (8, 2200, "snp", 8)])
+def test_shard_multiblock_plan(dev, monkeypatch, tmp_path, world, n, kind, et):
+    """The sharded DNJ's k_dnj_plan over a grid of listing blocks with the
+    decoupled look-back (the single engine's form past 15361 taxa; round 6):
+    CCG_PLAN_FR=1 gives one block per 960 rows at these sizes, with and
+    without the band search; the joins equal the single engine's."""
+    monkeypatch.setenv("CCG_PLAN_FR", "1")
+    D, bs = _typed(_data(kind, n), et)
+    ref = dev.tree(D, n, etype=et, byte_scale=bs, method=1, exact=True)[:3]
+    monkeypatch.setenv("CCG_SHARD_FORCE", "1")   # world 1: the sharded kernels, not the single engine
+    for split in ("16384", "100"):   # plain top-S listing, then band mode
+        monkeypatch.setenv("CCG_S_SPLIT_N", split)
+        if world == 1:
+            _same(dev.tree_shard(D, n, None, etype=et, byte_scale=bs, method=1, exact=True)[:3], ref)
+            continue
+        mp.start_processes(_rank_main, args=(world, _free_port(), n, kind, et, True, "gloo", 1, str(tmp_path)),
+                           nprocs=world, join=True, start_method="spawn")
+        for r in range(world):
+            fn, fd = np.load(tmp_path / f"f{r}.npy")
+            _same((np.load(tmp_path / f"j{r}.npy"), int(fn), fd), ref)
