@@ -648,8 +648,10 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
 def tree_cu_set(ncu, k, layout):
     """The tree context's compute units.  Mask bit c runs on XCD c % 8 (slot
     c // 8 there; tools/micro/cu_mask.hip, profiles/r06_cu_mask_map.txt), so
-    "low" (bits 0 .. k-1) already gives every XCD k / 8 CUs; "xcd" takes
-    bits 0 .. k/8 - 1 of each 32-bit word, another k / 8 CUs per XCD."""
+    "low" (bits 0 .. k-1) gives every XCD k / 8 CUs.  "xcd" (round 5: bits
+    0 .. k/8 - 1 of each 32-bit word) puts them on XCDs 0 .. k/8 - 1 only:
+    below k = 64 it leaves XCDs empty, which would run unmasked, and
+    ccg_ctx_configure refuses it; at 64 it equals "low"."""
     if layout == "xcd":
         per = max(1, k // 8)
         return [g * (ncu // 8) + i for g in range(8) for i in range(per)]
@@ -1324,8 +1326,9 @@ def main():
                          "the next matrix's dist on the rest (64: tools/overlap.py, 50k x 5 Mbp per matrix 7.59 s "
                          "against 7.71-7.90 s at 32-56 CUs); 0: dist then tree on the whole chip, step by step")
     ap.add_argument("--tree-layout", choices=["low", "xcd"], default="low",
-                    help="which CUs the pipelined tree takes: mask bits 0 .. --tree-cus - 1, or the first "
-                         "--tree-cus / 8 bits of each 32-bit mask word (both --tree-cus / 8 CUs per XCD)")
+                    help="which CUs the pipelined tree takes: mask bits 0 .. --tree-cus - 1 (--tree-cus / 8 CUs "
+                         "per XCD), or the first --tree-cus / 8 bits of each 32-bit mask word (round 5's form: "
+                         "XCDs 0 .. --tree-cus/8 - 1 only; refused below 64)")
     ap.add_argument("--headline-seed", type=int, default=3,
                     help="the alignment's seed in the sequential forms (the pipelined one alternates 3 and 4)")
     args = ap.parse_args()

@@ -90,6 +90,7 @@ int ccg_init(int device, ccg_ctx **out) {
 	ccg_ctx *c = (ccg_ctx *) calloc(1, sizeof(ccg_ctx));
 	if(!c) return CCG_ENOMEM;
 	c->device = device;
+	c->ncu = prop.multiProcessorCount;
 	snprintf(c->name, sizeof(c->name), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
 	if(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
 	   hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -147,6 +148,8 @@ int ccg_ctx_configure(ccg_ctx *c, const uint32_t *cu_mask, int mask_words, int f
 		}
 		c->stream = s;
 		c->masked = mask_words != 0;
+		c->cus = 0;
+		for(int k = 0; mask_words && k < c->ncu && k < 32 * mask_words; ++k) c->cus += (cu_mask[k / 32] >> (k % 32)) & 1u;
 	}
 	c->flags = flags;
 	return CCG_OK;

@@ -34,6 +34,7 @@ struct ccg_ctx {
 	float dist_ms;   // the last dist call's pair kernels (HIP events on the engine stream)
 	int flags;       // CCG_CTX_* (ccg_ctx_configure)
 	int masked;      // the stream was created with a CU mask (ccg_ctx_configure)
+	int ncu, cus;    // the device's CUs; the CUs the stream may use (0: all)
 	// the tree's device workspaces, kept across runs (grown on demand, freed
 	// by ccg_destroy): a tree run then makes no hipFree, which waits for every
 	// stream of the device, so a CCG_CTX_NOSYNC context never waits for another

@@ -2020,6 +2020,14 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 	g_grid = DnjGrid();
 	g_grid.load();
 	g_progress = getenv("CCG_PROGRESS") != nullptr;
+	// the compacted scans deal their units over a grid meant to be resident at
+	// once (cmp_blocks per 256 CUs): a CU-masked context sizes it to its CUs
+	const bool cmp_env = getenv("CCG_SCAN_CMPB") != nullptr;
+	auto cmp_share = [&](int blocks) {
+		return ctx->cus > 0 && ctx->cus < ctx->ncu ? (blocks * ctx->cus / ctx->ncu > 64 ? blocks * ctx->cus / ctx->ncu : 64)
+		                                           : blocks;
+	};
+	if(!cmp_env) g_grid.cmp_blocks = cmp_share(g_grid.cmp_blocks);
 	int rc = tree_alloc_ctx(ctx, &w, n0);
 	if(rc) return rc;
 	TreeBufs b = w.b;
@@ -2087,7 +2095,7 @@ static int tree_run_t(ccg_ctx *ctx, const ccg_tree_args *a, void *Dd, ccg_join *
 			// without, 4.78 s with the plan's helpers and the compaction); CCG_SCAN_PRUNE still forces it
 			if(!getenv("CCG_SCAN_PRUNE")) g_grid.scan_prune = 0;
 			// the bounded units are short: twice the waves (headline tree 4.84 -> 4.74 s, profiled)
-			if(!getenv("CCG_SCAN_CMPB")) g_grid.cmp_blocks = 2048;
+			if(!cmp_env) g_grid.cmp_blocks = cmp_share(2048);
 		} else {
 			(void) hipGetLastError();   // no room: the run goes without (the same joins)
 			lbmem = NULL;
