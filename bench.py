@@ -87,8 +87,8 @@ def _latest(*names):
     return os.path.join(ROOT, "profiles", names[-1])
 
 
-PMC_SUMMARY = _latest("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc.json")
-PMC_HEADLINE = _latest("r05_pmc_headline.json", "r04_pmc_headline.json", "r03_pmc_headline.json")
+PMC_SUMMARY = _latest("r06_pmc.json", "r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc.json")
+PMC_HEADLINE = _latest("r06_pmc_headline.json", "r05_pmc_headline.json", "r04_pmc_headline.json", "r03_pmc_headline.json")
 SHARD_LEG_TIMEOUT_S = 600
 HEADLINE_TIMEOUT_S = 1200
 
@@ -188,7 +188,7 @@ def pmc_traffic(kernel):
         return None, None
 
 
-KERNEL_STATS = _latest("r05_kernel_stats.csv", "r04_kernel_stats.csv", "r03_kernel_stats.csv", "r02_kernel_stats.csv")
+KERNEL_STATS = _latest("r06_kernel_stats.csv", "r05_kernel_stats.csv", "r04_kernel_stats.csv", "r03_kernel_stats.csv", "r02_kernel_stats.csv")
 KSYM = {"dnj_select": "k_dnj_select", "dnj_scan": "k_dnj_scan", "dnj_find": "k_dnj_plan", "update": "k_dnj_join",
         "dnj_requeue": "k_dnj_requeue", "nj_argmin": "k_nj_argmin", "nj_pop": "k_nj_pop", "exact_sum": "k_exact_sum"}
 
@@ -1104,7 +1104,7 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
     return out
 
 
-HEADLINE_STATS = _latest("r05_kernel_stats_headline.csv", "r04_kernel_stats_headline.csv", "r03_kernel_stats_headline.csv")
+HEADLINE_STATS = _latest("r06_kernel_stats_headline.csv", "r05_kernel_stats_headline.csv", "r04_kernel_stats_headline.csv", "r03_kernel_stats_headline.csv")
 HSYM = {"dist": ("k_snp_mfma2",), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan", "k_dnj_scan_g"),
         "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join_pf", "k_dnj_join"), "dnj_requeue": ("k_dnj_requeue",),
         "exact_sum": ("k_exact_sum",), "dnj_select": ("k_dnj_select",), "init": ("k_init_rows",)}
