@@ -400,7 +400,7 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
             "kernel": (("k_snp_mfma_pair" if mode_env == "1" else "k_snp_mfma2_pair") if pair
-                       else ("k_snp_mfma" if mode_env == "1" else "k_snp_mfma2")) if mfma
+                       else dist_kernel_name()) if mfma
             else ("k_snp_tile_pair" if pair else "k_snp_tile"),
             "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
             else valu_roofline(ops, dt, opw)}
@@ -1105,7 +1105,21 @@ def reference_tree_parity(D, n, exact_joins, fast_joins, td):
 
 
 HEADLINE_STATS = _latest("r06_kernel_stats_headline.csv", "r05_kernel_stats_headline.csv", "r04_kernel_stats_headline.csv", "r03_kernel_stats_headline.csv")
-HSYM = {"dist": ("k_snp_mfma2",), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan", "k_dnj_scan_g"),
+def dist_kernel_name():
+    """The non-pair dist kernel the engine launches (snp.hip: k_snp_mfma3, the
+    LDS-DMA staged form, unless CCG_DIST_GLDS=0 or CCG_DIST_KC=16; CCG_DIST_MFMA
+    1 / 0: the 128x128 MFMA / VALU tiles)."""
+    mode = os.environ.get("CCG_DIST_MFMA", "2")
+    if mode == "0":
+        return "k_snp_tile"
+    if mode == "1":
+        return "k_snp_mfma"
+    if os.environ.get("CCG_DIST_GLDS") == "0" or os.environ.get("CCG_DIST_KC") == "16":
+        return "k_snp_mfma2"
+    return "k_snp_mfma3"
+
+
+HSYM = {"dist": (dist_kernel_name(),), "dnj_scan": ("k_dnj_scan_v", "k_dnj_scan_w", "k_dnj_scan", "k_dnj_scan_g"),
         "dnj_find": ("k_dnj_plan",), "update": ("k_dnj_join_pf", "k_dnj_join"), "dnj_requeue": ("k_dnj_requeue",),
         "exact_sum": ("k_exact_sum",), "dnj_select": ("k_dnj_select",), "init": ("k_init_rows",)}
 
@@ -1156,7 +1170,7 @@ def headline_roofline(n, L, positions, elems, dist_kernel_ms, dist_launches, pst
     kernels = {}
     fl = FLOPS_PER_POSITION_PAIR * elems * float(positions)
     tf = fl / (dist_kernel_ms / 1e3) / 1e12
-    d = {"kernel": "k_snp_mfma2", "bound": "mfma", "achieved": round(tf, 1),
+    d = {"kernel": dist_kernel_name(), "bound": "mfma", "achieved": round(tf, 1),
          "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4),
          "frac_of_measured_issue_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
          "step_ms": round(dist_kernel_ms, 2), "launches": dist_launches,
@@ -1422,7 +1436,7 @@ def main():
         dk = roof["kernels"]["dist"]
         dk["cus"] = pipe["dist_cus"]
         dk["frac_of_cu_share"] = round(dk["frac"] * (pipe["dist_cus"] + pipe["tree_cus"]) / pipe["dist_cus"], 4)
-        if roof.get("kernel") == "k_snp_mfma2":
+        if roof.get("kernel", "").startswith("k_snp_mfma"):
             roof["cus"], roof["frac_of_cu_share"] = dk["cus"], dk["frac_of_cu_share"]
     result = {
         "metric": "taxa-pairs/sec (dist) + NJ iterations/sec at N taxa, 1/2/4/8 MI355X",

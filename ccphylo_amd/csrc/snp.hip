@@ -15,16 +15,19 @@
 // Pair mode keeps each taxon's mask m beside its planes:
 //   d += popc(((hi_a ^ hi_b) | (lo_a ^ lo_b)) & m_a & m_b), n += popc(m_a & m_b).
 // Two kernel families compute it:
-//   - the default, k_snp_mfma2 (non-pair) / k_snp_mfma_pair: the count as an
+//   - the default, k_snp_mfma3 (non-pair) / k_snp_mfma_pair: the count as an
 //     exact MX-fp4 dot product on the matrix cores (each code a +-1
 //     tetrahedron vector, dist = (3 L - dot) / 4), 256x256 pair tiles,
-//     MFMA-bound;
+//     MFMA-bound; k_snp_mfma3 stages its chunks by LDS-DMA and interleaves
+//     the plane-to-fp4 spreads with the MFMAs, k_snp_mfma2 (CCG_DIST_GLDS=0)
+//     is the register-staged form it replaced;
 //   - k_snp_tile / k_snp_tile_pair (CCG_DIST_MFMA=0): the popcount form
 //     above, VALU-integer-bound, 128x128 pair tiles, 8x8 pairs per thread in
 //     registers.
 // Both stage KC-word chunks of the two row panels through LDS.
 #include <cstring>
 #include <vector>
+#include <type_traits>
 #include "ccg_internal.h"
 #include "ccg_shard_layout.h"
 
@@ -832,6 +835,248 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2(const uint2 *__restrict__ 
 			if(BAND) {
 				const long long lb = L / SB;
 				i = (lb * world + rank) * SB + (L - lb * SB);
+			}
+			if(i >= n || (!BAND && (i < rowBegin || i >= rowEnd))) continue;
+			const long long base = BAND ? sh.off(i) : tri(i);
+#pragma unroll
+			for(int tb = 0; tb < 4; ++tb) {
+				const long long j = (long long) J * TILE2 + 128 * wc + 32 * tb + l32;
+				if(j < i) {
+					const unsigned d = (unsigned) ((L3 - (int) acc[ta][tb][r]) >> 2);
+					if(SPLIT) {
+						atomicAdd(&cnt[base + j - cbase], d);
+					} else {
+						const double v = nFactor * (double) d;
+						D[base + j] = Elem<ET>::put(v, 0.5, bs);
+					}
+				}
+			}
+		}
+	}
+}
+
+// ------------------------------------------------------------------ MFMA, 256 x 256 tiles, LDS-DMA staged
+// k_snp_mfma3: k_snp_mfma2's tile, its MX-fp4 steps and its epilogue, with the
+// panels staged by global_load_lds (no VGPR staging, no ds_write) through
+// NST3 stages of LDS, so that NST3 - 2 chunks stay in flight across each
+// barrier (cdna_hip_programming.md, "Pipelining across barriers": counted
+// vmcnt, raw s_barrier).  At one block per CU and 512 VGPRs the round-4/5
+// kernel had one chunk of register staging in flight and waited for it
+// before every barrier.  LDS image, one array: [stage][panel][slice][row] of
+// 16 bytes (two plane words of one row), so one wave-instruction (64 lanes x
+// 16 B, lane-linear) writes 64 consecutive rows of one slice, and a step's
+// 8-byte reads (row ra0 + 32x, word 2s + h) are 512 contiguous bytes per
+// wave.  Wave w stages slice w of both panels: 4 + 4 instructions per chunk.
+#define NST3 4
+#define KC3 8
+template <int ET, bool SPLIT, bool BAND>
+__global__ __launch_bounds__(256, 1) void k_snp_mfma3(const uint2 *__restrict__ P, int Wp, int n, long long t0,
+                                                      long long items, int S, int Wk, double nFactor, double bs,
+                                                      typename Elem<ET>::T *__restrict__ D, long long rowBegin,
+                                                      long long rowEnd, unsigned *__restrict__ cnt, long long cbase,
+                                                      const long long *__restrict__ pfx, int npanels, int rank,
+                                                      int world, int sorder) {
+	constexpr int NSL = KC3 / 2;   // 16-byte slices per chunk (one per wave)
+	static_assert(NSL == 4, "one slice per wave");
+	__shared__ __attribute__((aligned(16))) uint4 L[NST3 * 2 * NSL * TILE2];   // 128 KB
+	const long long item = t0 + xcd_tile(blockIdx.x, items), t = SPLIT ? item / S : item;
+	int I, J;
+	if(BAND) {
+		int lo = 0, hi = npanels - 1;
+		while(lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
+		}
+		I = lo;
+		J = (int) (t - pfx[lo]);
+	} else if(sorder) {
+		tile_ij_super(t, (rowEnd - 1) / TILE2, I, J);
+	} else {
+		tile_ij(t, I, J);
+	}
+	const int wb = SPLIT ? (int) (item % S) * Wk : 0;
+	const int Wl = SPLIT ? (wb + Wk < Wp ? Wk : Wp - wb) : Wp;
+	const Shard sh{rank, world};
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	// this lane's staging sources: rows q 64 + lane of both panels, words 2 wid, 2 wid + 1 of each chunk
+	const uint2 *srcA[4], *srcB[4];
+#pragma unroll
+	for(int q = 0; q < 4; ++q) {
+		const long long Lr = (long long) I * TILE2 + q * 64 + lane;
+		long long r = Lr;
+		if(BAND) {
+			const long long lb = Lr / SB;
+			r = (lb * world + rank) * SB + (Lr - lb * SB);
+			r = r < n ? r : 0;   // rows past n stage row 0 and are never stored
+		}
+		srcA[q] = P + (size_t) r * Wp + wb + 2 * wid;
+		srcB[q] = P + ((size_t) J * TILE2 + q * 64 + lane) * Wp + wb + 2 * wid;
+	}
+	const int nch = Wl / KC3;
+	// one LDS-DMA wave-instruction (64 lanes x 16 B, lane-linear at the
+	// wave-uniform LDS byte address lds): in inline asm, so that the compiler
+	// does not drain vmcnt(0) before every ds_read of the array (it cannot
+	// tell the stages apart); the counted waits below order the reads
+	const unsigned lbase = (unsigned) (uintptr_t) (__attribute__((address_space(3))) uint4 *) L;
+	auto glds = [&](const uint2 *src, unsigned lds) {
+		unsigned keep;
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+		             : "=&s"(keep)
+		             : "v"(src), "s"(lds)
+		             : "memory");
+	};
+	auto issue = [&](int c) {   // chunk c into stage c % NST3
+		const int st = c % NST3, w0 = c * KC3;
+#pragma unroll
+		for(int q = 0; q < 4; ++q) {
+			glds(srcA[q] + w0, __builtin_amdgcn_readfirstlane(lbase + (unsigned) ((((st * 2 + 0) * NSL + wid) * TILE2 + q * 64) * 16)));
+			glds(srcB[q] + w0, __builtin_amdgcn_readfirstlane(lbase + (unsigned) ((((st * 2 + 1) * NSL + wid) * TILE2 + q * 64) * 16)));
+		}
+	};
+	const int wr = wid >> 1, wc = wid & 1;
+	const int h = lane >> 5, l32 = lane & 31;
+	const int ra0 = 128 * wr + l32, rb0 = 128 * wc + l32;
+	v16f_t acc[4][4];
+#pragma unroll
+	for(int ta = 0; ta < 4; ++ta)
+#pragma unroll
+		for(int tb = 0; tb < 4; ++tb)
+#pragma unroll
+			for(int r = 0; r < 16; ++r) acc[ta][tb][r] = 0.0f;
+	// chunk c landed for every wave: this wave's counted wait (the later chunks
+	// stay in flight), then the raw barrier
+	auto land = [&](int c) {
+		const int ahead = nch - 1 - c < NST3 - 2 ? nch - 1 - c : NST3 - 2;
+		if(ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+		else if(ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+		else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		asm volatile("" ::: "memory");
+		__builtin_amdgcn_s_barrier();
+		asm volatile("" ::: "memory");
+	};
+	// step gs (64 positions): word 2 (gs % 4) + h of chunk gs / 4, rows ra0 + 32 x / rb0 + 32 x
+	auto rd = [&](int gs, uint2 (&a)[4], uint2 (&b)[4]) {
+		const int st = (gs >> 2) % NST3, sl = gs & 3;
+		const uint2 *Ac = (const uint2 *) &L[((st * 2 + 0) * NSL + sl) * TILE2];
+		const uint2 *Bc = (const uint2 *) &L[((st * 2 + 1) * NSL + sl) * TILE2];
+#pragma unroll
+		for(int x = 0; x < 4; ++x) {
+			a[x] = Ac[(ra0 + 32 * x) * 2 + h];
+			b[x] = Bc[(rb0 + 32 * x) * 2 + h];
+		}
+	};
+#define MF3(TA, TB, F, G)                                                                                         \
+	acc[TA][TB] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F, G, acc[TA][TB], MFMA_FP4, MFMA_FP4, 0, MFMA_SCALE1, \
+	                                                              0, MFMA_SCALE1)
+	for(int c = 0; c < NST3 - 1 && c < nch; ++c) issue(c);
+	land(0);
+	if(NST3 - 1 < nch) issue(NST3 - 1);
+	uint2 a[4], b[4];
+	v8i_t f0[4], g0[4];
+	rd(0, a, b);
+#pragma unroll
+	for(int x = 0; x < 4; ++x) {
+		f0[x] = fp4_spread(a[x].x);
+		g0[x] = fp4_spread(b[x].x);
+	}
+	// Each component's 16 MFMAs carry the VALU work of the next component
+	// (one spread or xor per MFMA slot, pinned by sched_group_barrier), so the
+	// matrix pipe does not idle while a wave spreads (k_snp_mfma2: 16 MFMAs,
+	// then the spreads; ~60% MFMA busy, profiles/r06_dist_clock.json):
+	//   comp 0 (f0, g0) + the spreads of lo (f1, g1)
+	//   comp 1 (f1, g1) + the xors (x0, y0) and the next step's LDS reads
+	//   comp 2 (x0, y0) + the next step's spreads of hi (f0, g0)
+	// A chunk's last step waits for the next chunk (counted vmcnt + barrier)
+	// between comp 0 and comp 1, so its reads follow the barrier.
+	auto step = [&](auto SI, int gs, bool more, bool open) {   // SI: the step's place in its chunk (sync group ids)
+		constexpr int G0 = 3 * decltype(SI)::value;
+		v8i_t f1[4], g1[4], x0[4], y0[4];
+#pragma unroll
+		for(int k = 0; k < 16; ++k) {
+			MF3(k >> 2, k & 3, f0[k >> 2], g0[k & 3]);
+			if(k < 8) {
+				if(k & 1) g1[k >> 1] = fp4_spread(b[k >> 1].y);
+				else f1[k >> 1] = fp4_spread(a[k >> 1].y);
+			}
+		}
+		// one spread (3 shifts, 4 bitop3) per MFMA on the first 8 (measured: 4 VALU per slot on 14 slots was
+		// slower, 6.43 against 6.26 s at 50k x 5 Mbp)
+#pragma unroll
+		for(int k = 0; k < 8; ++k) {
+			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0);
+			__builtin_amdgcn_sched_group_barrier(0x002, 7, G0);
+		}
+		__builtin_amdgcn_sched_group_barrier(0x008, 8, G0);
+		if(open) {   // the next step opens chunk (gs + 1) / 4
+			const int cn = (gs + 1) >> 2;
+			land(cn);
+			if(cn + NST3 - 1 < nch) issue(cn + NST3 - 1);
+		}
+		uint2 an[4], bn[4];
+		if(more) rd(gs + 1, an, bn);
+#pragma unroll
+		for(int k = 0; k < 16; ++k) {
+			MF3(k >> 2, k & 3, f1[k >> 2], g1[k & 3]);
+			if(k < 8) {
+				if(k & 1) y0[k >> 1] = fp4_xor_spread(g0[k >> 1], g1[k >> 1]);
+				else x0[k >> 1] = fp4_xor_spread(f0[k >> 1], f1[k >> 1]);
+			}
+		}
+		if(more) __builtin_amdgcn_sched_group_barrier(0x100, 8, G0 + 1);   // the next step's 8 LDS reads first
+#pragma unroll
+		for(int k = 0; k < 8; ++k) {
+			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0 + 1);
+			__builtin_amdgcn_sched_group_barrier(0x002, 4, G0 + 1);   // one xor (4 bitop3)
+		}
+		__builtin_amdgcn_sched_group_barrier(0x008, 8, G0 + 1);
+#pragma unroll
+		for(int k = 0; k < 16; ++k) {
+			MF3(k >> 2, k & 3, x0[k >> 2], y0[k & 3]);
+			if(more && k < 8) {
+				if(k & 1) g0[k >> 1] = fp4_spread(bn[k >> 1].x);
+				else f0[k >> 1] = fp4_spread(an[k >> 1].x);
+			}
+		}
+		if(more) {
+#pragma unroll
+			for(int k = 0; k < 8; ++k) {
+				__builtin_amdgcn_sched_group_barrier(0x008, 1, G0 + 2);
+				__builtin_amdgcn_sched_group_barrier(0x002, 7, G0 + 2);
+			}
+			__builtin_amdgcn_sched_group_barrier(0x008, 8, G0 + 2);
+#pragma unroll
+			for(int x = 0; x < 4; ++x) {
+				a[x] = an[x];
+				b[x] = bn[x];
+			}
+		}
+	};
+	for(int c = 0; c + 1 < nch; ++c) {   // every chunk but the last: 4 steps, the last one opens chunk c + 1
+		step(std::integral_constant<int, 0>(), 4 * c + 0, true, false);
+		step(std::integral_constant<int, 1>(), 4 * c + 1, true, false);
+		step(std::integral_constant<int, 2>(), 4 * c + 2, true, false);
+		step(std::integral_constant<int, 3>(), 4 * c + 3, true, true);
+	}
+	{   // the last chunk
+		const int g = 4 * (nch - 1);
+		step(std::integral_constant<int, 0>(), g + 0, true, false);
+		step(std::integral_constant<int, 1>(), g + 1, true, false);
+		step(std::integral_constant<int, 2>(), g + 2, true, false);
+		step(std::integral_constant<int, 3>(), g + 3, false, false);
+	}
+#undef MF3
+	// epilogue: k_snp_mfma2's
+	const int L3 = 3 * 32 * Wl;
+#pragma unroll
+	for(int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+		for(int r = 0; r < 16; ++r) {
+			const int l = 128 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+			const long long Lr = (long long) I * TILE2 + l;
+			long long i = Lr;
+			if(BAND) {
+				const long long lb = Lr / SB;
+				i = (lb * world + rank) * SB + (Lr - lb * SB);
 			}
 			if(i >= n || (!BAND && (i < rowBegin || i >= rowEnd))) continue;
 			const long long base = BAND ? sh.off(i) : tri(i);
@@ -1672,6 +1917,9 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	// a super-row start only)
 	const char *kce = getenv("CCG_DIST_KC"), *ore = getenv("CCG_DIST_ORDER");
 	const int kc = !PAIR && kce && atoi(kce) == KC2L && Wp % KC2L == 0 ? KC2L : KC2;
+	// the LDS-DMA staged kernel (CCG_DIST_GLDS=0: k_snp_mfma2)
+	const char *gle = getenv("CCG_DIST_GLDS");
+	const bool glds = !PAIR && !(gle && atoi(gle) == 0) && kc == KC3;
 	const int sorder = !PAIR && world == 0 && ore && atoi(ore) == 1 && (rb / TILE2) % 4 == 0;
 	const int chunks = Wp / kc;
 	int S = 1;
@@ -1744,7 +1992,27 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 			    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1,       \
 			    sorder);                                                                                             \
 	}
-		if(kc == KC2L) {
+		if(glds) {   // k_snp_mfma3 (KC3-word chunks, LDS-DMA staged)
+			if(world > 0) {
+				if(S > 1)
+					k_snp_mfma3<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels,
+					    rank, world, 0);
+				else
+					k_snp_mfma3<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, 0, n, cnt, 0, d_pfx, npanels,
+					    rank, world, 0);
+			} else {
+				if(S > 1)
+					k_snp_mfma3<ET, true, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    pl, Wp, (int) n, t, items, S, Wk, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1,
+					    sorder);
+				else
+					k_snp_mfma3<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(
+					    pl, Wp, (int) n, t, items, 1, Wp, nFactor, a->byteScale, (T *) D, rb, re, cnt, f0, NULL, 0, 0, 1,
+					    sorder);
+			}
+		} else if(kc == KC2L) {
 			MF2_LAUNCH(KC2L)
 		} else {
 			MF2_LAUNCH(KC2)
@@ -1852,7 +2120,7 @@ static int snp_launch(ccg_ctx *ctx, const ccg_snp_args *a, const void *planes, i
 		}
 		return CCG_OK;
 	}
-	// MFMA forms (k_snp_mfma2 the default, k_snp_mfma with CCG_DIST_MFMA=1,
+	// MFMA forms (k_snp_mfma3 / k_snp_mfma2 the default, k_snp_mfma with CCG_DIST_MFMA=1,
 	// the VALU tiles with 0): f32-exact while a slice holds < MFMA_KMAX words
 	if(dist_kernel_choice() == 2) return snp_launch_mfma2<ET>(ctx, a, planes, Wp, nFactor, D, rb, re, 0, 0);
 	const int use_mfma = dist_kernel_choice();

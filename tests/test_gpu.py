@@ -207,8 +207,11 @@ def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
     if pair:   # per-taxon masks: ~1/8 of the positions excluded, differently per taxon
         inc &= (rng.integers(-2**31, 2**31, inc.shape, dtype=np.int64) | 0x77777777).astype(np.int32)
     out = {}
-    for mode in ("0", "1", "2"):   # VALU tiles, k_snp_mfma (128 x 128), k_snp_mfma2 (256 x 256, the default)
-        monkeypatch.setenv("CCG_DIST_MFMA", mode)
+    # VALU tiles, k_snp_mfma (128 x 128), k_snp_mfma2 (256 x 256, register-staged), k_snp_mfma3 (256 x 256,
+    # LDS-DMA staged through 4 stages: the non-pair default)
+    for mode in ("0", "1", "2", "3"):
+        monkeypatch.setenv("CCG_DIST_MFMA", "2" if mode == "3" else mode)
+        monkeypatch.setenv("CCG_DIST_GLDS", "1" if mode == "3" else "0")
         s_d = torch.from_numpy(seqs).cuda()
         i_d = torch.from_numpy(inc).cuda()
         m = n * (n - 1) // 2
@@ -221,7 +224,7 @@ def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
         dev.snp_ltd_dev(s_d.data_ptr(), i_d.data_ptr(), n, L, W, D.data_ptr(), **kw)
         torch.cuda.synchronize()
         out[mode] = (D.cpu().numpy(), Nd.cpu().numpy() if pair else None)
-    for mode in ("1", "2"):
+    for mode in ("1", "2", "3"):
         assert (out["0"][0].view(np.uint8) == out[mode][0].view(np.uint8)).all(), mode
         if pair:
             assert (out["0"][1].view(np.uint8) == out[mode][1].view(np.uint8)).all(), mode

@@ -2,7 +2,7 @@
 (tools/profile_r06.sh clk): GRBM_GUI_ACTIVE over the dispatch's duration gives
 the clock the chip held while the kernel ran (the counter sums the 8 XCDs'
 GPU-busy cycles), SQ_BUSY_CYCLES / SQ_WAVE_CYCLES / SQ_INSTS_VALU /
-SQ_VALU_MFMA_BUSY_CYCLES the issue mix.  Per dispatch of k_snp_mfma2, then the
+SQ_VALU_MFMA_BUSY_CYCLES the issue mix.  Per dispatch of k_snp_mfma3 / k_snp_mfma2, then the
 mean.
 
     python tools/pmc_clock.py gpurun_out/prof_r06/pmc_clk profiles/r06_dist_clock.json
@@ -20,7 +20,7 @@ def main():
     disp = defaultdict(dict)
     for r in csv.DictReader(open(f"{src}/run_counter_collection.csv")):
         m = re.match(r"(?:void )?(\w+)", r["Kernel_Name"])
-        if not m or m.group(1) != "k_snp_mfma2":
+        if not m or m.group(1) not in ("k_snp_mfma2", "k_snp_mfma3"):
             continue
         d = disp[r["Dispatch_Id"]]
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -39,7 +39,7 @@ def main():
             row["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
         rows.append(row)
     mean = {k: statistics.mean(r[k] for r in rows) for k in rows[0]} if rows else {}
-    res = {"source": f"rocprofv3 --pmc (one pass) of tools/perf_dist.py 50000 5000000, dispatches of k_snp_mfma2 "
+    res = {"source": f"rocprofv3 --pmc (one pass) of tools/perf_dist.py 50000 5000000, dispatches of k_snp_mfma3 / k_snp_mfma2 "
                      f"({src})", "dispatches": rows, "mean": mean,
            "reading": "clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration: the clock the chip held while the fp4 MFMA "
                       "kernel ran (2.4 GHz nominal); mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x "

@@ -32,7 +32,7 @@ for part in "$@"; do
     ;;
   clk)
     echo "dist clock / issue counters"
-    timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $O/pmc_clk -o run -- python3 tools/perf_dist.py 50000 5000000 > $O/pmc_clk.log 2>&1
+    timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $O/pmc_clk -o run -- python3 tools/perf_dist.py 50000 5000000 > $O/pmc_clk.log 2>&1
     python3 tools/pmc_clock.py $O/pmc_clk $O/pmc_clk.json > /dev/null
     echo "clock summarised"
     ;;
