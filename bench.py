@@ -399,7 +399,9 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "kernel": (("k_snp_mfma_pair" if mode_env == "1" else "k_snp_mfma2_pair") if pair
+            "kernel": (("k_snp_mfma_pair" if mode_env == "1" else
+                                         "k_snp_mfma2_pair" if os.environ.get("CCG_DIST_GLDS") == "0"
+                                         else "k_snp_mfma3_pair") if pair
                        else dist_kernel_name()) if mfma
             else ("k_snp_tile_pair" if pair else "k_snp_tile"),
             "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
