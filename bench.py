@@ -68,10 +68,13 @@ VALU_NOMINAL_LANE_OPS = 256 * 4 * 32 * 2.4e9
 # Non-pair dist runs on the matrix cores (k_snp_mfma, the default): a code is
 # the tetrahedron vector (+-1)^3 in MX-fp4, 3 MACs = 6 flops per position pair
 # (dist = (3 L - dot) / 4, exact).  Peak: the MX-fp4 dense rate, ~10 PF
-# (MI355X_MICROARCH.md); tools/micro/mfma_fp4 (profiles/r02_mfma_fp4.txt)
-# issues 3.55e15 MAC/s = 7.1 PF from registers on this box.
+# (MI355X_MICROARCH.md).  Measured ceiling: tools/micro/mfma_valu
+# (profiles/r06_mfma_valu.txt) issues register-fed fp4 MFMAs, 16 accumulators
+# per wave, at 3.60e15 MAC/s = 7.2 PF sustained (one MFMA per 32.8 cycles at
+# the ~1.76 GHz the chip holds under that load; round 2's tools/micro/mfma_fp4,
+# 4 accumulators: 7.1 PF).
 MFMA_FP4_DENSE_TFLOPS = 10000.0
-MFMA_FP4_MEASURED_TFLOPS = 7098.0
+MFMA_FP4_MEASURED_TFLOPS = 7202.0
 FLOPS_PER_POSITION_PAIR = 6.0
 VALU_INT32_CEILING = 256 * 4 * 16 * 2.4e9
 OPS_PER_WORD_PAIR = 3.0
@@ -399,9 +402,7 @@ def dist_extra(dev, torch, n=8192, L=1_000_000, reps=3, rank=0, world=1, dist=No
     mode = "pair mode -f 3, D and N" if pair else "non-pair"
     return {"taxa_pairs_per_s": round(m / dt, 1), "nt_comparisons_per_s": m * L / dt, "seconds": round(dt, 4),
             "config": f"N={n} x L={L} random MSA ({mode}, double), input in HBM, LT rows sharded over {world} GPU(s)",
-            "kernel": (("k_snp_mfma_pair" if mode_env == "1" else
-                                         "k_snp_mfma2_pair" if os.environ.get("CCG_DIST_GLDS") == "0"
-                                         else "k_snp_mfma3_pair") if pair
+            "kernel": (("k_snp_mfma_pair" if mode_env == "1" else "k_snp_mfma2_pair") if pair
                        else dist_kernel_name()) if mfma
             else ("k_snp_tile_pair" if pair else "k_snp_tile"),
             "roofline": mfma_roofline(m * L / world, dt, 8.0 if pair else FLOPS_PER_POSITION_PAIR) if mfma
@@ -417,7 +418,8 @@ def mfma_roofline(position_pairs, dt, flops_per_pp=FLOPS_PER_POSITION_PAIR):
             "frac": round(tf / MFMA_FP4_DENSE_TFLOPS, 4), "measured_issue_peak": MFMA_FP4_MEASURED_TFLOPS,
             "frac_of_measured_peak": round(tf / MFMA_FP4_MEASURED_TFLOPS, 4),
             "form": "tetrahedron (+-1)^3 MX-fp4 operands, v_mfma_scale_f32_32x32x64_f8f6f4, dist = (3 L - dot) / 4",
-            "evidence": "profiles/r02_mfma_fp4.txt (tools/micro/mfma_fp4: lane map, register-fed rate)"}
+            "evidence": "profiles/r02_mfma_fp4.txt (tools/micro/mfma_fp4: lane map), profiles/r06_mfma_valu.txt "
+                        "(tools/micro/mfma_valu: register-fed rate, VALU per MFMA)"}
 
 
 def valu_roofline(ops, dt, opw):

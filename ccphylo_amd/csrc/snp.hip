@@ -15,7 +15,7 @@
 // Pair mode keeps each taxon's mask m beside its planes:
 //   d += popc(((hi_a ^ hi_b) | (lo_a ^ lo_b)) & m_a & m_b), n += popc(m_a & m_b).
 // Two kernel families compute it:
-//   - the default, k_snp_mfma3 (non-pair) / k_snp_mfma_pair: the count as an
+//   - the default, k_snp_mfma3 (non-pair) / k_snp_mfma2_pair: the count as an
 //     exact MX-fp4 dot product on the matrix cores (each code a +-1
 //     tetrahedron vector, dist = (3 L - dot) / 4), 256x256 pair tiles,
 //     MFMA-bound; k_snp_mfma3 stages its chunks by LDS-DMA and interleaves
@@ -999,8 +999,9 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma3(const uint2 *__restrict__ 
 				else f1[k >> 1] = fp4_spread(a[k >> 1].y);
 			}
 		}
-		// one spread (3 shifts, 4 bitop3) per MFMA on the first 8 (measured: 4 VALU per slot on 14 slots was
-		// slower, 6.43 against 6.26 s at 50k x 5 Mbp)
+		// one spread (3 shifts, 4 bitop3) per MFMA on the first 8.  Measured at 50k x 5 Mbp: 4 VALU per slot
+		// on 14 slots was slower (6.43 against 6.26 s), 4 / 3 on all 16 slots (and 2 on component 1's) the
+		// same (5.56 against 5.54 s, headline data)
 #pragma unroll
 		for(int k = 0; k < 8; ++k) {
 			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0);
@@ -1696,243 +1697,6 @@ __global__ __launch_bounds__(256, 1) void k_snp_mfma2_pair(const uint4 *__restri
 	}
 }
 
-// k_snp_mfma3_pair: k_snp_mfma2_pair's tiles, operands and epilogue with
-// k_snp_mfma3's staging and issue order.  The {hi, lo, m, 0} words of both
-// panels land by LDS-DMA (global_load_lds_dwordx4, inline asm as in
-// k_snp_mfma3) in a 3-stage ring, [stage][panel][word][row] of 16 bytes:
-// 8 words x (256 A + 128 B rows) = 48 KB per stage, 144 KB in all, so chunk
-// c + 2 is in flight while chunk c is computed.  Wave w stages words 2w and
-// 2w + 1 of both panels: 8 + 4 wave-instructions per chunk.  A 64-position
-// step is four groups of 8 MFMAs (mask, hi, lo, hi ^ lo); the VALU each
-// group carries, pinned by sched_group_barrier, is the next group's
-// operands: the hi spreads under the mask MFMAs, the lo spreads under the
-// hi ones, the xors and the next step's LDS reads under the lo ones, the
-// next step's mask spreads under the xor ones.
-#define NST3P 3
-template <int ET, bool SPLIT, bool BAND>
-__global__ __launch_bounds__(256, 1) void k_snp_mfma3_pair(const uint4 *__restrict__ P, int Wp, int n, long long t0,
-                                                           long long items, int S, int Wk, unsigned norm,
-                                                           unsigned minLength, double bs,
-                                                           typename Elem<ET>::T *__restrict__ D,
-                                                           typename Elem<ET>::T *__restrict__ Nm, long long rowBegin,
-                                                           long long rowEnd, unsigned *__restrict__ cd,
-                                                           unsigned *__restrict__ cn, long long cbase,
-                                                           const long long *__restrict__ pfx, int npanels, int rank,
-                                                           int world) {
-	constexpr int KW = KC2;                         // words per chunk
-	constexpr int SA = KW * TILE2, SBW = KW * 128;  // uint4 per stage: A slab, B slab
-	__shared__ __attribute__((aligned(16))) uint4 L[NST3P * (SA + SBW)];   // 144 KB
-	const long long item = t0 + xcd_tile(blockIdx.x, items), th = SPLIT ? item / S : item, t = th >> 1;
-	const int half = (int) (th & 1);
-	int I, J;
-	if(BAND) {
-		int lo = 0, hi = npanels - 1;
-		while(lo < hi) {
-			const int mid = (lo + hi + 1) >> 1;
-			if(pfx[mid] <= t) lo = mid; else hi = mid - 1;
-		}
-		I = lo;
-		J = (int) (t - pfx[lo]);
-	} else {
-		tile_ij(t, I, J);
-	}
-	const int wb = SPLIT ? (int) (item % S) * Wk : 0;
-	const int Wl = SPLIT ? (wb + Wk < Wp ? Wk : Wp - wb) : Wp;
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-	// staging sources of this lane: A rows q 64 + lane, B rows 128 half + q 64 + lane, word 2 wid of each chunk
-	const uint4 *srcA[4], *srcB[2];
-#pragma unroll
-	for(int q = 0; q < 4; ++q) {
-		const long long Lr = (long long) I * TILE2 + q * 64 + lane;
-		long long r = Lr;
-		if(BAND) {
-			const long long lb = Lr / SB;
-			r = (lb * world + rank) * SB + (Lr - lb * SB);
-			r = r < n ? r : 0;   // rows past n stage row 0 and are never stored
-		}
-		srcA[q] = P + (size_t) r * Wp + wb + 2 * wid;
-	}
-#pragma unroll
-	for(int q = 0; q < 2; ++q) srcB[q] = P + ((size_t) J * TILE2 + 128 * half + q * 64 + lane) * Wp + wb + 2 * wid;
-	const int nch = Wl / KW;
-	const unsigned lbase = (unsigned) (uintptr_t) (__attribute__((address_space(3))) uint4 *) L;
-	auto glds = [&](const uint4 *src, unsigned lds) {
-		unsigned keep;
-		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-		             : "=&s"(keep)
-		             : "v"(src), "s"(lds)
-		             : "memory");
-	};
-	auto issue = [&](int c) {   // chunk c into stage c % NST3P: 12 wave-instructions
-		const int st = c % NST3P, w0 = c * KW;
-#pragma unroll
-		for(int e = 0; e < 2; ++e) {
-			const int w = 2 * wid + e;
-#pragma unroll
-			for(int q = 0; q < 4; ++q)
-				glds(srcA[q] + w0 + e,
-				     __builtin_amdgcn_readfirstlane(lbase + (unsigned) ((st * (SA + SBW) + w * TILE2 + q * 64) * 16)));
-#pragma unroll
-			for(int q = 0; q < 2; ++q)
-				glds(srcB[q] + w0 + e,
-				     __builtin_amdgcn_readfirstlane(lbase + (unsigned) ((st * (SA + SBW) + SA + w * 128 + q * 64) * 16)));
-		}
-	};
-	auto land = [&](int c) {   // chunk c in LDS for every wave (chunk c + 1 may stay in flight)
-		if(c + 1 < nch) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-		else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		asm volatile("" ::: "memory");
-		__builtin_amdgcn_s_barrier();
-		asm volatile("" ::: "memory");
-	};
-	const int wr = wid >> 1, wc = wid & 1;
-	const int h = lane >> 5, l32 = lane & 31;
-	const int ra0 = 128 * wr + l32, rb0 = 64 * wc + l32;
-	auto rd = [&](int gs, uint4 (&a)[4], uint4 (&b)[2]) {   // step gs: word 2 (gs % 4) + h of chunk gs / 4
-		const int st = (gs >> 2) % NST3P, w = 2 * (gs & 3) + h;
-		const uint4 *Ac = &L[st * (SA + SBW) + w * TILE2], *Bc = &L[st * (SA + SBW) + SA + w * 128];
-#pragma unroll
-		for(int x = 0; x < 4; ++x) a[x] = Ac[ra0 + 32 * x];
-#pragma unroll
-		for(int y = 0; y < 2; ++y) b[y] = Bc[rb0 + 32 * y];
-	};
-	v16f_t acc[4][2], accn[4][2];
-#pragma unroll
-	for(int a = 0; a < 4; ++a)
-#pragma unroll
-		for(int c = 0; c < 2; ++c)
-#pragma unroll
-			for(int r = 0; r < 16; ++r) acc[a][c][r] = accn[a][c][r] = 0.0f;
-#define MF3P(ACC, TA, TB, F, G)                                                                                   \
-	ACC[TA][TB] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F, G, ACC[TA][TB], MFMA_FP4, MFMA_FP4, 0,       \
-	                                                              MFMA_SCALE1, 0, MFMA_SCALE1)
-	for(int c = 0; c < NST3P - 1 && c < nch; ++c) issue(c);
-	land(0);
-	if(NST3P - 1 < nch) issue(NST3P - 1);
-	uint4 av[4], bv[2];
-	v8i_t am[4], bm[2];
-	rd(0, av, bv);
-#pragma unroll
-	for(int x = 0; x < 4; ++x) am[x] = pair2_mask(av[x].z);
-#pragma unroll
-	for(int y = 0; y < 2; ++y) bm[y] = pair2_mask(bv[y].z);
-	auto step = [&](auto SI, int gs, bool more, bool open) {
-		constexpr int G0 = 4 * decltype(SI)::value;
-		v8i_t ah[4], bh[2], al[4], bl[2];
-		// mask group + the hi spreads (6 x 7 VALU)
-#pragma unroll
-		for(int k = 0; k < 8; ++k) {
-			MF3P(accn, k >> 1, k & 1, am[k >> 1], bm[k & 1]);
-			if(k < 4) ah[k] = pair2_comp(av[k].x, am[k]);
-			else if(k < 6) bh[k - 4] = pair2_comp(bv[k - 4].x, bm[k - 4]);
-		}
-#pragma unroll
-		for(int k = 0; k < 6; ++k) {
-			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0);
-			__builtin_amdgcn_sched_group_barrier(0x002, 7, G0);
-		}
-		__builtin_amdgcn_sched_group_barrier(0x008, 2, G0);
-		// hi group + the lo spreads
-#pragma unroll
-		for(int k = 0; k < 8; ++k) {
-			MF3P(acc, k >> 1, k & 1, ah[k >> 1], bh[k & 1]);
-			if(k < 4) al[k] = pair2_comp(av[k].y, am[k]);
-			else if(k < 6) bl[k - 4] = pair2_comp(bv[k - 4].y, bm[k - 4]);
-		}
-#pragma unroll
-		for(int k = 0; k < 6; ++k) {
-			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0 + 1);
-			__builtin_amdgcn_sched_group_barrier(0x002, 7, G0 + 1);
-		}
-		__builtin_amdgcn_sched_group_barrier(0x008, 2, G0 + 1);
-		if(open) {   // the next step opens chunk (gs + 1) / 4
-			const int cn = (gs + 1) >> 2;
-			land(cn);
-			if(cn + NST3P - 1 < nch) issue(cn + NST3P - 1);
-		}
-		uint4 an[4], bn[2];
-		if(more) rd(gs + 1, an, bn);
-		// lo group + the xors (6 x 4 VALU) and the next step's LDS reads
-#pragma unroll
-		for(int k = 0; k < 8; ++k) {
-			MF3P(acc, k >> 1, k & 1, al[k >> 1], bl[k & 1]);
-			if(k < 4) ah[k] = pair2_xor(ah[k], al[k], am[k]);
-			else if(k < 6) bh[k - 4] = pair2_xor(bh[k - 4], bl[k - 4], bm[k - 4]);
-		}
-		if(more) __builtin_amdgcn_sched_group_barrier(0x100, 6, G0 + 2);
-#pragma unroll
-		for(int k = 0; k < 6; ++k) {
-			__builtin_amdgcn_sched_group_barrier(0x008, 1, G0 + 2);
-			__builtin_amdgcn_sched_group_barrier(0x002, 4, G0 + 2);
-		}
-		__builtin_amdgcn_sched_group_barrier(0x008, 2, G0 + 2);
-		// xor group + the next step's mask spreads
-#pragma unroll
-		for(int k = 0; k < 8; ++k) {
-			MF3P(acc, k >> 1, k & 1, ah[k >> 1], bh[k & 1]);
-			if(more) {
-				if(k < 4) am[k] = pair2_mask(an[k].z);
-				else if(k < 6) bm[k - 4] = pair2_mask(bn[k - 4].z);
-			}
-		}
-		if(more) {
-#pragma unroll
-			for(int k = 0; k < 6; ++k) {
-				__builtin_amdgcn_sched_group_barrier(0x008, 1, G0 + 3);
-				__builtin_amdgcn_sched_group_barrier(0x002, 7, G0 + 3);
-			}
-			__builtin_amdgcn_sched_group_barrier(0x008, 2, G0 + 3);
-#pragma unroll
-			for(int x = 0; x < 4; ++x) av[x] = an[x];
-#pragma unroll
-			for(int y = 0; y < 2; ++y) bv[y] = bn[y];
-		}
-	};
-	for(int c = 0; c + 1 < nch; ++c) {
-		step(std::integral_constant<int, 0>(), 4 * c + 0, true, false);
-		step(std::integral_constant<int, 1>(), 4 * c + 1, true, false);
-		step(std::integral_constant<int, 2>(), 4 * c + 2, true, false);
-		step(std::integral_constant<int, 3>(), 4 * c + 3, true, true);
-	}
-	{
-		const int g = 4 * (nch - 1);
-		step(std::integral_constant<int, 0>(), g + 0, true, false);
-		step(std::integral_constant<int, 1>(), g + 1, true, false);
-		step(std::integral_constant<int, 2>(), g + 2, true, false);
-		step(std::integral_constant<int, 3>(), g + 3, false, false);
-	}
-#undef MF3P
-	// epilogue: k_snp_mfma2_pair's
-#pragma unroll
-	for(int ta = 0; ta < 4; ++ta) {
-#pragma unroll
-		for(int r = 0; r < 16; ++r) {
-			const long long Lr = (long long) I * TILE2 + 128 * wr + 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
-			long long i = Lr;
-			if(BAND) {
-				const long long lb = Lr / SB;
-				i = (lb * world + rank) * SB + (Lr - lb * SB);
-			}
-			if(i >= n || (!BAND && (i < rowBegin || i >= rowEnd))) continue;
-			const long long base = BAND ? Shard{rank, world}.off(i) : tri(i);
-#pragma unroll
-			for(int tb = 0; tb < 2; ++tb) {
-				const long long j = (long long) J * TILE2 + 128 * half + 64 * wc + 32 * tb + l32;
-				if(j < i) {
-					const int nn = (int) accn[ta][tb][r];
-					const unsigned d = (unsigned) ((3 * nn - (int) acc[ta][tb][r]) >> 2);
-					if(SPLIT) {
-						atomicAdd(&cd[base + j - cbase], d);
-						atomicAdd(&cn[base + j - cbase], (unsigned) nn);
-					} else {
-						pair_store<ET>(D, Nm, base + j, d, (uint32_t) nn, norm, minLength, bs);
-					}
-				}
-			}
-		}
-	}
-}
-
 // split-K epilogue of pair mode: the A7 store of the summed (dist, n)
 template <int ET>
 __global__ void k_snp_pair_finish(const unsigned *__restrict__ cd, const unsigned *__restrict__ cn, long long f0,
@@ -2156,7 +1920,7 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 	const int kc = !PAIR && kce && atoi(kce) == KC2L && Wp % KC2L == 0 ? KC2L : KC2;
 	// the LDS-DMA staged kernel (CCG_DIST_GLDS=0: k_snp_mfma2)
 	const char *gle = getenv("CCG_DIST_GLDS");
-	const bool glds = !(gle && atoi(gle) == 0) && (PAIR || kc == KC3);
+	const bool glds = !PAIR && !(gle && atoi(gle) == 0) && kc == KC3;
 	const int sorder = !PAIR && world == 0 && ore && atoi(ore) == 1 && (rb / TILE2) % 4 == 0;
 	const int chunks = Wp / kc;
 	int S = 1;
@@ -2190,29 +1954,6 @@ static int snp_launch_mfma2(ccg_ctx *ctx, const ccg_snp_args *a, const void *pla
 			const uint4 *pp = (const uint4 *) planes;
 			unsigned *cn = cnt ? cnt + (f1 - f0) : NULL;
 			T *Nn = world > 0 ? NULL : (T *) N;
-#define MF3P_LAUNCH(K)                                                                                               \
-	if(world > 0 && S > 1)                                                                                           \
-		K<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(pp, Wp, (int) n, t, items, S, Wk, a->norm,       \
-		                                                           a->minLength, a->byteScale, (T *) D, Nn, 0, n, cnt, \
-		                                                           cn, 0, d_pfx, npanels, rank, world);               \
-	else if(world > 0)                                                                                               \
-		K<ET, false, true><<<(unsigned) items, 256, 0, ctx->stream>>>(pp, Wp, (int) n, t, items, 1, Wp, a->norm,      \
-		                                                            a->minLength, a->byteScale, (T *) D, Nn, 0, n,    \
-		                                                            cnt, cn, 0, d_pfx, npanels, rank, world);         \
-	else if(S > 1)                                                                                                   \
-		K<ET, true, false><<<(unsigned) items, 256, 0, ctx->stream>>>(pp, Wp, (int) n, t, items, S, Wk, a->norm,      \
-		                                                            a->minLength, a->byteScale, (T *) D, Nn, rb, re,  \
-		                                                            cnt, cn, f0, NULL, 0, 0, 1);                      \
-	else                                                                                                             \
-		K<ET, false, false><<<(unsigned) items, 256, 0, ctx->stream>>>(pp, Wp, (int) n, t, items, 1, Wp, a->norm,     \
-		                                                             a->minLength, a->byteScale, (T *) D, Nn, rb, re, \
-		                                                             cnt, cn, f0, NULL, 0, 0, 1);
-			if(glds) {   // k_snp_mfma3_pair (LDS-DMA staged; CCG_DIST_GLDS=0: k_snp_mfma2_pair)
-				MF3P_LAUNCH(k_snp_mfma3_pair)
-				MF2_TRY(hipGetLastError());
-				continue;
-			}
-#undef MF3P_LAUNCH
 			if(world > 0 && S > 1)
 				k_snp_mfma2_pair<ET, true, true><<<(unsigned) items, 256, 0, ctx->stream>>>(
 				    pp, Wp, (int) n, t, items, S, Wk, a->norm, a->minLength, a->byteScale, (T *) D, Nn, 0, n, cnt, cn, 0,

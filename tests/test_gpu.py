@@ -189,8 +189,8 @@ def _related_msa(rng, n, L, rate, nrate=0.02):
                                               # and k_snp_mfma2_pair (column halves of 256 x 256 tiles) likewise
                                               (17000, 640, 8, None, True), (16500, 300, 4, (2000, 16001), True)])
 def test_dist_mfma_equals_valu(dev, monkeypatch, n, L, et, rows, pair):
-    """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma / k_snp_mfma2 / k_snp_mfma3, k_snp_mfma_pair / k_snp_mfma2_pair /
-    k_snp_mfma3_pair:
+    """The MFMA forms of fsacmp / fsacmpair (k_snp_mfma / k_snp_mfma2 / k_snp_mfma3, k_snp_mfma_pair /
+    k_snp_mfma2_pair:
     tetrahedron +-1 vectors in MX-fp4, dist = (3 L - dot) / 4, in pair mode
     masked with n from a fourth component) give the VALU tile kernels'
     matrices (and N) bit for bit: odd sizes, row ranges, split-K slices, every element type (the

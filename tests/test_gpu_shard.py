@@ -351,7 +351,7 @@ def test_dist_shard_layout_pair(dev, monkeypatch, n, L, et, proxi, world, mfma):
     """Pair mode (cmpairFsaThrd, fsacmp.c:587; -P: maskProxi fsacmp.c:355)
     into the band shards: each rank's buffer equals the band extract of the
     full pair-mode LT (itself checked against the oracle and goldens), with
-    the MFMA (k_snp_mfma3_pair, k_snp_mfma2_pair, k_snp_mfma_pair) and VALU (k_snp_tile_pair) band forms."""
+    the MFMA (k_snp_mfma2_pair, k_snp_mfma_pair) and VALU (k_snp_tile_pair) band forms."""
     import ccphylo_amd as cg
     monkeypatch.setenv("CCG_DIST_MFMA", mfma)
     from ccphylo_amd import native as nt
