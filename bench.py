@@ -655,7 +655,10 @@ def tree_cu_set(ncu, k, layout):
     "low" (bits 0 .. k-1) gives every XCD k / 8 CUs.  "xcd" (round 5: bits
     0 .. k/8 - 1 of each 32-bit word) puts them on XCDs 0 .. k/8 - 1 only:
     below k = 64 it leaves XCDs empty, which would run unmasked, and
-    ccg_ctx_configure refuses it; at 64 it equals "low"."""
+    ccg_ctx_configure refuses it; at 64 it equals "low".  Inside an XCD the
+    slots interleave its 4 shader engines and blocks are dealt round-robin
+    over them, so a context runs like 32 x (its fewest CUs per engine): k
+    should be a multiple of 32 (56 CUs run like 32, profiles/r06_tree_cus.jsonl)."""
     if layout == "xcd":
         per = max(1, k // 8)
         return [g * (ncu // 8) + i for g in range(8) for i in range(per)]

@@ -53,7 +53,11 @@ int ccg_init(int device, ccg_ctx **ctx);
  * run side by side -- e.g. one matrix's dist beside the previous matrix's tree.
  * On gfx950 bit k is a CU of XCD k % 8 (the first 64 bits: 8 CUs per XCD);
  * a mask that leaves an XCD without a CU is CCG_EINVAL (that XCD would run
- * unmasked).  May be called again; the previous stream is drained first.
+ * unmasked).  Within an XCD, bit k sits on shader engine (k / 8) % 4, and
+ * blocks are dealt round-robin over engines as over XCDs: a context runs like
+ * 32 x its fewest CUs on one engine, so masks of 32 j bits (j per engine) are
+ * the ones that pay (bits 0..55 run like 32 CUs).  May be called again; the
+ * previous stream is drained first.
  * A CU-masked stream is never destroyed (a ROCm 7.2 runtime defect: a later
  * stream's kernels hang after one is destroyed; tools/micro/cu_mask.hip), so
  * each masked configuration keeps one HIP stream until the process exits.
