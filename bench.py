@@ -533,7 +533,7 @@ def make_headline_alignment(torch, n, L, seed=3):
 
 
 def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barrier, profile_tree=True, capture_k=0,
-                 tree_mode="shard", pg=None, tree_cus=0, tree_layout="low", seed=3, dist_tail=0.0):
+                 tree_mode="shard", pg=None, tree_cus=0, tree_layout="low", seed=3):
     """The headline: dist + exact DNJ of one n x L alignment per step.
     world 1: ccg_snp_ltd_dev into the full double LT, ccg_tree_dev in place;
     world > 1, tree_mode "shard": ccg_snp_ltd_shard_dev into this rank's band
@@ -549,8 +549,7 @@ def pipeline_leg(dev, torch, rank, world, dist, coll, n, L, steps, warmup, barri
     world 1 with tree_cus > 0: the pipelined form (pipelined_leg, alignments
     of seeds 3 and 4 in turn); otherwise the alignment of `seed`."""
     if world == 1 and tree_cus > 0:
-        return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k, tree_layout,
-                             dist_tail)
+        return pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree, capture_k, tree_layout)
     if world > 1 and tree_mode == "gather-pipelined":
         return gather_pipelined_leg(dev, torch, rank, world, dist, n, L, steps, warmup, barrier, pg, profile_tree)
     import hashlib
@@ -666,8 +665,7 @@ def tree_cu_set(ncu, k, layout):
     return list(range(k))
 
 
-def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0, layout="low",
-                  dist_tail=0.0):
+def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tree=True, capture_k=0, layout="low"):
     """The headline on one GPU as a pipeline over a stream of alignments: two
     engine contexts on disjoint compute units (ccg_ctx_configure: the tree's
     stream on CUs [0, tree_cus), 8 per XCD, the dist's on the rest, neither
@@ -680,11 +678,7 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     rate is matrices completed per second in steady state.  tree_s / dist_s
     are each context's device time (HIP events on its own stream); the thread
     walls are reported beside them.  Same return value as pipeline_leg, plus
-    res["alignments"] (both) and res["joins_sha256_by_alignment"].
-    dist_tail > 0: the tree context, once its tree is done, computes the last
-    LT rows of matrix k + 1 (that fraction of its cells, ccg_snp_ltd_dev over
-    a row range) while the dist context computes the rows above, so the
-    tree's CUs do not idle while the dist finishes."""
+    res["alignments"] (both) and res["joins_sha256_by_alignment"]."""
     import hashlib
     import threading
     import ccphylo_amd as cg
@@ -704,10 +698,6 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     s0, i0, _ = aligns[0]
     inc0 = ddev.snp_ltd_dev(s0.data_ptr(), i0.data_ptr(), n, L, W, Ds[0].data_ptr())   # matrix 0
     cap = Ds[0][:capture_k].cpu().numpy() if capture_k else None
-    # the tail's first row: rows [r1, n) hold dist_tail of the LT's cells
-    r1 = n
-    if dist_tail > 0:
-        r1 = max(2, min(n - 1, int(round(n * (1.0 - dist_tail) ** 0.5))))
 
     def step(k, profile=False):
         res, err = {}, []
@@ -716,8 +706,7 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
             try:
                 sq, ic, _ = aligns[(k + 1) % 2]
                 t0 = time.perf_counter()
-                kw = {"row_range": (0, r1)} if r1 < n else {}
-                inc = ddev.snp_ltd_dev(sq.data_ptr(), ic.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr(), **kw)
+                inc = ddev.snp_ltd_dev(sq.data_ptr(), ic.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr())
                 res["d"] = (time.perf_counter() - t0, ddev.last_dist_ms(), inc)
             except Exception as e:  # noqa: BLE001
                 err.append(e)
@@ -727,13 +716,7 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
                 t0 = time.perf_counter()
                 j, fn, fd, st = tdev.tree_dev(Ds[k % 2].data_ptr(), n, method=cg.CCG_TREE_DNJ, exact=True,
                                               profile=profile)
-                tail_ms = 0.0
-                if r1 < n:   # the tail of matrix k + 1's dist on the tree's CUs
-                    sq, ic, _ = aligns[(k + 1) % 2]
-                    tdev.snp_ltd_dev(sq.data_ptr(), ic.data_ptr(), n, L, W, Ds[(k + 1) % 2].data_ptr(),
-                                     row_range=(r1, n))
-                    tail_ms = tdev.last_dist_ms()
-                res["t"] = (time.perf_counter() - t0, (j, fn, fd), st, tail_ms)
+                res["t"] = (time.perf_counter() - t0, (j, fn, fd), st)
             except Exception as e:  # noqa: BLE001
                 err.append(e)
         th = [threading.Thread(target=run_d), threading.Thread(target=run_t)]
@@ -743,10 +726,9 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
             x.join()
         if err:
             raise err[0]
-        # walls, the dist's kernel ms (both parts), joins, stats, included positions, the tree's device s
-        # (HIP events), the tail's kernel ms
-        return (res["d"][0], res["t"][0], res["d"][1] + res["t"][3], res["t"][1], res["t"][2], res["d"][2],
-                res["t"][2][3] / 1e6, res["t"][3])
+        # walls, the dist's kernel ms, joins, stats, included positions, the tree's device s (HIP events)
+        return (res["d"][0], res["t"][0], res["d"][1], res["t"][1], res["t"][2], res["d"][2],
+                res["t"][2][3] / 1e6)
 
     def sha_of(joins):
         jj, fn, fd = joins
@@ -773,18 +755,13 @@ def pipelined_leg(dev, torch, n, L, steps, warmup, barrier, tree_cus, profile_tr
     # the line's sha: alignment 0's (the sequential form's default matrix)
     sha = sorted(shas[0])[0] if 0 in shas else sha_of(joins)
     pst = step(k, profile=True)[4] if profile_tree else None   # an extra, untimed pipelined step
-    # with a tail: the dist context's part (its rows, its kernel time) is the dist figure; the tail is beside it
-    main_ms = sum(p[2] - p[7] for p in parts) / steps
-    res = {"dt": dt, "dist_s": main_ms / 1e3, "tree_s": sum(p[6] for p in parts) / steps,
+    res = {"dt": dt, "dist_s": sum(p[2] for p in parts) / steps / 1e3, "tree_s": sum(p[6] for p in parts) / steps,
            "dist_wall_s": sum(p[0] for p in parts) / steps, "tree_wall_s": sum(p[1] for p in parts) / steps,
-           "dist_kernel_ms": main_ms, "joins": len(joins[0]), "joins_sha256": sha,
-           **({"dist_elems": r1 * (r1 - 1) // 2} if r1 < n else {}),
+           "dist_kernel_ms": sum(p[2] for p in parts) / steps, "joins": len(joins[0]), "joins_sha256": sha,
            "joins_sha256_by_alignment": {str(a): sorted(v) for a, v in shas.items()},
            "rows_rescanned": int(st[0]), "cells_rescanned": int(st[1]), "included_positions": inc,
            "alignments": aligns,
            "pipelined": {"tree_cus": tree_cus, "dist_cus": ncu - tree_cus, "layout": layout,
-                         "dist_tail_rows": [r1, n] if r1 < n else None,
-                         "dist_tail_s": round(sum(p[7] for p in parts) / steps / 1e3, 3),
                          "matrix0_included_positions": inc0, "alignment_seeds": [3, 4]}}
     del Ds
     ddev.close()
@@ -1373,9 +1350,6 @@ def main():
                     help="which CUs the pipelined tree takes: mask bits 0 .. --tree-cus - 1 (--tree-cus / 8 CUs "
                          "per XCD), or the first --tree-cus / 8 bits of each 32-bit mask word (round 5's form: "
                          "XCDs 0 .. --tree-cus/8 - 1 only; refused below 64)")
-    ap.add_argument("--dist-tail", type=float, default=0.0,
-                    help="pipelined form: the fraction of matrix k + 1's LT cells (its last rows) the tree context "
-                         "computes after its tree, beside the dist context's rows above")
     ap.add_argument("--headline-seed", type=int, default=3,
                     help="the alignment's seed in the sequential forms (the pipelined one alternates 3 and 4)")
     args = ap.parse_args()
@@ -1455,8 +1429,7 @@ def main():
     head, joins, pst, (seqs, incs, W), cells = pipeline_leg(
         dev, torch, rank, world, dist if world > 1 else None, coll, n, L, args.steps, args.warmup, barrier,
         capture_k=256 * 255 // 2 if (world == 1 and not args.no_cpu) else 0, tree_mode=args.tree_mode, pg=pg,
-        tree_cus=args.tree_cus if world == 1 else 0, tree_layout=args.tree_layout, seed=args.headline_seed,
-        dist_tail=args.dist_tail)
+        tree_cus=args.tree_cus if world == 1 else 0, tree_layout=args.tree_layout, seed=args.headline_seed)
     if hwd is not None:
         hwd.cancel()
     dt = head["dt"]
@@ -1504,8 +1477,8 @@ def main():
                              "time (HIP events on its stream)" if pipe else
                              "dist and tree walls run concurrently (pipelined)"
                              if head.get("gather_pipelined") else "sequential",
-                  "dist_taxa_pairs_per_s": round(head.get("dist_elems", m) / max(head["dist_s"], 1e-9), 1),
-                  "dist_nt_comparisons_per_s": head.get("dist_elems", m) * float(L) / max(head["dist_s"], 1e-9),
+                  "dist_taxa_pairs_per_s": round(m / max(head["dist_s"], 1e-9), 1),
+                  "dist_nt_comparisons_per_s": m * float(L) / max(head["dist_s"], 1e-9),
                   "tree_nj_iterations_per_s": round(head["joins"] / max(head["tree_s"], 1e-9), 1),
                   "joins": head["joins"], "joins_sha256": head["joins_sha256"],
                   **({"dist_wall_s": round(head["dist_wall_s"], 3), "tree_wall_s": round(head["tree_wall_s"], 3),
