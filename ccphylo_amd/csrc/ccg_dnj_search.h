@@ -54,7 +54,10 @@ struct DnjGrid {
 	// 1024-join window listed more than prune_cells cells per join (CCG_PRUNE_CELLS; 0: always)
 	long long prune_cells = 20000000;
 	int prune_on = 1;
-	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 0, scan_wave = -1, plan_multi = 1;
+	// plan_qdelay: the listing waves hold their Q loads back by qdelay x 32 x 64 cycles so that wave 0's fold
+	// loads go first (round 6, profiles/r06_config1_sweep.txt: 0 -> 2 gives configs[1] 23.5k -> 23.9k joins/s,
+	// the headline tree 12.79k -> 12.90k; 4 and above lose at 10k)
+	int s_top = 0, s_bands = -1, s_split_n = 16384, plan_qdelay = 2, scan_wave = -1, plan_multi = 1;
 	int plan_regsel = 0, plan_fr = FIND_RPT;   // measured at 10k: S from registers 13.2 -> 15.4 us (Q arrives late), FR 1-8 within noise
 	// tests only (CCG_TEST_WITHHOLD): bit 0, k_dnj_plan's block 0 never publishes its entry count (the
 	// listing blocks' look-back must time out into an error); bit 1, it never tags the S header (the
@@ -102,7 +105,7 @@ struct DnjGrid {
 		if(const char *e = getenv("CCG_PRUNE_CELLS")) prune_cells = atoll(e) > 0 ? atoll(e) : 0;
 		prune_on = 1;
 		if(const char *e = getenv("CCG_SCAN_CMPB")) cmp_blocks = atoi(e) > 0 ? atoi(e) : 1024;
-		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 0;
+		if(const char *e = getenv("CCG_PLAN_QDELAY")) plan_qdelay = atoi(e) >= 0 ? atoi(e) : 2;
 		if(const char *e = getenv("CCG_SCAN_WAVE")) scan_wave = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_MULTI")) plan_multi = atoi(e);
 		if(const char *e = getenv("CCG_PLAN_REGSEL")) plan_regsel = atoi(e);

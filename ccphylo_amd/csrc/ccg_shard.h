@@ -15,8 +15,10 @@ struct ShRec {   // one rank's argmin record (q, flat index); zeros in other ran
 	long long f;
 };
 
-__device__ __forceinline__ void rec_fold(const ShRec *__restrict__ rec, int world, double &bq, long long &bf) {
-	bq = 1.0;
+// q0: the fold's start (NJ's initQ: 1.0; HNJ's minQ: DBL_MAX)
+__device__ __forceinline__ void rec_fold(const ShRec *__restrict__ rec, int world, double &bq, long long &bf,
+                                         double q0 = 1.0) {
+	bq = q0;
 	bf = -1;
 	for(int w = 0; w < world; ++w) {
 		const double q = rec[w].q;

@@ -1335,6 +1335,46 @@ __global__ __launch_bounds__(XS_NT) void k_exact_sum(TreeBufs b, int n, int G) {
 }
 
 // (q, f) cells of initQ: smaller q wins, equal q -> larger flat index f
+// ------------------------------------------------------------------ HNJ row minima (tree.hip, tree_shard.hip)
+// (q, k) `<=` rule over ascending k: smaller q, then the later k
+__device__ __forceinline__ void qk_take(double &bq, int &bk, double q, int k) {
+	if(q < bq || (q == bq && k > bk)) {
+		bq = q;
+		bk = k;
+	}
+}
+
+template <int NT>
+__device__ __forceinline__ void qk_block_reduce(double &bq, int &bk, double *sq, int *sk) {
+	for(int o = 32; o > 0; o >>= 1) {
+		const double oq = __shfl_xor(bq, o, 64);
+		const int ok = __shfl_xor(bk, o, 64);
+		qk_take(bq, bk, oq, ok);
+	}
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	if(lane == 0) {
+		sq[wid] = bq;
+		sk[wid] = bk;
+	}
+	__syncthreads();
+	if(threadIdx.x == 0) {
+		for(int w = 1; w < NT / 64; ++w) qk_take(bq, bk, sq[w], sk[w]);
+	}
+}
+
+// one wave: fold of G row-minimum partials (blocks in ascending k order)
+__device__ __forceinline__ void qk_fold_wave(const double *pq, const int *pk, int G, double &bq, int &bk) {
+	const int lane = threadIdx.x & 63;
+	bq = DBL_MAX;
+	bk = -1;
+	for(int g = lane; g < G; g += 64) qk_take(bq, bk, pq[g], pk[g]);
+	for(int o = 32; o > 0; o >>= 1) {
+		const double oq = __shfl_xor(bq, o, 64);
+		const int ok = __shfl_xor(bk, o, 64);
+		qk_take(bq, bk, oq, ok);
+	}
+}
+
 __device__ __forceinline__ void qf_wave_reduce(double &q, long long &f) {
 #define S_(C, R)                                          \
 	{                                                     \

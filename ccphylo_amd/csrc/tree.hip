@@ -1417,44 +1417,7 @@ __global__ __launch_bounds__(TB) void k_nj_pop(typename Elem<ET>::T *__restrict_
 //                 n-1 into row i (its minimum as partials) and column i with
 //                 `P < pos || q < Q`.
 
-// (q, k) `<=` rule over ascending k: smaller q, then the later k
-__device__ __forceinline__ void qk_take(double &bq, int &bk, double q, int k) {
-	if(q < bq || (q == bq && k > bk)) {
-		bq = q;
-		bk = k;
-	}
-}
-
-template <int NT>
-__device__ __forceinline__ void qk_block_reduce(double &bq, int &bk, double *sq, int *sk) {
-	for(int o = 32; o > 0; o >>= 1) {
-		const double oq = __shfl_xor(bq, o, 64);
-		const int ok = __shfl_xor(bk, o, 64);
-		qk_take(bq, bk, oq, ok);
-	}
-	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-	if(lane == 0) {
-		sq[wid] = bq;
-		sk[wid] = bk;
-	}
-	__syncthreads();
-	if(threadIdx.x == 0) {
-		for(int w = 1; w < NT / 64; ++w) qk_take(bq, bk, sq[w], sk[w]);
-	}
-}
-
-// one wave: fold of G row-minimum partials (blocks in ascending k order)
-__device__ __forceinline__ void qk_fold_wave(const double *pq, const int *pk, int G, double &bq, int &bk) {
-	const int lane = threadIdx.x & 63;
-	bq = DBL_MAX;
-	bk = -1;
-	for(int g = lane; g < G; g += 64) qk_take(bq, bk, pq[g], pk[g]);
-	for(int o = 32; o > 0; o >>= 1) {
-		const double oq = __shfl_xor(bq, o, 64);
-		const int ok = __shfl_xor(bk, o, 64);
-		qk_take(bq, bk, oq, ok);
-	}
-}
+// (qk_take, qk_block_reduce, qk_fold_wave: ccg_tree_common.h, shared with the sharded HNJ)
 
 template <int UNUSED = 0>
 __global__ __launch_bounds__(TB) void k_hnj_argmin(TreeBufs b, int n) {

@@ -29,6 +29,7 @@
 #define CCG_DNJ_NO_TRACE
 #include "ccg_tree_common.h"
 #include "ccg_shard.h"
+#include "ccg_dnj_search.h"   // k_init_hnj (initHNJ over the owned rows)
 
 #define SH_GRID 8192         // max argmin blocks (grid-stride over the tiles)
 
@@ -128,10 +129,11 @@ __global__ __launch_bounds__(TB) void k_sh_argmin(const typename Elem<ET>::T *__
 }
 
 // this rank's record (G argmin partials; G = 0 when it owns no tile)
-__global__ __launch_bounds__(TB) void k_sh_fold(TreeBufs b, int G, Shard sh, ShRec *__restrict__ rec) {
+__global__ __launch_bounds__(TB) void k_sh_fold(TreeBufs b, int G, Shard sh, ShRec *__restrict__ rec,
+                                                double q0 = 1.0) {
 	__shared__ double sq[TB / 64];
 	__shared__ long long sf[TB / 64];
-	double fq = 1.0;
+	double fq = q0;
 	long long ff = -1;
 	for(int g = threadIdx.x; g < G; g += TB) {
 		const double oq = b.qpart[g];
@@ -177,12 +179,12 @@ __global__ __launch_bounds__(TB) void k_sh_fold(TreeBufs b, int G, Shard sh, ShR
 template <int ET>
 __global__ __launch_bounds__(TB) void k_sh_lines(const typename Elem<ET>::T *__restrict__ D, TreeBufs b, int n,
                                                  Shard sh, const ShRec *__restrict__ rec,
-                                                 typename Elem<ET>::T *__restrict__ X) {
+                                                 typename Elem<ET>::T *__restrict__ X, double q0) {
 	const int k = blockIdx.x * TB + threadIdx.x;
 	if(b.ctl->done) return;
 	double bq;
 	long long bf;
-	rec_fold(rec, sh.world, bq, bf);
+	rec_fold(rec, sh.world, bq, bf, q0);
 	if(bf < 0) {
 		if(blockIdx.x == 0 && threadIdx.x == 0) {
 			b.ctl->done = 1;
@@ -209,12 +211,14 @@ __global__ __launch_bounds__(TB) void k_sh_lines(const typename Elem<ET>::T *__r
 }
 
 // limbLength, the join record and updateD (nj.c:836) over the gathered lines;
-// every rank computes the whole new line j and stores its own cells
+// every rank computes the whole new line j and stores its own cells (hnj:
+// also into X[n + k], thread k's own slot, for k_sh_hnj's row-j minimum and
+// column-j rule)
 template <int ET>
 __global__ __launch_bounds__(TB) void k_sh_join(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
                                                 Shard sh, const ShRec *__restrict__ rec,
-                                                const typename Elem<ET>::T *__restrict__ X,
-                                                typename Elem<ET>::T *__restrict__ Xm) {
+                                                typename Elem<ET>::T *__restrict__ X,
+                                                typename Elem<ET>::T *__restrict__ Xm, double q0, int hnj) {
 	__shared__ int s_stop, s_nj, s_neg, s_exact;
 	TreeCtl *ctl = b.ctl;
 	const int tid = threadIdx.x;
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(TB) void k_sh_join(typename Elem<ET>::T *__restrict
 	if(s_stop) return;
 	double bq;
 	long long bf;
-	rec_fold(rec, sh.world, bq, bf);
+	rec_fold(rec, sh.world, bq, bf, q0);
 	int i, j;
 	flat_to_ij(bf, i, j);
 	const double Dij = Elem<ET>::get(X[j], bs);
@@ -269,6 +273,7 @@ __global__ __launch_bounds__(TB) void k_sh_join(typename Elem<ET>::T *__restrict
 			D[sh.off(j) + k] = v;
 		}
 		if(k == n - 1) Xm[j] = v;   // row n-1 moves to slot i in the pop
+		if(hnj) X[n + k] = v;       // (this thread read its old value above)
 		b.sD[k] = sDk - (Dik + Dkj - d);
 		b.N[k] = Nk - 1;
 		cnt = 1;
@@ -344,6 +349,227 @@ __global__ __launch_bounds__(TB) void k_sh_pop(typename Elem<ET>::T *__restrict_
 	}
 }
 
+
+// ------------------------------------------------------------------ HNJ
+// hclust.c:1671 (-m hnj) over the row shards, tree.hip's k_hnj_argmin /
+// k_nj_join / k_hnj_update split the sharded NJ way.  Q and P are indexed by
+// global row; a row's (Q, P) is kept by its owner (updatePrevQ, the column-j
+// and column-i rules read the row's own cells), while the two minima a join
+// creates (row j from the new line j, row i from row n-1 moving into it) come
+// from the gathered lines, so every rank computes them alike.  Per join:
+//   k_sh_hnj_argmin  folds the last join's row-j / row-i minima into Q / P,
+//                    then this rank's owned rows into argmin partials
+//                    (minQ, hclust.c:353: smaller q, then the larger flat
+//                    index tri(r) + P[r]); k_sh_fold makes the record; the
+//                    records are allreduced with row n-1 behind them, as NJ;
+//   k_sh_lines / allreduce / k_sh_join  as NJ (fold start DBL_MAX), the new
+//                    line j kept in X[n + k];
+//   k_sh_hnj         the row sum of j (k_sh_pop's), updateHNJ's Q / P pass on
+//                    the owned rows, the row-j and row-i minima as partials,
+//                    and HNJ_popArrange's stores (hclust.c:1308).
+template <int UNUSED = 0>
+__global__ __launch_bounds__(TB) void k_sh_hnj_argmin(TreeBufs b, int n, Shard sh) {
+	__shared__ double sq[TB / 64], fq[2];
+	__shared__ long long sf[TB / 64];
+	__shared__ int fk[2];
+	const TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+	if(ctl->done) {
+		if(tid == 0) {
+			b.qpart[blockIdx.x] = DBL_MAX;
+			b.fpart[blockIdx.x] = -1;
+		}
+		return;
+	}
+	const int r = (int) blockIdx.x * TB + tid;
+	const int hj = ctl->hj, hi = ctl->hi;
+	const bool own_j = hj >= 0 && hj / TB == (int) blockIdx.x, own_i = hi >= 0 && hi / TB == (int) blockIdx.x;
+	if(blockIdx.x == 0 && tid == 0 && hi >= 0) {   // the pop's sD / N of row i (row n before the join)
+		b.sD[hi] = b.sD[n];
+		b.N[hi] = b.N[n];
+	}
+	if(own_j || own_i) {
+		if(wid < 2 && ((wid == 0 && own_j) || (wid == 1 && own_i))) {
+			double q;
+			int k;
+			if(wid == 0) qk_fold_wave(b.bmq, b.bmr, ctl->hjb, q, k);
+			else qk_fold_wave(b.cfq, b.cfp, ctl->hib, q, k);
+			if(lane == 0) {
+				fq[wid] = q;
+				fk[wid] = k;
+			}
+		}
+		__syncthreads();
+	}
+	double q = DBL_MAX;
+	long long f = -1;
+	if(r < n) {
+		double qr = b.Q[r];
+		int pr = b.P[r];
+		const int w = own_j && r == hj ? 0 : own_i && r == hi ? 1 : -1;
+		if(w >= 0) {
+			qr = fq[w];
+			pr = fk[w] < 0 ? 0 : fk[w];
+			b.Q[r] = qr;
+			b.P[r] = pr;
+		}
+		if(r >= 1 && sh.owns(r) && qr <= DBL_MAX) {
+			q = qr;
+			f = tri(r) + pr;
+		}
+	}
+	qf_wave_reduce(q, f);
+	if(lane == 0) {
+		sq[wid] = q;
+		sf[wid] = f;
+	}
+	__syncthreads();
+	if(tid == 0) {
+		for(int k = 1; k < TB / 64; ++k) {
+			if(sq[k] < q || (sq[k] == q && sf[k] > f)) {
+				q = sq[k];
+				f = sf[k];
+			}
+		}
+		b.qpart[blockIdx.x] = q;
+		b.fpart[blockIdx.x] = f;
+	}
+}
+
+template <int ET>
+__global__ __launch_bounds__(TB) void k_sh_hnj(typename Elem<ET>::T *__restrict__ D, double bs, TreeBufs b, int n,
+                                               Shard sh, const typename Elem<ET>::T *__restrict__ X,
+                                               const typename Elem<ET>::T *__restrict__ Xm) {
+	__shared__ double s_sd, sq[TB / 64], sq2[TB / 64];
+	__shared__ int s_nj, s_i, s_j, s_stop, s_serial, s_chain, sk[TB / 64], sk2[TB / 64];
+	TreeCtl *ctl = b.ctl;
+	const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+	const int k = (int) blockIdx.x * TB + tid;
+	if(wid == 0) {
+		const int done = ctl->done;
+		const bool exact = ctl->exact;
+		if(lane == 0) {
+			s_i = ctl->i;
+			s_j = ctl->j;
+			s_stop = done;
+		}
+		if(!done) {
+			double sd;
+			int nj;
+			bool need, chain;
+			row_sum_j_wave(b, n, exact, false, &sd, &nj, &need, &chain);
+			if(lane == 0) {
+				s_sd = sd;
+				s_nj = nj;
+				s_serial = need;
+				s_chain = chain;
+			}
+		}
+	}
+	__syncthreads();
+	if(s_stop) return;
+	const int i = s_i, j = s_j;
+	if(s_chain) {   // exact mode, a failed check of the parallel form: the serial chain (all threads)
+		const double r = serial_sum_t<TB>(b.contrib, n);
+		if(tid == 0) s_sd = r;
+		if(blockIdx.x == 0 && tid == 0) ctl->chain_sums++;
+		__syncthreads();
+	}
+	const double sdj = s_sd;
+	const int nj = s_nj;
+	const int nn = n - 1;
+	const bool move = i != nn;
+	if(blockIdx.x == 0 && tid == 0) {
+		b.sD[j] = sdj;
+		b.N[j] = nj;
+		ctl->hj = j;
+		ctl->hjb = (int) cdiv(j, TB);
+		// row i's sD / N (row nn's) wait for the next k_sh_hnj_argmin: sD[i]
+		// is still read below as a partner's sum
+		ctl->hi = move ? i : -1;
+		ctl->hib = (int) cdiv(i, TB);
+		if(s_serial) ctl->serial_sums++;
+	}
+	double rq = DBL_MAX, pq = DBL_MAX;
+	int rk = -1, pk2 = -1;
+	if(k < n) {
+		const bool own = sh.owns(k);
+		const int Nk = k == j ? nj : b.N[k];
+		const double sDk = k == j ? sdj : b.sD[k];
+		double Qk = b.Q[k];
+		int Pk = b.P[k];
+		if(own && k <= n - 2) {   // updatePrevQ (hclust.c:441-449): the row's own cell
+			const int pk = Pk;
+			const double d = Elem<ET>::get(D[sh.off(k) + pk], bs);
+			if(0 <= d) {
+				const int Np = pk == j ? nj : b.N[pk];
+				const double sDp = pk == j ? sdj : b.sD[pk];
+				Qk = ((Nk + Np - 4) >> 1) * d - sDk - sDp;
+			}
+		}
+		if(own && k > j && k != i) {   // column j (hclust.c:530-556): the new D(k, j)
+			const double d = Elem<ET>::get(X[n + k], bs);
+			if(0 <= d) {
+				const double q = ((nj + Nk - 4) >> 1) * d - sdj - sDk;
+				if(Pk == i || Pk == j) {
+					Qk = q;
+					Pk = j;
+				} else if(q <= Qk) {
+					Qk = q;
+					if(Pk < j) Pk = j;
+				}
+			}
+		}
+		if(k < j) {   // row j (hclust.c:497-511), from the gathered new line j
+			const double d = Elem<ET>::get(X[n + k], bs);
+			if(0 <= d) {
+				rq = ((nj + Nk - 4) >> 1) * d - sdj - sDk;
+				rk = k;
+			}
+		}
+		// HNJ_popArrange (hclust.c:1308): row nn (gathered in Xm) moves to row
+		// i (cells k < i: its minimum, on every rank) and column i (owned rows
+		// i < k < nn: `q <= Q && (P < pos || q < Q)`)
+		if(move && k < nn && k != i) {
+			const typename Elem<ET>::T vm = Xm[k];
+			const double d = Elem<ET>::get(vm, bs);
+			const double sDi = b.sD[nn];
+			const int Ni = b.N[nn];
+			const double q = 0 <= d ? d * ((Ni + Nk - 4) >> 1) - sDi - sDk : 0.0;
+			if(k < i) {
+				if(sh.owns(i)) D[sh.off(i) + k] = vm;
+				if(0 <= d) {
+					pq = q;
+					pk2 = k;
+				}
+			} else if(own) {
+				D[sh.off(k) + i] = vm;
+				if(0 <= d && q <= Qk && (Pk < i || q < Qk)) {
+					Qk = q;
+					Pk = i;
+				}
+			}
+		}
+		if(own && k != j) {
+			b.Q[k] = Qk;
+			b.P[k] = Pk;
+		}
+	}
+	if((int) blockIdx.x * TB < j) {
+		qk_block_reduce<TB>(rq, rk, sq, sk);
+		if(tid == 0) {
+			b.bmq[blockIdx.x] = rq;
+			b.bmr[blockIdx.x] = rk;
+		}
+	}
+	if(move && (int) blockIdx.x * TB < i) {
+		qk_block_reduce<TB>(pq, pk2, sq2, sk2);
+		if(tid == 0) {
+			b.cfq[blockIdx.x] = pq;
+			b.cfp[blockIdx.x] = pk2;
+		}
+	}
+}
 
 // RCCL, resolved with dlopen so the engine has no link-time dependency on it
 struct RcclApi {
@@ -490,7 +716,8 @@ static int sh_nlb(int n, const Shard &sh) {
 struct ShnLayout {
 	size_t o_sD, o_c, o_N, o_ws, o_wa, o_wc, o_we, o_qp, o_fp, o_j, o_ctl, o_F, o_rec, o_X, o_Xm;
 	size_t o_xa, o_xb, o_xcr, o_xt, o_rp, o_is, rec_b, sz = 0;
-	ShnLayout(int n0, int world, int es) {
+	size_t o_Q = 0, o_P = 0, o_bq = 0, o_br = 0, o_cq = 0, o_cp = 0;   // HNJ: Q / P and the row-minimum partials
+	ShnLayout(int n0, int world, int es, bool hnj = false) {
 		auto take = [&](size_t bytes) {
 			size_t off = sz;
 			sz += (bytes + 255) & ~(size_t) 255;
@@ -520,6 +747,14 @@ struct ShnLayout {
 		o_xt = take(nb * XB_CAP_T * sizeof(XsTie));
 		o_rp = take(sh_rp_bytes(n0));
 		o_is = take(sh_init_scratch_bytes(n0, world));
+		if(hnj) {
+			o_Q = take(((size_t) n0 + 1) * 8);
+			o_P = take(((size_t) n0 + 1) * 4);
+			o_bq = take(nb * 8);
+			o_br = take(nb * 4);
+			o_cq = take(nb * 8);
+			o_cp = take(nb * 4);
+		}
 	}
 };
 
@@ -539,7 +774,9 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	const Shard sh = {coll_in->rank, coll_in->world};
 	// device state: the single-GPU TreeBufs subset this loop uses
 	const int nseg0 = (int) cdiv(n0 - 1, NJ_SEG);
-	const ShnLayout L(n0, coll_in->world, ET);
+	const bool hnj = a->method == CCG_TREE_HNJ;
+	if(hnj && cdiv(n0, TB) > SH_GRID) return CCG_EINVAL;   // the minQ partials (one per 256 rows)
+	const ShnLayout L(n0, coll_in->world, ET, hnj);
 	const size_t rec_b = L.rec_b, sz = L.sz;
 	const size_t o_sD = L.o_sD, o_c = L.o_c, o_N = L.o_N, o_ws = L.o_ws, o_wa = L.o_wa, o_wc = L.o_wc, o_we = L.o_we;
 	const size_t o_qp = L.o_qp, o_fp = L.o_fp, o_j = L.o_j, o_ctl = L.o_ctl, o_F = L.o_F, o_rec = L.o_rec;
@@ -575,6 +812,14 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	b.xblk = (XsBlk *) (m + o_xb);
 	b.xcr = (XsCross *) (m + o_xcr);
 	b.xti = (XsTie *) (m + o_xt);
+	if(hnj) {
+		b.Q = (double *) (m + L.o_Q);
+		b.P = (int *) (m + L.o_P);
+		b.bmq = (double *) (m + L.o_bq);
+		b.bmr = (int *) (m + L.o_br);
+		b.cfq = (double *) (m + L.o_cq);
+		b.cfp = (int *) (m + L.o_cp);
+	}
 	long long *F = (long long *) (m + o_F);
 	ShRec *rec = (ShRec *) (m + o_rec);
 	T *X = (T *) (m + o_X), *Xm = (T *) (m + o_Xm);
@@ -589,6 +834,7 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 	init.neg = (a->flags & 2) != 0;
 	init.exact = a->exact != 0;
 	init.method = a->method;
+	init.hj = init.hi = -1;
 #define SH_TRY(x)                    \
 	do {                             \
 		if((rc = (x)) != CCG_OK) goto out; \
@@ -621,28 +867,41 @@ static int tree_shard_run_t(ccg_ctx *ctx, const ccg_tree_args *a, const ccg_coll
 			goto out;
 		}
 	}
+	if(hnj) {   // initHNJ (hclust.c:56) over the owned rows
+		k_init_hnj<ET><<<cdiv(n0, TB / 64), TB, 0, st>>>(sh, D, n0, bs, b.sD, b.N, b.Q, b.P);
+		SH_HIP(hipGetLastError());
+		++launches;
+	}
 	{
 		int since_check = 0;
 		const int stop_n = a->max_joins > 0 && a->max_joins < n0 - 2 ? n0 - a->max_joins : 2;
 		while(n > stop_n) {
 			T *Xmr = (T *) ((char *) rec + rec_b);   // row n-1, gathered with the records
 			k_sh_xm<ET><<<cdiv(n - 1, TB), TB, 0, st>>>(D, n, sh, Xmr);
-			const int nlb = sh_nlb(n, sh), nseg = (int) cdiv(n - 1, NJ_SEG);
-			int sstar = 0;
-			while(sstar < nseg && hF[sstar + 1] - hF[sstar] < nlb) ++sstar;
-			const long long tiles = (long long) sstar * nlb - hF[sstar];
-			const int G = (int) (tiles < SH_GRID ? tiles : SH_GRID);
-			if(G > 0) k_sh_argmin<ET><<<G, TB, 0, st>>>(D, bs, b, n, sh, F, nlb, sstar, tiles);
-			k_sh_fold<<<1, TB, 0, st>>>(b, G, sh, rec);
+			const unsigned gn = cdiv(n, TB);
+			int G = 0;
+			if(hnj) {   // minQ over the owned rows' (Q, P)
+				G = (int) gn;
+				k_sh_hnj_argmin<><<<gn, TB, 0, st>>>(b, n, sh);
+			} else {
+				const int nlb = sh_nlb(n, sh), nseg = (int) cdiv(n - 1, NJ_SEG);
+				int sstar = 0;
+				while(sstar < nseg && hF[sstar + 1] - hF[sstar] < nlb) ++sstar;
+				const long long tiles = (long long) sstar * nlb - hF[sstar];
+				G = (int) (tiles < SH_GRID ? tiles : SH_GRID);
+				if(G > 0) k_sh_argmin<ET><<<G, TB, 0, st>>>(D, bs, b, n, sh, F, nlb, sstar, tiles);
+			}
+			const double q0 = hnj ? DBL_MAX : 1.0;   // HNJ's minQ starts at DBL_MAX, NJ's initQ at 1
+			k_sh_fold<<<1, TB, 0, st>>>(b, G, sh, rec, q0);
 			kt.mark(CCG_K_ARGMIN);
 			SH_TRY(cr.allreduce(rec, rec_b + (size_t) (n - 1) * ET));
-			const unsigned gn = cdiv(n, TB);
-			k_sh_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, rec, X);
+			k_sh_lines<ET><<<gn, TB, 0, st>>>(D, b, n, sh, rec, X, q0);
 			kt.mark(CCG_K_UPDATE);
 			SH_TRY(cr.allreduce(X, (size_t) 2 * n * ET));
-			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xmr);
+			k_sh_join<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, rec, X, Xmr, q0, hnj);
 			kt.mark(CCG_K_UPDATE);
-			k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xmr);
+			if(hnj) k_sh_hnj<ET><<<gn, TB, 0, st>>>(D, bs, b, n, sh, X, Xmr);
+			else k_sh_pop<ET><<<gn, TB, 0, st>>>(D, b, n, sh, Xmr);
 			kt.mark(CCG_K_POP);
 			SH_HIP(hipGetLastError());
 			launches += (G > 0) + 5;   // k_sh_xm, fold, lines, join, pop
@@ -789,10 +1048,10 @@ int ccg_rccl_open(ccg_ctx *ctx, const void *id, int rank, int world, ccg_coll *o
 int ccg_tree_shard_bytes(int64_t n, int etype, int method, int world, int64_t *device_bytes, int64_t *gather_bytes) {
 	if(!device_bytes || n < 3 || n > INT32_MAX - 512 || world < 1) return CCG_EINVAL;
 	if(etype != 8 && etype != 4 && etype != 2 && etype != 1) return CCG_EINVAL;
-	if(method != CCG_TREE_NJ && method != CCG_TREE_DNJ) return CCG_EINVAL;
+	if(method != CCG_TREE_NJ && method != CCG_TREE_DNJ && method != CCG_TREE_HNJ) return CCG_EINVAL;
 	const int n0 = (int) n;
 	*device_bytes = (int64_t) (method == CCG_TREE_DNJ ? ccg_shard_dnj_bytes(n0, world, etype)
-	                                                  : ShnLayout(n0, world, etype).sz);
+	                                                  : ShnLayout(n0, world, etype, method == CCG_TREE_HNJ).sz);
 	// sh_init_chunk's bound on the hard-column gather buffer (a quarter of the
 	// free memory, at most 16 GB, at least 256 columns)
 	if(gather_bytes) {
@@ -832,8 +1091,8 @@ int ccg_rccl_close(ccg_coll *c) {
 
 static int shard_check(ccg_ctx *c, const ccg_tree_args *a, const ccg_coll *coll) {
 	if(!c || !a) return CCG_EINVAL;
-	if(a->method == CCG_TREE_HNJ) return CCG_EUNSUP;   // HNJ runs on one GPU
-	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ)) return CCG_EINVAL;
+	if(a->n < 3 || (a->method != CCG_TREE_NJ && a->method != CCG_TREE_DNJ && a->method != CCG_TREE_HNJ))
+		return CCG_EINVAL;
 	if(a->etype != 8 && a->etype != 4 && a->etype != 2 && a->etype != 1) return CCG_EINVAL;
 	if((a->etype == 2 || a->etype == 1) && !(a->byteScale != 0)) return CCG_EINVAL;
 	if(coll && (coll->world < 1 || coll->rank < 0 || coll->rank >= coll->world || !coll->allreduce_sum_u8 ||

@@ -225,10 +225,6 @@ static int main_tree(int argc, char **argv) {
 	}
 	if((et == 2 || et == 1) && bs == 0) die_opt("Invalid", et == 2 ? "\"--short_precision\"" : "\"--byte_precision\"");
 	if(gpus < 0) die_opt("Invalid", "\"--gpus\"");
-	if(gpus && m == CCG_TREE_HNJ) {
-		fprintf(stderr, "ccphylo_amd: -m hnj runs on one GPU (--gpus shards nj and dnj).\n");
-		return 1;
-	}
 
 	FILE *out = (outname[0] == '-' && outname[1] == 0) ? stdout : fopen(outname, "wb");
 	if(!out) {
@@ -326,7 +322,7 @@ static int dist_help(FILE *out) {
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 't', "threads", "Number of threads", "1");
 	fprintf(out, "#    -%c, --%-16s\t%-32s\t%s\n", 'h', "help", "Shows this helpmessage", "");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree", "Also build the tree in HBM, Newick to FILE", "off");
-	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_method", "nj / dnj (/ hnj, 1 GPU) for --tree", "dnj");
+	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_method", "nj / dnj / hnj for --tree", "dnj");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "tree_flag", "tree -f flags for --tree", "0");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "gpus", "Shard --tree over G GPUs", "1");
 	fprintf(out, "#        --%-16s\t%-32s\t%s\n", "transport", "rccl / host collectives for --gpus", "rccl");
@@ -601,10 +597,9 @@ static int dist_tree(const char *in, const char *treename, const char *tmethod, 
 	int m;
 	if(!strcmp(tmethod, "dnj")) m = CCG_TREE_DNJ;
 	else if(!strcmp(tmethod, "nj")) m = CCG_TREE_NJ;
-	else if(!strcmp(tmethod, "hnj") && gpus <= 1) m = CCG_TREE_HNJ;
+	else if(!strcmp(tmethod, "hnj")) m = CCG_TREE_HNJ;
 	else {
-		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline runs nj and dnj (hnj with --gpus 1).\n",
-		        tmethod);
+		fprintf(stderr, "ccphylo_amd: --tree_method %s: the fused pipeline runs nj, dnj and hnj.\n", tmethod);
 		return 1;
 	}
 	if(norm && (et == 2 || et == 1)) {

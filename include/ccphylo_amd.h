@@ -307,8 +307,9 @@ int ccg_rccl_close(ccg_coll *coll);
  * (the multi-GPU CLI calls it on every rank's communicator when one fails). */
 int ccg_rccl_abort(ccg_coll *coll);
 
-/* NJ (a->method = CCG_TREE_NJ, nj_thread nj.c:1612) or DNJ (CCG_TREE_DNJ,
- * dnj_thread dnj.c:1054) on the rank's rows.  Every rank returns the full
+/* NJ (a->method = CCG_TREE_NJ, nj_thread nj.c:1612), DNJ (CCG_TREE_DNJ,
+ * dnj_thread dnj.c:1054) or HNJ (CCG_TREE_HNJ, hclust.c:1671) on the rank's
+ * rows.  Every rank returns the full
  * join list, identical on all ranks and bit-identical to ccg_tree with the
  * same method and `exact` flag for any world size.  Dloc_dev holds the
  * rank's ccg_shard_elems(n, rank, world) elements and is consumed.

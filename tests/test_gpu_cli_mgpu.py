@@ -25,8 +25,8 @@ def cli(args, **kw):
 
 
 TREE_CASES = [c for c in golden_cases("tree")
-              if not c["name"].startswith(("miss", "multi")) and "hnj" not in c["args"]
-              and ("-m" not in c["args"] or c["args"][c["args"].index("-m") + 1] in ("nj", "dnj"))]
+              if not c["name"].startswith(("miss", "multi"))
+              and ("-m" not in c["args"] or c["args"][c["args"].index("-m") + 1] in ("nj", "dnj", "hnj"))]
 
 
 @pytest.mark.parametrize("case", TREE_CASES, ids=lambda c: c["name"])
@@ -41,7 +41,7 @@ def _write_phylip(path, D, n):
     native.write_phylip(str(path), D, n, [f"t{k}" for k in range(n)])
 
 
-@pytest.mark.parametrize("method", ["dnj", "nj"])
+@pytest.mark.parametrize("method", ["dnj", "nj", "hnj"])
 @pytest.mark.parametrize("fast", [False, True])
 def test_cli_tree_gpus8_matches_one_gpu(tmp_path, method, fast):
     """8 ranks (the driver's node size) on the one GPU through the host
@@ -56,11 +56,16 @@ def test_cli_tree_gpus8_matches_one_gpu(tmp_path, method, fast):
     assert eight == one
 
 
-def test_cli_tree_gpus_refuses_hnj(tmp_path):
-    import ccphylo_amd as cg
-    p = subprocess.run([cg.CLI_PATH, "tree", "-i", os.path.join(GOLDEN, "test.phy.gz"), "-m", "hnj", "--gpus", "2",
-                        "--transport", "host"], capture_output=True, timeout=120)
-    assert p.returncode == 1 and b"hnj" in p.stderr
+def test_cli_dist_tree_fused_hnj(tmp_path):
+    """`dist --tree --tree_method hnj` over 3 ranks: the Newick of `dist | tree -m hnj`."""
+    src = os.path.join(GOLDEN, "msa300.fsa")
+    phy = tmp_path / "d.phy"
+    with open(phy, "wb") as f:
+        f.write(cli(["dist", "-i", src]))
+    two_step = cli(["tree", "-i", str(phy), "-m", "hnj"])
+    out = tmp_path / "t.nwk"
+    cli(["dist", "-i", src, "--tree", str(out), "--tree_method", "hnj", "--gpus", "3", "--transport", "host"])
+    assert out.read_bytes() == two_step
 
 
 DIST_MSAS = ["msa64.fsa", "msa300.fsa", "msa_crlf.fsa", "msa_odd.fsa", "msa_word.fsa"]

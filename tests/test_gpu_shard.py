@@ -83,7 +83,7 @@ def _data(kind, n):
     return {"euc": _euclid, "snp": _snp, "clade": _clade}[kind](n, n)
 
 
-@pytest.mark.parametrize("method", [0, 1], ids=["nj", "dnj"])
+@pytest.mark.parametrize("method", [0, 1, 2], ids=["nj", "dnj", "hnj"])
 @pytest.mark.parametrize("n,kind,et,exact", [(600, "euc", 8, True), (600, "euc", 8, False), (1100, "snp", 8, True),
                                              (700, "snp", 4, True), (700, "snp", 2, False), (500, "snp", 1, True),
                                              (2100, "euc", 8, False), (3000, "clade", 8, True)])
@@ -95,8 +95,7 @@ def test_shard_world1_matches_single(dev, n, kind, et, exact, method):
 
 
 # miss80 and multi.phy's second matrix hold missing entries (CCG_EUNSUP below)
-@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if not c["name"].startswith(("miss", "multi"))
-                                  and "hnj" not in c["args"]],
+@pytest.mark.parametrize("case", [c for c in golden_cases("tree") if not c["name"].startswith(("miss", "multi"))],
                          ids=lambda c: c["name"])
 def test_shard_golden(dev, case):
     import ccphylo_amd as cg
@@ -115,7 +114,7 @@ def test_shard_refuses_missing(dev):
     n = 50
     D = _euclid(n, 1)
     D[17] = -1.0
-    for method in (0, 1):
+    for method in (0, 1, 2):
         with pytest.raises(cg.CcgError, match="not supported"):
             dev.tree_shard(D, n, None, method=method)
 
@@ -173,7 +172,13 @@ def _rank_main(rank, world, port, n, kind, et, exact, transport, method, out_dir
                                                                     # world 8, the driver's node size, rehearsed as 8
                                                                     # processes on the one GPU
                                                                     (8, 1200, "euc", 8, True, "gloo", 1),
-                                                                    (8, 800, "snp", 8, True, "gloo", 0)])
+                                                                    (8, 800, "snp", 8, True, "gloo", 0),
+                                                                    # HNJ (hclust.c:1671) over the row shards
+                                                                    (2, 700, "euc", 8, True, "gloo", 2),
+                                                                    (3, 450, "snp", 8, True, "gloo", 2),
+                                                                    (2, 400, "snp", 2, False, "gloo", 2),
+                                                                    (1, 900, "euc", 8, True, "rccl", 2),
+                                                                    (8, 800, "snp", 8, True, "gloo", 2)])
 def test_shard_multiprocess(dev, tmp_path, world, n, kind, et, exact, transport, method):
     D, bs = _typed(_data(kind, n), et)
     ref_j, ref_fn, ref_fd, _ = dev.tree(D, n, etype=et, byte_scale=bs, method=method, exact=exact)
@@ -255,12 +260,21 @@ def test_max_joins_prefix(dev):
     assert (j == fullq[:k]).all()
 
 
-def test_shard_hnj_unsupported(dev):
-    """HNJ runs on one GPU: the sharded kernels say so (CCG_EUNSUP)."""
+def test_shard_hnj_prefix_and_ties(dev):
+    """Sharded HNJ (k_sh_hnj_argmin / k_sh_hnj): max_joins prefixes of the
+    single engine's join list, and a matrix of equal entries (minQ's `<=`
+    rule, hclust.c:353, and the column rules' ties decide every join)."""
     import ccphylo_amd as cg
-    D = np.arange(10 * 9 // 2, dtype=np.float64)
-    with pytest.raises(cg.CcgError, match="not supported"):
-        dev.tree_shard(D, 10, None, method=cg.CCG_TREE_HNJ)
+    n, k = 500, 37
+    D = _euclid(n, 5)
+    full = dev.tree(D, n, method=cg.CCG_TREE_HNJ)[0]
+    j, fin, fd, _ = dev.tree_shard(D, n, None, method=cg.CCG_TREE_HNJ, max_joins=k)
+    assert len(j) == k and fin == n - k and fd == -1.0 and (j == full[:k]).all()
+    for et in (8, 1):
+        E = np.full(300 * 299 // 2, 7.0)
+        E, bs = _typed(E, et)
+        _same(dev.tree_shard(E, 300, None, etype=et, byte_scale=bs, method=cg.CCG_TREE_HNJ)[:3],
+              dev.tree(E, 300, etype=et, byte_scale=bs, method=cg.CCG_TREE_HNJ)[:3])
 
 
 @pytest.mark.parametrize("method", [0, 1, 2], ids=["nj", "dnj", "hnj"])
