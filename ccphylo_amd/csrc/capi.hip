@@ -159,7 +159,7 @@ void ccg_destroy(ccg_ctx *c) {
 	if(!c) return;
 	hipSetDevice(c->device);
 	if(!(c->masked && g_shut)) hipStreamSynchronize(c->stream);
-	for(int k = 0; k < 2; ++k)
+	for(int k = 0; k < 3; ++k)
 		if(c->ws[k]) hipFree(c->ws[k]);
 	hipEventDestroy(c->ev0);
 	hipEventDestroy(c->ev1);

@@ -35,11 +35,12 @@ struct ccg_ctx {
 	int flags;       // CCG_CTX_* (ccg_ctx_configure)
 	int masked;      // the stream was created with a CU mask (ccg_ctx_configure)
 	int ncu, cus;    // the device's CUs; the CUs the stream may use (0: all)
-	// the tree's device workspaces, kept across runs (grown on demand, freed
-	// by ccg_destroy): a tree run then makes no hipFree, which waits for every
-	// stream of the device, so a CCG_CTX_NOSYNC context never waits for another
-	void *ws[2];
-	size_t ws_bytes[2];
+	// device workspaces kept across runs (grown on demand, freed by
+	// ccg_destroy): slots 0 / 1 the tree's, slot 2 the dist's bit planes in a
+	// CCG_CTX_NOSYNC context.  A run then makes no hipFree, which waits for
+	// every stream of the device, so such a context never waits for another
+	void *ws[3];
+	size_t ws_bytes[3];
 };
 // slot k of the context's workspace cache, at least `bytes` long
 int ccg_ctx_workspace(ccg_ctx *c, int k, size_t bytes, void **p);

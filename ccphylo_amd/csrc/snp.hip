@@ -2473,16 +2473,37 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	const size_t esz = a->pair ? sizeof(uint4) : sizeof(uint2);
 	void *planes = NULL;
 	int *d_inc = NULL, *d_widx = NULL;
-	CCG_CHECK(hipMalloc(&planes, (size_t) npad * Wp * esz));
-	if(hipMalloc(&d_inc, sizeof(int)) != hipSuccess ||
-	   (!keep.empty() && hipMalloc(&d_widx, keep.size() * sizeof(int)) != hipSuccess)) {
+	// a CCG_CTX_NOSYNC context (a pipeline's dist) keeps its planes in the
+	// workspace cache: no hipMalloc / hipFree per matrix (hipFree waits for
+	// every stream of the device, the other context's too)
+	// (with the small buffers behind them: the count and the word list)
+	const bool cached = (ctx->flags & CCG_CTX_NOSYNC) != 0;
+	const size_t planes_b = ((size_t) npad * Wp * esz + 255) & ~(size_t) 255;
+	auto free_bufs = [&]() {
+		if(cached) return;
 		hipFree(planes);
 		hipFree(d_inc);
-		return CCG_ENOMEM;
+		hipFree(d_widx);
+	};
+	if(cached) {
+		const int wrc = ccg_ctx_workspace(ctx, 2, planes_b + 256 + keep.size() * sizeof(int), &planes);
+		if(wrc != CCG_OK) return wrc;
+		d_inc = (int *) ((char *) planes + planes_b);
+		if(!keep.empty()) d_widx = (int *) ((char *) planes + planes_b + 256);
+	} else {
+		CCG_CHECK(hipMalloc(&planes, planes_b));
+		if(hipMalloc(&d_inc, sizeof(int)) != hipSuccess ||
+		   (!keep.empty() && hipMalloc(&d_widx, keep.size() * sizeof(int)) != hipSuccess)) {
+			hipFree(planes);
+			hipFree(d_inc);
+			return CCG_ENOMEM;
+		}
 	}
 	uint32_t *mask = NULL;
 	int prc = CCG_OK;
-	if(hipMemsetAsync(planes, 0, (size_t) npad * Wp * esz, ctx->stream) != hipSuccess ||
+	// k_planes writes every word of rows < n: only the padding rows need zeros
+	if(hipMemsetAsync((char *) planes + (size_t) a->n * Wp * esz, 0, (size_t) (npad - a->n) * Wp * esz,
+	                  ctx->stream) != hipSuccess ||
 	   (d_widx && hipMemcpyAsync(d_widx, keep.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice,
 	                             ctx->stream) != hipSuccess))
 		prc = CCG_EHIP;
@@ -2494,9 +2515,7 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	}
 	if(prc) {
 		hipStreamSynchronize(ctx->stream);
-		hipFree(planes);
-		hipFree(d_inc);
-		hipFree(d_widx);
+		free_bufs();
 		hipFree(mask);
 		return prc;
 	}
@@ -2507,7 +2526,8 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 		CCG_CHECK(hipStreamSynchronize(ctx->stream));
 	}
 	if(mask) CCG_CHECK(hipFree(mask));
-	if(d_widx) CCG_CHECK(hipFree(d_widx));
+	if(d_widx && !cached) CCG_CHECK(hipFree(d_widx));
+	d_widx = NULL;
 	double nFactor = 1.0;
 	if(!a->pair && a->norm) {
 		nFactor = a->norm;
@@ -2516,8 +2536,7 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	long long rb = a->row_begin, re = a->row_end;
 	if(rb == 0 && re == 0) re = a->n;
 	if(rb < 0 || re > a->n || rb > re) {
-		hipFree(planes);
-		hipFree(d_inc);
+		free_bufs();
 		return CCG_EINVAL;
 	}
 	int rc = CCG_OK;
@@ -2541,8 +2560,10 @@ static int snp_run(ccg_ctx *ctx, const ccg_snp_args *a, void *D, void *N, int *i
 	CCG_CHECK(hipEventRecord(ctx->ev1, ctx->stream));
 	CCG_CHECK(hipStreamSynchronize(ctx->stream));
 	if(rc == CCG_OK) CCG_CHECK(hipEventElapsedTime(&ctx->dist_ms, ctx->ev0, ctx->ev1));
-	CCG_CHECK(hipFree(planes));
-	CCG_CHECK(hipFree(d_inc));
+	if(!cached) {
+		CCG_CHECK(hipFree(planes));
+		CCG_CHECK(hipFree(d_inc));
+	}
 	if(inc_out) *inc_out = inc;
 	return rc;
 }
