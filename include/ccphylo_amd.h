@@ -63,7 +63,10 @@ int ccg_init(int device, ccg_ctx **ctx);
  * each masked configuration keeps one HIP stream until the process exits.
  * flags CCG_CTX_NOSYNC: the device-pointer entry points do not wait for the
  * whole device first (the caller orders its inputs; a device-wide wait would
- * wait for the other context's work). */
+ * wait for the other context's work), and the context keeps its workspaces
+ * -- the tree's, and the dist's bit planes (about n x L / 4 bytes) -- until
+ * ccg_destroy, so that no call frees device memory (hipFree waits for every
+ * stream of the device). */
 #define CCG_CTX_NOSYNC 1
 int ccg_ctx_configure(ccg_ctx *ctx, const uint32_t *cu_mask, int mask_words, int flags);
 /* Process end, after the last HIP work of the process: destroys the CU-masked
