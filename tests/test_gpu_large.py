@@ -187,10 +187,15 @@ def _config3_rank(rank, world, port, n, k, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = cg.Device(0)
-    loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
+    # the ranks build their shards one after another: 8 ranks share the one
+    # GPU, and each generator's temporaries (a few GB) should not peak together
+    for r in range(world):
+        if r == rank:
+            loc = euclid_shard_dev(torch, n, rank, world, dtype=torch.float32)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        dist.barrier()
     assert loc.numel() == nt.shard_elems(n, rank, world)
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()   # the generator's temporaries: 8 ranks share the one GPU
     coll = nt.HostColl(dist)
     dist.barrier()
     t0 = time.perf_counter()
@@ -249,6 +254,8 @@ def test_config3_dnj_prefix(dev, monkeypatch, tmp_path):
     import gc
     gc.collect()
     torch.cuda.empty_cache()   # this process's cached blocks (earlier tests') back to the device for the 8 ranks
+    free_b, total_b = torch.cuda.mem_get_info()
+    print(f"device memory before the 8 ranks: {free_b / 2**30:.1f} GiB free of {total_b / 2**30:.1f}", flush=True)
     mp.start_processes(_config3_rank, args=(world, _free_port(), n, kw, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     ref = pyoracle.tree(host, n, etype=4, method=cg.CCG_TREE_DNJ, max_joins=k, threads=THREADS, copy=False)
