@@ -21,7 +21,10 @@ def euclid_shard_dev(torch, n, rank, world, seed=4, dim=8, band=8, chunk_rows=51
     Every rank draws the same points (CPU generator, fixed seed); computed in
     double, stored as `dtype` (default float64; float32 = `-p`).  cdist: the
     round-4 form (torch.cdist per chunk of rows), kept to reproduce that
-    round's configs[3] matrix."""
+    round's configs[3] matrix.  On this image's PyTorch-ROCm build
+    torch.cdist gives wrong cells once a chunk has more than ~32k columns
+    (tools/cdist_check.py, profiles/r06_generator_check.txt), so at n = 200k
+    that form is not a Euclidean matrix."""
     g = torch.Generator().manual_seed(seed)
     pts = torch.rand((n, dim), generator=g, dtype=torch.float64).cuda()
     nb = (n + band - 1) // band
